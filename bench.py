@@ -1,0 +1,189 @@
+#!/usr/bin/env python
+"""RecBLR training-step benchmark on MI355X (BASELINE.json metric).
+
+One step = RecBLR.calculate_loss (CE over all items) + backward + Adam step at
+B=2048 sequences per GPU, L=200, d=128 (H=256), 2 layers, n_items=10,544
+(amazon-beauty), train mode (dropout 0.2) — SURVEY.md §8(d).  Inputs are
+synthetic RecBole-shaped batches already resident in HBM; weights are the
+reference init.  Multi-GPU: one process per GPU (torchrun), batch-DP with
+DDP gradient all-reduce over RCCL, weak scaling (2048 per GPU).
+
+Prints ONE JSON line on rank 0 with the throughput, the HBM roofline of the
+dominant HIP kernel (HIP-event timed inside the timed region) and the CPU
+oracle baseline (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from datamining_recblr_amd import kernels  # noqa: E402
+from datamining_recblr_amd.distributed import (barrier, init_from_env, max_over_ranks,  # noqa: E402
+                                               synthetic_interaction, wrap_ddp)
+from datamining_recblr_amd.model import RecBLR  # noqa: E402
+from datamining_recblr_amd.recbole_compat import SyntheticDataset  # noqa: E402
+
+METRIC = "sequences/sec fwd+bwd at B=2048 L=200 d=128; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+DOMINANT = "rb_gate_scan_bwd"  # the HIP kernel moving the most bytes per step
+
+
+def make_cfg(args):
+    return dict(hidden_size=args.hidden, loss_type="CE", num_layers=args.layers,
+                dropout_prob=args.dropout, expand=2, d_conv=4, bd_lru_only=False,
+                disable_conv1d=False, disable_ffn=False, MAX_ITEM_LIST_LENGTH=args.seq_len)
+
+
+def cpu_baseline(args, state_dict):
+    """The CPU oracle (serial-scan restatement of the reference) on a bounded
+    sample of the same workload: one fwd+bwd+Adam step over `cpu_sample`
+    sequences, median of 3 after 1 warm-up."""
+    from oracle import recblr_oracle as orc
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = make_cfg(args)
+    params = {k: v.detach().cpu().clone().requires_grad_(v.dtype.is_floating_point)
+              for k, v in state_dict.items()}
+    leaves = [p for p in params.values() if p.requires_grad]
+    opt = torch.optim.Adam(leaves, lr=1e-3)
+    inter = synthetic_interaction(args.cpu_sample, args.seq_len, args.n_items, "cpu", seed=0)
+    times = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        opt.zero_grad(set_to_none=True)
+        loss = orc.calculate_loss(params, cfg, inter["item_id_list"], inter["item_length"],
+                                  inter["item_id"])
+        loss.backward()
+        opt.step()
+        times.append(time.perf_counter() - t0)
+    med = sorted(times[1:])[1]
+    return {"value": round(args.cpu_sample / med, 3), "unit": "sequences/sec", "cores": threads,
+            "kind": "port",
+            "sample": (f"oracle (serial-scan CPU restatement) CE fwd+bwd+Adam step on "
+                       f"{args.cpu_sample} of the {args.batch} sequences, L={args.seq_len}, "
+                       f"d={args.hidden}, n_items={args.n_items}, dropout off; median of 3 "
+                       f"after 1 warm-up; {med:.2f} s/step on {threads} threads")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2048, help="sequences per GPU")
+    ap.add_argument("--seq-len", type=int, default=200)
+    ap.add_argument("--hidden", type=int, default=128)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--n-items", type=int, default=10544)
+    ap.add_argument("--dropout", type=float, default=0.2)
+    ap.add_argument("--cpu-sample", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    env = init_from_env()
+    if env.world_size != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}", file=sys.stderr)
+    dev = torch.device("cuda", env.local_rank)
+    torch.cuda.set_device(dev)
+
+    torch.manual_seed(2020)  # the reference run's seed (LOG51:6); same on every rank
+    model = RecBLR(make_cfg(args), SyntheticDataset(args.n_items)).to(dev).train()
+    step_mod = wrap_ddp(model, env)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    batches = [synthetic_interaction(args.batch, args.seq_len, args.n_items, dev,
+                                     seed=1000 * env.rank + i) for i in range(4)]
+
+    def step(i):
+        opt.zero_grad(set_to_none=True)
+        loss = step_mod(batches[i % len(batches)])
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    barrier(env)
+    torch.cuda.synchronize()
+
+    timing = kernels.kernel_timing() if not args.no_kernel_timing else None
+    timer = timing.__enter__() if timing else None
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    barrier(env)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if timing:
+        timing.__exit__(None, None, None)
+    elapsed = max_over_ranks(elapsed, env, dev)
+    ms = 1000.0 * elapsed / args.steps
+    value = env.world_size * args.batch * args.steps / elapsed
+    if not torch.isfinite(loss):
+        raise RuntimeError(f"non-finite loss {loss}")
+
+    roofline = None
+    kernels_report = None
+    if timer is not None:
+        summ = timer.summary()
+        kernels_report = {}
+        for name, d in summ.items():
+            gbs = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
+            kernels_report[name] = {"launches_per_step": d["launches"] / args.steps,
+                                    "avg_us": round(d["avg_ms"] * 1e3, 2),
+                                    "algo_bytes": int(d["avg_bytes"]),
+                                    "achieved_gbs": round(gbs, 1),
+                                    "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if DOMINANT in summ:
+            d = summ[DOMINANT]
+            ach = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
+            roofline = {"kernel": DOMINANT, "bound": "hbm", "achieved": round(ach, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                        "traffic": None,
+                        "algo_bytes_per_launch": int(d["avg_bytes"]),
+                        "avg_launch_us": round(d["avg_ms"] * 1e3, 2)}
+        tot_b = sum(d["bytes"] for d in summ.values())
+        tot_ms = sum(d["ms"] for d in summ.values())
+        kernels_report["fused_path_total"] = {
+            "ms_per_step": round(tot_ms / args.steps, 4),
+            "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
+            "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    cpu = None
+    if env.rank == 0 and env.world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, model.state_dict())
+
+    if env.rank == 0:
+        H = 2 * args.hidden
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "sequences/sec",
+            "n_gpus": env.world_size, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic RecBole-shaped batches (ids ~U{1..n_items-1}, lengths ~U{1..L}, "
+                    "right-padded), reference init (seed 2020), resident in HBM",
+            "config": {"workload": "RecBLR train step: calculate_loss(CE)+backward+Adam",
+                       "batch_per_gpu": args.batch, "global_batch": args.batch * env.world_size,
+                       "seq_len": args.seq_len, "hidden_size": args.hidden, "inner_H": H,
+                       "num_layers": args.layers, "n_items": args.n_items,
+                       "dropout": args.dropout, "parallelism": f"dp{env.world_size}"},
+            "roofline": roofline,
+            "kernels": kernels_report,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,86 @@
+"""ctypes binding of the C-ABI in include/recblr_hip.h.
+
+The shared library is built in-tree by ``datamining_recblr_amd.build`` (or
+``__graft_entry__.build()``) as ``datamining_recblr_amd/lib/libdmrecblr.so``.
+There is no fallback: if the library is missing, every product entry point
+raises ``RecBLRNativeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libdmrecblr.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
+
+RB_EINVAL = -1
+RB_TILE = 64
+ABI_VERSION = 1
+
+_i64 = ctypes.c_int64
+_fp = ctypes.c_void_p  # device pointers are passed as integers
+
+# name -> (restype, argtypes); kept in the order of include/recblr_hip.h
+SIGNATURES = {
+    "rb_version": (ctypes.c_int, []),
+    "rb_last_error_string": (ctypes.c_char_p, []),
+    "rb_num_kernels": (ctypes.c_int, []),
+    "rb_scan_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp]),
+    "rb_scan_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp]),
+    "rb_conv_silu_fwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64, _i64, _fp]),
+    "rb_conv_silu_bwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
+                                        _i64, _i64, _i64, _i64, _fp]),
+    "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp,
+                                        _i64, _i64, _i64, _fp]),
+    "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _i64,
+                                        _fp, _fp, _i64, _fp, _fp, _i64, _i64, _i64, _fp]),
+}
+
+
+class RecBLRNativeError(RuntimeError):
+    """The HIP extension is missing, failed to load, or a kernel call failed."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and return the native library with typed prototypes."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RecBLRNativeError(
+                f"HIP extension not built: {p} is missing. Run "
+                "`python -m datamining_recblr_amd.build` (hipcc --offload-arch=gfx950)."
+            )
+        try:
+            lib = ctypes.CDLL(p)
+        except OSError as exc:  # pragma: no cover - depends on the host
+            raise RecBLRNativeError(f"failed to load {p}: {exc}") from exc
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.rb_version() != ABI_VERSION:
+            raise RecBLRNativeError(
+                f"ABI mismatch: library {lib.rb_version()} vs binding {ABI_VERSION}; rebuild")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def call(name: str, *args) -> None:
+    """Invoke a C-ABI entry point and raise on a non-zero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.rb_last_error_string()
+        msg = msg.decode() if msg else ""
+        kind = "invalid argument" if rc == RB_EINVAL else f"hipError {rc}"
+        raise RecBLRNativeError(f"{name} failed ({kind}): {msg}")

@@ -1,0 +1,106 @@
+"""Batch-axis data parallelism over RCCL (one process per GPU).
+
+The reference has no distributed path.  The encoder's
+work shards perfectly on the batch axis: every (batch row, channel)
+recurrence is independent and the pad-prefix state is batch independent, so
+the only exchange per training step is the parameter-gradient all-reduce,
+which DistributedDataParallel buckets and overlaps with the backward pass
+(backend "nccl" is RCCL on ROCm; xGMI between the GPUs of a node).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+from torch import nn
+
+__all__ = ["DistEnv", "init_from_env", "LossModule", "wrap_ddp", "synthetic_interaction",
+           "max_over_ranks", "shard_range", "barrier"]
+
+
+class DistEnv:
+    def __init__(self, rank=0, local_rank=0, world_size=1):
+        self.rank, self.local_rank, self.world_size = rank, local_rank, world_size
+
+    @property
+    def distributed(self):
+        return self.world_size > 1
+
+
+def init_from_env(backend: str | None = None) -> DistEnv:
+    """Read RANK / LOCAL_RANK / WORLD_SIZE (torchrun) and join the process group."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    env = DistEnv(rank, local, world)
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return env
+
+
+class LossModule(nn.Module):
+    """Routes DDP's forward() to ``model.calculate_loss`` so the reducer's
+    per-iteration bookkeeping runs (RecBole's Trainer calls calculate_loss)."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+
+    def forward(self, interaction):
+        return self.model.calculate_loss(interaction)
+
+
+def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float = 32.0) -> nn.Module:
+    step = LossModule(model)
+    if not env.distributed:
+        return step
+    dev = next(model.parameters()).device
+    kw = dict(device_ids=[dev.index]) if dev.type == "cuda" else {}
+    return nn.parallel.DistributedDataParallel(
+        step, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
+        broadcast_buffers=False, **kw)
+
+
+def synthetic_interaction(batch: int, seq_len: int, n_items: int, device, seed: int,
+                          with_neg: bool = False) -> dict:
+    """RecBole-shaped batch: ids ~ U{1..n_items-1}, lengths ~ U{1..seq_len},
+    sequences right-padded with item 0 past their length."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lengths = torch.randint(1, seq_len + 1, (batch,), generator=g)
+    seq = torch.randint(1, n_items, (batch, seq_len), generator=g)
+    seq = seq * (torch.arange(seq_len)[None, :] < lengths[:, None])
+    inter = {"item_id_list": seq, "item_length": lengths,
+             "item_id": torch.randint(1, n_items, (batch,), generator=g)}
+    if with_neg:
+        inter["neg_item_id"] = torch.randint(1, n_items, (batch,), generator=g)
+    return {k: v.to(device) for k, v in inter.items()}
+
+
+def shard_range(global_batch: int, rank: int, world: int):
+    """[start, stop) of this rank's rows under strong scaling (balanced split)."""
+    base, rem = divmod(global_batch, world)
+    start = rank * base + min(rank, rem)
+    return start, start + base + (1 if rank < rem else 0)
+
+
+def max_over_ranks(value: float, env: DistEnv, device=None) -> float:
+    if not env.distributed:
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(env: DistEnv) -> None:
+    if env.distributed:
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()

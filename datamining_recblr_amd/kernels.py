@@ -1,0 +1,233 @@
+"""Typed Python callers for the C-ABI entry points.
+
+Each function validates device, dtype, shape and layout (mirroring the
+reference's asserts, parallel_scan.py:86-89 and :102-104), allocates outputs
+with torch's caching allocator, and launches on the current torch stream.
+No function here has a CPU path: tensors must live on a ROCm GPU.
+"""
+from __future__ import annotations
+
+import contextlib
+
+import torch
+
+from . import _lib
+from ._lib import RB_TILE, RecBLRNativeError
+
+__all__ = [
+    "scan_fwd", "scan_bwd", "conv_silu_fwd", "conv_silu_bwd", "gate_scan_fwd",
+    "gate_scan_bwd", "num_tiles", "RecBLRNativeError", "kernel_timing", "KernelTimer",
+]
+
+
+class KernelTimer:
+    """HIP-event timing of every C-ABI launch, recorded on the stream the
+    kernel is launched on (torch's current stream).  Used by bench.py."""
+
+    def __init__(self):
+        self.records = []   # (name, algorithmic bytes, start event, end event)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, nbytes, e0, e1 in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0})
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["bytes"] += nbytes
+        for d in out.values():
+            d["avg_ms"] = d["ms"] / d["launches"]
+            d["avg_bytes"] = d["bytes"] / d["launches"]
+        return out
+
+
+_timer: KernelTimer | None = None
+
+
+@contextlib.contextmanager
+def kernel_timing():
+    global _timer
+    prev, _timer = _timer, KernelTimer()
+    try:
+        yield _timer
+    finally:
+        _timer = prev
+
+
+def _launch(name: str, nbytes: int, *args) -> None:
+    t = _timer
+    if t is None:
+        _lib.call(name, *args)
+        return
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    _lib.call(name, *args)
+    e1.record()
+    t.records.append((name, nbytes, e0, e1))
+
+
+def num_tiles(L: int) -> int:
+    return (L + RB_TILE - 1) // RB_TILE
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check(t: torch.Tensor, name: str) -> None:
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RecBLRNativeError(
+            f"{name} is on {t.device}; the RecBLR HIP path needs a ROCm GPU tensor "
+            "(there is no CPU fallback)")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32, got {t.dtype}")
+
+
+def _row_stride(t: torch.Tensor, name: str, H: int) -> int:
+    """Row stride of a [B, L, >=H] view whose (b, t) rows are uniformly spaced."""
+    if t.dim() != 3 or t.shape[2] != H:
+        raise ValueError(f"{name} must be [B, L, {H}], got {tuple(t.shape)}")
+    B, L, _ = t.shape
+    if t.stride(2) != 1 and H > 1:
+        raise ValueError(f"{name} must have unit channel stride")
+    rs = t.stride(1) if L > 1 else (t.stride(0) if B > 1 else H)
+    if L > 1 and B > 1 and t.stride(0) != rs * L:
+        raise ValueError(f"{name}: rows are not uniformly strided")
+    if rs < H:
+        raise ValueError(f"{name}: row stride {rs} < {H}")
+    return rs
+
+
+def scan_fwd(gates: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
+    _check(gates, "gates")
+    _check(tokens, "tokens")
+    if gates.dim() != 3 or tokens.shape != gates.shape:
+        raise ValueError("gates and tokens must both be [B, C, T] of equal shape")
+    if not (gates.is_contiguous() and tokens.is_contiguous()):
+        raise ValueError("gates and tokens must be contiguous")
+    B, C, T = gates.shape
+    states = torch.empty_like(tokens)
+    if states.numel():
+        _launch("rb_scan_fwd", 3 * gates.numel() * 4, gates.data_ptr(), tokens.data_ptr(), states.data_ptr(),
+                  B, C, T, _stream(gates))
+    return states
+
+
+def scan_bwd(gates: torch.Tensor, states: torch.Tensor, grad: torch.Tensor):
+    for t, n in ((gates, "gates"), (states, "states"), (grad, "grad")):
+        _check(t, n)
+        if not t.is_contiguous():
+            raise ValueError(f"{n} must be contiguous")
+    if states.shape != gates.shape or grad.shape != gates.shape:
+        raise ValueError("shape mismatch")
+    B, C, T = gates.shape
+    d_gates = torch.empty_like(gates)
+    d_tokens = torch.empty_like(gates)
+    if gates.numel():
+        _launch("rb_scan_bwd", 5 * gates.numel() * 4, gates.data_ptr(), states.data_ptr(), grad.data_ptr(),
+                  d_gates.data_ptr(), d_tokens.data_ptr(), B, C, T, _stream(gates))
+    return d_gates, d_tokens
+
+
+def conv_silu_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """x: [B, L, H] (row-strided view ok); weight: [H, K]; bias: [H] -> xc [B, L, H]."""
+    _check(x, "x")
+    _check(weight, "conv weight")
+    _check(bias, "conv bias")
+    B, L, H = x.shape
+    x_rs = _row_stride(x, "x", H)
+    w = weight.reshape(H, -1).contiguous()
+    K = w.shape[1]
+    xc = torch.empty((B, L, H), device=x.device, dtype=torch.float32)
+    _launch("rb_conv_silu_fwd", 2 * B * L * H * 4, x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
+              xc.data_ptr(), H, B, L, H, K, _stream(x))
+    return xc
+
+
+def conv_silu_bwd(x, weight, bias, g1, g2, dx):
+    """Writes dx (a [B, L, H] row-strided view) and returns (dweight [H, K], dbias [H])."""
+    _check(x, "x")
+    _check(g1, "g1")
+    _check(dx, "dx")
+    B, L, H = x.shape
+    x_rs = _row_stride(x, "x", H)
+    dx_rs = _row_stride(dx, "dx", H)
+    if not g1.is_contiguous() or g1.shape != (B, L, H):
+        raise ValueError("g1 must be contiguous [B, L, H]")
+    if g2 is not None:
+        _check(g2, "g2")
+        if not g2.is_contiguous() or g2.shape != (B, L, H):
+            raise ValueError("g2 must be contiguous [B, L, H]")
+    w = weight.reshape(H, -1).contiguous()
+    K = w.shape[1]
+    dw_part = torch.empty((B, K, H), device=x.device, dtype=torch.float32)
+    db_part = torch.empty((B, H), device=x.device, dtype=torch.float32)
+    _launch("rb_conv_silu_bwd", (3 if g2 is None else 4) * B * L * H * 4, x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
+              g1.data_ptr(), 0 if g2 is None else g2.data_ptr(), dx.data_ptr(), dx_rs,
+              dw_part.data_ptr(), db_part.data_ptr(), B, L, H, K, _stream(x))
+    return dw_part.sum(0).t().contiguous(), db_part.sum(0)
+
+
+def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None):
+    """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
+
+    rg: [B, L, 2H]; xc, z: [B, L, H] views; lam: [H]; h0: [H] or None.
+    Returns (y [B, L, H], carries [B, nT, H])."""
+    for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (lam, "Lambda")):
+        _check(t, n)
+    B, L, H = xc.shape
+    rg_rs = _row_stride(rg, "rg", 2 * H)
+    xc_rs = _row_stride(xc, "xc", H)
+    z_rs = _row_stride(z, "z", H)
+    if z.shape[:2] != (B, L) or rg.shape[:2] != (B, L):
+        raise ValueError("rg, xc, z batch/length mismatch")
+    if lam.shape != (H,):
+        raise ValueError(f"Lambda must be [{H}]")
+    if h0 is not None:
+        _check(h0, "h0")
+        if h0.shape != (H,):
+            raise ValueError(f"h0 must be [{H}]")
+        h0 = h0.contiguous()
+    if y is None:
+        y = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
+    y_rs = _row_stride(y, "y", H)
+    carries = torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
+    _launch("rb_gate_scan_fwd", 5 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
+              lam.contiguous().data_ptr(), 0 if h0 is None else h0.data_ptr(), y.data_ptr(),
+              y_rs, carries.data_ptr(), B, L, H, _stream(xc))
+    return y, carries
+
+
+def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None):
+    """Backward of gate_scan_fwd.  Writes dz (a row-strided view) and returns
+    (drg [B, L, 2H], dxc [B, L, H], dlam [H], dgate_bias [2H], dh0 [H])."""
+    B, L, H = xc.shape
+    _check(dy, "dy")
+    _check(dz, "dz")
+    _check(carries, "carries")
+    if not dy.is_contiguous() or dy.shape != (B, L, H):
+        raise ValueError("dy must be contiguous [B, L, H]")
+    if carries.shape != (B, num_tiles(L), H) or not carries.is_contiguous():
+        raise ValueError("carries shape mismatch")
+    rg_rs = _row_stride(rg, "rg", 2 * H)
+    xc_rs = _row_stride(xc, "xc", H)
+    z_rs = _row_stride(z, "z", H)
+    dz_rs = _row_stride(dz, "dz", H)
+    if drg is None:
+        drg = torch.empty((B, L, 2 * H), device=xc.device, dtype=torch.float32)
+    drg_rs = _row_stride(drg, "drg", 2 * H)
+    if dxc is None:
+        dxc = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
+    elif not dxc.is_contiguous() or dxc.shape != (B, L, H):
+        raise ValueError("dxc must be contiguous [B, L, H]")
+    part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
+    dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
+    _launch("rb_gate_scan_bwd", 9 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
+              lam.contiguous().data_ptr(), carries.data_ptr(), dy.data_ptr(), drg.data_ptr(),
+              drg_rs, dxc.data_ptr(), dz.data_ptr(), dz_rs, part.data_ptr(), dh0_part.data_ptr(),
+              B, L, H, _stream(xc))
+    sums = part.sum(1)
+    return drg, dxc, sums[0], torch.cat([sums[1], sums[2]]), dh0_part.sum(0)

@@ -1,0 +1,191 @@
+"""RecBLR sequential recommender on the MI355X encoder.
+
+Drop-in for the reference's ``RecBLR.py``: same class names, constructor
+arguments, config keys (RecBLR.py:22-30), submodule and parameter names
+(``item_embedding``, ``recurrent_layers.{i}.behavior_modeling.{input, conv1d,
+gates, Lambda, output}``, ``...ffn.{w_1, w_2, layer_norm}``, ...), so RecBole
+checkpoints and ``state_dict``s move between the two unchanged.  Modules are
+created in the reference's order, so under the same seed the initial weights
+are identical too.
+
+What differs is ``GatedRecurrentLayer.forward``: the reference's ~25-kernel
+chain (pad copy, transposes, conv, a dozen elementwise gate ops, Triton scan,
+truncate, merge) is replaced by two fused HIP kernels around the gates GEMM
+(see ``recurrence.py``).  It needs a ROCm GPU; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from ._lib import RecBLRNativeError
+from .recbole_compat import BPRLoss, SequentialRecommender
+from .recurrence import bd_lru, pow2_pad_len
+
+__all__ = ["RecBLR", "RecurrentLayer", "GatedRecurrentLayer", "FeedForward",
+           "softplus_inverse", "lambda_init_range"]
+
+
+def softplus_inverse(x):
+    """log(exp(x) - 1): the Lambda init helper (RecBLR.py:14-15)."""
+    return torch.log(torch.exp(x) - 1)
+
+
+def lambda_init_range(r_min: float = 0.9, r_max: float = 0.999):
+    """Lambda endpoints such that exp(-softplus(Lambda)) spans [r_min, r_max]
+    (RecBLR.py:153-158), computed in fp32 like the reference."""
+    lo = softplus_inverse(torch.tensor(-math.log(r_min))).item()
+    hi = softplus_inverse(torch.tensor(-math.log(r_max))).item()
+    return lo, hi
+
+
+class GatedRecurrentLayer(nn.Module):
+    """in-proj -> causal conv + SiLU -> BD-LRU gates -> scan -> silu(z)*h -> out-proj.
+
+    Parameters as RecBLR.py:149-167.  ``bd_lru_only`` is stored but, as in the
+    reference (:151), does not change this block."""
+
+    def __init__(self, d_model=64, expansion_factor=2, kernel_size=4, bd_lru_only=False,
+                 disable_conv1d=False):
+        super().__init__()
+        self.bd_lru_only = bd_lru_only
+        self.disable_conv1d = disable_conv1d
+        lo, hi = lambda_init_range()
+        hidden = int(d_model * expansion_factor)
+        self.hidden = hidden
+        self.input = nn.Linear(d_model, 2 * hidden, bias=False)
+        self.conv1d = nn.Conv1d(hidden, hidden, kernel_size, groups=hidden,
+                                padding=kernel_size - 1, bias=True)
+        self.gates = nn.Linear(hidden, 2 * hidden, bias=True)
+        self.Lambda = nn.Parameter(torch.linspace(lo, hi, hidden))
+        self.output = nn.Linear(hidden, d_model, bias=False)
+
+    def forward(self, x):
+        if x.device.type != "cuda":
+            raise RecBLRNativeError(
+                "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
+                "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
+        xz = self.input(x)
+        y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
+                   self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d)
+        return self.output(y)
+
+    @staticmethod
+    def pad_len(seq_len: int) -> int:
+        return pow2_pad_len(seq_len)
+
+
+class FeedForward(nn.Module):
+    """Position-wise FFN with SiLU, residual and LayerNorm (RecBLR.py:210-227)."""
+
+    def __init__(self, d_model, inner_size, dropout=0.2):
+        super().__init__()
+        self.w_1 = nn.Linear(d_model, inner_size)
+        self.w_2 = nn.Linear(inner_size, d_model)
+        self.dropout = nn.Dropout(dropout)
+        self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
+
+    def forward(self, input_tensor):
+        h = self.dropout(F.silu(self.w_1(input_tensor)))
+        h = self.dropout(self.w_2(h))
+        return self.layer_norm(h + input_tensor)
+
+
+class RecurrentLayer(nn.Module):
+    """GRL + dropout + residual LayerNorm, then the FFN (RecBLR.py:124-145)."""
+
+    def __init__(self, d_model, d_conv, expand, dropout, num_layers, bd_lru_only,
+                 disable_conv1d, disable_ffn):
+        super().__init__()
+        self.num_layers = num_layers
+        self.disable_ffn = disable_ffn
+        self.behavior_modeling = GatedRecurrentLayer(
+            d_model=d_model, expansion_factor=expand, kernel_size=d_conv,
+            bd_lru_only=bd_lru_only, disable_conv1d=disable_conv1d)
+        self.dropout = nn.Dropout(dropout)
+        self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
+        self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
+
+    def forward(self, input_tensor):
+        h = self.behavior_modeling(input_tensor)
+        h = self.layer_norm(self.dropout(h) + input_tensor)
+        return h if self.disable_ffn else self.ffn(h)
+
+
+class RecBLR(SequentialRecommender):
+    """RecBole sequential recommender with the BD-LRU encoder (RecBLR.py:18-122)."""
+
+    def __init__(self, config, dataset):
+        super().__init__(config, dataset)
+        self.hidden_size = config["hidden_size"]
+        self.loss_type = config["loss_type"]
+        self.num_layers = config["num_layers"]
+        self.dropout_prob = config["dropout_prob"]
+        self.expand = config["expand"]
+        self.d_conv = config["d_conv"]
+        self.bd_lru_only = config["bd_lru_only"]
+        self.disable_conv1d = config["disable_conv1d"]
+        self.disable_ffn = config["disable_ffn"]
+        if self.bd_lru_only:  # RecBLR.py:33-35
+            self.disable_conv1d = True
+            self.disable_ffn = True
+
+        self.item_embedding = nn.Embedding(self.n_items, self.hidden_size, padding_idx=0)
+        self.layer_norm = nn.LayerNorm(self.hidden_size, eps=1e-12)
+        self.dropout = nn.Dropout(self.dropout_prob)
+        self.recurrent_layers = nn.ModuleList(
+            RecurrentLayer(d_model=self.hidden_size, d_conv=self.d_conv, expand=self.expand,
+                           dropout=self.dropout_prob, num_layers=self.num_layers,
+                           bd_lru_only=self.bd_lru_only, disable_conv1d=self.disable_conv1d,
+                           disable_ffn=self.disable_ffn)
+            for _ in range(self.num_layers))
+        if self.loss_type == "BPR":
+            self.loss_fct = BPRLoss()
+        elif self.loss_type == "CE":
+            self.loss_fct = nn.CrossEntropyLoss()
+        else:
+            raise NotImplementedError("Make sure 'loss_type' in ['BPR', 'CE']!")
+        self.apply(self._init_weights)
+
+    @staticmethod
+    def _init_weights(module):
+        # RecBLR.py:66-73: N(0, 0.02) for Linear/Embedding (every embedding row,
+        # padding_idx included), zero Linear biases, LayerNorm (1, 0); the conv
+        # keeps PyTorch's default init.
+        if isinstance(module, (nn.Linear, nn.Embedding)):
+            module.weight.data.normal_(std=0.02)
+        elif isinstance(module, nn.LayerNorm):
+            module.bias.data.zero_()
+            module.weight.data.fill_(1.0)
+        if isinstance(module, nn.Linear) and module.bias is not None:
+            module.bias.data.zero_()
+
+    def forward(self, item_seq, item_seq_len):
+        h = self.layer_norm(self.dropout(self.item_embedding(item_seq)))
+        for layer in self.recurrent_layers:
+            h = layer(h)
+        return self.gather_indexes(h, item_seq_len - 1)
+
+    def _scores_all(self, seq_output):
+        return seq_output @ self.item_embedding.weight.t()
+
+    def calculate_loss(self, interaction):
+        seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
+        pos_items = interaction[self.POS_ITEM_ID]
+        if self.loss_type == "BPR":
+            neg_items = interaction[self.NEG_ITEM_ID]
+            pos_score = (seq_output * self.item_embedding(pos_items)).sum(-1)
+            neg_score = (seq_output * self.item_embedding(neg_items)).sum(-1)
+            return self.loss_fct(pos_score, neg_score)
+        return self.loss_fct(self._scores_all(seq_output), pos_items)
+
+    def predict(self, interaction):
+        seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
+        return (seq_output * self.item_embedding(interaction[self.ITEM_ID])).sum(dim=1)
+
+    def full_sort_predict(self, interaction):
+        seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
+        return self._scores_all(seq_output)

@@ -1,0 +1,106 @@
+"""The fused BD-LRU block of ``GatedRecurrentLayer.forward``.
+
+Reference span: RecBLR.py:173-206.  The reference materialises a power-of-two
+left padding (:176-179), runs the conv on the padded ``[B, H, T]`` transpose
+(:185), computes the gates with ~12 elementwise torch kernels (:196-199),
+transposes twice into ``parallel_scan`` (:200), truncates (:203-204) and
+merges (:206).
+
+Here the padding is never materialised.  Pad positions carry zeros into the
+conv, so every pad step sees the same per-channel constants
+``xc_p = silu(conv.bias)``, ``(r_p, i_p) = gates(xc_p)``, ``alpha_p``,
+``b'_p = beta_p * xc_p`` (batch independent).  After ``P = T - L`` such steps
+the recurrence holds ``h0 = b'_p (1 - alpha_p^P) / (1 - alpha_p)``, which seeds
+the scan over the L real steps; real steps never see pad inputs through the
+conv because the reference's causal conv already zero-pads the history.  The
+``[H]``-sized prefix stays in torch (it is differentiable there, so the
+parameter gradients through the pad steps come from autograd), and everything
+``[B, L, *]``-sized runs in the HIP kernels:
+
+    K1  rb_conv_silu_fwd    x -> xc                    (R x, W xc)
+    G   torch addmm         xc @ W_g^T + b_g -> rg     (MFMA GEMM)
+    K2  rb_gate_scan_fwd    rg, xc, z -> y             (R r,i,xc,z; W y)
+and the mirror-image backward (K2^T, two GEMMs, K1^T).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import kernels
+
+__all__ = ["pow2_pad_len", "pad_prefix_state", "BDLRUCore", "bd_lru"]
+
+
+def pow2_pad_len(seq_len: int) -> int:
+    """Left padding the reference adds so T is a power of two (RecBLR.py:177)."""
+    return (1 << (seq_len - 1).bit_length()) - seq_len
+
+
+def pad_prefix_state(conv_bias, gate_w, gate_b, lam, pad_len: int):
+    """Recurrent state after the ``pad_len`` constant pad steps (see module doc).
+
+    All operands are ``[H]`` / ``[2H, H]`` parameters; the result is ``[H]`` and
+    differentiable w.r.t. every one of them."""
+    xc_p = F.silu(conv_bias)
+    r_p, i_p = F.linear(xc_p, gate_w, gate_b).chunk(2, dim=-1)
+    s = F.softplus(lam) * torch.sigmoid(r_p)          # alpha_p = exp(-s)
+    alpha = torch.exp(-s)
+    beta = torch.sqrt(1 - alpha * alpha + 1e-8) * torch.sigmoid(i_p)
+    b_p = beta * xc_p
+    s = s.clamp_min(1e-20)
+    # sum_{k<P} alpha^k = (1 - alpha^P) / (1 - alpha), cancellation-free
+    return b_p * (torch.expm1(-pad_len * s) / torch.expm1(-s))
+
+
+class BDLRUCore(torch.autograd.Function):
+    """xz [B, L, 2H] -> y = silu(z) * BD-LRU(conv_silu(x)) [B, L, H]."""
+
+    @staticmethod
+    def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv):
+        B, L, H2 = xz.shape
+        H = H2 // 2
+        x, z = xz[..., :H], xz[..., H:]
+        if use_conv:
+            xc = kernels.conv_silu_fwd(x, conv_w, conv_b)
+        else:
+            xc = x
+        rg = torch.addmm(gate_b, xc.reshape(B * L, H), gate_w.t()).view(B, L, H2)
+        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0)
+        ctx.use_conv = use_conv
+        ctx.has_h0 = h0 is not None
+        ctx.save_for_backward(xz, xc if use_conv else None, rg, carries, conv_w, conv_b,
+                              gate_w, lam)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xz, xc, rg, carries, conv_w, conv_b, gate_w, lam = ctx.saved_tensors
+        B, L, H2 = xz.shape
+        H = H2 // 2
+        x, z = xz[..., :H], xz[..., H:]
+        if xc is None:
+            xc = x
+        dy = dy.contiguous()
+        dxz = torch.empty_like(xz)
+        drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
+            rg, xc, z, lam, carries, dy, dxz[..., H:])
+        drg2 = drg.view(B * L, H2)
+        dgate_w = drg2.t() @ xc.reshape(B * L, H)
+        dxc.view(B * L, H).addmm_(drg2, gate_w)      # + dL/dxc through the gates GEMM
+        dconv_w = dconv_b = None
+        if ctx.use_conv:
+            dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, None, dxz[..., :H])
+            dconv_w = dw.view_as(conv_w)
+        else:
+            dxz[..., :H].copy_(dxc)
+        return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
+                dh0 if ctx.has_h0 else None, None)
+
+
+def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True):
+    """Everything between the in- and out-projections of RecBLR.py:170-207."""
+    L = xz.shape[1]
+    P = pow2_pad_len(L)
+    h0 = pad_prefix_state(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
+    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv)

@@ -1,0 +1,126 @@
+/*
+ * recblr_hip.h — C-ABI of the MI355X (gfx950) RecBLR sequence-encoder kernels.
+ *
+ * This is the drop-in boundary beneath the Python mirror of the reference API
+ * (datamining_recblr_amd.parallel_scan / GatedRecurrentLayer).  Every entry
+ * point takes raw device pointers, int64 sizes/row strides and a hipStream_t
+ * passed as void*.  Nothing here allocates, synchronises or keeps mutable
+ * global state, so every call is capturable into a hipGraph and reentrant per
+ * stream.  All tensors are fp32.
+ *
+ * Return value: 0 on success; RB_EINVAL (-1) for a bad argument (shape,
+ * stride, alignment, null pointer); a positive hipError_t when the launch
+ * failed.  rb_last_error_string() describes the last failure of the calling
+ * thread.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo root):
+ *   rb_scan_fwd        parallel_scan.py:44-60  (forward_scan Triton kernel)
+ *                      + parallel_scan.py:84-95 (Scan.forward)
+ *   rb_scan_bwd        parallel_scan.py:63-80  (backward_scan Triton kernel)
+ *                      + parallel_scan.py:97-114 (Scan.backward glue: shifted
+ *                      gates, reverse scan, d_gates = h_{t-1} * d_t)
+ *   rb_conv_silu_fwd   RecBLR.py:182-193 (causal depthwise conv1d + SiLU on
+ *                      the left-padded sequence; causal_conv1d_fn or the
+ *                      F.conv1d fallback at :185)
+ *   rb_conv_silu_bwd   autograd of RecBLR.py:185 (dx, dW, dbias)
+ *   rb_gate_scan_fwd   RecBLR.py:196-206 minus the GEMMs: alpha/beta gates
+ *                      (:197-199), parallel_scan (:200), truncation (:203-204)
+ *                      and the silu(z)*h merge (:206)
+ *   rb_gate_scan_bwd   autograd of the same span (Scan.backward + gate math)
+ *
+ * Layout (channel-last, "rows" = (batch, time) pairs):
+ *   element (b, t, c) of a [B, L, *] activation lives at
+ *   ptr[(b * L + t) * row_stride + c]; row_stride >= H.
+ */
+#ifndef RECBLR_HIP_H
+#define RECBLR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RB_EINVAL (-1)
+
+/* Time-tile length of the fused gate/scan kernels: rb_gate_scan_fwd writes one
+ * carry (the recurrent state entering the tile) per (b, tile, c) and
+ * rb_gate_scan_bwd reads them back.  carries has B * ceil(L / RB_TILE) * H
+ * floats. */
+#define RB_TILE 64
+
+/* ABI version; bumped on any signature change. */
+int rb_version(void);
+
+/* Human-readable description of the last error on the calling thread. */
+const char* rb_last_error_string(void);
+
+/* Number of device kernels compiled into the library for gfx950 (sanity). */
+int rb_num_kernels(void);
+
+/* parallel_scan forward on the reference layout [B, C, T], T contiguous:
+ *   states[b,c,t] = gates[b,c,t] * states[b,c,t-1] + tokens[b,c,t],
+ *   states[b,c,-1] = 0.
+ * Any T >= 1 (the reference needs a power of two; this does not). */
+int rb_scan_fwd(const float* gates, const float* tokens, float* states,
+                int64_t B, int64_t C, int64_t T, void* stream);
+
+/* parallel_scan backward (parallel_scan.py:97-114):
+ *   d[t]       = grad[t] + gates[t+1] * d[t+1],  d[T] = 0
+ *   d_gates[t] = states[t-1] * d[t]  (states[-1] = 0)
+ *   d_tokens   = d                                              */
+int rb_scan_bwd(const float* gates, const float* states, const float* grad,
+                float* d_gates, float* d_tokens,
+                int64_t B, int64_t C, int64_t T, void* stream);
+
+/* Causal depthwise conv (kernel K, zero history) + bias + SiLU:
+ *   xc[b,t,c] = silu(bias[c] + sum_k w[c,k] * x[b, t-K+1+k, c])
+ * x: [B, L, H] view with row stride x_rs (e.g. the first half of the
+ * in-projection output [B, L, 2H]); w: [H, K] contiguous; xc: [B, L, H]
+ * with row stride xc_rs.  1 <= K <= 8. */
+int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w,
+                     const float* bias, float* xc, int64_t xc_rs,
+                     int64_t B, int64_t L, int64_t H, int64_t K, void* stream);
+
+/* Backward of rb_conv_silu_fwd.  dxc = g1 + g2 (g2 may be NULL), both
+ * [B, L, H] contiguous.  Writes dx (row stride dx_rs) and per-batch partial
+ * sums dw_part[b, k, c] (B*K*H floats) and db_part[b, c] (B*H floats); the
+ * caller sums the partials over b (deterministic, no atomics). */
+int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w,
+                     const float* bias, const float* g1, const float* g2,
+                     float* dx, int64_t dx_rs, float* dw_part, float* db_part,
+                     int64_t B, int64_t L, int64_t H, int64_t K, void* stream);
+
+/* Fused BD-LRU forward (everything between the gates GEMM and the output
+ * GEMM):
+ *   alpha = exp(-softplus(lam[c]) * sigmoid(r)),
+ *   beta  = sqrt(1 - alpha^2 + 1e-8) * sigmoid(i),
+ *   h_t   = alpha_t * h_{t-1} + beta_t * xc_t,   h_{-1} = h0[c] (0 if NULL),
+ *   y     = silu(z) * h.
+ * rg: [B, L, 2H] view (r = columns [0,H), i = columns [H,2H)), row stride
+ * rg_rs; xc, z, y: [B, L, H] views with their own row strides; lam, h0: [H].
+ * carries: B * ceil(L/RB_TILE) * H floats (written, consumed by the bwd). */
+int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
+                     int64_t xc_rs, const float* z, int64_t z_rs,
+                     const float* lam, const float* h0, float* y, int64_t y_rs,
+                     float* carries, int64_t B, int64_t L, int64_t H,
+                     void* stream);
+
+/* Backward of rb_gate_scan_fwd given dy = dL/dy ([B, L, H] contiguous).
+ * Writes drg ([B, L, 2H] view: dr | di, row stride drg_rs), dxc ([B, L, H]
+ * contiguous, the gate path's share of dL/dxc), dz (row stride dz_rs),
+ * part[3, B, H] = per-batch sums over t of {dlam, dr, di} and
+ * dh0_part[B, H] = dL/dh_{-1} per batch row (caller sums over b). */
+int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
+                     int64_t xc_rs, const float* z, int64_t z_rs,
+                     const float* lam, const float* carries, const float* dy,
+                     float* drg, int64_t drg_rs, float* dxc, float* dz,
+                     int64_t dz_rs, float* part, float* dh0_part,
+                     int64_t B, int64_t L, int64_t H, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RECBLR_HIP_H */

@@ -1,0 +1,1 @@
+"""CPU oracle (test infrastructure only; never imported by the product)."""

@@ -1,0 +1,77 @@
+"""world_size-2 gloo test of the batch-DP path used by bench.py --gpus N:
+env-driven init, the DDP LossModule wrapper, per-rank sharding and the
+max-over-ranks timer.  The encoder itself needs a GPU, so the CPU stand-in
+model here exercises the same wrapper and all-reduce plumbing."""
+import os
+import socket
+
+import torch
+import torch.multiprocessing as mp
+from torch import nn
+
+
+class TinyRec(nn.Module):
+    """calculate_loss-shaped model: embedding -> mean -> CE over all items."""
+
+    def __init__(self, n_items=30, d=8):
+        super().__init__()
+        self.item_embedding = nn.Embedding(n_items, d)
+        self.proj = nn.Linear(d, d)
+
+    def calculate_loss(self, inter):
+        h = self.proj(self.item_embedding(inter["item_id_list"]).mean(1))
+        return nn.functional.cross_entropy(h @ self.item_embedding.weight.t(), inter["item_id"])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, queue):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from datamining_recblr_amd.distributed import (init_from_env, max_over_ranks, shard_range,
+                                                   synthetic_interaction, wrap_ddp)
+
+    env = init_from_env(backend="gloo")
+    torch.manual_seed(0)
+    model = TinyRec()
+    step = wrap_ddp(model, env)
+    full = synthetic_interaction(12, 6, 30, "cpu", seed=3)
+    lo, hi = shard_range(12, env.rank, env.world_size)
+    shard = {k: v[lo:hi] for k, v in full.items()}
+    loss = step(shard)
+    loss.backward()
+    t = max_over_ranks(float(rank + 1), env)
+    grads = {n: p.grad.detach().numpy().copy() for n, p in model.named_parameters()}
+    queue.put((rank, t, grads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_gloo_world2_matches_full_batch():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from datamining_recblr_amd.distributed import synthetic_interaction
+
+    torch.manual_seed(0)
+    ref = TinyRec()
+    ref.calculate_loss(synthetic_interaction(12, 6, 30, "cpu", seed=3)).backward()
+    for rank, tmax, grads in results:
+        assert tmax == float(world)
+        for n, p in ref.named_parameters():
+            torch.testing.assert_close(torch.from_numpy(grads[n]), p.grad, atol=1e-6, rtol=1e-5)

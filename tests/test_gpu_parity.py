@@ -1,0 +1,257 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference's golden
+vectors and the CPU oracle.  Tolerance: 1e-4 absolute on fp32 (north star),
+with a relative term for gradients summed over B*L positions."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import load_golden
+from oracle import recblr_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+ATOL = 1e-4
+RTOL = 1e-4
+
+
+def close(a, b, atol=ATOL, rtol=RTOL, what=""):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol)
+    assert not bad.any(), f"{what}: max err {err.max().item():.3e} (max |ref| {b.abs().max().item():.3e})"
+
+
+# ---------------------------------------------------------------- scan shim
+@pytest.mark.parametrize("idx", range(6))
+def test_scan_vs_reference_golden(cuda, idx):
+    from datamining_recblr_amd import parallel_scan
+
+    case = load_golden("scan_golden.pt")[idx]
+    g = case["gates"].to(cuda).requires_grad_()
+    x = case["tokens"].to(cuda).requires_grad_()
+    s = parallel_scan(g, x)
+    s.backward(case["grad"].to(cuda))
+    close(s, case["states"], what="states")
+    close(g.grad, case["d_gates"], what="d_gates")
+    close(x.grad, case["d_tokens"], what="d_tokens")
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (2, 3, 5), (3, 7, 100), (2, 5, 257), (1, 3, 1000),
+                                   (2, 2, 4099), (64, 64, 256)])
+def test_scan_any_length_vs_oracle(cuda, shape):
+    """T need not be a power of two here (the reference requires it)."""
+    from datamining_recblr_amd import parallel_scan
+
+    gen = torch.Generator().manual_seed(sum(shape))
+    gates = torch.rand(shape, generator=gen) * 0.2 + 0.8
+    tokens = torch.randn(shape, generator=gen)
+    grad = torch.randn(shape, generator=gen)
+    gr = gates.clone().requires_grad_()
+    tr = tokens.clone().requires_grad_()
+    ref = orc.oracle_parallel_scan(gr, tr)
+    ref.backward(grad)
+    gd = gates.to(cuda).requires_grad_()
+    td = tokens.to(cuda).requires_grad_()
+    out = parallel_scan(gd, td)
+    out.backward(grad.to(cuda))
+    close(out, ref, what="states")
+    close(gd.grad, gr.grad, what="d_gates")
+    close(td.grad, tr.grad, what="d_tokens")
+
+
+def test_scan_misaligned_rows(cuda):
+    """Odd T and an offset storage start force the scalar (non-float4) path."""
+    from datamining_recblr_amd import kernels
+
+    base = torch.randn(1 + 4 * 6 * 37, device=cuda)
+    g = (base[1:].view(4, 6, 37).sigmoid()).contiguous()
+    x_store = torch.randn(1 + 4 * 6 * 37, device=cuda)
+    x = x_store[1:].view(4, 6, 37)
+    assert x.data_ptr() % 16 != 0
+    out = kernels.scan_fwd(g, x)
+    close(out, orc.serial_scan(g.cpu(), x.cpu()), what="states")
+
+
+def test_scan_precondition_errors(cuda):
+    from datamining_recblr_amd import parallel_scan
+
+    g = torch.rand(2, 3, 8, device=cuda)
+    with pytest.raises(AssertionError):
+        parallel_scan(g, torch.rand(2, 3, 4, device=cuda))
+    with pytest.raises(AssertionError):
+        parallel_scan(g.transpose(1, 2).contiguous().transpose(1, 2), torch.rand(2, 3, 8, device=cuda))
+
+
+# ---------------------------------------------------------------- conv + silu
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("B,L,H", [(2, 37, 32), (3, 200, 256), (1, 5, 80)])
+def test_conv_silu_vs_torch(cuda, K, B, L, H):
+    from datamining_recblr_amd import kernels
+
+    gen = torch.Generator().manual_seed(K * 1000 + L)
+    xz = torch.randn(B, L, 2 * H, generator=gen)
+    w = torch.randn(H, 1, K, generator=gen) * 0.5
+    b = torch.randn(H, generator=gen) * 0.5
+    g1 = torch.randn(B, L, H, generator=gen)
+    g2 = torch.randn(B, L, H, generator=gen)
+    # CPU reference: the reference's conv call (RecBLR.py:185) on the unpadded input
+    xr = xz[..., :H].clone().requires_grad_()
+    wr = w.clone().requires_grad_()
+    br = b.clone().requires_grad_()
+    ref = F.silu(F.conv1d(xr.transpose(1, 2), wr, br, padding=K - 1, groups=H)[..., :L].transpose(1, 2))
+    (ref * (g1 + g2)).sum().backward()
+
+    xzd = xz.to(cuda)
+    xc = kernels.conv_silu_fwd(xzd[..., :H], w.to(cuda), b.to(cuda))
+    close(xc, ref, what="xc")
+    dxz = torch.zeros_like(xzd)
+    dw, db = kernels.conv_silu_bwd(xzd[..., :H], w.to(cuda), b.to(cuda), g1.to(cuda), g2.to(cuda),
+                                   dxz[..., :H])
+    close(dxz[..., :H], xr.grad, what="dx")
+    assert dxz[..., H:].abs().max().item() == 0.0, "dx wrote outside its view"
+    close(dw.view_as(w), wr.grad, what="dw", rtol=3e-4)
+    close(db, br.grad, what="db", rtol=3e-4)
+
+
+# ---------------------------------------------------------------- GRL vs reference golden
+@pytest.mark.parametrize("idx", range(9))
+def test_grl_vs_reference_golden(cuda, idx):
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    case = load_golden("grl_golden.pt")[idx]
+    layer = GatedRecurrentLayer(d_model=case["d"], kernel_size=case["kernel_size"],
+                                disable_conv1d=case["disable_conv1d"])
+    layer.load_state_dict(case["params"])
+    layer = layer.to(cuda)
+    x = case["x"].to(cuda).requires_grad_()
+    y = layer(x)
+    (y * case["gy"].to(cuda)).sum().backward()
+    close(y, case["y"], what="y")
+    close(x.grad, case["dx"], what="dx")
+    for n, p in layer.named_parameters():
+        if case["disable_conv1d"] and n.startswith("conv1d"):
+            assert p.grad is None or p.grad.abs().max() == 0
+            continue
+        close(p.grad, case["grads"][n], what=f"d{n}")
+
+
+# ---------------------------------------------------------------- model vs reference golden
+def _model_from_case(case, cuda):
+    from datamining_recblr_amd.model import RecBLR
+    from datamining_recblr_amd.recbole_compat import SyntheticDataset
+
+    model = RecBLR(case["cfg"], SyntheticDataset(case["n_items"]))
+    model.load_state_dict(case["init_state"])
+    return model.to(cuda).eval()
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_model_vs_reference_golden(cuda, idx):
+    case = load_golden("model_golden.pt")[idx]
+    model = _model_from_case(case, cuda)
+    inter = {"item_id_list": case["item_seq"].to(cuda), "item_length": case["item_seq_len"].to(cuda),
+             "item_id": case["pos_items"].to(cuda), "neg_item_id": case["neg_items"].to(cuda)}
+    loss = model.calculate_loss(inter)
+    loss.backward()
+    close(loss, case["loss"], what="loss")
+    for n, p in model.named_parameters():
+        if n in case["grads"]:
+            close(p.grad, case["grads"][n], what=f"d{n}")
+        else:
+            assert p.grad is None or p.grad.abs().max() == 0, n
+    with torch.no_grad():
+        close(model.forward(inter["item_id_list"], inter["item_length"]), case["seq_output"],
+              what="seq_output")
+        close(model.full_sort_predict(inter), case["full_sort"], what="full_sort_predict")
+        close(model.predict(inter), case["predict"], what="predict")
+
+
+# ---------------------------------------------------------------- full-size properties
+def test_full_size_grl_rows_match_oracle(cuda):
+    """C2 shape (B=2048, L=200, d=128): batch rows are independent, so the full
+    GPU result restricted to a random subset of rows must equal the oracle run
+    on just those rows (a size-independent check at the benchmark size)."""
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    torch.manual_seed(7)
+    B, L, d = 2048, 200, 128
+    layer = GatedRecurrentLayer(d_model=d).to(cuda)
+    x = torch.randn(B, L, d, device=cuda, requires_grad=True)
+    gy = torch.randn(B, L, d, device=cuda)
+    y = layer(x)
+    (y * gy).sum().backward()
+    rows = torch.tensor([0, 1, 777, 1500, 2047])
+    params = {k: v.detach().cpu().requires_grad_() for k, v in layer.state_dict().items()}
+    xs = x.detach()[rows.to(cuda)].cpu().requires_grad_()
+    ys = orc.grl_forward(params, "", xs)
+    (ys * gy[rows.to(cuda)].cpu()).sum().backward()
+    close(y[rows.to(cuda)], ys, what="y rows")
+    close(x.grad[rows.to(cuda)], xs.grad, what="dx rows")
+
+
+def test_full_size_scan_vs_serial(cuda):
+    """[2048, 256, 256] scan (the reference's C2 scan launch) vs a serial fp32 scan."""
+    from datamining_recblr_amd import kernels
+
+    torch.manual_seed(3)
+    g = torch.rand(2048, 256, 256, device=cuda) * 0.1 + 0.9
+    x = torch.randn(2048, 256, 256, device=cuda)
+    out = kernels.scan_fwd(g, x)
+    ref = orc.serial_scan(g, x)
+    close(out, ref, what="states")
+
+
+def test_determinism(cuda):
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    torch.manual_seed(5)
+    layer = GatedRecurrentLayer(d_model=64).to(cuda)
+    x = torch.randn(64, 200, 64, device=cuda)
+
+    def run():
+        layer.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_()
+        y = layer(xi)
+        y.square().sum().backward()
+        return [y.detach().clone(), xi.grad.clone()] + [p.grad.clone() for p in layer.parameters()]
+
+    a, b = run(), run()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("B,L,d", [(1, 1, 16), (3, 2, 16), (2, 64, 40), (5, 129, 24), (2, 1000, 32)])
+def test_grl_edge_shapes_vs_oracle(cuda, B, L, d):
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    torch.manual_seed(B * 100 + L)
+    layer = GatedRecurrentLayer(d_model=d)
+    with torch.no_grad():
+        layer.conv1d.bias.mul_(3.0)   # exaggerate the pad-prefix state
+    params = {k: v.detach().clone().requires_grad_() for k, v in layer.state_dict().items()}
+    layer = layer.to(cuda)
+    x = torch.randn(B, L, d)
+    gy = torch.randn(B, L, d)
+    xr = x.clone().requires_grad_()
+    yr = orc.grl_forward(params, "", xr)
+    (yr * gy).sum().backward()
+    xd = x.to(cuda).requires_grad_()
+    y = layer(xd)
+    (y * gy.to(cuda)).sum().backward()
+    close(y, yr, what="y")
+    close(xd.grad, xr.grad, what="dx")
+    for n, p in layer.named_parameters():
+        close(p.grad, params[n].grad, what=f"d{n}", rtol=3e-4)
+
+
+def test_native_errors(cuda):
+    from datamining_recblr_amd import RecBLRNativeError, kernels
+
+    x = torch.randn(2, 8, 16, device=cuda)
+    with pytest.raises(RecBLRNativeError):
+        kernels.conv_silu_fwd(x, torch.randn(16, 1, 9, device=cuda), torch.randn(16, device=cuda))
+    with pytest.raises(RecBLRNativeError):
+        kernels.scan_fwd(torch.rand(2, 2, 2), torch.rand(2, 2, 2))   # CPU tensors

@@ -1,0 +1,144 @@
+"""Host-side logic that needs no GPU: padding arithmetic, the pad-prefix
+closed form, module/parameter layout and init parity with the reference,
+error behaviour."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import load_golden
+from datamining_recblr_amd import RecBLRNativeError, kernels
+from datamining_recblr_amd.distributed import shard_range, synthetic_interaction
+from datamining_recblr_amd.model import GatedRecurrentLayer, RecBLR, lambda_init_range
+from datamining_recblr_amd.recbole_compat import SyntheticDataset
+from datamining_recblr_amd.recurrence import pad_prefix_state, pow2_pad_len
+from oracle import recblr_oracle as orc
+
+
+def test_pow2_pad_len_matches_reference_formula():
+    for L in range(1, 5000):
+        ref = 2 ** ((L - 1).bit_length()) - L      # RecBLR.py:177
+        assert pow2_pad_len(L) == ref
+        T = L + ref
+        assert T & (T - 1) == 0 and T >= L
+
+
+@pytest.mark.parametrize("P", [1, 14, 56, 1000])
+def test_pad_prefix_closed_form_matches_serial_pad_steps(P):
+    """h after P pad steps == running the reference's padded recurrence on the
+    constant pad inputs (value and parameter gradients)."""
+    torch.manual_seed(P)
+    H = 32
+    conv_b = (torch.randn(H) * 2).requires_grad_()
+    gw = (torch.randn(2 * H, H) * 0.2).requires_grad_()
+    gb = torch.randn(2 * H).requires_grad_()
+    lo, hi = lambda_init_range()
+    lam = torch.linspace(lo, hi, H).requires_grad_()
+    h0 = pad_prefix_state(conv_b, gw, gb, lam, P)
+    (h0 * torch.arange(H)).sum().backward()
+    g1 = [t.grad.clone() for t in (conv_b, gw, gb, lam)]
+    for t in (conv_b, gw, gb, lam):
+        t.grad = None
+    # pad-step constants in fp32 exactly as the reference computes them
+    # (RecBLR.py:185,196-199 on an all-zero padded input), then the P serial
+    # recurrence steps in fp64 so only the closed form itself is under test
+    xc = F.silu(conv_b)
+    r, i = (xc @ gw.t() + gb).chunk(2)
+    a = torch.exp(-F.softplus(lam) * torch.sigmoid(r))
+    bp = torch.sqrt(1 - a.pow(2) + 1e-8) * torch.sigmoid(i) * xc
+    a, bp = a.double(), bp.double()
+    h = torch.zeros(H, dtype=torch.float64)
+    for _ in range(P):
+        h = a * h + bp
+    (h * torch.arange(H)).sum().backward()
+    # fp32 rounding of alpha compounds over P steps: ~P * 6e-8 relative
+    torch.testing.assert_close(h0.detach().double(), h.detach(), atol=1e-5, rtol=5e-5)
+    for ga, t in zip(g1, (conv_b, gw, gb, lam)):
+        torch.testing.assert_close(ga, t.grad, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("idx", range(6))
+def test_init_and_state_dict_parity_with_reference(idx):
+    """Same seed -> bit-identical initial weights and identical state_dict keys."""
+    case = load_golden("model_golden.pt")[idx]
+    torch.manual_seed(2020)
+    model = RecBLR(case["cfg"], SyntheticDataset(case["n_items"]))
+    sd = model.state_dict()
+    assert list(sd.keys()) == list(case["init_state"].keys())
+    for k, v in case["init_state"].items():
+        assert torch.equal(sd[k], v), k
+
+
+def test_lambda_init_range():
+    lo, hi = lambda_init_range()
+    sp = F.softplus(torch.tensor([lo, hi]))
+    torch.testing.assert_close(torch.exp(-sp), torch.tensor([0.9, 0.999]))
+
+
+def test_cpu_forward_fails_loudly():
+    layer = GatedRecurrentLayer(d_model=16)
+    with pytest.raises(RecBLRNativeError):
+        layer(torch.randn(2, 5, 16))
+    with pytest.raises(RecBLRNativeError):
+        kernels.scan_fwd(torch.rand(1, 2, 3), torch.rand(1, 2, 3))
+    with pytest.raises(RecBLRNativeError):
+        kernels.gate_scan_fwd(torch.rand(1, 2, 8), torch.rand(1, 2, 4), torch.rand(1, 2, 4),
+                              torch.rand(4))
+
+
+def test_bad_loss_type():
+    cfg = dict(hidden_size=16, loss_type="XX", num_layers=1, dropout_prob=0.1, expand=2, d_conv=4,
+               bd_lru_only=False, disable_conv1d=False, disable_ffn=False, MAX_ITEM_LIST_LENGTH=10)
+    with pytest.raises(NotImplementedError):
+        RecBLR(cfg, SyntheticDataset(10))
+
+
+def test_bd_lru_only_implies_flags():
+    cfg = dict(hidden_size=16, loss_type="CE", num_layers=2, dropout_prob=0.1, expand=2, d_conv=4,
+               bd_lru_only=True, disable_conv1d=False, disable_ffn=False, MAX_ITEM_LIST_LENGTH=10)
+    m = RecBLR(cfg, SyntheticDataset(10))
+    assert m.disable_conv1d and m.disable_ffn
+    assert all(layer.disable_ffn for layer in m.recurrent_layers)
+    assert all(layer.behavior_modeling.disable_conv1d for layer in m.recurrent_layers)
+
+
+def test_recbole_field_names():
+    cfg = dict(hidden_size=16, loss_type="CE", num_layers=1, dropout_prob=0.1, expand=2, d_conv=4,
+               bd_lru_only=False, disable_conv1d=False, disable_ffn=False, MAX_ITEM_LIST_LENGTH=10)
+    m = RecBLR(cfg, SyntheticDataset(10))
+    assert (m.ITEM_SEQ, m.ITEM_SEQ_LEN, m.POS_ITEM_ID, m.NEG_ITEM_ID, m.ITEM_ID) == \
+        ("item_id_list", "item_length", "item_id", "neg_item_id", "item_id")
+    out = torch.arange(2 * 5 * 3, dtype=torch.float32).view(2, 5, 3)
+    assert torch.equal(m.gather_indexes(out, torch.tensor([0, 4])), out[[0, 1], [0, 4]])
+
+
+def test_shard_range_and_synthetic_batch():
+    for n in (1, 7, 2048, 16384):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+    inter = synthetic_interaction(16, 20, 50, "cpu", seed=0, with_neg=True)
+    seq, lens = inter["item_id_list"], inter["item_length"]
+    assert seq.shape == (16, 20) and lens.min() >= 1 and lens.max() <= 20
+    for b in range(16):
+        assert (seq[b, :lens[b]] > 0).all() and (seq[b, lens[b]:] == 0).all()
+
+
+def test_oracle_scan_reverse_matches_autograd_of_loop():
+    """SerialScan.backward (the reference's glue, parallel_scan.py:106-113) ==
+    autograd through the plain serial loop."""
+    torch.manual_seed(0)
+    g = torch.rand(2, 3, 17).requires_grad_()
+    x = torch.randn(2, 3, 17).requires_grad_()
+    gy = torch.randn(2, 3, 17)
+    orc.oracle_parallel_scan(g, x).backward(gy)
+    g2 = g.detach().clone().requires_grad_()
+    x2 = x.detach().clone().requires_grad_()
+    h = torch.zeros(2, 3)
+    outs = []
+    for t in range(17):
+        h = h * g2[..., t] + x2[..., t]
+        outs.append(h)
+    torch.stack(outs, -1).backward(gy)
+    torch.testing.assert_close(g.grad, g2.grad)
+    torch.testing.assert_close(x.grad, x2.grad)
