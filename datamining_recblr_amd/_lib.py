@@ -16,8 +16,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "libdmrecblr.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
-RB_TILE = 64
-ABI_VERSION = 1
+RB_TILE = 16
+ABI_VERSION = 2
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers

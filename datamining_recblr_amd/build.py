@@ -6,6 +6,7 @@ without a GPU, so it runs in the CPU container as well as on the GPU box.
 """
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -13,7 +14,9 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
-SOURCES = [os.path.join(_HERE, "csrc", "recblr_kernels.hip")]
+SOURCES = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")))
+HEADERS = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.h"))) + [
+    os.path.join(ROOT, "include", "recblr_hip.h")]
 OUT = os.path.join(_HERE, "lib", "libdmrecblr.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
@@ -35,16 +38,18 @@ def _stale() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = SOURCES + [os.path.join(ROOT, "include", "recblr_hip.h")]
+    deps = SOURCES + HEADERS
     return any(os.path.getmtime(s) > t for s in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
     if not force and not _stale():
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     tmp = OUT + ".tmp"
     cmd = [hipcc(), *FLAGS, "-I", os.path.join(ROOT, "include"), "-o", tmp, *SOURCES]
+    if jobs > 1:
+        cmd.insert(1, f"-parallel-jobs={jobs}")
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

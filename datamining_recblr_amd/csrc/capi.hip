@@ -1,0 +1,123 @@
+// capi.hip — the extern "C" boundary declared in include/recblr_hip.h:
+// argument validation, error reporting, dispatch to the kernel launchers.
+#include "common.h"
+
+namespace rb {
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+int fail(const char* msg) {
+  g_last_error = msg;
+  return RB_EINVAL;
+}
+
+int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+    return static_cast<int>(e);
+  }
+  return 0;
+}
+
+namespace {
+
+// Per-lane offsets inside one batch row are 32-bit: L * row_stride must fit.
+int check_dims(const char* fn, int64_t B, int64_t L, int64_t H, int64_t max_rs) {
+  (void)fn;
+  if (B <= 0 || L <= 0 || H <= 0) return fail("B, L and H must be positive");
+  if (L * max_rs + max_rs >= (int64_t(1) << 31)) return fail("L * row_stride exceeds 2^31");
+  if (B * ((H + 15) / 16) / 4 + 1 > 0x7fffffffLL) return fail("grid too large");
+  return 0;
+}
+
+int64_t max4(int64_t a, int64_t b, int64_t c = 0, int64_t d = 0) {
+  return std::max(std::max(a, b), std::max(c, d));
+}
+
+}  // namespace
+}  // namespace rb
+
+using namespace rb;
+
+extern "C" {
+
+int rb_version(void) { return 2; }
+
+const char* rb_last_error_string(void) { return g_last_error.c_str(); }
+
+int rb_num_kernels(void) { return 6; }
+
+int rb_scan_fwd(const float* gates, const float* tokens, float* states, int64_t B, int64_t C,
+                int64_t T, void* stream) {
+  if (!gates || !tokens || !states) return fail("rb_scan_fwd: null pointer");
+  if (B <= 0 || C <= 0 || T <= 0) return fail("rb_scan_fwd: B, C, T must be positive");
+  const int64_t rows = B * C;
+  if ((rows + 3) / 4 > 0x7fffffffLL) return fail("rb_scan_fwd: too many rows");
+  return launch_scan_fwd(gates, tokens, states, rows, T, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,
+                float* d_tokens, int64_t B, int64_t C, int64_t T, void* stream) {
+  if (!gates || !states || !grad || !d_gates || !d_tokens)
+    return fail("rb_scan_bwd: null pointer");
+  if (B <= 0 || C <= 0 || T <= 0) return fail("rb_scan_bwd: B, C, T must be positive");
+  const int64_t rows = B * C;
+  if ((rows + 3) / 4 > 0x7fffffffLL) return fail("rb_scan_bwd: too many rows");
+  return launch_scan_bwd(gates, states, grad, d_gates, d_tokens, rows, T,
+                         reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
+                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, void* stream) {
+  if (!x || !w || !bias || !xc) return fail("rb_conv_silu_fwd: null pointer");
+  if (K < 1 || K > 8) return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
+  if (x_rs < H || xc_rs < H) return fail("rb_conv_silu_fwd: row stride < H");
+  if (int r = check_dims("rb_conv_silu_fwd", B, L, H, max4(x_rs, xc_rs))) return r;
+  return launch_conv_fwd(x, x_rs, w, bias, xc, xc_rs, B, L, H, K,
+                         reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
+                     const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
+                     float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, void* stream) {
+  if (!x || !w || !bias || !g1 || !dx || !dw_part || !db_part)
+    return fail("rb_conv_silu_bwd: null pointer");
+  if (K < 1 || K > 8) return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
+  if (x_rs < H || dx_rs < H) return fail("rb_conv_silu_bwd: row stride < H");
+  if (int r = check_dims("rb_conv_silu_bwd", B, L, H, max4(x_rs, dx_rs, H))) return r;
+  return launch_conv_bwd(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K,
+                         reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                     const float* z, int64_t z_rs, const float* lam, const float* h0, float* y,
+                     int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
+                     void* stream) {
+  if (!rg || !xc || !z || !lam || !y) return fail("rb_gate_scan_fwd: null pointer");
+  if (rg_rs < 2 * H || xc_rs < H || z_rs < H || y_rs < H)
+    return fail("rb_gate_scan_fwd: row stride too small");
+  if (int r = check_dims("rb_gate_scan_fwd", B, L, H, max4(rg_rs, xc_rs, z_rs, y_rs))) return r;
+  return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, y, y_rs, carries, B, L, H,
+                         reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                     const float* z, int64_t z_rs, const float* lam, const float* carries,
+                     const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
+                     int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
+                     int64_t H, void* stream) {
+  if (!rg || !xc || !z || !lam || !carries || !dy || !drg || !dxc || !dz || !part || !dh0_part)
+    return fail("rb_gate_scan_bwd: null pointer");
+  if (rg_rs < 2 * H || xc_rs < H || z_rs < H || drg_rs < 2 * H || dz_rs < H)
+    return fail("rb_gate_scan_bwd: row stride too small");
+  if (int r = check_dims("rb_gate_scan_bwd", B, L, H,
+                         max4(max4(rg_rs, xc_rs, z_rs, drg_rs), dz_rs, H)))
+    return r;
+  return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
+                         dz_rs, part, dh0_part, B, L, H, reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

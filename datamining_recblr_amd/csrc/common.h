@@ -1,0 +1,106 @@
+// common.h — shared device helpers for the RecBLR gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/recblr_hip.h"
+
+namespace rb {
+
+constexpr int kWave = 64;
+
+// ---- error reporting (host) -------------------------------------------------
+int fail(const char* msg);
+int launch_status(const char* what);
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// ---- scalar math, following torch's definitions ------------------------------
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+// torch.nn.functional.softplus(beta=1, threshold=20)
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float dsoftplus_f(float x) { return x > 20.0f ? 1.0f : sigm(x); }
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+// d/dx silu(x) = s (1 + x (1 - s)), s = sigmoid(x)
+__device__ __forceinline__ float dsilu_f(float x) {
+  const float s = sigm(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// ---- hardware transcendentals (v_exp_f32 / v_rcp_f32 / v_sqrt_f32, ~1 ulp) ----
+// The libm forms above expand to ~10-15 instructions each (range reduction,
+// IEEE division); in the [B, L, H] kernels they made the VALU co-bound with
+// HBM.  The native forms keep every quantity within a few ulp, which stays
+// far inside the 1e-4 parity budget: the one cancellation-prone value,
+// 1 - alpha^2 with alpha -> 0.999, depends on alpha's absolute error (~ulp(1))
+// exactly as it does with expf.
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ float fsigm(float x) { return frcp(1.0f + fexp(-x)); }
+__device__ __forceinline__ float fsilu(float x) { return x * fsigm(x); }
+__device__ __forceinline__ float fdsilu(float x) {
+  const float s = fsigm(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// ---- VEC-wide loads/stores (VEC = 4 -> one 16-B access per lane) -------------
+template <int V>
+__device__ __forceinline__ void ldv(float (&o)[V], const float* p) {
+  if constexpr (V == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+  } else if constexpr (V == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    o[0] = t.x; o[1] = t.y;
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) o[v] = p[v];
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void stv(float* p, const float (&o)[V]) {
+  if constexpr (V == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
+  } else if constexpr (V == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(o[0], o[1]);
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) p[v] = o[v];
+  }
+}
+
+// ---- channel-last wave layout ---------------------------------------------------
+// The [B, L, H] kernels give each wave one batch row b and a span of G*VEC
+// channels.  Lane = q * G + g: g picks VEC consecutive channels (so the G lanes
+// of one chunk read one contiguous G*VEC*4-byte segment of a row), q picks one
+// of Q consecutive time chunks of TC steps inside a tile of Q*TC steps.
+// Summaries of the Q chunks are combined across lanes with shuffles at stride
+// G; no LDS and no barriers.
+
+// host launch helpers (defined in the .hip files)
+int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
+                    int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st);
+int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
+                    const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
+                    float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st);
+int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                    const float* z, int64_t z_rs, const float* lam, const float* h0, float* y,
+                    int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
+                    hipStream_t st);
+int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                    const float* z, int64_t z_rs, const float* lam, const float* carries,
+                    const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
+                    int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
+                    int64_t H, hipStream_t st);
+int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,
+                    int64_t T, hipStream_t st);
+int launch_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,
+                    float* d_tokens, int64_t rows, int64_t T, hipStream_t st);
+
+}  // namespace rb

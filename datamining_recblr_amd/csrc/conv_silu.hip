@@ -1,0 +1,275 @@
+// conv_silu.hip — causal depthwise conv1d (kernel K, zero history) + bias +
+// SiLU on channel-last [B, L, H] (reference RecBLR.py:182-193), fwd and bwd.
+//
+// Same wave layout as the gate scan (common.h): lane = (time chunk q, channel
+// group g), VEC = 4 channels per lane so every access is a 16-B load/store
+// and one wave-instruction touches Q contiguous 256-B row segments.
+#include "common.h"
+
+namespace rb {
+namespace {
+
+template <int K, int VEC, int Q, int TC>
+__global__ void __launch_bounds__(256)
+k_conv_silu_fwd(const float* __restrict__ x, int x_rs, const float* __restrict__ w,
+                const float* __restrict__ bias, float* __restrict__ xc, int xc_rs, int64_t B,
+                int L, int H, int ncw, int ntile) {
+  constexpr int G = kWave / Q;
+  constexpr int NX = TC + K - 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int q = lane / G;
+  const int g = lane - q * G;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int tile = (int)(wid % ntile);
+  const int64_t tmp = wid / ntile;
+  const int cw = (int)(tmp % ncw);
+  const int64_t b = tmp / ncw;
+  if (b >= B) return;
+  const int c0 = cw * (G * VEC) + g * VEC;
+  const bool cv = c0 < H;
+  const int cc = cv ? c0 : 0;
+  const float* xb = x + b * L * x_rs + cc;
+  float* ob = xc + b * L * xc_rs + cc;
+  float wk[K][VEC], bi[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k][v] = w[(cc + v) * K + k];
+  }
+  ldv(bi, bias + cc);
+  const int t0 = tile * (Q * TC) + q * TC;
+  float xs[NX][VEC];   // x[t0-K+1 .. t0+TC-1]
+#pragma unroll
+  for (int m = 0; m < NX; ++m) {
+    const int t = t0 - (K - 1) + m;
+    const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
+    ldv(xs[m], xb + tc * x_rs);
+    if (t < 0) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) xs[m][v] = 0.0f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TC; ++j) {
+    float out[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      float acc = bi[v];
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc = acc + wk[k][v] * xs[j + k][v];
+      out[v] = fsilu(acc);
+    }
+    if (cv && t0 + j < L) stv(ob + (t0 + j) * xc_rs, out);
+  }
+}
+
+// Backward.  A wave owns (b, channels) for the whole sequence so its dW/dbias
+// partial sums are complete per batch row (written to dw_part/db_part, summed
+// over b by the caller: deterministic, no atomics).  Tiles are walked from the
+// end; the K-1 "look-ahead" du values a chunk needs come from the next chunk's
+// lane by shuffle, or from the previous (later) tile for the last chunk.
+template <int K, int VEC, int Q, int TC>
+__global__ void __launch_bounds__(256)
+k_conv_silu_bwd(const float* __restrict__ x, int x_rs, const float* __restrict__ w,
+                const float* __restrict__ bias, const float* __restrict__ g1,
+                const float* __restrict__ g2, float* __restrict__ dx, int dx_rs,
+                float* __restrict__ dw_part, float* __restrict__ db_part, int64_t B, int L,
+                int H, int ncw) {
+  constexpr int G = kWave / Q;
+  constexpr int NX = TC + K - 1;
+  constexpr int KH = K > 1 ? K - 1 : 1;
+  static_assert(TC >= K - 1, "chunk must cover the look-ahead");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int q = lane / G;
+  const int g = lane - q * G;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = wid / ncw;
+  if (b >= B) return;
+  const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
+  const bool cv = c0 < H;
+  const int cc = cv ? c0 : 0;
+  const float* xb = x + b * L * x_rs + cc;
+  const float* g1b = g1 + b * L * H + cc;
+  const float* g2b = g2 ? g2 + b * L * H + cc : nullptr;
+  float* dxb = dx + b * L * dx_rs + cc;
+  float wk[K][VEC], bi[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k][v] = w[(cc + v) * K + k];
+  }
+  ldv(bi, bias + cc);
+  float accw[K][VEC], accb[VEC], halo[KH][VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    accb[v] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) accw[k][v] = 0.0f;
+#pragma unroll
+    for (int m = 0; m < KH; ++m) halo[m][v] = 0.0f;
+  }
+  constexpr int TILE = Q * TC;
+  const int nT = (L + TILE - 1) / TILE;
+  for (int tile = nT - 1; tile >= 0; --tile) {
+    const int t0 = tile * TILE + q * TC;
+    float xs[NX][VEC], du[TC][VEC];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) {
+      const int t = t0 - (K - 1) + m;
+      const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
+      ldv(xs[m], xb + tc * x_rs);
+      if (t < 0) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) xs[m][v] = 0.0f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int tc = min(t0 + j, L - 1);
+      ldv(du[j], g1b + tc * H);
+      if (g2b != nullptr) {
+        float t2[VEC];
+        ldv(t2, g2b + tc * H);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) du[j][v] = du[j][v] + t2[v];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const bool ok = t0 + j < L;
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        float acc = bi[v];
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = acc + wk[k][v] * xs[j + k][v];
+        du[j][v] = ok ? du[j][v] * fdsilu(acc) : 0.0f;
+        if (ok) {
+          accb[v] = accb[v] + du[j][v];
+#pragma unroll
+          for (int k = 0; k < K; ++k) accw[k][v] = accw[k][v] + du[j][v] * xs[j + k][v];
+        }
+      }
+    }
+    // look-ahead du[t0+TC .. t0+TC+K-2]
+    float dn[KH][VEC];
+#pragma unroll
+    for (int m = 0; m < KH; ++m) {
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        const float nb = __shfl_down(du[m][v], G, kWave);
+        dn[m][v] = (q == Q - 1) ? halo[m][v] : nb;
+        halo[m][v] = __shfl(du[m][v], g, kWave);   // chunk 0 of this tile, for the next one
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      float out[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          const int m = j + K - 1 - k;   // du index, may run into the look-ahead
+          const float dv = m < TC ? du[m < TC ? m : 0][v] : dn[m >= TC ? m - TC : 0][v];
+          acc = acc + wk[k][v] * dv;
+        }
+        out[v] = acc;
+      }
+      if (cv && t0 + j < L) stv(dxb + (t0 + j) * dx_rs, out);
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+#pragma unroll
+    for (int s = G; s < kWave; s <<= 1) {
+      accb[v] += __shfl_xor(accb[v], s, kWave);
+#pragma unroll
+      for (int k = 0; k < K; ++k) accw[k][v] += __shfl_xor(accw[k][v], s, kWave);
+    }
+  }
+  if (q == 0 && cv) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) stv(dw_part + (b * K + k) * H + c0, accw[k]);
+    stv(db_part + b * H + c0, accb);
+  }
+}
+
+constexpr int kConvQ = 4;
+
+template <int K, int TC>
+int conv_fwd_t(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
+               int64_t xc_rs, int64_t B, int64_t L, int64_t H, bool vec, hipStream_t st) {
+  const int V = vec ? 4 : 1;
+  const int span = (kWave / kConvQ) * V;
+  const int ncw = (int)((H + span - 1) / span);
+  const int ntile = (int)((L + kConvQ * TC - 1) / (kConvQ * TC));
+  const int64_t waves = B * ncw * ntile;
+  const int64_t blocks = (waves + 3) / 4;
+  if (blocks > 0x7fffffffLL) return fail("rb_conv_silu_fwd: grid too large");
+  if (vec)
+    hipLaunchKernelGGL((k_conv_silu_fwd<K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
+  else
+    hipLaunchKernelGGL((k_conv_silu_fwd<K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
+  return launch_status("rb_conv_silu_fwd");
+}
+
+template <int K, int TC>
+int conv_bwd_t(const float* x, int64_t x_rs, const float* w, const float* bias, const float* g1,
+               const float* g2, float* dx, int64_t dx_rs, float* dw_part, float* db_part,
+               int64_t B, int64_t L, int64_t H, bool vec, hipStream_t st) {
+  const int V = vec ? 4 : 1;
+  const int span = (kWave / kConvQ) * V;
+  const int ncw = (int)((H + span - 1) / span);
+  const int64_t blocks = (B * ncw + 3) / 4;
+  if (vec)
+    hipLaunchKernelGGL((k_conv_silu_bwd<K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
+                       (int)L, (int)H, ncw);
+  else
+    hipLaunchKernelGGL((k_conv_silu_bwd<K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
+                       st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
+                       (int)L, (int)H, ncw);
+  return launch_status("rb_conv_silu_bwd");
+}
+
+}  // namespace
+
+int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
+                    int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
+  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && xc_rs % 4 == 0 && aligned16(x) &&
+                   aligned16(xc) && aligned16(bias);
+  switch (K) {
+    case 1: return conv_fwd_t<1, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 2: return conv_fwd_t<2, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 3: return conv_fwd_t<3, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 4: return conv_fwd_t<4, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 5: return conv_fwd_t<5, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 6: return conv_fwd_t<6, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 7: return conv_fwd_t<7, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 8: return conv_fwd_t<8, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    default: return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
+  }
+}
+
+int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
+                    const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
+                    float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
+  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && dx_rs % 4 == 0 && aligned16(x) &&
+                   aligned16(g1) && (g2 == nullptr || aligned16(g2)) && aligned16(dx) &&
+                   aligned16(dw_part) && aligned16(db_part) && aligned16(bias);
+  switch (K) {
+    case 1: return conv_bwd_t<1, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 2: return conv_bwd_t<2, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 3: return conv_bwd_t<3, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 4: return conv_bwd_t<4, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 5: return conv_bwd_t<5, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 6: return conv_bwd_t<6, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 7: return conv_bwd_t<7, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 8: return conv_bwd_t<8, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    default: return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
+  }
+}
+
+}  // namespace rb

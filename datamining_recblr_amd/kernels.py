@@ -171,11 +171,11 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx):
     return dw_part.sum(0).t().contiguous(), db_part.sum(0)
 
 
-def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None):
+def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True):
     """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
 
     rg: [B, L, 2H]; xc, z: [B, L, H] views; lam: [H]; h0: [H] or None.
-    Returns (y [B, L, H], carries [B, nT, H])."""
+    Returns (y [B, L, H], carries [B, nT, H] or None when not wanted)."""
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (lam, "Lambda")):
         _check(t, n)
     B, L, H = xc.shape
@@ -194,10 +194,11 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None):
     if y is None:
         y = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
     y_rs = _row_stride(y, "y", H)
-    carries = torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
+    carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
+               if want_carries else None)
     _launch("rb_gate_scan_fwd", 5 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
               lam.contiguous().data_ptr(), 0 if h0 is None else h0.data_ptr(), y.data_ptr(),
-              y_rs, carries.data_ptr(), B, L, H, _stream(xc))
+              y_rs, 0 if carries is None else carries.data_ptr(), B, L, H, _stream(xc))
     return y, carries
 
 

@@ -66,7 +66,8 @@ class BDLRUCore(torch.autograd.Function):
         else:
             xc = x
         rg = torch.addmm(gate_b, xc.reshape(B * L, H), gate_w.t()).view(B, L, H2)
-        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0)
+        train = any(ctx.needs_input_grad)
+        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train)
         ctx.use_conv = use_conv
         ctx.has_h0 = h0 is not None
         ctx.save_for_backward(xz, xc if use_conv else None, rg, carries, conv_w, conv_b,

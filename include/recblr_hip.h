@@ -48,7 +48,7 @@ extern "C" {
  * carry (the recurrent state entering the tile) per (b, tile, c) and
  * rb_gate_scan_bwd reads them back.  carries has B * ceil(L / RB_TILE) * H
  * floats. */
-#define RB_TILE 64
+#define RB_TILE 16
 
 /* ABI version; bumped on any signature change. */
 int rb_version(void);
@@ -100,7 +100,8 @@ int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w,
  *   y     = silu(z) * h.
  * rg: [B, L, 2H] view (r = columns [0,H), i = columns [H,2H)), row stride
  * rg_rs; xc, z, y: [B, L, H] views with their own row strides; lam, h0: [H].
- * carries: B * ceil(L/RB_TILE) * H floats (written, consumed by the bwd). */
+ * carries: B * ceil(L/RB_TILE) * H floats (written, consumed by the bwd);
+ * may be NULL for inference (no checkpoints written). */
 int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t xc_rs, const float* z, int64_t z_rs,
                      const float* lam, const float* h0, float* y, int64_t y_rs,

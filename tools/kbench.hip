@@ -1,0 +1,179 @@
+// kbench.hip — standalone variant sweep of the channel-last kernels at the
+// benchmark shape (B=2048, L=200, H=256 by default).  Includes the kernel
+// sources directly so every template variant can be instantiated and timed
+// with hipEvents in one process (interleaved rounds, median).
+//
+//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 \
+//       -I include tools/kbench.hip -o tools/kbench && tools/kbench [B L H]
+#include "../datamining_recblr_amd/csrc/capi.hip"
+#include "../datamining_recblr_amd/csrc/conv_silu.hip"
+#include "../datamining_recblr_amd/csrc/gate_scan.hip"
+#include "../datamining_recblr_amd/csrc/scan_rows.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <vector>
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));    \
+      exit(1);                                                                     \
+    }                                                                              \
+  } while (0)
+
+using namespace rb;
+
+struct Case {
+  const char* name;
+  double bytes;
+  std::function<void()> run;
+  std::vector<float> ms;
+};
+
+__global__ void fill(float* p, int64_t n, uint32_t seed, float lo, float hi) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    p[i] = lo + (hi - lo) * (h & 0xffffff) / 16777216.0f;
+  }
+}
+
+static float* dalloc(int64_t n, uint32_t seed, float lo = -1.f, float hi = 1.f) {
+  float* p;
+  CK(hipMalloc(&p, n * sizeof(float)));
+  hipLaunchKernelGGL(fill, dim3(2048), dim3(256), 0, 0, p, n, seed, lo, hi);
+  return p;
+}
+
+template <int VEC, int Q, int TC>
+void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, float* rg, float* xc,
+              float* z, float* lam, float* y, float* car, float* dy, float* drg, float* dxc,
+              float* dz, float* part, float* dh0, double N) {
+  constexpr int G = 64 / Q;
+  const int ncw = (H + G * VEC - 1) / (G * VEC);
+  const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
+  char* f = (char*)malloc(64);
+  snprintf(f, 64, "gate_fwd %s", nm);
+  cs.push_back({f, 5 * N * 4, [=] {
+    hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
+                       xc, H, z, 2 * H, lam, nullptr, y, H, car, (int64_t)B, L, H, ncw);
+  }, {}});
+  char* f2 = (char*)malloc(64);
+  snprintf(f2, 64, "gate_bwd %s", nm);
+  cs.push_back({f2, 9 * N * 4, [=] {
+    hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
+                       xc, H, z, 2 * H, lam, car, dy, drg, 2 * H, dxc, dz, 2 * H, part, dh0,
+                       (int64_t)B, L, H, ncw);
+  }, {}});
+}
+
+template <int K, int VEC, int Q, int TC>
+void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float* x, float* w,
+              float* bias, float* xc, float* g1, float* dx, float* dwp, float* dbp, double N) {
+  constexpr int G = 64 / Q;
+  const int ncw = (H + G * VEC - 1) / (G * VEC);
+  const int ntile = (L + Q * TC - 1) / (Q * TC);
+  char* f = (char*)malloc(64);
+  snprintf(f, 64, "conv_fwd %s", nm);
+  cs.push_back({f, 2 * N * 4, [=] {
+    const int64_t blocks = ((int64_t)B * ncw * ntile + 3) / 4;
+    hipLaunchKernelGGL((k_conv_silu_fwd<K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, x, 2 * H,
+                       w, bias, xc, H, (int64_t)B, L, H, ncw, ntile);
+  }, {}});
+  char* f2 = (char*)malloc(64);
+  snprintf(f2, 64, "conv_bwd %s", nm);
+  cs.push_back({f2, 3 * N * 4, [=] {
+    const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
+    hipLaunchKernelGGL((k_conv_silu_bwd<K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, x, 2 * H,
+                       w, bias, g1, nullptr, dx, 2 * H, dwp, dbp, (int64_t)B, L, H, ncw);
+  }, {}});
+}
+
+int main(int argc, char** argv) {
+  const int B = argc > 1 ? atoi(argv[1]) : 2048;
+  const int L = argc > 2 ? atoi(argv[2]) : 200;
+  const int H = argc > 3 ? atoi(argv[3]) : 256;
+  const int rounds = argc > 4 ? atoi(argv[4]) : 15;
+  const double N = (double)B * L * H;
+  const int64_t n = (int64_t)B * L * H;
+  const int nT = (L + RB_TILE - 1) / RB_TILE;
+  float* rg = dalloc(2 * n, 1, -2, 2);
+  float* xz = dalloc(2 * n, 2);
+  float* xc = dalloc(n, 3);
+  float* lam = dalloc(H, 4, -7, -2);
+  float* y = dalloc(n, 5);
+  float* car = dalloc((int64_t)B * nT * H, 6);
+  float* dy = dalloc(n, 7);
+  float* drg = dalloc(2 * n, 8);
+  float* dxc = dalloc(n, 9);
+  float* dz = dalloc(2 * n, 10);
+  float* part = dalloc(3 * (int64_t)B * H, 11);
+  float* dh0 = dalloc((int64_t)B * H, 12);
+  float* w = dalloc(H * 8, 13);
+  float* bias = dalloc(H, 14);
+  float* dwp = dalloc((int64_t)B * 9 * H, 15);
+  float* dbp = dalloc((int64_t)B * H, 16);
+  float* g1 = dalloc(n, 17);
+  float* dxo = dalloc(2 * n, 18);
+  float* sg = dalloc(n, 19, 0.9f, 1.0f);   // [B, H, T] scan operands (T = L here)
+  float* sx = dalloc(n, 20);
+  float* so = dalloc(n, 21);
+  float* sd = dalloc(n, 22);
+  CK(hipDeviceSynchronize());
+
+  std::vector<Case> cs;
+  add_gate<4, 4, 4>(cs, "v4 q4 tc4", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<2, 4, 4>(cs, "v2 q4 tc4", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<1, 4, 4>(cs, "v1 q4 tc4", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<4, 8, 2>(cs, "v4 q8 tc2", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<2, 8, 2>(cs, "v2 q8 tc2", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<4, 16, 1>(cs, "v4 q16 tc1", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<2, 16, 1>(cs, "v2 q16 tc1", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_gate<2, 2, 8>(cs, "v2 q2 tc8", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+  add_conv<4, 4, 4, 8>(cs, "v4 q4 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<4, 4, 4, 4>(cs, "v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<4, 2, 4, 4>(cs, "v2 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<4, 4, 2, 8>(cs, "v4 q2 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<4, 2, 2, 8>(cs, "v2 q2 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<4, 4, 8, 4>(cs, "v4 q8 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  cs.push_back({"scan_rows_fwd [B,H,L]", 3 * N * 4, [=] {
+    launch_scan_fwd(sg, sx, so, (int64_t)B * H, L, 0);
+  }, {}});
+  cs.push_back({"scan_rows_bwd [B,H,L]", 5 * N * 4, [=] {
+    launch_scan_bwd(sg, so, sx, sd, y, (int64_t)B * H, L, 0);
+  }, {}});
+  cs.push_back({"hipMemcpy d2d (R+W)", 2 * N * 4, [=] {
+    CK(hipMemcpyAsync(dxc, xc, n * sizeof(float), hipMemcpyDeviceToDevice, 0));
+  }, {}});
+
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (auto& c : cs) c.run();  // warm-up
+  CK(hipDeviceSynchronize());
+  for (int r = 0; r < rounds; ++r) {
+    for (auto& c : cs) {
+      CK(hipEventRecord(e0, 0));
+      c.run();
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      c.ms.push_back(ms);
+    }
+  }
+  CK(hipGetLastError());
+  printf("B=%d L=%d H=%d  N=%.0f  (median of %d)\n", B, L, H, N, rounds);
+  for (auto& c : cs) {
+    std::sort(c.ms.begin(), c.ms.end());
+    const double med = c.ms[c.ms.size() / 2];
+    printf("%-26s %9.1f us  %7.1f GB/s  %.3f of 8 TB/s\n", c.name, med * 1e3,
+           c.bytes / (med * 1e-3) / 1e9, c.bytes / (med * 1e-3) / 8e12);
+  }
+  return 0;
+}
