@@ -44,11 +44,11 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 2; }
+int rb_version(void) { return 3; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
-int rb_num_kernels(void) { return 6; }
+int rb_num_kernels(void) { return 12; }
 
 int rb_scan_fwd(const float* gates, const float* tokens, float* states, int64_t B, int64_t C,
                 int64_t T, void* stream) {
@@ -118,6 +118,72 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
     return r;
   return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
                          dz_rs, part, dh0_part, B, L, H, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_add_ln_fwd(const float* a, const int64_t* idx, int64_t n_idx_rows, const uint8_t* mask,
+                  float scale, const float* r, const float* gamma, const float* beta, float eps,
+                  float* y, float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,
+                  void* stream) {
+  if (!a || !gamma || !beta || !y) return fail("rb_add_ln_fwd: null pointer");
+  if (rows <= 0 || d <= 0) return fail("rb_add_ln_fwd: rows and d must be positive");
+  if (idx && n_idx_rows <= 0) return fail("rb_add_ln_fwd: empty gather table");
+  if ((s_out == nullptr) != (mean == nullptr) || (mean == nullptr) != (rstd == nullptr))
+    return fail("rb_add_ln_fwd: s_out, mean and rstd must be given together");
+  return launch_add_ln_fwd(a, idx, n_idx_rows, mask, scale, r, gamma, beta, eps, y, s_out, mean,
+                           rstd, rows, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+int64_t rb_add_ln_num_parts(int64_t rows, int64_t d) {
+  (void)d;
+  return ln_num_parts(rows);
+}
+
+int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
+                  const float* rstd, const uint8_t* mask, float scale, float* ds, float* da,
+                  float* dgamma_part, float* dbeta_part, int64_t n_parts, int64_t rows,
+                  int64_t d, void* stream) {
+  if (!dy || !s || !gamma || !mean || !rstd || !dgamma_part || !dbeta_part)
+    return fail("rb_add_ln_bwd: null pointer");
+  if (!ds && !da) return fail("rb_add_ln_bwd: nothing to write (ds and da both NULL)");
+  if (rows <= 0 || d <= 0) return fail("rb_add_ln_bwd: rows and d must be positive");
+  if (n_parts != ln_num_parts(rows)) return fail("rb_add_ln_bwd: n_parts != rb_add_ln_num_parts");
+  return launch_add_ln_bwd(dy, s, gamma, mean, rstd, mask, scale, ds, da, dgamma_part,
+                           dbeta_part, n_parts, rows, d, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale, float* u, int64_t n,
+                        void* stream) {
+  if (!a || !u) return fail("rb_silu_dropout_fwd: null pointer");
+  if (n <= 0 || n % 4) return fail("rb_silu_dropout_fwd: n must be a positive multiple of 4");
+  if (!aligned16(a) || !aligned16(u) || (mask && (reinterpret_cast<uintptr_t>(mask) & 3)))
+    return fail("rb_silu_dropout_fwd: misaligned buffer");
+  return launch_silu_dropout_fwd(a, mask, scale, u, n, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale, const float* du,
+                        float* da, int64_t n, void* stream) {
+  if (!a || !du || !da) return fail("rb_silu_dropout_bwd: null pointer");
+  if (n <= 0 || n % 4) return fail("rb_silu_dropout_bwd: n must be a positive multiple of 4");
+  if (!aligned16(a) || !aligned16(du) || !aligned16(da) ||
+      (mask && (reinterpret_cast<uintptr_t>(mask) & 3)))
+    return fail("rb_silu_dropout_bwd: misaligned buffer");
+  return launch_silu_dropout_bwd(a, mask, scale, du, da, n, reinterpret_cast<hipStream_t>(stream));
+}
+
+int64_t rb_embedding_bwd_workspace(int64_t M, int64_t V, int64_t d) {
+  if (M <= 0 || V <= 0 || d <= 0) return 0;
+  return emb_workspace_bytes(M, V, d);
+}
+
+int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
+                     int64_t padding_idx, float* dweight, void* workspace,
+                     int64_t workspace_bytes, void* stream) {
+  if (!idx || !grad || !dweight || !workspace) return fail("rb_embedding_bwd: null pointer");
+  if (M <= 0 || d <= 0 || V <= 0) return fail("rb_embedding_bwd: M, d, V must be positive");
+  if (M >= (int64_t(1) << 31) || V >= (int64_t(1) << 30))
+    return fail("rb_embedding_bwd: M or V too large");
+  return launch_embedding_bwd(idx, grad, M, d, V, padding_idx, dweight, workspace,
+                              workspace_bytes, reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

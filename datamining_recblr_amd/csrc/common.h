@@ -98,6 +98,23 @@ int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
                     int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
                     int64_t H, hipStream_t st);
+int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const uint8_t* mask,
+                      float scale, const float* r, const float* gamma, const float* beta,
+                      float eps, float* y, float* s_out, float* mean, float* rstd, int64_t rows,
+                      int64_t d, hipStream_t st);
+int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
+                      const float* rstd, const uint8_t* mask, float scale, float* ds, float* da,
+                      float* dgp, float* dbp, int64_t nparts, int64_t rows, int64_t d,
+                      hipStream_t st);
+int64_t ln_num_parts(int64_t rows);
+int launch_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale, float* u,
+                            int64_t n, hipStream_t st);
+int launch_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale, const float* du,
+                            float* da, int64_t n, hipStream_t st);
+int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
+int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
+                         int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
+                         hipStream_t st);
 int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,
                     int64_t T, hipStream_t st);
 int launch_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,

@@ -1,0 +1,242 @@
+// embedding.hip — deterministic scatter-add backward of the item embedding
+// gather (reference RecBLR.py:76, nn.Embedding(n_items, d, padding_idx=0)).
+//
+//   dW[v] = sum over positions p with idx[p] == v of grad[p]   (dW[pad] = 0)
+//
+// torch sorts the indices and runs a segmented reduction whose sum_and_scatter
+// kernel took ~4.8 ms per training step at B=2048 L=200 d=128.  Here:
+//   1. keys = int32(idx), vals = position; rocPRIM stable radix sort on the
+//      log2(V) key bits (positions stay in order inside every key);
+//   2. seg[v] = lower_bound(sorted keys, v) for v in [0, V];
+//   3. every key's run is cut into chunks of kChunk rows (long runs of very
+//      popular items are spread over many waves); chunk offsets by a scan;
+//   4. one wave per chunk sums its rows in position order; single-chunk keys
+//      write dW directly, the rest write a partial;
+//   5. one wave per multi-chunk key adds its partials in chunk order.
+// Every sum has a fixed order, so the result is bitwise reproducible, and no
+// float atomics are used.
+#include "common.h"
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+namespace rb {
+namespace {
+
+constexpr int kChunk = 64;
+
+__global__ void k_emb_prep(const int64_t* __restrict__ idx, int* __restrict__ keys,
+                           int* __restrict__ vals, int64_t M) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < M;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    keys[i] = (int)idx[i];
+    vals[i] = (int)i;
+  }
+}
+
+// seg[v] = first sorted position with key >= v, v in [0, V]; keys outside
+// [0, V) fall outside every segment and are ignored (never dereferenced)
+__global__ void k_emb_segments(const int* __restrict__ keys, int64_t M, int V,
+                               int* __restrict__ seg) {
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v <= V; v += gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = M;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    seg[v] = (int)lo;
+  }
+}
+
+// nch[v] = chunks of key v for v < V, nch[V] = 0 (so the scan's last entry is the total)
+__global__ void k_emb_chunks(const int* __restrict__ seg, int V, int* __restrict__ nch) {
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v <= V; v += gridDim.x * blockDim.x) {
+    const int n = v < V ? seg[v + 1] - seg[v] : 0;
+    nch[v] = (n + kChunk - 1) / kChunk;
+  }
+}
+
+// One wave per chunk.  choff = exclusive scan of nch (choff[V] = total).
+template <int NV>
+__global__ void __launch_bounds__(256)
+k_emb_chunk_sum(const int* __restrict__ vals, const int* __restrict__ seg,
+                const int* __restrict__ nch, const int* __restrict__ choff,
+                const float* __restrict__ grad, int d, int V, int padding_idx,
+                float* __restrict__ dw, float* __restrict__ partial) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int total = choff[V];
+  if (c >= total) return;
+  // key owning chunk c: last v with choff[v] <= c
+  int lo = 0, hi = V;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (choff[mid] <= c) lo = mid; else hi = mid;
+  }
+  const int v = lo;
+  const int ci = (int)(c - choff[v]);
+  const int beg = seg[v] + ci * kChunk;
+  const int end = min(seg[v + 1], beg + kChunk);
+  float acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0f;
+  int j = beg;
+  for (; j + 4 <= end; j += 4) {   // 4 rows in flight
+    int p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) p[u] = vals[j + u];
+    float x[4][NV];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int col = lane + k * kWave;
+        x[u][k] = col < d ? grad[(int64_t)p[u] * d + col] : 0.0f;
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] += x[u][k];
+  }
+  for (; j < end; ++j) {
+    const int p = vals[j];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int col = lane + k * kWave;
+      acc[k] += col < d ? grad[(int64_t)p * d + col] : 0.0f;
+    }
+  }
+  const bool single = nch[v] == 1;
+  float* out = single ? dw + (int64_t)v * d : partial + c * d;
+  const float keep = (single && v == padding_idx) ? 0.0f : 1.0f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int col = lane + k * kWave;
+    if (col < d) out[col] = acc[k] * keep;
+  }
+}
+
+// One wave per key: keys with no rows get zeros, multi-chunk keys sum partials.
+template <int NV>
+__global__ void __launch_bounds__(256)
+k_emb_finish(const int* __restrict__ nch, const int* __restrict__ choff,
+             const float* __restrict__ partial, int d, int V, int padding_idx,
+             float* __restrict__ dw) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (v >= V) return;
+  const int n = nch[v];
+  if (n == 1) return;   // written by k_emb_chunk_sum
+  float acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = 0.0f;
+  for (int c = choff[v]; c < choff[v] + n; ++c)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int col = lane + k * kWave;
+      acc[k] += col < d ? partial[(int64_t)c * d + col] : 0.0f;
+    }
+  const float keep = (v == padding_idx) ? 0.0f : 1.0f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int col = lane + k * kWave;
+    if (col < d) dw[v * d + col] = acc[k] * keep;
+  }
+}
+
+int key_bits(int64_t V) {
+  int b = 1;
+  while ((int64_t(1) << b) < V) ++b;
+  return b;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct EmbWs {
+  size_t keys_in, keys_out, vals_in, vals_out, seg, nch, choff, partial, sort_tmp, scan_tmp;
+  size_t sort_bytes, scan_bytes, total;
+};
+
+EmbWs emb_layout(int64_t M, int64_t V, int64_t d) {
+  EmbWs w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off = align256(off + bytes); return o; };
+  w.keys_in = take(M * 4);
+  w.keys_out = take(M * 4);
+  w.vals_in = take(M * 4);
+  w.vals_out = take(M * 4);
+  w.seg = take((V + 1) * 4);
+  w.nch = take((V + 1) * 4);
+  w.choff = take((V + 1) * 4);
+  const int64_t max_chunks = M / kChunk + V + 1;
+  w.partial = take((size_t)max_chunks * d * 4);
+  w.sort_bytes = 0;
+  rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (const int*)nullptr, (int*)nullptr,
+                            (const int*)nullptr, (int*)nullptr, (size_t)M, 0, key_bits(V));
+  w.sort_tmp = take(w.sort_bytes);
+  w.scan_bytes = 0;
+  rocprim::exclusive_scan(nullptr, w.scan_bytes, (const int*)nullptr, (int*)nullptr, 0,
+                          (size_t)(V + 1), rocprim::plus<int>());
+  w.scan_tmp = take(w.scan_bytes);
+  w.total = off;
+  return w;
+}
+
+template <int NV>
+int emb_sums(const EmbWs& w, char* ws, const float* grad, int64_t M, int64_t d, int64_t V,
+             int64_t padding_idx, float* dw, hipStream_t st) {
+  const int* vals = reinterpret_cast<const int*>(ws + w.vals_out);
+  const int* seg = reinterpret_cast<const int*>(ws + w.seg);
+  const int* nch = reinterpret_cast<const int*>(ws + w.nch);
+  const int* choff = reinterpret_cast<const int*>(ws + w.choff);
+  float* partial = reinterpret_cast<float*>(ws + w.partial);
+  const int64_t max_chunks = M / kChunk + V + 1;
+  hipLaunchKernelGGL((k_emb_chunk_sum<NV>), dim3((unsigned)((max_chunks + 3) / 4)), dim3(256), 0,
+                     st, vals, seg, nch, choff, grad, (int)d, (int)V, (int)padding_idx, dw,
+                     partial);
+  hipLaunchKernelGGL((k_emb_finish<NV>), dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, nch,
+                     choff, partial, (int)d, (int)V, (int)padding_idx, dw);
+  return launch_status("rb_embedding_bwd");
+}
+
+}  // namespace
+
+int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d) {
+  return (int64_t)emb_layout(M, V, d).total;
+}
+
+int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
+                         int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
+                         hipStream_t st) {
+  const EmbWs w = emb_layout(M, V, d);
+  if (ws_bytes < (int64_t)w.total) return fail("rb_embedding_bwd: workspace too small");
+  char* ws = static_cast<char*>(workspace);
+  int* keys_in = reinterpret_cast<int*>(ws + w.keys_in);
+  int* keys_out = reinterpret_cast<int*>(ws + w.keys_out);
+  int* vals_in = reinterpret_cast<int*>(ws + w.vals_in);
+  int* vals_out = reinterpret_cast<int*>(ws + w.vals_out);
+  int* seg = reinterpret_cast<int*>(ws + w.seg);
+  int* nch = reinterpret_cast<int*>(ws + w.nch);
+  int* choff = reinterpret_cast<int*>(ws + w.choff);
+  const int64_t pblocks = std::min<int64_t>(4096, (M + 255) / 256);
+  hipLaunchKernelGGL(k_emb_prep, dim3((unsigned)pblocks), dim3(256), 0, st, idx, keys_in, vals_in,
+                     M);
+  size_t sb = w.sort_bytes;
+  if (rocprim::radix_sort_pairs(ws + w.sort_tmp, sb, keys_in, keys_out, vals_in, vals_out,
+                                (size_t)M, 0, key_bits(V), st) != hipSuccess)
+    return fail("rb_embedding_bwd: radix sort failed");
+  const unsigned vb = (unsigned)((V + 256) / 256);
+  hipLaunchKernelGGL(k_emb_segments, dim3(vb), dim3(256), 0, st, keys_out, M, (int)V, seg);
+  hipLaunchKernelGGL(k_emb_chunks, dim3(vb), dim3(256), 0, st, seg, (int)V, nch);
+  size_t scb = w.scan_bytes;
+  if (rocprim::exclusive_scan(ws + w.scan_tmp, scb, nch, choff, 0, (size_t)(V + 1),
+                              rocprim::plus<int>(), st) != hipSuccess)
+    return fail("rb_embedding_bwd: scan failed");
+  if (d <= 64) return emb_sums<1>(w, ws, grad, M, d, V, padding_idx, dw, st);
+  if (d <= 128) return emb_sums<2>(w, ws, grad, M, d, V, padding_idx, dw, st);
+  if (d <= 256) return emb_sums<4>(w, ws, grad, M, d, V, padding_idx, dw, st);
+  if (d <= 512) return emb_sums<8>(w, ws, grad, M, d, V, padding_idx, dw, st);
+  return fail("rb_embedding_bwd: d must be <= 512");
+}
+
+}  // namespace rb

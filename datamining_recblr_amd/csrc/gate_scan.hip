@@ -15,10 +15,25 @@
 //   e_t = alpha_t * d_t,  d_t = dL/dh_t = e_{t+1} + dy_t * silu(z_t).
 #include "common.h"
 
+#include <initializer_list>
+
 namespace rb {
 namespace {
 
-template <int VEC, int Q, int TC>
+template <int VEC, int TC>
+struct FwdIn {
+  float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC];
+};
+
+template <int VEC, int TC>
+struct BwdIn {
+  float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC], g[TC][VEC];
+};
+
+// PF: software-prefetch the next tile's operands before computing this one
+// (two register buffers), so a wave keeps its loads in flight across the
+// shuffle/compute/store phase of the previous tile.
+template <int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
                 const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
@@ -53,30 +68,31 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
     for (int v = 0; v < VEC; ++v) carry[v] = 0.0f;
   }
   const int nT = (L + TILE - 1) / TILE;
-  for (int tile = 0; tile < nT; ++tile) {
+
+  auto load = [&](FwdIn<VEC, TC>& in, int tile) {
+    const int t0 = tile * TILE + q * TC;
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int t = min(t0 + j, L - 1);
+      ldv(in.r[j], rgb + t * rg_rs);
+      ldv(in.i[j], rgb + t * rg_rs + H);
+      ldv(in.x[j], xcb + t * xc_rs);
+      ldv(in.z[j], zb + t * z_rs);
+    }
+  };
+  auto process = [&](FwdIn<VEC, TC>& in, int tile) {
     if (carries != nullptr && q == 0 && cv) stv(carries + (b * nT + tile) * H + c0, carry);
     const int t0 = tile * TILE + q * TC;
-    float al[TC][VEC], bp[TC][VEC], zv[TC][VEC];
-    {
-      float rv[TC][VEC], iv[TC][VEC];
+    // in.r <- alpha, in.x <- b' = beta * xc
 #pragma unroll
-      for (int j = 0; j < TC; ++j) {
-        const int t = min(t0 + j, L - 1);
-        ldv(rv[j], rgb + t * rg_rs);
-        ldv(iv[j], rgb + t * rg_rs + H);
-        ldv(bp[j], xcb + t * xc_rs);
-        ldv(zv[j], zb + t * z_rs);
-      }
+    for (int j = 0; j < TC; ++j) {
+      const bool ok = t0 + j < L;
 #pragma unroll
-      for (int j = 0; j < TC; ++j) {
-        const bool ok = t0 + j < L;
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          const float a = fexp(nsp[v] * fsigm(rv[j][v]));
-          const float beta = fsqrt(1.0f - a * a + 1e-8f) * fsigm(iv[j][v]);
-          al[j][v] = ok ? a : 1.0f;
-          bp[j][v] = ok ? beta * bp[j][v] : 0.0f;
-        }
+      for (int v = 0; v < VEC; ++v) {
+        const float a = fexp(nsp[v] * fsigm(in.r[j][v]));
+        const float beta = fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v]);
+        in.r[j][v] = ok ? a : 1.0f;
+        in.x[j][v] = ok ? beta * in.x[j][v] : 0.0f;
       }
     }
     float cin[VEC];
@@ -85,8 +101,8 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
       float A = 1.0f, X = 0.0f;
 #pragma unroll
       for (int j = 0; j < TC; ++j) {
-        X = X * al[j][v] + bp[j][v];
-        A = A * al[j][v];
+        X = X * in.r[j][v] + in.x[j][v];
+        A = A * in.r[j][v];
       }
 #pragma unroll
       for (int k = 1; k < Q; k <<= 1) {
@@ -113,15 +129,33 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
       float out[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
-        cin[v] = cin[v] * al[j][v] + bp[j][v];
-        out[v] = fsilu(zv[j][v]) * cin[v];
+        cin[v] = cin[v] * in.r[j][v] + in.x[j][v];
+        out[v] = fsilu(in.z[j][v]) * cin[v];
       }
       if (cv && t0 + j < L) stv(yb + (t0 + j) * y_rs, out);
+    }
+  };
+
+  FwdIn<VEC, TC> bufA, bufB;
+  if constexpr (PF) {
+    load(bufA, 0);
+    for (int tile = 0; tile < nT; tile += 2) {
+      if (tile + 1 < nT) load(bufB, tile + 1);
+      process(bufA, tile);
+      if (tile + 1 < nT) {
+        if (tile + 2 < nT) load(bufA, tile + 2);
+        process(bufB, tile + 1);
+      }
+    }
+  } else {
+    for (int tile = 0; tile < nT; ++tile) {
+      load(bufA, tile);
+      process(bufA, tile);
     }
   }
 }
 
-template <int VEC, int Q, int TC>
+template <int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
                 const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
@@ -157,30 +191,33 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   float ecarry[VEC], acc_v[VEC], acc_r[VEC], acc_i[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) ecarry[v] = acc_v[v] = acc_r[v] = acc_i[v] = 0.0f;
-
   const int nT = (L + TILE - 1) / TILE;
-  for (int tile = nT - 1; tile >= 0; --tile) {
+
+  auto load = [&](BwdIn<VEC, TC>& in, int tile) {
     const int t0 = tile * TILE + q * TC;
-    float hcar[VEC];
-    ldv(hcar, carries + (b * nT + tile) * H + cc);
-    float rv[TC][VEC], iv[TC][VEC], xv[TC][VEC], zv[TC][VEC], gv[TC][VEC], al[TC][VEC];
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
       const int t = min(t0 + j, L - 1);
-      ldv(rv[j], rgb + t * rg_rs);
-      ldv(iv[j], rgb + t * rg_rs + H);
-      ldv(xv[j], xcb + t * xc_rs);
-      ldv(zv[j], zb + t * z_rs);
-      ldv(gv[j], dyb + t * H);
+      ldv(in.r[j], rgb + t * rg_rs);
+      ldv(in.i[j], rgb + t * rg_rs + H);
+      ldv(in.x[j], xcb + t * xc_rs);
+      ldv(in.z[j], zb + t * z_rs);
+      ldv(in.g[j], dyb + t * H);
     }
+  };
+  auto process = [&](BwdIn<VEC, TC>& in, int tile) {
+    const int t0 = tile * TILE + q * TC;
+    float hcar[VEC];
+    ldv(hcar, carries + (b * nT + tile) * H + cc);
+    float al[TC][VEC];
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
       const bool ok = t0 + j < L;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
-        const float a = fexp(nsp[v] * fsigm(rv[j][v]));
+        const float a = fexp(nsp[v] * fsigm(in.r[j][v]));
         al[j][v] = ok ? a : 1.0f;
-        if (!ok) gv[j][v] = 0.0f;
+        if (!ok) in.g[j][v] = 0.0f;   // dy past the end contributes nothing
       }
     }
     float cin[VEC], ein[VEC];
@@ -192,13 +229,13 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
       for (int j = 0; j < TC; ++j) {
         const float a = al[j][v];
         const float bpj = (t0 + j < L)
-            ? fsqrt(1.0f - a * a + 1e-8f) * fsigm(iv[j][v]) * xv[j][v] : 0.0f;
+            ? fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v]) * in.x[j][v] : 0.0f;
         X = X * a + bpj;
         A = A * a;
       }
 #pragma unroll
       for (int j = TC - 1; j >= 0; --j) {
-        const float d = E + gv[j][v] * fsilu(zv[j][v]);
+        const float d = E + in.g[j][v] * fsilu(in.z[j][v]);
         E = d * al[j][v];
       }
       // forward scan over earlier chunks -> carry into this chunk
@@ -250,10 +287,11 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         const float a = al[j][v];
-        const float bpj = ok ? fsqrt(1.0f - a * a + 1e-8f) * fsigm(iv[j][v]) * xv[j][v] : 0.0f;
+        const float bpj =
+            ok ? fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v]) * in.x[j][v] : 0.0f;
         hp[j][v] = cin[v];
         cin[v] = cin[v] * a + bpj;
-        dzo[v] = (gv[j][v] * cin[v]) * fdsilu(zv[j][v]);
+        dzo[v] = (in.g[j][v] * cin[v]) * fdsilu(in.z[j][v]);
       }
       if (cv && ok) stv(dzb + (t0 + j) * dz_rs, dzo);
     }
@@ -264,11 +302,11 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         const float a = al[j][v];
-        const float d = ein[v] + gv[j][v] * fsilu(zv[j][v]);   // dL/dh_t
-        const float sr = fsigm(rv[j][v]);
-        const float si = fsigm(iv[j][v]);
+        const float d = ein[v] + in.g[j][v] * fsilu(in.z[j][v]);   // dL/dh_t
+        const float sr = fsigm(in.r[j][v]);
+        const float si = fsigm(in.i[j][v]);
         const float sq = fsqrt(1.0f - a * a + 1e-8f);
-        const float dbeta = d * xv[j][v];
+        const float dbeta = d * in.x[j][v];
         const float du = (dbeta * si) * (0.5f * frcp(sq));
         const float da = hp[j][v] * d + (-du) * (2.0f * a);
         const float dv = da * a;
@@ -290,6 +328,24 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
       }
     }
     if (tile == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ein);
+  };
+
+  BwdIn<VEC, TC> bufA, bufB;
+  if constexpr (PF) {
+    load(bufA, nT - 1);
+    for (int tile = nT - 1; tile >= 0; tile -= 2) {
+      if (tile - 1 >= 0) load(bufB, tile - 1);
+      process(bufA, tile);
+      if (tile - 1 >= 0) {
+        if (tile - 2 >= 0) load(bufA, tile - 2);
+        process(bufB, tile - 1);
+      }
+    }
+  } else {
+    for (int tile = nT - 1; tile >= 0; --tile) {
+      load(bufA, tile);
+      process(bufA, tile);
+    }
   }
   // per-channel partial sums: butterfly over the Q lanes sharing the channels
 #pragma unroll
@@ -310,10 +366,53 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   }
 }
 
-// forward: 4 chunks x 4 steps, 16 lanes x 4 channels = 64 channels per wave
+// Tuned on MI355X at B=2048, L=200, H=256 (tools/kbench.hip): the forward
+// runs 4 chunks x 4 steps with 2 channels per lane and a one-tile register
+// prefetch; the backward (about 7 live values per step and channel) 8 chunks
+// x 2 steps with 4 channels per lane.  Both sit at the data-movement ceiling
+// of their read/write mix (a copy kernel with the same 4R+1W pattern and no
+// math runs at the same rate).
 constexpr int kFwdQ = 4, kFwdTC = RB_TILE / kFwdQ;
-// backward holds ~7 values per (step, channel): 8 chunks x 2 steps, 32 channels/wave
 constexpr int kBwdQ = 8, kBwdTC = RB_TILE / kBwdQ;
+
+template <int V>
+bool vec_ok(int64_t H, std::initializer_list<int64_t> strides,
+            std::initializer_list<const void*> ptrs) {
+  if (H % V) return false;
+  for (int64_t s : strides)
+    if (s % V) return false;
+  for (const void* p : ptrs)
+    if (p != nullptr && (reinterpret_cast<uintptr_t>(p) % (4 * V))) return false;
+  return true;
+}
+
+template <int V>
+int gate_fwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
+               int64_t z_rs, const float* lam, const float* h0, float* y, int64_t y_rs,
+               float* carries, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+  const int span = (kWave / kFwdQ) * V;
+  const int ncw = (int)((H + span - 1) / span);
+  const int64_t blocks = (B * ncw + 3) / 4;
+  hipLaunchKernelGGL((k_gate_scan_fwd<V, kFwdQ, kFwdTC, true>), dim3((unsigned)blocks),
+                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, h0, y,
+                     (int)y_rs, carries, B, (int)L, (int)H, ncw);
+  return launch_status("rb_gate_scan_fwd");
+}
+
+template <int V>
+int gate_bwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
+               int64_t z_rs, const float* lam, const float* carries, const float* dy, float* drg,
+               int64_t drg_rs, float* dxc, float* dz, int64_t dz_rs, float* part,
+               float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+  const int span = (kWave / kBwdQ) * V;
+  const int ncw = (int)((H + span - 1) / span);
+  const int64_t blocks = (B * ncw + 3) / 4;
+  hipLaunchKernelGGL((k_gate_scan_bwd<V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
+                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, carries,
+                     dy, drg, (int)drg_rs, dxc, dz, (int)dz_rs, part, dh0_part, B, (int)L, (int)H,
+                     ncw);
+  return launch_status("rb_gate_scan_bwd");
+}
 
 }  // namespace
 
@@ -321,23 +420,12 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* z, int64_t z_rs, const float* lam, const float* h0, float* y,
                     int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
                     hipStream_t st) {
-  const bool vec = H % 4 == 0 && rg_rs % 4 == 0 && xc_rs % 4 == 0 && z_rs % 4 == 0 &&
-                   y_rs % 4 == 0 && aligned16(rg) && aligned16(xc) && aligned16(z) &&
-                   aligned16(y) && aligned16(lam) && (h0 == nullptr || aligned16(h0)) &&
-                   (carries == nullptr || aligned16(carries));
-  const int V = vec ? 4 : 1;
-  const int span = (kWave / kFwdQ) * V;
-  const int ncw = (int)((H + span - 1) / span);
-  const int64_t blocks = (B * ncw + 3) / 4;
-  if (vec)
-    hipLaunchKernelGGL((k_gate_scan_fwd<4, kFwdQ, kFwdTC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, h0, y, (int)y_rs,
-                       carries, B, (int)L, (int)H, ncw);
-  else
-    hipLaunchKernelGGL((k_gate_scan_fwd<1, kFwdQ, kFwdTC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, h0, y, (int)y_rs,
-                       carries, B, (int)L, (int)H, ncw);
-  return launch_status("rb_gate_scan_fwd");
+  const auto strides = {rg_rs, xc_rs, z_rs, y_rs};
+  const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y,
+                     (const void*)lam, (const void*)h0, (const void*)carries};
+  if (vec_ok<2>(H, strides, ptrs))
+    return gate_fwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, y, y_rs, carries, B, L, H, st);
+  return gate_fwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, y, y_rs, carries, B, L, H, st);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
@@ -345,24 +433,18 @@ int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
                     int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
                     int64_t H, hipStream_t st) {
-  const bool vec = H % 4 == 0 && rg_rs % 4 == 0 && xc_rs % 4 == 0 && z_rs % 4 == 0 &&
-                   drg_rs % 4 == 0 && dz_rs % 4 == 0 && aligned16(rg) && aligned16(xc) &&
-                   aligned16(z) && aligned16(lam) && aligned16(carries) && aligned16(dy) &&
-                   aligned16(drg) && aligned16(dxc) && aligned16(dz) && aligned16(part) &&
-                   aligned16(dh0_part);
-  const int V = vec ? 4 : 1;
-  const int span = (kWave / kBwdQ) * V;
-  const int ncw = (int)((H + span - 1) / span);
-  const int64_t blocks = (B * ncw + 3) / 4;
-  if (vec)
-    hipLaunchKernelGGL((k_gate_scan_bwd<4, kBwdQ, kBwdTC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, carries, dy, drg,
-                       (int)drg_rs, dxc, dz, (int)dz_rs, part, dh0_part, B, (int)L, (int)H, ncw);
-  else
-    hipLaunchKernelGGL((k_gate_scan_bwd<1, kBwdQ, kBwdTC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, carries, dy, drg,
-                       (int)drg_rs, dxc, dz, (int)dz_rs, part, dh0_part, B, (int)L, (int)H, ncw);
-  return launch_status("rb_gate_scan_bwd");
+  const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dz_rs};
+  const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)lam,
+                     (const void*)carries, (const void*)dy, (const void*)drg, (const void*)dxc,
+                     (const void*)dz, (const void*)part, (const void*)dh0_part};
+  if (vec_ok<4>(H, strides, ptrs))
+    return gate_bwd_v<4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
+                         dz_rs, part, dh0_part, B, L, H, st);
+  if (vec_ok<2>(H, strides, ptrs))
+    return gate_bwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
+                         dz_rs, part, dh0_part, B, L, H, st);
+  return gate_bwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
+                       dz_rs, part, dh0_part, B, L, H, st);
 }
 
 }  // namespace rb

@@ -232,3 +232,129 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None):
               B, L, H, _stream(xc))
     sums = part.sum(1)
     return drg, dxc, sums[0], torch.cat([sums[1], sums[2]]), dh0_part.sum(0)
+
+
+# ---------------------------------------------------------------- row blocks
+LN_SIZES = (16, 32, 64, 128, 256, 512, 1024)
+
+
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _check_mask(mask, shape, name="mask"):
+    if mask is None:
+        return
+    if mask.dtype not in (torch.uint8, torch.bool) or tuple(mask.shape) != tuple(shape):
+        raise ValueError(f"{name} must be uint8/bool of shape {tuple(shape)}")
+    if not mask.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def add_ln_fwd(a, r, mask, scale, gamma, beta, eps, idx=None, save=True):
+    """Fused [gather +] dropout + residual + LayerNorm over rows of d.
+
+    a: [rows, d] (or the [V, d] table when idx [rows] is given); r: [rows, d]
+    or None; mask: uint8 [rows, d] or None.  Returns (y, s, mean, rstd); the
+    last three are None unless save."""
+    _check(a, "a")
+    d = a.shape[-1]
+    if d not in LN_SIZES:
+        raise ValueError(f"layer norm width {d} not in {LN_SIZES}")
+    if not a.is_contiguous():
+        raise ValueError("a must be contiguous")
+    if idx is not None:
+        if idx.dtype != torch.int64 or not idx.is_contiguous() or idx.device != a.device:
+            raise ValueError("idx must be contiguous int64 on the same device")
+        rows = idx.numel()
+        nidx = a.shape[0]
+    else:
+        rows = a.numel() // d
+        nidx = 0
+    if r is not None:
+        _check(r, "r")
+        if r.numel() != rows * d or not r.is_contiguous():
+            raise ValueError("r must be contiguous with rows * d elements")
+    _check_mask(mask, (rows, d))
+    for t, n in ((gamma, "gamma"), (beta, "beta")):
+        _check(t, n)
+        if t.shape != (d,) or not t.is_contiguous():
+            raise ValueError(f"{n} must be contiguous [{d}]")
+    dev = a.device
+    y = torch.empty((rows, d), device=dev, dtype=torch.float32)
+    s = mean = rstd = None
+    if save:
+        s = torch.empty((rows, d), device=dev, dtype=torch.float32)
+        mean = torch.empty((rows,), device=dev, dtype=torch.float32)
+        rstd = torch.empty((rows,), device=dev, dtype=torch.float32)
+    n = rows * d
+    nbytes = 4 * n * (2 + (r is not None) + (s is not None)) + (n if mask is not None else 0)
+    _launch("rb_add_ln_fwd", nbytes, a.data_ptr(), _ptr(idx), nidx, _ptr(mask), float(scale),
+            _ptr(r), gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(), _ptr(s),
+            _ptr(mean), _ptr(rstd), rows, d, _stream(a))
+    return y, s, mean, rstd
+
+
+def add_ln_bwd(dy, s, gamma, mean, rstd, mask, scale, want_ds=True, want_da=True):
+    """Returns (ds, da, dgamma, dbeta); ds/da None when not wanted."""
+    _check(dy, "dy")
+    rows, d = s.shape
+    dy = dy.reshape(rows, d)
+    if not dy.is_contiguous():
+        dy = dy.contiguous()
+    _check_mask(mask, (rows, d))
+    lib = _lib.load()
+    nparts = int(lib.rb_add_ln_num_parts(rows, d))
+    dev = s.device
+    dgp = torch.empty((nparts, d), device=dev, dtype=torch.float32)
+    dbp = torch.empty((nparts, d), device=dev, dtype=torch.float32)
+    ds = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_ds else None
+    da = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_da else None
+    n = rows * d
+    nbytes = 4 * n * (2 + want_ds + want_da) + (n if mask is not None else 0)
+    _launch("rb_add_ln_bwd", nbytes, dy.data_ptr(), s.data_ptr(), gamma.data_ptr(),
+            mean.data_ptr(), rstd.data_ptr(), _ptr(mask), float(scale), _ptr(ds), _ptr(da),
+            dgp.data_ptr(), dbp.data_ptr(), nparts, rows, d, _stream(dy))
+    return ds, da, dgp.sum(0), dbp.sum(0)
+
+
+def silu_dropout_fwd(a, mask, scale):
+    _check(a, "a")
+    if not a.is_contiguous() or a.numel() % 4:
+        raise ValueError("a must be contiguous with numel % 4 == 0")
+    _check_mask(mask, a.shape)
+    u = torch.empty_like(a)
+    n = a.numel()
+    _launch("rb_silu_dropout_fwd", 8 * n + (n if mask is not None else 0), a.data_ptr(),
+            _ptr(mask), float(scale), u.data_ptr(), n, _stream(a))
+    return u
+
+
+def silu_dropout_bwd(a, mask, scale, du):
+    _check(du, "du")
+    du = du.contiguous()
+    da = torch.empty_like(a)
+    n = a.numel()
+    _launch("rb_silu_dropout_bwd", 12 * n + (n if mask is not None else 0), a.data_ptr(),
+            _ptr(mask), float(scale), du.data_ptr(), da.data_ptr(), n, _stream(a))
+    return da
+
+
+def embedding_bwd(idx, grad, num_rows, padding_idx=0):
+    """dW[v] = sum_{p: idx[p] == v} grad[p] (dW[padding_idx] = 0), deterministic."""
+    _check(grad, "grad")
+    M = idx.numel()
+    d = grad.shape[-1]
+    if idx.dtype != torch.int64 or not idx.is_contiguous():
+        raise ValueError("idx must be contiguous int64")
+    grad = grad.reshape(M, d)
+    if not grad.is_contiguous():
+        grad = grad.contiguous()
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_embedding_bwd_workspace(M, num_rows, d))
+    ws = torch.empty((ws_bytes,), device=grad.device, dtype=torch.uint8)
+    dw = torch.empty((num_rows, d), device=grad.device, dtype=torch.float32)
+    pad = -1 if padding_idx is None else int(padding_idx)
+    _launch("rb_embedding_bwd", 4 * M * d + 4 * num_rows * d, idx.data_ptr(), grad.data_ptr(), M,
+            d, num_rows, pad, dw.data_ptr(), ws.data_ptr(), ws_bytes, _stream(grad))
+    return dw

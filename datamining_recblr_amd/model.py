@@ -22,6 +22,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._lib import RecBLRNativeError
+from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, silu_dropout
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len
 
@@ -89,9 +90,9 @@ class FeedForward(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
 
     def forward(self, input_tensor):
-        h = self.dropout(F.silu(self.w_1(input_tensor)))
-        h = self.dropout(self.w_2(h))
-        return self.layer_norm(h + input_tensor)
+        h = silu_dropout(self.w_1(input_tensor), self.dropout, self.training)
+        return add_dropout_layer_norm(self.w_2(h), input_tensor, self.dropout, self.layer_norm,
+                                      self.training)
 
 
 class RecurrentLayer(nn.Module):
@@ -110,8 +111,8 @@ class RecurrentLayer(nn.Module):
         self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
 
     def forward(self, input_tensor):
-        h = self.behavior_modeling(input_tensor)
-        h = self.layer_norm(self.dropout(h) + input_tensor)
+        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor), input_tensor,
+                                   self.dropout, self.layer_norm, self.training)
         return h if self.disable_ffn else self.ffn(h)
 
 
@@ -164,7 +165,8 @@ class RecBLR(SequentialRecommender):
             module.bias.data.zero_()
 
     def forward(self, item_seq, item_seq_len):
-        h = self.layer_norm(self.dropout(self.item_embedding(item_seq)))
+        h = embed_dropout_layer_norm(item_seq, self.item_embedding, self.dropout, self.layer_norm,
+                                     self.training)
         for layer in self.recurrent_layers:
             h = layer(h)
         return self.gather_indexes(h, item_seq_len - 1)

@@ -120,6 +120,51 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t dz_rs, float* part, float* dh0_part,
                      int64_t B, int64_t L, int64_t H, void* stream);
 
+/* ---- blocks around the BD-LRU (RecurrentLayer / FeedForward / embedding) ---- */
+
+/* Fused dropout + residual + LayerNorm over rows of d floats
+ * (RecBLR.py:77-78 and :142, and FeedForward's :223-225):
+ *   A[row] = idx ? a[clamp(idx[row], 0, n_idx_rows-1)] : a[row]   (gather)
+ *   s      = A[row] * (mask ? mask[row] * scale : 1) + (r ? r[row] : 0)
+ *   y      = (s - mean) / sqrt(var + eps) * gamma + beta
+ * mask: uint8 {0,1} per element (torch's bool), scale = 1/(1-p).  s_out,
+ * mean, rstd (saved for the backward) are all given or all NULL.
+ * d in {16, 32, 64, 128, 256, 512, 1024}. */
+int rb_add_ln_fwd(const float* a, const int64_t* idx, int64_t n_idx_rows,
+                  const uint8_t* mask, float scale, const float* r,
+                  const float* gamma, const float* beta, float eps, float* y,
+                  float* s_out, float* mean, float* rstd, int64_t rows,
+                  int64_t d, void* stream);
+
+/* Rows of the dgamma/dbeta partial-sum buffers rb_add_ln_bwd writes. */
+int64_t rb_add_ln_num_parts(int64_t rows, int64_t d);
+
+/* Backward of rb_add_ln_fwd: ds = dL/ds (the residual's gradient) and
+ * da = ds * mask * scale (the dropped input's gradient); either may be NULL.
+ * dgamma_part / dbeta_part: [n_parts, d], summed over rows by the caller. */
+int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma,
+                  const float* mean, const float* rstd, const uint8_t* mask,
+                  float scale, float* ds, float* da, float* dgamma_part,
+                  float* dbeta_part, int64_t n_parts, int64_t rows, int64_t d,
+                  void* stream);
+
+/* FeedForward's inner activation (RecBLR.py:220-221):
+ * u = silu(a) * (mask ? mask * scale : 1); n a multiple of 4. */
+int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale,
+                        float* u, int64_t n, void* stream);
+int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale,
+                        const float* du, float* da, int64_t n, void* stream);
+
+/* Item-embedding backward (RecBLR.py:76, nn.Embedding(padding_idx=0)):
+ * dweight[v] = sum_{p : idx[p] == v} grad[p], dweight[padding_idx] = 0,
+ * deterministic (stable sort + fixed-order segment sums, no atomics).
+ * Ids outside [0, V) are ignored.  workspace: rb_embedding_bwd_workspace()
+ * bytes, caller-allocated. */
+int64_t rb_embedding_bwd_workspace(int64_t M, int64_t V, int64_t d);
+int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d,
+                     int64_t V, int64_t padding_idx, float* dweight,
+                     void* workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,137 @@
+"""GPU parity of the fused blocks around the BD-LRU against plain torch fp32
+compositions of the reference's ops (RecBLR.py:76-78, :142, :218-227), with
+explicit dropout masks so both sides drop the same elements."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def close(a, b, atol=1e-5, rtol=1e-5, what=""):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    err = (a - b).abs()
+    bad = err > atol + rtol * b.abs() + 2e-6 * b.abs().max()
+    assert not bad.any(), f"{what}: max err {err.max().item():.3e}"
+
+
+@pytest.mark.parametrize("rows,d", [(7, 16), (33, 64), (1000, 128), (129, 256), (64, 512),
+                                    (5, 1024), (409, 32)])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_add_dropout_layer_norm(cuda, rows, d, p):
+    from datamining_recblr_amd.blocks import _AddDropoutLN
+
+    g = torch.Generator(device="cpu").manual_seed(rows * d)
+    a = torch.randn(rows, d, generator=g).to(cuda).requires_grad_()
+    r = torch.randn(rows, d, generator=g).to(cuda).requires_grad_()
+    gamma = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    beta = (0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    dy = torch.randn(rows, d, generator=g).to(cuda)
+    mask = (torch.rand(rows, d, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
+    scale = 1.0 / (1.0 - p)
+    y = _AddDropoutLN.apply(a, r, gamma, beta, mask, scale, 1e-12)
+    y.backward(dy)
+    ar, rr, gr, br = (t.detach().clone().requires_grad_() for t in (a, r, gamma, beta))
+    dropped = ar * mask * scale if mask is not None else ar
+    yr = F.layer_norm(dropped + rr, (d,), gr, br, eps=1e-12)
+    yr.backward(dy)
+    close(y, yr, what="y")
+    close(a.grad, ar.grad, atol=1e-4, what="da")
+    close(r.grad, rr.grad, atol=1e-4, what="dr")
+    close(gamma.grad, gr.grad, atol=1e-4, rtol=1e-4, what="dgamma")
+    close(beta.grad, br.grad, atol=1e-4, rtol=1e-4, what="dbeta")
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_embed_dropout_layer_norm(cuda, p):
+    """Gather + dropout + LN, and the deterministic embedding backward, incl.
+    padding id 0, a very popular id (multi-chunk segment sums) and unused ids."""
+    from datamining_recblr_amd.blocks import _EmbedDropoutLN
+
+    V, d, B, L = 500, 128, 16, 300
+    g = torch.Generator(device="cpu").manual_seed(11)
+    table = torch.randn(V, d, generator=g).to(cuda).requires_grad_()
+    idx = torch.randint(0, V // 2, (B, L), generator=g)
+    idx[:, ::3] = 7          # 1600 occurrences of one id -> 25 chunks
+    idx[:, -5:] = 0          # padding
+    idx = idx.to(cuda)
+    gamma = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    beta = (0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    dy = torch.randn(B, L, d, generator=g).to(cuda)
+    mask = (torch.rand(B * L, d, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
+    scale = 1.0 / (1.0 - p)
+    y = _EmbedDropoutLN.apply(table, idx, gamma, beta, mask, scale, 1e-12, 0)
+    y.backward(dy)
+    tr, gr, br = (t.detach().clone().requires_grad_() for t in (table, gamma, beta))
+    e = F.embedding(idx, tr, padding_idx=0)
+    if mask is not None:
+        e = e * mask.view(B, L, d) * scale
+    yr = F.layer_norm(e, (d,), gr, br, eps=1e-12)
+    yr.backward(dy)
+    close(y, yr, what="y")
+    close(table.grad, tr.grad, atol=1e-4, rtol=1e-4, what="dtable")
+    assert table.grad[0].abs().max().item() == 0.0
+    assert table.grad[V // 2:].abs().max().item() == 0.0
+    close(gamma.grad, gr.grad, atol=1e-4, rtol=1e-4, what="dgamma")
+    close(beta.grad, br.grad, atol=1e-4, rtol=1e-4, what="dbeta")
+
+
+def test_embedding_bwd_skewed_and_deterministic(cuda):
+    from datamining_recblr_amd import kernels
+
+    V, d, M = 10544, 128, 409600
+    g = torch.Generator(device="cpu").manual_seed(5)
+    # Zipf-like: a few ids take most of the mass
+    w = 1.0 / torch.arange(1, V + 1, dtype=torch.float64) ** 1.1
+    idx = torch.multinomial(w, M, replacement=True, generator=g).to(cuda)
+    grad = torch.randn(M, d, generator=g).to(cuda)
+    dw = kernels.embedding_bwd(idx, grad, V, padding_idx=0)
+    ref = torch.zeros(V, d, dtype=torch.float64, device=cuda).index_add_(0, idx, grad.double())
+    ref[0] = 0
+    close(dw, ref.float(), atol=1e-3, rtol=1e-5, what="dW")
+    assert torch.equal(dw, kernels.embedding_bwd(idx, grad, V, padding_idx=0))
+
+
+@pytest.mark.parametrize("p", [0.0, 0.3])
+def test_silu_dropout(cuda, p):
+    from datamining_recblr_amd.blocks import _SiluDropout
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    a = (3 * torch.randn(37, 512, generator=g)).to(cuda).requires_grad_()
+    du = torch.randn(37, 512, generator=g).to(cuda)
+    mask = (torch.rand(37, 512, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
+    scale = 1.0 / (1.0 - p)
+    u = _SiluDropout.apply(a, mask, scale)
+    u.backward(du)
+    ar = a.detach().clone().requires_grad_()
+    ur = F.silu(ar)
+    if mask is not None:
+        ur = ur * mask * scale
+    ur.backward(du)
+    close(u, ur, what="u")
+    close(a.grad, ar.grad, what="da")
+
+
+def test_train_mode_dropout_statistics(cuda):
+    """Train-mode model: masks are drawn per call (outputs differ run to run),
+    p = 0 in train mode equals eval, and the loss stays finite."""
+    from datamining_recblr_amd.model import RecBLR
+    from datamining_recblr_amd.recbole_compat import SyntheticDataset
+
+    cfg = dict(hidden_size=64, loss_type="CE", num_layers=2, dropout_prob=0.2, expand=2,
+               d_conv=4, bd_lru_only=False, disable_conv1d=False, disable_ffn=False,
+               MAX_ITEM_LIST_LENGTH=50)
+    torch.manual_seed(0)
+    model = RecBLR(cfg, SyntheticDataset(300)).to(cuda)
+    seq = torch.randint(1, 300, (32, 50), device=cuda)
+    lens = torch.randint(1, 51, (32,), device=cuda)
+    model.train()
+    a = model.forward(seq, lens)
+    b = model.forward(seq, lens)
+    assert not torch.equal(a, b)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    c = model.forward(seq, lens)
+    model.eval()
+    close(c, model.forward(seq, lens), what="p=0 train == eval")

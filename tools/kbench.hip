@@ -50,7 +50,7 @@ static float* dalloc(int64_t n, uint32_t seed, float lo = -1.f, float hi = 1.f) 
   return p;
 }
 
-template <int VEC, int Q, int TC>
+template <int VEC, int Q, int TC, bool PF = false>
 void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, float* rg, float* xc,
               float* z, float* lam, float* y, float* car, float* dy, float* drg, float* dxc,
               float* dz, float* part, float* dh0, double N) {
@@ -60,13 +60,13 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, float*
   char* f = (char*)malloc(64);
   snprintf(f, 64, "gate_fwd %s", nm);
   cs.push_back({f, 5 * N * 4, [=] {
-    hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
+    hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
                        xc, H, z, 2 * H, lam, nullptr, y, H, car, (int64_t)B, L, H, ncw);
   }, {}});
   char* f2 = (char*)malloc(64);
   snprintf(f2, 64, "gate_bwd %s", nm);
   cs.push_back({f2, 9 * N * 4, [=] {
-    hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
+    hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
                        xc, H, z, 2 * H, lam, car, dy, drg, 2 * H, dxc, dz, 2 * H, part, dh0,
                        (int64_t)B, L, H, ncw);
   }, {}});
@@ -92,6 +92,55 @@ void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float*
     hipLaunchKernelGGL((k_conv_silu_bwd<K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, x, 2 * H,
                        w, bias, g1, nullptr, dx, 2 * H, dwp, dbp, (int64_t)B, L, H, ncw);
   }, {}});
+}
+
+// pure data movement: 4 reads + 1 write per element, flat float4 grid-stride
+__global__ void flat4to1(const float4* a, const float4* b, const float4* c, const float4* d,
+                         float4* o, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float4 x = a[i], y = b[i], z = c[i], w = d[i];
+    o[i] = make_float4(x.x + y.x + z.x + w.x, x.y + y.y + z.y + w.y, x.z + y.z + z.z + w.z,
+                       x.w + y.w + z.w + w.w);
+  }
+}
+
+// same wave/lane layout and row strides as k_gate_scan_fwd, trivial math
+template <int Q, int TC>
+__global__ void __launch_bounds__(256)
+pattern4to1(const float* rg, int rg_rs, const float* xc, int xc_rs, const float* z, int z_rs,
+            float* y, int y_rs, int64_t B, int L, int H, int ncw) {
+  constexpr int G = 64 / Q, VEC = 4, TILE = Q * TC;
+  const int lane = threadIdx.x & 63, q = lane / G, g = lane - q * G;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = wid / ncw;
+  if (b >= B) return;
+  const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
+  const int64_t row0 = b * L;
+  const float* rgb = rg + row0 * rg_rs + c0;
+  const float* xcb = xc + row0 * xc_rs + c0;
+  const float* zb = z + row0 * z_rs + c0;
+  float* yb = y + row0 * y_rs + c0;
+  const int nT = (L + TILE - 1) / TILE;
+  for (int tile = 0; tile < nT; ++tile) {
+    const int t0 = tile * TILE + q * TC;
+    float r[TC][4], i[TC][4], x[TC][4], zz[TC][4];
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int t = min(t0 + j, L - 1);
+      ldv(r[j], rgb + t * rg_rs);
+      ldv(i[j], rgb + t * rg_rs + H);
+      ldv(x[j], xcb + t * xc_rs);
+      ldv(zz[j], zb + t * z_rs);
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      float o[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) o[v] = r[j][v] + i[j][v] + x[j][v] + zz[j][v];
+      if (t0 + j < L) stv(yb + (t0 + j) * y_rs, o);
+    }
+  }
 }
 
 int main(int argc, char** argv) {
@@ -127,14 +176,14 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   std::vector<Case> cs;
-  add_gate<4, 4, 4>(cs, "v4 q4 tc4", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<2, 4, 4>(cs, "v2 q4 tc4", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<1, 4, 4>(cs, "v1 q4 tc4", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<4, 8, 2>(cs, "v4 q8 tc2", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<2, 8, 2>(cs, "v2 q8 tc2", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<4, 16, 1>(cs, "v4 q16 tc1", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<2, 16, 1>(cs, "v2 q16 tc1", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
-  add_gate<2, 2, 8>(cs, "v2 q2 tc8", B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N);
+#define GATE(V, Q, TC, PF, NM) add_gate<V, Q, TC, PF>(cs, NM, B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N)
+  GATE(4, 4, 4, false, "v4 q4 tc4");
+  GATE(4, 4, 4, true, "v4 q4 tc4 pf");
+  GATE(2, 4, 4, false, "v2 q4 tc4");
+  GATE(2, 4, 4, true, "v2 q4 tc4 pf");
+  GATE(4, 8, 2, false, "v4 q8 tc2");
+  GATE(4, 8, 2, true, "v4 q8 tc2 pf");
+  GATE(2, 2, 8, true, "v2 q2 tc8 pf");
   add_conv<4, 4, 4, 8>(cs, "v4 q4 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
   add_conv<4, 4, 4, 4>(cs, "v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
   add_conv<4, 2, 4, 4>(cs, "v2 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
@@ -146,6 +195,20 @@ int main(int argc, char** argv) {
   }, {}});
   cs.push_back({"scan_rows_bwd [B,H,L]", 5 * N * 4, [=] {
     launch_scan_bwd(sg, so, sx, sd, y, (int64_t)B * H, L, 0);
+  }, {}});
+  cs.push_back({"flat4to1 (4R+1W float4)", 5 * N * 4, [=] {
+    hipLaunchKernelGGL(flat4to1, dim3(4096), dim3(256), 0, 0, (const float4*)rg, (const float4*)(rg + n),
+                       (const float4*)xc, (const float4*)g1, (float4*)y, n / 4);
+  }, {}});
+  cs.push_back({"pattern4to1 q4 tc4", 5 * N * 4, [=] {
+    const int ncw = H / 64;
+    hipLaunchKernelGGL((pattern4to1<4, 4>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0, rg,
+                       2 * H, xc, H, xz + H, 2 * H, y, H, (int64_t)B, L, H, ncw);
+  }, {}});
+  cs.push_back({"pattern4to1 q1 tc16", 5 * N * 4, [=] {
+    const int ncw = H / 256;
+    hipLaunchKernelGGL((pattern4to1<1, 16>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0, rg,
+                       2 * H, xc, H, xz + H, 2 * H, y, H, (int64_t)B, L, H, ncw);
   }, {}});
   cs.push_back({"hipMemcpy d2d (R+W)", 2 * N * 4, [=] {
     CK(hipMemcpyAsync(dxc, xc, n * sizeof(float), hipMemcpyDeviceToDevice, 0));
