@@ -74,6 +74,7 @@ k_emb_chunk_sum(const int* __restrict__ vals, const int* __restrict__ seg,
     if (choff[mid] <= c) lo = mid; else hi = mid;
   }
   const int v = lo;
+  if (v == padding_idx) return;   // its row is zeroed by k_emb_finish
   const int ci = (int)(c - choff[v]);
   const int beg = seg[v] + ci * kChunk;
   const int end = min(seg[v + 1], beg + kChunk);
@@ -106,42 +107,43 @@ k_emb_chunk_sum(const int* __restrict__ vals, const int* __restrict__ seg,
       acc[k] += col < d ? grad[(int64_t)p * d + col] : 0.0f;
     }
   }
-  const bool single = nch[v] == 1;
-  float* out = single ? dw + (int64_t)v * d : partial + c * d;
-  const float keep = (single && v == padding_idx) ? 0.0f : 1.0f;
+  float* out = nch[v] == 1 ? dw + (int64_t)v * d : partial + c * d;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int col = lane + k * kWave;
-    if (col < d) out[col] = acc[k] * keep;
+    if (col < d) out[col] = acc[k];
   }
 }
 
-// One wave per key: keys with no rows get zeros, multi-chunk keys sum partials.
+// One 4-wave block per key: keys with no rows (and the padding id) get zeros;
+// multi-chunk keys sum their partials, wave w taking chunks w, w+4, ... and
+// the four wave sums combined in a fixed order (bitwise reproducible).
 template <int NV>
 __global__ void __launch_bounds__(256)
 k_emb_finish(const int* __restrict__ nch, const int* __restrict__ choff,
              const float* __restrict__ partial, int d, int V, int padding_idx,
              float* __restrict__ dw) {
+  __shared__ float red[4][NV * kWave];
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (v >= V) return;
-  const int n = nch[v];
+  const int wv = threadIdx.x >> 6;
+  const int v = blockIdx.x;
+  const int n = v == padding_idx ? 0 : nch[v];
   if (n == 1) return;   // written by k_emb_chunk_sum
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.0f;
-  for (int c = choff[v]; c < choff[v] + n; ++c)
+  const int c0 = choff[v];
+  for (int c = c0 + wv; c < c0 + n; c += 4)
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int col = lane + k * kWave;
       acc[k] += col < d ? partial[(int64_t)c * d + col] : 0.0f;
     }
-  const float keep = (v == padding_idx) ? 0.0f : 1.0f;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int col = lane + k * kWave;
-    if (col < d) dw[v * d + col] = acc[k] * keep;
-  }
+  for (int k = 0; k < NV; ++k) red[wv][lane + k * kWave] = acc[k];
+  __syncthreads();
+  for (int col = threadIdx.x; col < d; col += blockDim.x)
+    dw[(int64_t)v * d + col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
 }
 
 int key_bits(int64_t V) {
@@ -194,7 +196,7 @@ int emb_sums(const EmbWs& w, char* ws, const float* grad, int64_t M, int64_t d, 
   hipLaunchKernelGGL((k_emb_chunk_sum<NV>), dim3((unsigned)((max_chunks + 3) / 4)), dim3(256), 0,
                      st, vals, seg, nch, choff, grad, (int)d, (int)V, (int)padding_idx, dw,
                      partial);
-  hipLaunchKernelGGL((k_emb_finish<NV>), dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, nch,
+  hipLaunchKernelGGL((k_emb_finish<NV>), dim3((unsigned)V), dim3(256), 0, st, nch,
                      choff, partial, (int)d, (int)V, (int)padding_idx, dw);
   return launch_status("rb_embedding_bwd");
 }

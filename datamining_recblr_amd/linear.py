@@ -1,0 +1,65 @@
+"""Projection GEMMs with split-K weight gradients.
+
+Every projection of the encoder is tall and skinny: X [B*L, K] @ W^T with
+B*L = 409,600 rows at the benchmark shape and K, N in {128, 256, 512}.  The
+forward and dX GEMMs have plenty of output tiles, but the weight gradient
+dW = dY^T X [N, K] has only a few dozen tiles and a 409,600-long reduction, on
+which the BLAS picks un-split kernels running at ~46 TFLOP/s (MI355X fp32
+MFMA peak 157).  Splitting the reduction into S row blocks as one batched GEMM
+([S, N, M/S] x [S, M/S, K], ~1000 tiles) and summing the S partials in a fixed
+order runs 2-4.5x faster (tools/gemm_probe.py) and is deterministic.
+
+All GEMMs run on hipBLASLt/rocBLAS MFMA kernels through torch; the math is
+exactly nn.Linear's (RecBLR.py:162,165,167,213,214).
+"""
+from __future__ import annotations
+
+import torch
+
+__all__ = ["linear", "wgrad", "LinearFn"]
+
+SPLIT_K = 64
+MIN_ROWS_FOR_SPLIT = 16384
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.Tensor:
+    """dW = dy2^T @ x2 for dy2 [M, N], x2 [M, K] (row-strided views allowed)."""
+    M = dy2.shape[0]
+    if M < MIN_ROWS_FOR_SPLIT or splits <= 1:
+        return dy2.t() @ x2
+    mk = M // splits
+    main = mk * splits
+    a = dy2[:main].unflatten(0, (splits, mk)).transpose(1, 2)
+    b = x2[:main].unflatten(0, (splits, mk))
+    out = torch.bmm(a, b).sum(0)
+    if main < M:
+        out += dy2[main:].t() @ x2[main:]
+    return out
+
+
+class LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.addmm(bias, x2, weight.t()) if bias is not None else x2 @ weight.t()
+        ctx.save_for_backward(x2, weight)
+        ctx.has_bias = bias is not None
+        return y.view(*x.shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = wgrad(dy2, x2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy2.sum(0)
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, module: torch.nn.Linear) -> torch.Tensor:
+    """module(x) with the split-K weight gradient."""
+    return LinearFn.apply(x, module.weight, module.bias)

@@ -8,10 +8,15 @@ checkpoints and ``state_dict``s move between the two unchanged.  Modules are
 created in the reference's order, so under the same seed the initial weights
 are identical too.
 
-What differs is ``GatedRecurrentLayer.forward``: the reference's ~25-kernel
-chain (pad copy, transposes, conv, a dozen elementwise gate ops, Triton scan,
-truncate, merge) is replaced by two fused HIP kernels around the gates GEMM
-(see ``recurrence.py``).  It needs a ROCm GPU; there is no CPU fallback.
+What differs is the execution:
+* ``GatedRecurrentLayer.forward``: the reference's ~25-kernel chain (pad copy,
+  transposes, conv, a dozen elementwise gate ops, Triton scan, truncate,
+  merge) is two fused HIP kernels around the gates GEMM (``recurrence.py``);
+* embedding -> dropout -> LayerNorm, dropout + residual + LayerNorm and the
+  FFN's SiLU + dropout are fused HIP kernels (``blocks.py``), with a
+  deterministic sort-based embedding backward;
+* projections are MFMA GEMMs with split-K weight gradients (``linear.py``).
+Everything needs a ROCm GPU; there is no CPU fallback.
 """
 from __future__ import annotations
 
@@ -23,6 +28,7 @@ from torch import nn
 
 from ._lib import RecBLRNativeError
 from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, silu_dropout
+from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len
 
@@ -69,10 +75,10 @@ class GatedRecurrentLayer(nn.Module):
             raise RecBLRNativeError(
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
                 "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
-        xz = self.input(x)
+        xz = linear(x, self.input)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d)
-        return self.output(y)
+        return linear(y, self.output)
 
     @staticmethod
     def pad_len(seq_len: int) -> int:
@@ -90,9 +96,9 @@ class FeedForward(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
 
     def forward(self, input_tensor):
-        h = silu_dropout(self.w_1(input_tensor), self.dropout, self.training)
-        return add_dropout_layer_norm(self.w_2(h), input_tensor, self.dropout, self.layer_norm,
-                                      self.training)
+        h = silu_dropout(linear(input_tensor, self.w_1), self.dropout, self.training)
+        return add_dropout_layer_norm(linear(h, self.w_2), input_tensor, self.dropout,
+                                      self.layer_norm, self.training)
 
 
 class RecurrentLayer(nn.Module):

@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from . import kernels
+from .linear import wgrad
 
 __all__ = ["pow2_pad_len", "pad_prefix_state", "BDLRUCore", "bd_lru"]
 
@@ -87,7 +88,7 @@ class BDLRUCore(torch.autograd.Function):
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
             rg, xc, z, lam, carries, dy, dxz[..., H:])
         drg2 = drg.view(B * L, H2)
-        dgate_w = drg2.t() @ xc.reshape(B * L, H)
+        dgate_w = wgrad(drg2, xc.reshape(B * L, H))
         dxc.view(B * L, H).addmm_(drg2, gate_w)      # + dL/dxc through the gates GEMM
         dconv_w = dconv_b = None
         if ctx.use_conv:

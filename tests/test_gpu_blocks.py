@@ -135,3 +135,26 @@ def test_train_mode_dropout_statistics(cuda):
     c = model.forward(seq, lens)
     model.eval()
     close(c, model.forward(seq, lens), what="p=0 train == eval")
+
+
+@pytest.mark.parametrize("M", [1000, 409600, 409637])
+def test_split_k_weight_gradient(cuda, M):
+    """linear.LinearFn: forward == F.linear, split-K dW (incl. a ragged tail) ==
+    the plain GEMM within fp32 re-association error."""
+    from datamining_recblr_amd.linear import LinearFn, wgrad
+
+    g = torch.Generator(device="cpu").manual_seed(M)
+    x = torch.randn(M, 128, generator=g).to(cuda).requires_grad_()
+    w = (0.05 * torch.randn(256, 128, generator=g)).to(cuda).requires_grad_()
+    b = torch.randn(256, generator=g).to(cuda).requires_grad_()
+    dy = torch.randn(M, 256, generator=g).to(cuda)
+    y = LinearFn.apply(x, w, b)
+    y.backward(dy)
+    xr, wr, br = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    F.linear(xr, wr, br).backward(dy)
+    close(y, F.linear(xr, wr, br), atol=1e-4, what="y")
+    close(x.grad, xr.grad, atol=1e-4, what="dx")
+    ref = (dy.double().t() @ x.detach().double()).float()
+    close(w.grad, ref, atol=1e-3, rtol=1e-5, what="dW")
+    close(b.grad, br.grad, atol=1e-3, rtol=1e-5, what="db")
+    assert torch.equal(wgrad(dy, x.detach()), wgrad(dy, x.detach()))
