@@ -33,6 +33,7 @@ from datamining_recblr_amd.recbole_compat import SyntheticDataset  # noqa: E402
 
 METRIC = "sequences/sec fwd+bwd at B=2048 L=200 d=128; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP32_MFMA_PEAK_TFS = 157.3     # MI355X dense fp32 MFMA spec (MI355X_MICROARCH.md)
 DOMINANT = "rb_gate_scan_bwd"  # the HIP kernel moving the most bytes per step
 
 
@@ -72,6 +73,31 @@ def cpu_baseline(args, state_dict):
                        f"{args.cpu_sample} of the {args.batch} sequences, L={args.seq_len}, "
                        f"d={args.hidden}, n_items={args.n_items}, dropout off; median of 3 "
                        f"after 1 warm-up; {med:.2f} s/step on {threads} threads")}
+
+
+def scan_microbench(args, dev, reps=20):
+    """BASELINE configs[1]: forward-only parallel_scan at B=2048, C=H=256,
+    T=L=200 on the reference layout [B, C, T] (the reference pads T to 256;
+    rb_scan_fwd does not need to).  Algorithmic bytes 3*N*4 (R gates, tokens;
+    W states)."""
+    B, C, T = args.batch, 2 * args.hidden, args.seq_len
+    g = torch.rand(B, C, T, device=dev) * 0.1 + 0.9
+    x = torch.randn(B, C, T, device=dev)
+    kernels.scan_fwd(g, x)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        kernels.scan_fwd(g, x)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    ms = sorted(ts)[len(ts) // 2]
+    gbs = 3 * g.numel() * 4 / (ms * 1e-3) / 1e9
+    return {"shape_BCT": [B, C, T], "us": round(ms * 1e3, 1), "achieved_gbs": round(gbs, 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "sequences_per_sec": round(B / (ms * 1e-3), 1)}
 
 
 def main():
@@ -135,8 +161,19 @@ def main():
 
     roofline = None
     kernels_report = None
+    gemm = None
     if timer is not None:
         summ = timer.summary()
+        g = summ.pop("gemm", None)
+        if g is not None:
+            tf = g["bytes"] / (g["ms"] * 1e-3) / 1e12
+            gemm = {"bound": "mfma", "dtype": "f32", "achieved": round(tf, 1),
+                    "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": round(tf / FP32_MFMA_PEAK_TFS, 4),
+                    "ms_per_step": round(g["ms"] / args.steps, 3),
+                    "gemms_per_step": g["launches"] / args.steps,
+                    "flops_per_step": int(g["bytes"] / args.steps),
+                    "library": "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)"}
         kernels_report = {}
         for name, d in summ.items():
             gbs = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
@@ -160,6 +197,7 @@ def main():
             "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
             "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    scan = scan_microbench(args, dev) if env.rank == 0 else None
     cpu = None
     if env.rank == 0 and env.world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, model.state_dict())
@@ -179,7 +217,9 @@ def main():
                        "num_layers": args.layers, "n_items": args.n_items,
                        "dropout": args.dropout, "parallelism": f"dp{env.world_size}"},
             "roofline": roofline,
+            "gemm": gemm,
             "kernels": kernels_report,
+            "scan_fwd_only": scan,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -63,9 +63,11 @@ def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float = 32.0) -> nn.
         return step
     dev = next(model.parameters()).device
     kw = dict(device_ids=[dev.index]) if dev.type == "cuda" else {}
+    # ablation flags (RecBLR.py:28-35) leave the conv / FFN parameters unused
+    unused = bool(getattr(model, "disable_conv1d", False) or getattr(model, "disable_ffn", False))
     return nn.parallel.DistributedDataParallel(
         step, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
-        broadcast_buffers=False, **kw)
+        broadcast_buffers=False, find_unused_parameters=unused, **kw)
 
 
 def synthetic_interaction(batch: int, seq_len: int, n_items: int, device, seed: int,

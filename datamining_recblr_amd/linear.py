@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import torch
 
+from . import kernels
+
 __all__ = ["linear", "wgrad", "LinearFn"]
 
 SPLIT_K = 64
@@ -37,11 +39,29 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.T
     return out
 
 
+def _timed(kind, flops, fn, *args):
+    """Run a GEMM, bracketed by HIP events when bench.py's kernel timer is on."""
+    t = kernels._timer
+    if t is None:
+        return fn(*args)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    out = fn(*args)
+    e1.record()
+    t.records.append((kind, flops, e0, e1))
+    return out
+
+
 class LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias):
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(bias, x2, weight.t()) if bias is not None else x2 @ weight.t()
+        flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
+        if bias is not None:
+            y = _timed("gemm", flops, torch.addmm, bias, x2, weight.t())
+        else:
+            y = _timed("gemm", flops, torch.mm, x2, weight.t())
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         return y.view(*x.shape[:-1], weight.shape[0])
@@ -50,11 +70,12 @@ class LinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, weight = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
+        flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = (dy2 @ weight).view(*dy.shape[:-1], weight.shape[1])
+            dx = _timed("gemm", flops, torch.mm, dy2, weight).view(*dy.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = wgrad(dy2, x2)
+            dw = _timed("gemm", flops, wgrad, dy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy2.sum(0)
         return dx, dw, db

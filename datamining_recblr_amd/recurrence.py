@@ -28,7 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from . import kernels
-from .linear import wgrad
+from .linear import _timed, wgrad
 
 __all__ = ["pow2_pad_len", "pad_prefix_state", "BDLRUCore", "bd_lru"]
 
@@ -66,7 +66,9 @@ class BDLRUCore(torch.autograd.Function):
             xc = kernels.conv_silu_fwd(x, conv_w, conv_b)
         else:
             xc = x
-        rg = torch.addmm(gate_b, xc.reshape(B * L, H), gate_w.t()).view(B, L, H2)
+        gflops = 2 * B * L * H * H2
+        rg = _timed("gemm", gflops, torch.addmm, gate_b, xc.reshape(B * L, H),
+                    gate_w.t()).view(B, L, H2)
         train = any(ctx.needs_input_grad)
         y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train)
         ctx.use_conv = use_conv
@@ -88,8 +90,10 @@ class BDLRUCore(torch.autograd.Function):
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
             rg, xc, z, lam, carries, dy, dxz[..., H:])
         drg2 = drg.view(B * L, H2)
-        dgate_w = wgrad(drg2, xc.reshape(B * L, H))
-        dxc.view(B * L, H).addmm_(drg2, gate_w)      # + dL/dxc through the gates GEMM
+        gflops = 2 * B * L * H * H2
+        dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(B * L, H))
+        # + dL/dxc through the gates GEMM, accumulated in place (beta = 1)
+        _timed("gemm", gflops, dxc.view(B * L, H).addmm_, drg2, gate_w)
         dconv_w = dconv_b = None
         if ctx.use_conv:
             dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, None, dxz[..., :H])
