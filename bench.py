@@ -15,6 +15,7 @@ oracle baseline (rank 0, N=1 only).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -73,6 +74,23 @@ def cpu_baseline(args, state_dict):
                        f"{args.cpu_sample} of the {args.batch} sequences, L={args.seq_len}, "
                        f"d={args.hidden}, n_items={args.n_items}, dropout off; median of 3 "
                        f"after 1 warm-up; {med:.2f} s/step on {threads} threads")}
+
+
+def pmc_traffic(args, kernel_prefix):
+    """HBM bytes per launch of `kernel_prefix` from the newest committed PMC
+    summary (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE and
+    WRITE_SIZE passes of this bench at its default shape, gfx950 read
+    correction applied).  None unless this run is that default shape."""
+    if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    data = json.load(open(files[-1]))
+    for name, k in data.get("kernels", {}).items():
+        if name.startswith(kernel_prefix) and k.get("traffic_bytes"):
+            return int(k["traffic_bytes"]), os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def scan_microbench(args, dev, reps=20):
@@ -185,9 +203,10 @@ def main():
         if DOMINANT in summ:
             d = summ[DOMINANT]
             ach = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
+            traffic, src = pmc_traffic(args, "k_gate_scan_bwd")
             roofline = {"kernel": DOMINANT, "bound": "hbm", "achieved": round(ach, 1),
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                        "traffic": None,
+                        "traffic": traffic, "traffic_source": src,
                         "algo_bytes_per_launch": int(d["avg_bytes"]),
                         "avg_launch_us": round(d["avg_ms"] * 1e3, 2)}
         tot_b = sum(d["bytes"] for d in summ.values())
