@@ -17,11 +17,12 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
 _f32 = ctypes.c_float
+_u64 = ctypes.c_uint64
 
 # name -> (restype, argtypes); kept in the order of include/recblr_hip.h
 SIGNATURES = {
@@ -37,13 +38,15 @@ SIGNATURES = {
                                         _i64, _i64, _i64, _fp]),
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _i64,
                                         _fp, _fp, _i64, _fp, _fp, _i64, _i64, _i64, _fp]),
-    "rb_add_ln_fwd": (ctypes.c_int, [_fp, _fp, _i64, _fp, _f32, _fp, _fp, _fp, _f32, _fp, _fp, _fp,
-                                     _fp, _i64, _i64, _fp]),
-    "rb_add_ln_num_parts": (ctypes.c_int64, [_i64, _i64]),
-    "rb_add_ln_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _f32, _fp, _fp, _fp, _fp, _i64,
-                                     _i64, _i64, _fp]),
-    "rb_silu_dropout_fwd": (ctypes.c_int, [_fp, _fp, _f32, _fp, _i64, _fp]),
-    "rb_silu_dropout_bwd": (ctypes.c_int, [_fp, _fp, _f32, _fp, _fp, _i64, _fp]),
+    "rb_add_ln_fwd": (ctypes.c_int, [_fp, _fp, _i64, _fp, _u64, _f32, _fp, _fp, _fp, _f32, _fp,
+                                     _fp, _fp, _fp, _i64, _i64, _fp]),
+    "rb_row_num_parts": (ctypes.c_int64, [_i64, _i64]),
+    "rb_add_ln_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _u64, _f32, _fp, _fp, _fp, _fp,
+                                     _fp, _i64, _i64, _i64, _fp]),
+    "rb_silu_dropout_fwd": (ctypes.c_int, [_fp, _fp, _u64, _f32, _fp, _i64, _i64, _fp]),
+    "rb_silu_dropout_bwd": (ctypes.c_int, [_fp, _fp, _u64, _f32, _fp, _fp, _fp, _i64, _i64, _i64,
+                                           _fp]),
+    "rb_dropout_mask": (ctypes.c_int, [_u64, _f32, _fp, _i64, _fp]),
     "rb_embedding_bwd_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
     "rb_embedding_bwd": (ctypes.c_int, [_fp, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp]),
 }

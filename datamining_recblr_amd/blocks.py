@@ -1,11 +1,19 @@
-"""Fused HIP blocks around the BD-LRU: embedding gather + dropout + LayerNorm,
-dropout + residual + LayerNorm, and the FFN's SiLU + dropout.
+"""Fused HIP blocks around the BD-LRU.
 
 Reference spans: RecBLR.py:76-78 (embedding -> dropout -> LayerNorm), :142
-(LayerNorm(dropout(GRL(x)) + x)), :219-225 (FeedForward).  Dropout masks are
-drawn with torch's generator (``bernoulli_``), so ``torch.manual_seed`` keeps
-training reproducible; in eval mode or at p = 0 there is no mask at all.
-LayerNorm widths outside ``kernels.LN_SIZES`` use torch's own (GPU) ops.
+(LayerNorm(dropout(GRL(x)) + x)), :210-227 (FeedForward).
+
+Dropout keep-flags are a Philox4x32-10 stream inside the kernels, keyed by a
+64-bit seed drawn from torch's default (CPU) generator for every dropout site
+and call — so ``torch.manual_seed`` makes training reproducible and no mask
+tensor is ever written; the backward regenerates the same flags.  In eval mode
+or at p = 0 there is no dropout.  Row widths outside ``kernels.ROW_SIZES`` use
+torch's own GPU ops.
+
+The FeedForward block is one autograd function: w_1 GEMM -> SiLU+dropout ->
+w_2 GEMM -> dropout+residual+LayerNorm.  Its backward takes both bias
+gradients from column partials of the row kernels (no separate reduction
+passes) and adds the residual gradient inside the dX GEMM (beta = 1).
 """
 from __future__ import annotations
 
@@ -14,18 +22,20 @@ import torch.nn.functional as F
 
 from . import kernels
 from ._lib import RecBLRNativeError
+from .linear import _timed, linear, wgrad
 
-__all__ = ["dropout_mask", "add_dropout_layer_norm", "embed_dropout_layer_norm",
-           "silu_dropout"]
+__all__ = ["draw_seed", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
+           "feed_forward"]
 
 
-def dropout_mask(shape, p: float, training: bool, device):
-    """uint8 keep-mask ~ Bernoulli(1 - p) and the 1/(1-p) scale (None, 1 if off)."""
-    if not training or p == 0.0:
-        return None, 1.0
-    if p >= 1.0:
-        return torch.zeros(shape, dtype=torch.uint8, device=device), 0.0
-    return torch.empty(shape, dtype=torch.uint8, device=device).bernoulli_(1.0 - p), 1.0 / (1.0 - p)
+def draw_seed() -> int:
+    """63-bit dropout seed from torch's default generator (host side, no sync)."""
+    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+
+
+def _drop(dropout: torch.nn.Dropout, training: bool):
+    p = float(dropout.p) if training else 0.0
+    return p, (draw_seed() if p > 0.0 else 0)
 
 
 def _require_gpu(t):
@@ -36,13 +46,13 @@ def _require_gpu(t):
 
 class _AddDropoutLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, r, gamma, beta, mask, scale, eps):
+    def forward(ctx, a, r, gamma, beta, mask, seed, p, eps):
         d = a.shape[-1]
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a.reshape(-1, d).contiguous(),
-                                              r.reshape(-1, d).contiguous(), mask, scale,
-                                              gamma, beta, eps, save=save)
-        ctx.scale = scale
+                                              r.reshape(-1, d).contiguous(), gamma, beta, eps,
+                                              mask=mask, seed=seed, p=p, save=save)
+        ctx.seed, ctx.p = seed, p
         ctx.save_for_backward(s, mean, rstd, gamma, mask)
         return y.view(a.shape)
 
@@ -50,75 +60,127 @@ class _AddDropoutLN(torch.autograd.Function):
     def backward(ctx, dy):
         s, mean, rstd, gamma, mask = ctx.saved_tensors
         need_a, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
-        ds, da, dg, db = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask, ctx.scale,
-                                            want_ds=need_r, want_da=need_a or not need_r)
+        ds, da, dg, db, _ = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask=mask,
+                                               seed=ctx.seed, p=ctx.p, want_ds=need_r,
+                                               want_da=need_a or not need_r)
         shape = dy.shape
         return (da.view(shape) if need_a else None, ds.view(shape) if need_r else None,
-                dg, db, None, None, None)
+                dg, db, None, None, None, None)
 
 
 class _EmbedDropoutLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, table, idx, gamma, beta, mask, scale, eps, padding_idx):
+    def forward(ctx, table, idx, gamma, beta, mask, seed, p, eps, padding_idx):
         save = any(ctx.needs_input_grad)
         flat = idx.reshape(-1).contiguous()
-        y, s, mean, rstd = kernels.add_ln_fwd(table, None, mask, scale, gamma, beta, eps,
-                                              idx=flat, save=save)
-        ctx.scale, ctx.padding_idx, ctx.num_rows = scale, padding_idx, table.shape[0]
+        y, s, mean, rstd = kernels.add_ln_fwd(table, None, gamma, beta, eps, mask=mask,
+                                              seed=seed, p=p, idx=flat, save=save)
+        ctx.seed, ctx.p = seed, p
+        ctx.padding_idx, ctx.num_rows = padding_idx, table.shape[0]
         ctx.save_for_backward(s, mean, rstd, gamma, mask, flat)
         return y.view(*idx.shape, table.shape[1])
 
     @staticmethod
     def backward(ctx, dy):
         s, mean, rstd, gamma, mask, flat = ctx.saved_tensors
-        _, da, dg, db = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask, ctx.scale,
-                                           want_ds=False, want_da=True)
+        _, da, dg, db, _ = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask=mask,
+                                              seed=ctx.seed, p=ctx.p, want_ds=False,
+                                              want_da=True)
         dtable = (kernels.embedding_bwd(flat, da, ctx.num_rows, ctx.padding_idx)
                   if ctx.needs_input_grad[0] else None)
-        return dtable, None, dg, db, None, None, None, None
+        return dtable, None, dg, db, None, None, None, None, None
 
 
 class _SiluDropout(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, mask, scale):
+    def forward(ctx, a, mask, seed, p):
         a = a.contiguous()
-        ctx.scale = scale
+        ctx.seed, ctx.p = seed, p
         ctx.save_for_backward(a, mask)
-        return kernels.silu_dropout_fwd(a, mask, scale)
+        return kernels.silu_dropout_fwd(a, mask=mask, seed=seed, p=p)
 
     @staticmethod
     def backward(ctx, du):
         a, mask = ctx.saved_tensors
-        return kernels.silu_dropout_bwd(a, mask, ctx.scale, du), None, None
+        da, _ = kernels.silu_dropout_bwd(a, du, mask=mask, seed=ctx.seed, p=ctx.p)
+        return da, None, None, None
+
+
+class _FeedForward(torch.autograd.Function):
+    """LN(dropout(W2 dropout(silu(W1 x + b1)) + b2) + x), RecBLR.py:218-227."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, seed1, seed2, p, eps):
+        d = x.shape[-1]
+        x2 = x.reshape(-1, d)
+        M, inner = x2.shape[0], w1.shape[0]
+        f = 2 * M * d * inner
+        a1 = _timed("gemm", f, torch.addmm, b1, x2, w1.t())
+        u = kernels.silu_dropout_fwd(a1, seed=seed1, p=p)
+        a2 = _timed("gemm", f, torch.addmm, b2, u, w2.t())
+        save = any(ctx.needs_input_grad)
+        y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
+                                              p=p, save=save)
+        ctx.seed1, ctx.seed2, ctx.p = seed1, seed2, p
+        ctx.save_for_backward(x2, a1, u, s, mean, rstd, w1, w2, gamma)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, a1, u, s, mean, rstd, w1, w2, gamma = ctx.saved_tensors
+        M, d = x2.shape
+        f = 2 * M * d * w1.shape[0]
+        ds, da2, dgamma, dbeta, db2 = kernels.add_ln_bwd(
+            dy, s, gamma, mean, rstd, seed=ctx.seed2, p=ctx.p, want_ds=True, want_da=True,
+            want_dbias=True)
+        du = _timed("gemm", f, torch.mm, da2, w2)
+        dw2 = _timed("gemm", f, wgrad, da2, u)
+        da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True)
+        dx = _timed("gemm", f, torch.addmm, ds, da1, w1)   # residual grad + W1^T path
+        dw1 = _timed("gemm", f, wgrad, da1, x2)
+        return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None)
 
 
 def add_dropout_layer_norm(a, residual, dropout: torch.nn.Dropout, ln: torch.nn.LayerNorm,
                            training: bool):
-    """ln(dropout(a) + residual) — RecBLR.py:142 and :224-225."""
+    """ln(dropout(a) + residual) — RecBLR.py:142."""
     _require_gpu(a)
-    d = a.shape[-1]
-    if d not in kernels.LN_SIZES or a.numel() % 4:
+    if a.shape[-1] not in kernels.ROW_SIZES:
         return ln(dropout(a) + residual)
-    mask, scale = dropout_mask((a.numel() // d, d), dropout.p, training, a.device)
-    return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, mask, scale, ln.eps)
+    p, seed = _drop(dropout, training)
+    return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, None, seed, p, ln.eps)
 
 
 def embed_dropout_layer_norm(idx, emb: torch.nn.Embedding, dropout: torch.nn.Dropout,
                              ln: torch.nn.LayerNorm, training: bool):
     """ln(dropout(emb(idx))) — RecBLR.py:76-78."""
     _require_gpu(emb.weight)
-    d = emb.weight.shape[1]
-    if d not in kernels.LN_SIZES:
+    if emb.weight.shape[1] not in kernels.ROW_SIZES:
         return ln(dropout(emb(idx)))
-    mask, scale = dropout_mask((idx.numel(), d), dropout.p, training, idx.device)
-    return _EmbedDropoutLN.apply(emb.weight, idx, ln.weight, ln.bias, mask, scale, ln.eps,
+    p, seed = _drop(dropout, training)
+    return _EmbedDropoutLN.apply(emb.weight, idx, ln.weight, ln.bias, None, seed, p, ln.eps,
                                  emb.padding_idx)
 
 
 def silu_dropout(a, dropout: torch.nn.Dropout, training: bool):
     """dropout(silu(a)) — RecBLR.py:220-221."""
     _require_gpu(a)
-    if a.numel() % 4:
+    if a.shape[-1] not in kernels.ROW_SIZES:
         return dropout(F.silu(a))
-    mask, scale = dropout_mask(a.shape, dropout.p, training, a.device)
-    return _SiluDropout.apply(a, mask, scale)
+    p, seed = _drop(dropout, training)
+    return _SiluDropout.apply(a, None, seed, p)
+
+
+def feed_forward(x, ffn, training: bool):
+    """The whole FeedForward block (RecBLR.py:218-227) as one fused function."""
+    _require_gpu(x)
+    d, inner = x.shape[-1], ffn.w_1.weight.shape[0]
+    if d not in kernels.ROW_SIZES or inner not in kernels.ROW_SIZES:
+        h = silu_dropout(linear(x, ffn.w_1), ffn.dropout, training)
+        return add_dropout_layer_norm(linear(h, ffn.w_2), x, ffn.dropout, ffn.layer_norm,
+                                      training)
+    p, seed1 = _drop(ffn.dropout, training)
+    seed2 = draw_seed() if p > 0.0 else 0
+    return _FeedForward.apply(x, ffn.w_1.weight, ffn.w_1.bias, ffn.w_2.weight, ffn.w_2.bias,
+                              ffn.layer_norm.weight, ffn.layer_norm.bias, seed1, seed2, p,
+                              ffn.layer_norm.eps)

@@ -38,13 +38,25 @@ int64_t max4(int64_t a, int64_t b, int64_t c = 0, int64_t d = 0) {
 }
 
 }  // namespace
+
+DropSpec make_drop(const uint8_t* mask, uint64_t seed, float p) {
+  DropSpec d{};
+  d.mask = mask;
+  d.scale = p > 0.0f ? 1.0f / (1.0f - p) : 1.0f;
+  d.key0 = (uint32_t)seed;
+  d.key1 = (uint32_t)(seed >> 32);
+  const double keep = 1.0 - (double)p;
+  d.keep_thresh = keep >= 1.0 ? 0xFFFFFFFFu : (uint32_t)(keep * 4294967296.0);
+  d.mode = mask ? 1 : (p > 0.0f ? 2 : 0);
+  return d;
+}
 }  // namespace rb
 
 using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 3; }
+int rb_version(void) { return 4; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -121,53 +133,72 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
 }
 
 int rb_add_ln_fwd(const float* a, const int64_t* idx, int64_t n_idx_rows, const uint8_t* mask,
-                  float scale, const float* r, const float* gamma, const float* beta, float eps,
-                  float* y, float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,
-                  void* stream) {
+                  uint64_t seed, float p, const float* r, const float* gamma, const float* beta,
+                  float eps, float* y, float* s_out, float* mean, float* rstd, int64_t rows,
+                  int64_t d, void* stream) {
   if (!a || !gamma || !beta || !y) return fail("rb_add_ln_fwd: null pointer");
   if (rows <= 0 || d <= 0) return fail("rb_add_ln_fwd: rows and d must be positive");
   if (idx && n_idx_rows <= 0) return fail("rb_add_ln_fwd: empty gather table");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_add_ln_fwd: dropout p must be in [0, 1)");
   if ((s_out == nullptr) != (mean == nullptr) || (mean == nullptr) != (rstd == nullptr))
     return fail("rb_add_ln_fwd: s_out, mean and rstd must be given together");
-  return launch_add_ln_fwd(a, idx, n_idx_rows, mask, scale, r, gamma, beta, eps, y, s_out, mean,
-                           rstd, rows, d, reinterpret_cast<hipStream_t>(stream));
+  return launch_add_ln_fwd(a, idx, n_idx_rows, make_drop(mask, seed, p), r, gamma, beta, eps, y,
+                           s_out, mean, rstd, rows, d, reinterpret_cast<hipStream_t>(stream));
 }
 
-int64_t rb_add_ln_num_parts(int64_t rows, int64_t d) {
-  (void)d;
-  return ln_num_parts(rows);
+int64_t rb_row_num_parts(int64_t rows, int64_t width) {
+  if (rows <= 0 || width <= 0) return 0;
+  return ln_num_parts(rows, width);
 }
 
 int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
-                  const float* rstd, const uint8_t* mask, float scale, float* ds, float* da,
-                  float* dgamma_part, float* dbeta_part, int64_t n_parts, int64_t rows,
-                  int64_t d, void* stream) {
+                  const float* rstd, const uint8_t* mask, uint64_t seed, float p, float* ds,
+                  float* da, float* dgamma_part, float* dbeta_part, float* dbias_part,
+                  int64_t n_parts, int64_t rows, int64_t d, void* stream) {
   if (!dy || !s || !gamma || !mean || !rstd || !dgamma_part || !dbeta_part)
     return fail("rb_add_ln_bwd: null pointer");
-  if (!ds && !da) return fail("rb_add_ln_bwd: nothing to write (ds and da both NULL)");
+  if (!ds && !da && !dbias_part) return fail("rb_add_ln_bwd: nothing to write");
   if (rows <= 0 || d <= 0) return fail("rb_add_ln_bwd: rows and d must be positive");
-  if (n_parts != ln_num_parts(rows)) return fail("rb_add_ln_bwd: n_parts != rb_add_ln_num_parts");
-  return launch_add_ln_bwd(dy, s, gamma, mean, rstd, mask, scale, ds, da, dgamma_part,
-                           dbeta_part, n_parts, rows, d, reinterpret_cast<hipStream_t>(stream));
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_add_ln_bwd: dropout p must be in [0, 1)");
+  if (n_parts != ln_num_parts(rows, d)) return fail("rb_add_ln_bwd: n_parts != rb_row_num_parts");
+  return launch_add_ln_bwd(dy, s, gamma, mean, rstd, make_drop(mask, seed, p), ds, da,
+                           dgamma_part, dbeta_part, dbias_part, n_parts, rows, d,
+                           reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale, float* u, int64_t n,
-                        void* stream) {
+int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, uint64_t seed, float p, float* u,
+                        int64_t rows, int64_t cols, void* stream) {
   if (!a || !u) return fail("rb_silu_dropout_fwd: null pointer");
-  if (n <= 0 || n % 4) return fail("rb_silu_dropout_fwd: n must be a positive multiple of 4");
+  if (rows <= 0 || cols <= 0) return fail("rb_silu_dropout_fwd: rows and cols must be positive");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_silu_dropout_fwd: dropout p must be in [0, 1)");
   if (!aligned16(a) || !aligned16(u) || (mask && (reinterpret_cast<uintptr_t>(mask) & 3)))
     return fail("rb_silu_dropout_fwd: misaligned buffer");
-  return launch_silu_dropout_fwd(a, mask, scale, u, n, reinterpret_cast<hipStream_t>(stream));
+  return launch_silu_dropout_fwd(a, make_drop(mask, seed, p), u, rows, cols,
+                                 reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale, const float* du,
-                        float* da, int64_t n, void* stream) {
+int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, uint64_t seed, float p,
+                        const float* du, float* da, float* dbias_part, int64_t n_parts,
+                        int64_t rows, int64_t cols, void* stream) {
   if (!a || !du || !da) return fail("rb_silu_dropout_bwd: null pointer");
-  if (n <= 0 || n % 4) return fail("rb_silu_dropout_bwd: n must be a positive multiple of 4");
+  if (rows <= 0 || cols <= 0) return fail("rb_silu_dropout_bwd: rows and cols must be positive");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_silu_dropout_bwd: dropout p must be in [0, 1)");
   if (!aligned16(a) || !aligned16(du) || !aligned16(da) ||
       (mask && (reinterpret_cast<uintptr_t>(mask) & 3)))
     return fail("rb_silu_dropout_bwd: misaligned buffer");
-  return launch_silu_dropout_bwd(a, mask, scale, du, da, n, reinterpret_cast<hipStream_t>(stream));
+  if (dbias_part && n_parts != ln_num_parts(rows, cols))
+    return fail("rb_silu_dropout_bwd: n_parts != rb_row_num_parts");
+  return launch_silu_dropout_bwd(a, make_drop(mask, seed, p), du, da, dbias_part,
+                                 ln_num_parts(rows, cols), rows, cols,
+                                 reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_dropout_mask(uint64_t seed, float p, uint8_t* out, int64_t n, void* stream) {
+  if (!out) return fail("rb_dropout_mask: null pointer");
+  if (n <= 0 || n % 4) return fail("rb_dropout_mask: n must be a positive multiple of 4");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_dropout_mask: dropout p must be in [0, 1)");
+  return launch_dropout_mask(make_drop(nullptr, seed, p), out, n,
+                             reinterpret_cast<hipStream_t>(stream));
 }
 
 int64_t rb_embedding_bwd_workspace(int64_t M, int64_t V, int64_t d) {

@@ -75,6 +75,51 @@ __device__ __forceinline__ void stv(float* p, const float (&o)[V]) {
   }
 }
 
+// ---- dropout keep-flags ------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11): counter = element index / 4, key =
+// 64-bit seed, 4 uniform u32 per call -> keep flags of 4 consecutive elements.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Dropout of one tensor: no-op, an explicit uint8 keep-mask laid out like the
+// data, or a Philox stream regenerated on demand (forward and backward see
+// the same flags for the same element index).  mode is launch-uniform.
+struct DropSpec {
+  const uint8_t* mask;
+  uint32_t key0, key1, keep_thresh;
+  float scale;
+  int mode;   // 0 none, 1 mask, 2 philox
+
+  // multipliers (0 or scale) for elements e .. e+3, e % 4 == 0
+  __device__ __forceinline__ void get4(int64_t e, float (&m)[4]) const {
+    if (mode == 0) {
+      m[0] = m[1] = m[2] = m[3] = 1.0f;
+    } else if (mode == 1) {
+      const uchar4 t = *reinterpret_cast<const uchar4*>(mask + e);
+      m[0] = t.x * scale; m[1] = t.y * scale; m[2] = t.z * scale; m[3] = t.w * scale;
+    } else {
+      const uint64_t g = (uint64_t)e >> 2;
+      const uint4 r = philox4x32_10(make_uint4((uint32_t)g, (uint32_t)(g >> 32), 0u, 0u), key0,
+                                    key1);
+      m[0] = r.x < keep_thresh ? scale : 0.0f;
+      m[1] = r.y < keep_thresh ? scale : 0.0f;
+      m[2] = r.z < keep_thresh ? scale : 0.0f;
+      m[3] = r.w < keep_thresh ? scale : 0.0f;
+    }
+  }
+};
+
+DropSpec make_drop(const uint8_t* mask, uint64_t seed, float p);
+
 // ---- channel-last wave layout ---------------------------------------------------
 // The [B, L, H] kernels give each wave one batch row b and a span of G*VEC
 // channels.  Lane = q * G + g: g picks VEC consecutive channels (so the G lanes
@@ -98,19 +143,21 @@ int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
                     int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
                     int64_t H, hipStream_t st);
-int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const uint8_t* mask,
-                      float scale, const float* r, const float* gamma, const float* beta,
-                      float eps, float* y, float* s_out, float* mean, float* rstd, int64_t rows,
-                      int64_t d, hipStream_t st);
-int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
-                      const float* rstd, const uint8_t* mask, float scale, float* ds, float* da,
-                      float* dgp, float* dbp, int64_t nparts, int64_t rows, int64_t d,
+int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
+                      const float* r, const float* gamma, const float* beta, float eps, float* y,
+                      float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,
                       hipStream_t st);
-int64_t ln_num_parts(int64_t rows);
-int launch_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale, float* u,
-                            int64_t n, hipStream_t st);
-int launch_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale, const float* du,
-                            float* da, int64_t n, hipStream_t st);
+int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
+                      const float* rstd, const DropSpec& drop, float* ds, float* da, float* dgp,
+                      float* dbp, float* dbiasp, int64_t nparts, int64_t rows, int64_t d,
+                      hipStream_t st);
+int64_t ln_num_parts(int64_t rows, int64_t d);
+int launch_silu_dropout_fwd(const float* a, const DropSpec& drop, float* u, int64_t rows,
+                            int64_t cols, hipStream_t st);
+int launch_silu_dropout_bwd(const float* a, const DropSpec& drop, const float* du, float* da,
+                            float* dbias_part, int64_t nparts, int64_t rows, int64_t cols,
+                            hipStream_t st);
+int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
 int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
                          int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,

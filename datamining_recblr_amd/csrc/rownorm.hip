@@ -1,16 +1,19 @@
-// rownorm.hip — fused "dropout + residual + LayerNorm" row kernels and the
-// FFN's fused SiLU + dropout, for the blocks around the BD-LRU
+// rownorm.hip — fused row kernels around the BD-LRU: dropout + residual +
+// LayerNorm (with an optional embedding gather) and the FFN's SiLU + dropout
 // (reference RecBLR.py:76-78 embedding -> dropout -> LayerNorm,
 // :142 LayerNorm(dropout(GRL(x)) + x), :219-225 FeedForward).
 //
-//   s = A[row] * mask * scale + r[row]      (A[row] = table[idx[row]] if idx)
+//   s = A[row] * keep * scale + r[row]      (A[row] = table[idx[row]] if idx)
 //   y = (s - mean) * rstd * gamma + beta,   rstd = 1 / sqrt(var + eps)
 //
-// torch runs each of these as 3-5 separate kernels with a [rows, d] HBM round
-// trip between each (and its LayerNorm launches one workgroup per 128-float
-// row).  Here one wave handles 64/LPR rows at a time, each row spread over LPR
-// lanes holding NV float4s (LPR * NV * 4 = d); row statistics are reduced
-// with shuffles inside the row's lane group.
+// Rows of D floats are spread over LPR lanes holding NV float4s each
+// (LPR * NV * 4 = D), so one wave covers 64/LPR rows per step; row statistics
+// are shuffle reductions inside the lane group.  Dropout keep-flags come from
+// an explicit uint8 mask or are regenerated from a counter-based Philox
+// stream (common.h), identically in forward and backward.  Column sums that
+// torch would compute with separate reduction kernels (dgamma, dbeta, the
+// bias gradient of the producing GEMM) are per-block partials, summed in a
+// fixed order by the caller.
 #include "common.h"
 
 namespace rb {
@@ -23,17 +26,14 @@ __device__ __forceinline__ float row_sum(float v) {
   return v;
 }
 
-__device__ __forceinline__ void ld_mask4(float (&m)[4], const uint8_t* p) {
-  const uchar4 t = *reinterpret_cast<const uchar4*>(p);
-  m[0] = t.x; m[1] = t.y; m[2] = t.z; m[3] = t.w;
-}
+constexpr int kRowBlocks = 1024;   // 4 waves each; grid-stride over rows
 
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
 k_add_ln_fwd(const float* __restrict__ a, const int64_t* __restrict__ idx, int64_t nidx,
-             const uint8_t* __restrict__ mask, float scale, const float* __restrict__ r,
-             const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
-             float* __restrict__ y, float* __restrict__ s_out, float* __restrict__ mean_out,
+             DropSpec drop, const float* __restrict__ r, const float* __restrict__ gamma,
+             const float* __restrict__ beta, float eps, float* __restrict__ y,
+             float* __restrict__ s_out, float* __restrict__ mean_out,
              float* __restrict__ rstd_out, int64_t rows) {
   constexpr int D = LPR * NV * 4;
   constexpr int RPW = kWave / LPR;   // rows per wave step
@@ -61,12 +61,10 @@ k_add_ln_fwd(const float* __restrict__ a, const int64_t* __restrict__ idx, int64
     for (int k = 0; k < NV; ++k) {
       const int c = (l + k * LPR) * 4;
       ldv(s[k], arow + c);
-      if (mask) {
-        float m[4];
-        ld_mask4(m, mask + rr * D + c);
+      float m[4];
+      drop.get4(rr * D + c, m);
 #pragma unroll
-        for (int v = 0; v < 4; ++v) s[k][v] = s[k][v] * m[v] * scale;
-      }
+      for (int v = 0; v < 4; ++v) s[k][v] = s[k][v] * m[v];
       if (r) {
         float t[4];
         ldv(t, r + rr * D + c);
@@ -107,30 +105,31 @@ k_add_ln_fwd(const float* __restrict__ a, const int64_t* __restrict__ idx, int64
 
 // Backward of k_add_ln_fwd given the saved s, mean, rstd:
 //   xh = (s - mean) rstd, g = dy * gamma,
-//   ds = rstd (g - mean(g) - xh mean(g xh)),  da = ds * mask * scale,
-//   dgamma += dy * xh, dbeta += dy (per-block partial sums, deterministic).
+//   ds = rstd (g - mean(g) - xh mean(g xh)),  da = ds * keep * scale,
+// partial column sums per block: dgamma += dy xh, dbeta += dy and, if asked,
+// dbias += da (the bias gradient of the GEMM that produced a).
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
 k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
              const float* __restrict__ gamma, const float* __restrict__ mean,
-             const float* __restrict__ rstd, const uint8_t* __restrict__ mask, float scale,
-             float* __restrict__ ds_out, float* __restrict__ da_out,
-             float* __restrict__ dgamma_part, float* __restrict__ dbeta_part, int64_t rows) {
+             const float* __restrict__ rstd, DropSpec drop, float* __restrict__ ds_out,
+             float* __restrict__ da_out, float* __restrict__ dgamma_part,
+             float* __restrict__ dbeta_part, float* __restrict__ dbias_part, int64_t rows) {
   constexpr int D = LPR * NV * 4;
   constexpr int RPW = kWave / LPR;
-  __shared__ float red[2][4][D];
+  __shared__ float red[3][4][D];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = threadIdx.x >> 6;
   const int sub = lane / LPR;
   const int l = lane - sub * LPR;
   const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
-  float gm[NV][4], accg[NV][4], accb[NV][4];
+  float gm[NV][4], accg[NV][4], accb[NV][4], acca[NV][4];
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     ldv(gm[k], gamma + (l + k * LPR) * 4);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) accg[k][v] = accb[k][v] = 0.0f;
+    for (int v = 0; v < 4; ++v) accg[k][v] = accb[k][v] = acca[k][v] = 0.0f;
   }
   for (int64_t row0 = wave * RPW; row0 < rows; row0 += nwaves * RPW) {
     const int64_t row = row0 + sub;
@@ -158,27 +157,26 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
     }
     const float mg = row_sum<LPR>(sg) * (1.0f / D);
     const float mgx = row_sum<LPR>(sgx) * (1.0f / D);
-    if (ok) {
 #pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int c = (l + k * LPR) * 4;
-        float d[4];
+    for (int k = 0; k < NV; ++k) {
+      const int c = (l + k * LPR) * 4;
+      float d[4];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) d[v] = rs * (g[k][v] - mg - xh[k][v] * mgx);
-        if (ds_out) stv(ds_out + row * D + c, d);
-        if (da_out) {
-          if (mask) {
-            float m[4];
-            ld_mask4(m, mask + row * D + c);
+      for (int v = 0; v < 4; ++v) d[v] = ok ? rs * (g[k][v] - mg - xh[k][v] * mgx) : 0.0f;
+      if (ok && ds_out) stv(ds_out + row * D + c, d);
+      if (da_out || dbias_part) {
+        float m[4];
+        drop.get4(rr * D + c, m);
 #pragma unroll
-            for (int v = 0; v < 4; ++v) d[v] = d[v] * m[v] * scale;
-          }
-          stv(da_out + row * D + c, d);
+        for (int v = 0; v < 4; ++v) {
+          d[v] = d[v] * m[v];
+          acca[k][v] += d[v];
         }
+        if (ok && da_out) stv(da_out + row * D + c, d);
       }
     }
   }
-  // dgamma / dbeta: reduce the RPW row groups of the wave, then the 4 waves
+  // column partials: reduce the RPW row groups of the wave, then the 4 waves
 #pragma unroll
   for (int k = 0; k < NV; ++k)
 #pragma unroll
@@ -187,6 +185,7 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
       for (int o = LPR; o < kWave; o <<= 1) {
         accg[k][v] += __shfl_xor(accg[k][v], o, kWave);
         accb[k][v] += __shfl_xor(accb[k][v], o, kWave);
+        acca[k][v] += __shfl_xor(acca[k][v], o, kWave);
       }
   if (sub == 0) {
 #pragma unroll
@@ -196,131 +195,212 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
       for (int v = 0; v < 4; ++v) {
         red[0][wv][c + v] = accg[k][v];
         red[1][wv][c + v] = accb[k][v];
+        red[2][wv][c + v] = acca[k][v];
       }
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
-    dgamma_part[(int64_t)blockIdx.x * D + c] =
-        ((red[0][0][c] + red[0][1][c]) + red[0][2][c]) + red[0][3][c];
-    dbeta_part[(int64_t)blockIdx.x * D + c] =
-        ((red[1][0][c] + red[1][1][c]) + red[1][2][c]) + red[1][3][c];
+    const int64_t o = (int64_t)blockIdx.x * D + c;
+    dgamma_part[o] = ((red[0][0][c] + red[0][1][c]) + red[0][2][c]) + red[0][3][c];
+    dbeta_part[o] = ((red[1][0][c] + red[1][1][c]) + red[1][2][c]) + red[1][3][c];
+    if (dbias_part) dbias_part[o] = ((red[2][0][c] + red[2][1][c]) + red[2][2][c]) + red[2][3][c];
   }
 }
 
-// u = silu(a) * mask * scale (mask optional); the FFN's inner activation.
+// FFN inner activation on rows of C = LPR * NV * 4: u = silu(a) * keep * scale
+template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
-k_silu_dropout_fwd(const float4* __restrict__ a, const uchar4* __restrict__ mask, float scale,
-                   float4* __restrict__ u, int64_t n4) {
+k_silu_dropout_fwd(const float* __restrict__ a, DropSpec drop, float* __restrict__ u,
+                   int64_t rows) {
+  constexpr int C = LPR * NV * 4;
+  constexpr int RPW = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int sub = lane / LPR;
+  const int l = lane - sub * LPR;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t row0 = wave * RPW; row0 < rows; row0 += nwaves * RPW) {
+    const int64_t row = row0 + sub;
+    if (row >= rows) continue;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t e = row * C + (l + k * LPR) * 4;
+      float x[4], m[4], o[4];
+      ldv(x, a + e);
+      drop.get4(e, m);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) o[v] = fsilu(x[v]) * m[v];
+      stv(u + e, o);
+    }
+  }
+}
+
+// da = du * keep * scale * silu'(a); column partials of da = the bias
+// gradient of the GEMM that produced a.
+template <int NV, int LPR>
+__global__ void __launch_bounds__(256)
+k_silu_dropout_bwd(const float* __restrict__ a, DropSpec drop, const float* __restrict__ du,
+                   float* __restrict__ da, float* __restrict__ dbias_part, int64_t rows) {
+  constexpr int C = LPR * NV * 4;
+  constexpr int RPW = kWave / LPR;
+  __shared__ float red[4][C];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = threadIdx.x >> 6;
+  const int sub = lane / LPR;
+  const int l = lane - sub * LPR;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  float acc[NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) acc[k][v] = 0.0f;
+  for (int64_t row0 = wave * RPW; row0 < rows; row0 += nwaves * RPW) {
+    const int64_t row = row0 + sub;
+    if (row >= rows) continue;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t e = row * C + (l + k * LPR) * 4;
+      float x[4], g[4], m[4], o[4];
+      ldv(x, a + e);
+      ldv(g, du + e);
+      drop.get4(e, m);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        o[v] = (g[v] * m[v]) * fdsilu(x[v]);
+        acc[k][v] += o[v];
+      }
+      stv(da + e, o);
+    }
+  }
+  if (dbias_part == nullptr) return;   // grid-uniform
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int o = LPR; o < kWave; o <<= 1) acc[k][v] += __shfl_xor(acc[k][v], o, kWave);
+  if (sub == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) red[wv][(l + k * LPR) * 4 + v] = acc[k][v];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    dbias_part[(int64_t)blockIdx.x * C + c] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+// explicit keep-mask materialisation of a Philox stream (tests, debugging)
+__global__ void k_dropout_mask(DropSpec drop, uint8_t* __restrict__ out, int64_t n4) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 x = a[i];
-    float4 o = make_float4(fsilu(x.x), fsilu(x.y), fsilu(x.z), fsilu(x.w));
-    if (mask) {
-      const uchar4 m = mask[i];
-      o.x *= m.x * scale; o.y *= m.y * scale; o.z *= m.z * scale; o.w *= m.w * scale;
-    }
-    u[i] = o;
+    float m[4];
+    drop.get4(i * 4, m);
+    uchar4 o;
+    o.x = m[0] != 0.0f; o.y = m[1] != 0.0f; o.z = m[2] != 0.0f; o.w = m[3] != 0.0f;
+    reinterpret_cast<uchar4*>(out)[i] = o;
   }
 }
 
-__global__ void __launch_bounds__(256)
-k_silu_dropout_bwd(const float4* __restrict__ a, const uchar4* __restrict__ mask, float scale,
-                   const float4* __restrict__ du, float4* __restrict__ da, int64_t n4) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const float4 x = a[i];
-    float4 g = du[i];
-    if (mask) {
-      const uchar4 m = mask[i];
-      g.x *= m.x * scale; g.y *= m.y * scale; g.z *= m.z * scale; g.w *= m.w * scale;
-    }
-    da[i] = make_float4(g.x * fdsilu(x.x), g.y * fdsilu(x.y), g.z * fdsilu(x.z),
-                        g.w * fdsilu(x.w));
-  }
+template <int LPR>
+int64_t row_blocks(int64_t rows) {
+  constexpr int RPB = 4 * (kWave / LPR);
+  return std::max<int64_t>(1, std::min<int64_t>(kRowBlocks, (rows + RPB - 1) / RPB));
 }
-
-constexpr int kRowBlocks = 1024;   // 4 waves each; grid-stride over rows
 
 template <int NV, int LPR>
-int ln_fwd_t(const float* a, const int64_t* idx, int64_t nidx, const uint8_t* mask, float scale, const float* r,
-             const float* gamma, const float* beta, float eps, float* y, float* s_out,
-             float* mean, float* rstd, int64_t rows, hipStream_t st) {
-  constexpr int RPB = 4 * (kWave / LPR);
-  const int64_t blocks = std::min<int64_t>(kRowBlocks * 2, (rows + RPB - 1) / RPB);
-  hipLaunchKernelGGL((k_add_ln_fwd<NV, LPR>), dim3((unsigned)blocks), dim3(256), 0, st, a, idx,
-                     nidx, mask, scale, r, gamma, beta, eps, y, s_out, mean, rstd, rows);
+int add_ln_fwd_t(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
+                 const float* r, const float* gamma, const float* beta, float eps, float* y,
+                 float* s_out, float* mean, float* rstd, int64_t rows, hipStream_t st) {
+  hipLaunchKernelGGL((k_add_ln_fwd<NV, LPR>), dim3((unsigned)row_blocks<LPR>(rows)), dim3(256), 0,
+                     st, a, idx, nidx, drop, r, gamma, beta, eps, y, s_out, mean, rstd, rows);
   return launch_status("rb_add_ln_fwd");
 }
 
 template <int NV, int LPR>
-int ln_bwd_t(const float* dy, const float* s, const float* gamma, const float* mean,
-             const float* rstd, const uint8_t* mask, float scale, float* ds, float* da,
-             float* dgp, float* dbp, int64_t nparts, int64_t rows, hipStream_t st) {
+int add_ln_bwd_t(const float* dy, const float* s, const float* gamma, const float* mean,
+                 const float* rstd, const DropSpec& drop, float* ds, float* da, float* dgp,
+                 float* dbp, float* dbiasp, int64_t nparts, int64_t rows, hipStream_t st) {
   hipLaunchKernelGGL((k_add_ln_bwd<NV, LPR>), dim3((unsigned)nparts), dim3(256), 0, st, dy, s,
-                     gamma, mean, rstd, mask, scale, ds, da, dgp, dbp, rows);
+                     gamma, mean, rstd, drop, ds, da, dgp, dbp, dbiasp, rows);
   return launch_status("rb_add_ln_bwd");
+}
+
+template <int NV, int LPR>
+int silu_fwd_t(const float* a, const DropSpec& drop, float* u, int64_t rows, hipStream_t st) {
+  hipLaunchKernelGGL((k_silu_dropout_fwd<NV, LPR>), dim3((unsigned)(2 * row_blocks<LPR>(rows))),
+                     dim3(256), 0, st, a, drop, u, rows);
+  return launch_status("rb_silu_dropout_fwd");
+}
+
+template <int NV, int LPR>
+int silu_bwd_t(const float* a, const DropSpec& drop, const float* du, float* da,
+               float* dbias_part, int64_t nparts, int64_t rows, hipStream_t st) {
+  hipLaunchKernelGGL((k_silu_dropout_bwd<NV, LPR>), dim3((unsigned)nparts), dim3(256), 0, st, a,
+                     drop, du, da, dbias_part, rows);
+  return launch_status("rb_silu_dropout_bwd");
 }
 
 }  // namespace
 
-int64_t ln_num_parts(int64_t rows) {
-  return std::max<int64_t>(1, std::min<int64_t>(kRowBlocks, (rows + 31) / 32));
+int64_t ln_num_parts(int64_t rows, int64_t d) {
+  switch (d) {
+    case 16: return row_blocks<4>(rows);
+    case 32: return row_blocks<8>(rows);
+    case 64: return row_blocks<16>(rows);
+    case 128: return row_blocks<32>(rows);
+    default: return row_blocks<64>(rows);
+  }
 }
 
-// d -> (NV, LPR): LPR lanes per row, NV float4 per lane, LPR * NV * 4 == d
-#define RB_LN_DISPATCH(D, CALL)                 \
-  switch (D) {                                  \
-    case 16: return CALL(1, 4);                 \
-    case 32: return CALL(1, 8);                 \
-    case 64: return CALL(1, 16);                \
-    case 128: return CALL(1, 32);               \
-    case 256: return CALL(1, 64);               \
-    case 512: return CALL(2, 64);               \
-    case 1024: return CALL(4, 64);              \
-    default: return fail("layer norm: d must be one of 16, 32, 64, 128, 256, 512, 1024"); \
+// width -> (NV, LPR): LPR lanes per row, NV float4 per lane, LPR * NV * 4 == width
+#define RB_ROW_DISPATCH(D, FN, ...)                          \
+  switch (D) {                                               \
+    case 16: return FN<1, 4>(__VA_ARGS__);                   \
+    case 32: return FN<1, 8>(__VA_ARGS__);                   \
+    case 64: return FN<1, 16>(__VA_ARGS__);                  \
+    case 128: return FN<1, 32>(__VA_ARGS__);                 \
+    case 256: return FN<1, 64>(__VA_ARGS__);                 \
+    case 512: return FN<2, 64>(__VA_ARGS__);                 \
+    case 1024: return FN<4, 64>(__VA_ARGS__);                \
+    default:                                                 \
+      return fail("row kernels: width must be one of 16, 32, 64, 128, 256, 512, 1024"); \
   }
 
-int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const uint8_t* mask,
-                      float scale,
+int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
                       const float* r, const float* gamma, const float* beta, float eps, float* y,
                       float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,
                       hipStream_t st) {
-#define RB_CALL(NV, LPR) \
-  ln_fwd_t<NV, LPR>(a, idx, nidx, mask, scale, r, gamma, beta, eps, y, s_out, mean, rstd, rows, st)
-  RB_LN_DISPATCH(d, RB_CALL)
-#undef RB_CALL
+  RB_ROW_DISPATCH(d, add_ln_fwd_t, a, idx, nidx, drop, r, gamma, beta, eps, y, s_out, mean,
+                  rstd, rows, st)
 }
 
 int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
-                      const float* rstd, const uint8_t* mask, float scale, float* ds, float* da,
-                      float* dgp, float* dbp, int64_t nparts, int64_t rows, int64_t d,
+                      const float* rstd, const DropSpec& drop, float* ds, float* da, float* dgp,
+                      float* dbp, float* dbiasp, int64_t nparts, int64_t rows, int64_t d,
                       hipStream_t st) {
-#define RB_CALL(NV, LPR) \
-  ln_bwd_t<NV, LPR>(dy, s, gamma, mean, rstd, mask, scale, ds, da, dgp, dbp, nparts, rows, st)
-  RB_LN_DISPATCH(d, RB_CALL)
-#undef RB_CALL
+  RB_ROW_DISPATCH(d, add_ln_bwd_t, dy, s, gamma, mean, rstd, drop, ds, da, dgp, dbp, dbiasp,
+                  nparts, rows, st)
 }
 
-int launch_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale, float* u,
-                            int64_t n, hipStream_t st) {
-  const int64_t n4 = n / 4;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(8192, (n4 + 255) / 256));
-  hipLaunchKernelGGL(k_silu_dropout_fwd, dim3((unsigned)blocks), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(a), reinterpret_cast<const uchar4*>(mask),
-                     scale, reinterpret_cast<float4*>(u), n4);
-  return launch_status("rb_silu_dropout_fwd");
+int launch_silu_dropout_fwd(const float* a, const DropSpec& drop, float* u, int64_t rows,
+                            int64_t cols, hipStream_t st) {
+  RB_ROW_DISPATCH(cols, silu_fwd_t, a, drop, u, rows, st)
 }
 
-int launch_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale, const float* du,
-                            float* da, int64_t n, hipStream_t st) {
+int launch_silu_dropout_bwd(const float* a, const DropSpec& drop, const float* du, float* da,
+                            float* dbias_part, int64_t nparts, int64_t rows, int64_t cols,
+                            hipStream_t st) {
+  RB_ROW_DISPATCH(cols, silu_bwd_t, a, drop, du, da, dbias_part, nparts, rows, st)
+}
+
+int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st) {
   const int64_t n4 = n / 4;
-  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(8192, (n4 + 255) / 256));
-  hipLaunchKernelGGL(k_silu_dropout_bwd, dim3((unsigned)blocks), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(a), reinterpret_cast<const uchar4*>(mask),
-                     scale, reinterpret_cast<const float4*>(du), reinterpret_cast<float4*>(da),
-                     n4);
-  return launch_status("rb_silu_dropout_bwd");
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>(4096, (n4 + 255) / 256));
+  hipLaunchKernelGGL(k_dropout_mask, dim3((unsigned)blocks), dim3(256), 0, st, drop, out, n4);
+  return launch_status("rb_dropout_mask");
 }
 
 }  // namespace rb

@@ -235,7 +235,8 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None):
 
 
 # ---------------------------------------------------------------- row blocks
-LN_SIZES = (16, 32, 64, 128, 256, 512, 1024)
+ROW_SIZES = (16, 32, 64, 128, 256, 512, 1024)
+LN_SIZES = ROW_SIZES
 
 
 def _ptr(t):
@@ -251,16 +252,27 @@ def _check_mask(mask, shape, name="mask"):
         raise ValueError(f"{name} must be contiguous")
 
 
-def add_ln_fwd(a, r, mask, scale, gamma, beta, eps, idx=None, save=True):
+def _check_p(p):
+    if not 0.0 <= p < 1.0:
+        raise ValueError(f"dropout p must be in [0, 1), got {p}")
+
+
+def row_num_parts(rows: int, width: int) -> int:
+    return int(_lib.load().rb_row_num_parts(rows, width))
+
+
+def add_ln_fwd(a, r, gamma, beta, eps, mask=None, seed=0, p=0.0, idx=None, save=True):
     """Fused [gather +] dropout + residual + LayerNorm over rows of d.
 
     a: [rows, d] (or the [V, d] table when idx [rows] is given); r: [rows, d]
-    or None; mask: uint8 [rows, d] or None.  Returns (y, s, mean, rstd); the
-    last three are None unless save."""
+    or None.  Dropout: explicit uint8 `mask` [rows, d], else Philox(`seed`)
+    when p > 0.  Returns (y, s, mean, rstd); the last three are None unless
+    save."""
     _check(a, "a")
+    _check_p(p)
     d = a.shape[-1]
-    if d not in LN_SIZES:
-        raise ValueError(f"layer norm width {d} not in {LN_SIZES}")
+    if d not in ROW_SIZES:
+        raise ValueError(f"layer norm width {d} not in {ROW_SIZES}")
     if not a.is_contiguous():
         raise ValueError("a must be contiguous")
     if idx is not None:
@@ -289,55 +301,87 @@ def add_ln_fwd(a, r, mask, scale, gamma, beta, eps, idx=None, save=True):
         rstd = torch.empty((rows,), device=dev, dtype=torch.float32)
     n = rows * d
     nbytes = 4 * n * (2 + (r is not None) + (s is not None)) + (n if mask is not None else 0)
-    _launch("rb_add_ln_fwd", nbytes, a.data_ptr(), _ptr(idx), nidx, _ptr(mask), float(scale),
-            _ptr(r), gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(), _ptr(s),
-            _ptr(mean), _ptr(rstd), rows, d, _stream(a))
+    _launch("rb_add_ln_fwd", nbytes, a.data_ptr(), _ptr(idx), nidx, _ptr(mask), int(seed),
+            float(p), _ptr(r), gamma.data_ptr(), beta.data_ptr(), float(eps), y.data_ptr(),
+            _ptr(s), _ptr(mean), _ptr(rstd), rows, d, _stream(a))
     return y, s, mean, rstd
 
 
-def add_ln_bwd(dy, s, gamma, mean, rstd, mask, scale, want_ds=True, want_da=True):
-    """Returns (ds, da, dgamma, dbeta); ds/da None when not wanted."""
+def add_ln_bwd(dy, s, gamma, mean, rstd, mask=None, seed=0, p=0.0, want_ds=True,
+               want_da=True, want_dbias=False):
+    """Returns (ds, da, dgamma, dbeta, dbias); unwanted outputs are None."""
     _check(dy, "dy")
+    _check_p(p)
     rows, d = s.shape
     dy = dy.reshape(rows, d)
     if not dy.is_contiguous():
         dy = dy.contiguous()
     _check_mask(mask, (rows, d))
-    lib = _lib.load()
-    nparts = int(lib.rb_add_ln_num_parts(rows, d))
+    nparts = row_num_parts(rows, d)
     dev = s.device
     dgp = torch.empty((nparts, d), device=dev, dtype=torch.float32)
     dbp = torch.empty((nparts, d), device=dev, dtype=torch.float32)
+    dbias_p = torch.empty((nparts, d), device=dev, dtype=torch.float32) if want_dbias else None
     ds = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_ds else None
     da = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_da else None
     n = rows * d
     nbytes = 4 * n * (2 + want_ds + want_da) + (n if mask is not None else 0)
     _launch("rb_add_ln_bwd", nbytes, dy.data_ptr(), s.data_ptr(), gamma.data_ptr(),
-            mean.data_ptr(), rstd.data_ptr(), _ptr(mask), float(scale), _ptr(ds), _ptr(da),
-            dgp.data_ptr(), dbp.data_ptr(), nparts, rows, d, _stream(dy))
-    return ds, da, dgp.sum(0), dbp.sum(0)
+            mean.data_ptr(), rstd.data_ptr(), _ptr(mask), int(seed), float(p), _ptr(ds),
+            _ptr(da), dgp.data_ptr(), dbp.data_ptr(), _ptr(dbias_p), nparts, rows, d,
+            _stream(dy))
+    return ds, da, dgp.sum(0), dbp.sum(0), (dbias_p.sum(0) if want_dbias else None)
 
 
-def silu_dropout_fwd(a, mask, scale):
+def _rows_cols(a):
+    cols = a.shape[-1]
+    if cols not in ROW_SIZES:
+        raise ValueError(f"row width {cols} not in {ROW_SIZES}")
+    return a.numel() // cols, cols
+
+
+def silu_dropout_fwd(a, mask=None, seed=0, p=0.0):
     _check(a, "a")
-    if not a.is_contiguous() or a.numel() % 4:
-        raise ValueError("a must be contiguous with numel % 4 == 0")
-    _check_mask(mask, a.shape)
+    _check_p(p)
+    if not a.is_contiguous():
+        raise ValueError("a must be contiguous")
+    rows, cols = _rows_cols(a)
+    _check_mask(mask, (rows, cols))
     u = torch.empty_like(a)
     n = a.numel()
     _launch("rb_silu_dropout_fwd", 8 * n + (n if mask is not None else 0), a.data_ptr(),
-            _ptr(mask), float(scale), u.data_ptr(), n, _stream(a))
+            _ptr(mask), int(seed), float(p), u.data_ptr(), rows, cols, _stream(a))
     return u
 
 
-def silu_dropout_bwd(a, mask, scale, du):
+def silu_dropout_bwd(a, du, mask=None, seed=0, p=0.0, want_dbias=False):
+    """Returns (da, dbias or None)."""
     _check(du, "du")
+    _check_p(p)
     du = du.contiguous()
+    rows, cols = _rows_cols(a)
+    _check_mask(mask, (rows, cols))
     da = torch.empty_like(a)
+    nparts = row_num_parts(rows, cols)
+    dbias_p = (torch.empty((nparts, cols), device=a.device, dtype=torch.float32)
+               if want_dbias else None)
     n = a.numel()
     _launch("rb_silu_dropout_bwd", 12 * n + (n if mask is not None else 0), a.data_ptr(),
-            _ptr(mask), float(scale), du.data_ptr(), da.data_ptr(), n, _stream(a))
-    return da
+            _ptr(mask), int(seed), float(p), du.data_ptr(), da.data_ptr(), _ptr(dbias_p), nparts,
+            rows, cols, _stream(a))
+    return da, (dbias_p.sum(0) if want_dbias else None)
+
+
+def dropout_mask(seed, p, shape, device):
+    """uint8 keep-mask of the Philox stream the row kernels use for (seed, p)."""
+    _check_p(p)
+    out = torch.empty(shape, dtype=torch.uint8, device=device)
+    n = out.numel()
+    if n % 4:
+        raise ValueError("numel must be a multiple of 4")
+    _launch("rb_dropout_mask", n, int(seed), float(p), out.data_ptr(), n,
+            torch.cuda.current_stream(out.device).cuda_stream)
+    return out
 
 
 def embedding_bwd(idx, grad, num_rows, padding_idx=0):

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._lib import RecBLRNativeError
-from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, silu_dropout
+from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, feed_forward
 from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len
@@ -96,9 +96,7 @@ class FeedForward(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
 
     def forward(self, input_tensor):
-        h = silu_dropout(linear(input_tensor, self.w_1), self.dropout, self.training)
-        return add_dropout_layer_norm(linear(h, self.w_2), input_tensor, self.dropout,
-                                      self.layer_norm, self.training)
+        return feed_forward(input_tensor, self, self.training)
 
 
 class RecurrentLayer(nn.Module):

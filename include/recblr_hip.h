@@ -122,38 +122,53 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
 
 /* ---- blocks around the BD-LRU (RecurrentLayer / FeedForward / embedding) ---- */
 
+/* Dropout in the row kernels (nn.Dropout(p), train mode): element e is kept
+ * with probability 1-p and scaled by 1/(1-p).  The keep flags come from
+ * `mask` (uint8 {0,1}, laid out like the data) when it is non-NULL, otherwise
+ * from a Philox4x32-10 stream keyed by `seed` with counter e/4 — regenerated
+ * bit-identically by the backward.  p = 0 and mask = NULL: no dropout.
+ * Row widths (d, cols) must be one of 16, 32, 64, 128, 256, 512, 1024. */
+
 /* Fused dropout + residual + LayerNorm over rows of d floats
  * (RecBLR.py:77-78 and :142, and FeedForward's :223-225):
  *   A[row] = idx ? a[clamp(idx[row], 0, n_idx_rows-1)] : a[row]   (gather)
- *   s      = A[row] * (mask ? mask[row] * scale : 1) + (r ? r[row] : 0)
+ *   s      = dropout(A[row]) + (r ? r[row] : 0)
  *   y      = (s - mean) / sqrt(var + eps) * gamma + beta
- * mask: uint8 {0,1} per element (torch's bool), scale = 1/(1-p).  s_out,
- * mean, rstd (saved for the backward) are all given or all NULL.
- * d in {16, 32, 64, 128, 256, 512, 1024}. */
+ * s_out, mean, rstd (saved for the backward) are all given or all NULL. */
 int rb_add_ln_fwd(const float* a, const int64_t* idx, int64_t n_idx_rows,
-                  const uint8_t* mask, float scale, const float* r,
+                  const uint8_t* mask, uint64_t seed, float p, const float* r,
                   const float* gamma, const float* beta, float eps, float* y,
                   float* s_out, float* mean, float* rstd, int64_t rows,
                   int64_t d, void* stream);
 
-/* Rows of the dgamma/dbeta partial-sum buffers rb_add_ln_bwd writes. */
-int64_t rb_add_ln_num_parts(int64_t rows, int64_t d);
+/* Rows of the per-block column partial-sum buffers the row backward kernels
+ * write ([n_parts, width]; the caller sums them over n_parts). */
+int64_t rb_row_num_parts(int64_t rows, int64_t width);
 
-/* Backward of rb_add_ln_fwd: ds = dL/ds (the residual's gradient) and
- * da = ds * mask * scale (the dropped input's gradient); either may be NULL.
- * dgamma_part / dbeta_part: [n_parts, d], summed over rows by the caller. */
+/* Backward of rb_add_ln_fwd: ds = dL/ds (the residual's gradient),
+ * da = dropout-backward(ds) (the dropped input's gradient) and dbias_part =
+ * column partials of da (the bias gradient of the GEMM that produced a);
+ * any of the three may be NULL.  dgamma_part / dbeta_part: [n_parts, d]. */
 int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma,
                   const float* mean, const float* rstd, const uint8_t* mask,
-                  float scale, float* ds, float* da, float* dgamma_part,
-                  float* dbeta_part, int64_t n_parts, int64_t rows, int64_t d,
-                  void* stream);
+                  uint64_t seed, float p, float* ds, float* da,
+                  float* dgamma_part, float* dbeta_part, float* dbias_part,
+                  int64_t n_parts, int64_t rows, int64_t d, void* stream);
 
-/* FeedForward's inner activation (RecBLR.py:220-221):
- * u = silu(a) * (mask ? mask * scale : 1); n a multiple of 4. */
-int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, float scale,
-                        float* u, int64_t n, void* stream);
-int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, float scale,
-                        const float* du, float* da, int64_t n, void* stream);
+/* FeedForward's inner activation (RecBLR.py:220-221) on [rows, cols]:
+ * u = dropout(silu(a)); backward da = dropout-backward(du) * silu'(a) with
+ * optional column partials of da (the w_1 bias gradient). */
+int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, uint64_t seed,
+                        float p, float* u, int64_t rows, int64_t cols,
+                        void* stream);
+int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, uint64_t seed,
+                        float p, const float* du, float* da,
+                        float* dbias_part, int64_t n_parts, int64_t rows,
+                        int64_t cols, void* stream);
+
+/* Materialise the keep-mask of a Philox dropout stream (n % 4 == 0). */
+int rb_dropout_mask(uint64_t seed, float p, uint8_t* out, int64_t n,
+                    void* stream);
 
 /* Item-embedding backward (RecBLR.py:76, nn.Embedding(padding_idx=0)):
  * dweight[v] = sum_{p : idx[p] == v} grad[p], dweight[padding_idx] = 0,

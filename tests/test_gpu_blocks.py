@@ -1,6 +1,8 @@
 """GPU parity of the fused blocks around the BD-LRU against plain torch fp32
-compositions of the reference's ops (RecBLR.py:76-78, :142, :218-227), with
-explicit dropout masks so both sides drop the same elements."""
+compositions of the reference's ops (RecBLR.py:76-78, :142, :210-227).  Both
+sides drop the same elements: either an explicit mask is passed to the
+kernels, or the kernels' Philox keep-mask is materialised (rb_dropout_mask)
+and applied on the torch side."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -15,24 +17,35 @@ def close(a, b, atol=1e-5, rtol=1e-5, what=""):
     assert not bad.any(), f"{what}: max err {err.max().item():.3e}"
 
 
+def _mask(g, shape, p, cuda):
+    return (torch.rand(shape, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
+
+
 @pytest.mark.parametrize("rows,d", [(7, 16), (33, 64), (1000, 128), (129, 256), (64, 512),
                                     (5, 1024), (409, 32)])
-@pytest.mark.parametrize("p", [0.0, 0.2])
-def test_add_dropout_layer_norm(cuda, rows, d, p):
+@pytest.mark.parametrize("mode", ["none", "mask", "philox"])
+def test_add_dropout_layer_norm(cuda, rows, d, mode):
+    from datamining_recblr_amd import kernels
     from datamining_recblr_amd.blocks import _AddDropoutLN
 
+    p = 0.0 if mode == "none" else 0.2
     g = torch.Generator(device="cpu").manual_seed(rows * d)
     a = torch.randn(rows, d, generator=g).to(cuda).requires_grad_()
     r = torch.randn(rows, d, generator=g).to(cuda).requires_grad_()
     gamma = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
     beta = (0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
     dy = torch.randn(rows, d, generator=g).to(cuda)
-    mask = (torch.rand(rows, d, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
-    scale = 1.0 / (1.0 - p)
-    y = _AddDropoutLN.apply(a, r, gamma, beta, mask, scale, 1e-12)
+    seed = 1234 + rows
+    if mode == "mask":
+        mask = _mask(g, (rows, d), p, cuda)
+        ref_mask = mask
+    else:
+        mask = None
+        ref_mask = kernels.dropout_mask(seed, p, (rows, d), cuda) if p else None
+    y = _AddDropoutLN.apply(a, r, gamma, beta, mask, seed, p, 1e-12)
     y.backward(dy)
     ar, rr, gr, br = (t.detach().clone().requires_grad_() for t in (a, r, gamma, beta))
-    dropped = ar * mask * scale if mask is not None else ar
+    dropped = ar * ref_mask / (1 - p) if ref_mask is not None else ar
     yr = F.layer_norm(dropped + rr, (d,), gr, br, eps=1e-12)
     yr.backward(dy)
     close(y, yr, what="y")
@@ -42,10 +55,25 @@ def test_add_dropout_layer_norm(cuda, rows, d, p):
     close(beta.grad, br.grad, atol=1e-4, rtol=1e-4, what="dbeta")
 
 
+def test_philox_mask_statistics_and_determinism(cuda):
+    from datamining_recblr_amd import kernels
+
+    m1 = kernels.dropout_mask(7, 0.2, (4096, 512), cuda)
+    m2 = kernels.dropout_mask(7, 0.2, (4096, 512), cuda)
+    m3 = kernels.dropout_mask(8, 0.2, (4096, 512), cuda)
+    assert torch.equal(m1, m2) and not torch.equal(m1, m3)
+    keep = m1.float().mean().item()
+    assert abs(keep - 0.8) < 2e-3, keep
+    # no structure along rows or columns
+    assert (m1.float().mean(0) - 0.8).abs().max() < 0.03
+    assert (m1.float().mean(1) - 0.8).abs().max() < 0.03
+
+
 @pytest.mark.parametrize("p", [0.0, 0.2])
 def test_embed_dropout_layer_norm(cuda, p):
     """Gather + dropout + LN, and the deterministic embedding backward, incl.
     padding id 0, a very popular id (multi-chunk segment sums) and unused ids."""
+    from datamining_recblr_amd import kernels
     from datamining_recblr_amd.blocks import _EmbedDropoutLN
 
     V, d, B, L = 500, 128, 16, 300
@@ -58,14 +86,13 @@ def test_embed_dropout_layer_norm(cuda, p):
     gamma = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
     beta = (0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
     dy = torch.randn(B, L, d, generator=g).to(cuda)
-    mask = (torch.rand(B * L, d, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
-    scale = 1.0 / (1.0 - p)
-    y = _EmbedDropoutLN.apply(table, idx, gamma, beta, mask, scale, 1e-12, 0)
+    seed = 99
+    y = _EmbedDropoutLN.apply(table, idx, gamma, beta, None, seed, p, 1e-12, 0)
     y.backward(dy)
     tr, gr, br = (t.detach().clone().requires_grad_() for t in (table, gamma, beta))
     e = F.embedding(idx, tr, padding_idx=0)
-    if mask is not None:
-        e = e * mask.view(B, L, d) * scale
+    if p:
+        e = e * kernels.dropout_mask(seed, p, (B, L, d), cuda) / (1 - p)
     yr = F.layer_norm(e, (d,), gr, br, eps=1e-12)
     yr.backward(dy)
     close(y, yr, what="y")
@@ -92,29 +119,69 @@ def test_embedding_bwd_skewed_and_deterministic(cuda):
     assert torch.equal(dw, kernels.embedding_bwd(idx, grad, V, padding_idx=0))
 
 
-@pytest.mark.parametrize("p", [0.0, 0.3])
-def test_silu_dropout(cuda, p):
+@pytest.mark.parametrize("mode", ["none", "mask", "philox"])
+def test_silu_dropout(cuda, mode):
+    from datamining_recblr_amd import kernels
     from datamining_recblr_amd.blocks import _SiluDropout
 
+    p = 0.0 if mode == "none" else 0.3
     g = torch.Generator(device="cpu").manual_seed(3)
     a = (3 * torch.randn(37, 512, generator=g)).to(cuda).requires_grad_()
     du = torch.randn(37, 512, generator=g).to(cuda)
-    mask = (torch.rand(37, 512, generator=g) >= p).to(torch.uint8).to(cuda) if p else None
-    scale = 1.0 / (1.0 - p)
-    u = _SiluDropout.apply(a, mask, scale)
+    seed = 5
+    mask = _mask(g, (37, 512), p, cuda) if mode == "mask" else None
+    ref_mask = mask if mode == "mask" else (kernels.dropout_mask(seed, p, (37, 512), cuda)
+                                            if p else None)
+    u = _SiluDropout.apply(a, mask, seed, p)
     u.backward(du)
     ar = a.detach().clone().requires_grad_()
     ur = F.silu(ar)
-    if mask is not None:
-        ur = ur * mask * scale
+    if ref_mask is not None:
+        ur = ur * ref_mask / (1 - p)
     ur.backward(du)
     close(u, ur, what="u")
     close(a.grad, ar.grad, what="da")
 
 
-def test_train_mode_dropout_statistics(cuda):
-    """Train-mode model: masks are drawn per call (outputs differ run to run),
-    p = 0 in train mode equals eval, and the loss stays finite."""
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_fused_feed_forward(cuda, p):
+    """_FeedForward (two GEMMs, SiLU+dropout, dropout+residual+LN, folded bias
+    grads, residual grad through addmm) == the reference FeedForward math."""
+    from datamining_recblr_amd import kernels
+    from datamining_recblr_amd.blocks import _FeedForward
+
+    g = torch.Generator(device="cpu").manual_seed(21)
+    M, d = 3000, 128
+    x = torch.randn(M, d, generator=g).to(cuda).requires_grad_()
+    w1 = (0.05 * torch.randn(4 * d, d, generator=g)).to(cuda).requires_grad_()
+    b1 = (0.1 * torch.randn(4 * d, generator=g)).to(cuda).requires_grad_()
+    w2 = (0.05 * torch.randn(d, 4 * d, generator=g)).to(cuda).requires_grad_()
+    b2 = (0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    gamma = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    beta = (0.1 * torch.randn(d, generator=g)).to(cuda).requires_grad_()
+    dy = torch.randn(M, d, generator=g).to(cuda)
+    s1, s2 = 31, 32
+    y = _FeedForward.apply(x, w1, b1, w2, b2, gamma, beta, s1, s2, p, 1e-12)
+    y.backward(dy)
+    leaves = [t.detach().clone().requires_grad_() for t in (x, w1, b1, w2, b2, gamma, beta)]
+    xr, w1r, b1r, w2r, b2r, gr, br = leaves
+    h = F.silu(F.linear(xr, w1r, b1r))
+    if p:
+        h = h * kernels.dropout_mask(s1, p, (M, 4 * d), cuda) / (1 - p)
+    h = F.linear(h, w2r, b2r)
+    if p:
+        h = h * kernels.dropout_mask(s2, p, (M, d), cuda) / (1 - p)
+    yr = F.layer_norm(h + xr, (d,), gr, br, eps=1e-12)
+    yr.backward(dy)
+    close(y, yr, atol=1e-4, what="y")
+    for name, a, b in zip(("dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta"),
+                          (x, w1, b1, w2, b2, gamma, beta), leaves):
+        close(a.grad, b.grad, atol=1e-4, rtol=1e-4, what=name)
+
+
+def test_train_mode_dropout(cuda):
+    """Train-mode model: fresh dropout per call (outputs differ run to run),
+    reproducible under torch.manual_seed, and p = 0 in train mode == eval."""
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
 
@@ -126,9 +193,13 @@ def test_train_mode_dropout_statistics(cuda):
     seq = torch.randint(1, 300, (32, 50), device=cuda)
     lens = torch.randint(1, 51, (32,), device=cuda)
     model.train()
+    torch.manual_seed(5)
     a = model.forward(seq, lens)
     b = model.forward(seq, lens)
+    torch.manual_seed(5)
+    a2 = model.forward(seq, lens)
     assert not torch.equal(a, b)
+    assert torch.equal(a, a2)
     for m in model.modules():
         if isinstance(m, torch.nn.Dropout):
             m.p = 0.0
