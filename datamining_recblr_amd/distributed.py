@@ -20,21 +20,25 @@ __all__ = ["DistEnv", "init_from_env", "LossModule", "wrap_ddp", "synthetic_inte
 
 
 class DistEnv:
-    def __init__(self, rank=0, local_rank=0, world_size=1):
+    def __init__(self, rank=0, local_rank=0, world_size=1, forced=False):
         self.rank, self.local_rank, self.world_size = rank, local_rank, world_size
+        self.forced = forced
 
     @property
     def distributed(self):
-        return self.world_size > 1
+        return self.world_size > 1 or self.forced
 
 
 def init_from_env(backend: str | None = None) -> DistEnv:
-    """Read RANK / LOCAL_RANK / WORLD_SIZE (torchrun) and join the process group."""
+    """Read RANK / LOCAL_RANK / WORLD_SIZE (torchrun) and join the process group.
+
+    RB_FORCE_DIST=1 joins a group (and wraps in DDP) even at world size 1, to
+    exercise the RCCL/DDP path on a single-GPU machine."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    env = DistEnv(rank, local, world)
-    if world > 1 and not dist.is_initialized():
+    env = DistEnv(rank, local, world, forced=os.environ.get("RB_FORCE_DIST") == "1")
+    if env.distributed and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         if backend is None:
