@@ -56,7 +56,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 4; }
+int rb_version(void) { return 5; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -118,18 +118,19 @@ int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
 
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                      const float* z, int64_t z_rs, const float* lam, const float* carries,
-                     const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
-                     int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
-                     int64_t H, void* stream) {
+                     const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
+                     float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B,
+                     int64_t L, int64_t H, void* stream) {
   if (!rg || !xc || !z || !lam || !carries || !dy || !drg || !dxc || !dz || !part || !dh0_part)
     return fail("rb_gate_scan_bwd: null pointer");
-  if (rg_rs < 2 * H || xc_rs < H || z_rs < H || drg_rs < 2 * H || dz_rs < H)
+  if (rg_rs < 2 * H || xc_rs < H || z_rs < H || drg_rs < 2 * H || dxc_rs < H || dz_rs < H)
     return fail("rb_gate_scan_bwd: row stride too small");
   if (int r = check_dims("rb_gate_scan_bwd", B, L, H,
-                         max4(max4(rg_rs, xc_rs, z_rs, drg_rs), dz_rs, H)))
+                         max4(max4(rg_rs, xc_rs, z_rs, drg_rs), dz_rs, dxc_rs, H)))
     return r;
-  return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
-                         dz_rs, part, dh0_part, B, L, H, reinterpret_cast<hipStream_t>(stream));
+  return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+                         dxc_rs, dz, dz_rs, part, dh0_part, B, L, H,
+                         reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_add_ln_fwd(const float* a, const int64_t* idx, int64_t n_idx_rows, const uint8_t* mask,

@@ -140,8 +140,8 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     hipStream_t st);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* carries,
-                    const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
-                    int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
+                    const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
+                    float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
                     int64_t H, hipStream_t st);
 int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
                       const float* r, const float* gamma, const float* beta, float eps, float* y,

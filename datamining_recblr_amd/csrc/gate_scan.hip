@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(256)
 k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
                 const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
                 const float* __restrict__ carries, const float* __restrict__ dy,
-                float* __restrict__ drg, int drg_rs, float* __restrict__ dxc,
+                float* __restrict__ drg, int drg_rs, float* __restrict__ dxc, int dxc_rs,
                 float* __restrict__ dz, int dz_rs, float* __restrict__ part,
                 float* __restrict__ dh0_part, int64_t B, int L, int H, int ncw) {
   constexpr int G = kWave / Q;
@@ -181,7 +181,7 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   const float* zb = z + row0 * z_rs + cc;
   const float* dyb = dy + row0 * H + cc;
   float* drgb = drg + row0 * drg_rs + cc;
-  float* dxcb = dxc + row0 * H + cc;
+  float* dxcb = dxc + row0 * dxc_rs + cc;
   float* dzb = dz + row0 * dz_rs + cc;
 
   float lamv[VEC], nsp[VEC];
@@ -324,7 +324,7 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
         const int t = t0 + j;
         stv(drgb + t * drg_rs, dro);
         stv(drgb + t * drg_rs + H, dio);
-        stv(dxcb + t * H, dxo);
+        stv(dxcb + t * dxc_rs, dxo);
       }
     }
     if (tile == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ein);
@@ -402,15 +402,15 @@ int gate_fwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, c
 template <int V>
 int gate_bwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
                int64_t z_rs, const float* lam, const float* carries, const float* dy, float* drg,
-               int64_t drg_rs, float* dxc, float* dz, int64_t dz_rs, float* part,
+               int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz, int64_t dz_rs, float* part,
                float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const int span = (kWave / kBwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_bwd<V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, carries,
-                     dy, drg, (int)drg_rs, dxc, dz, (int)dz_rs, part, dh0_part, B, (int)L, (int)H,
-                     ncw);
+                     dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part, dh0_part, B,
+                     (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_bwd");
 }
 
@@ -430,21 +430,21 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* carries,
-                    const float* dy, float* drg, int64_t drg_rs, float* dxc, float* dz,
-                    int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
+                    const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
+                    float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
                     int64_t H, hipStream_t st) {
-  const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dz_rs};
+  const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
   const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)lam,
                      (const void*)carries, (const void*)dy, (const void*)drg, (const void*)dxc,
                      (const void*)dz, (const void*)part, (const void*)dh0_part};
   if (vec_ok<4>(H, strides, ptrs))
-    return gate_bwd_v<4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
-                         dz_rs, part, dh0_part, B, L, H, st);
+    return gate_bwd_v<4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+                         dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
   if (vec_ok<2>(H, strides, ptrs))
-    return gate_bwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
-                         dz_rs, part, dh0_part, B, L, H, st);
-  return gate_bwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc, dz,
-                       dz_rs, part, dh0_part, B, L, H, st);
+    return gate_bwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+                         dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+  return gate_bwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+                       dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
 }
 
 }  // namespace rb

@@ -222,14 +222,13 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None):
     drg_rs = _row_stride(drg, "drg", 2 * H)
     if dxc is None:
         dxc = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
-    elif not dxc.is_contiguous() or dxc.shape != (B, L, H):
-        raise ValueError("dxc must be contiguous [B, L, H]")
+    dxc_rs = _row_stride(dxc, "dxc", H)
     part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
     dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
-    _launch("rb_gate_scan_bwd", 9 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
-              lam.contiguous().data_ptr(), carries.data_ptr(), dy.data_ptr(), drg.data_ptr(),
-              drg_rs, dxc.data_ptr(), dz.data_ptr(), dz_rs, part.data_ptr(), dh0_part.data_ptr(),
-              B, L, H, _stream(xc))
+    _launch("rb_gate_scan_bwd", 9 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs,
+            z.data_ptr(), z_rs, lam.contiguous().data_ptr(), carries.data_ptr(), dy.data_ptr(),
+            drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
+            part.data_ptr(), dh0_part.data_ptr(), B, L, H, _stream(xc))
     sums = part.sum(1)
     return drg, dxc, sums[0], torch.cat([sums[1], sums[2]]), dh0_part.sum(0)
 

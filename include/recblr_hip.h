@@ -109,15 +109,15 @@ int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
                      void* stream);
 
 /* Backward of rb_gate_scan_fwd given dy = dL/dy ([B, L, H] contiguous).
- * Writes drg ([B, L, 2H] view: dr | di, row stride drg_rs), dxc ([B, L, H]
- * contiguous, the gate path's share of dL/dxc), dz (row stride dz_rs),
+ * Writes drg ([B, L, 2H] view: dr | di, row stride drg_rs), dxc (the gate
+ * path's share of dL/dxc, row stride dxc_rs), dz (row stride dz_rs),
  * part[3, B, H] = per-batch sums over t of {dlam, dr, di} and
  * dh0_part[B, H] = dL/dh_{-1} per batch row (caller sums over b). */
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t xc_rs, const float* z, int64_t z_rs,
                      const float* lam, const float* carries, const float* dy,
-                     float* drg, int64_t drg_rs, float* dxc, float* dz,
-                     int64_t dz_rs, float* part, float* dh0_part,
+                     float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
+                     float* dz, int64_t dz_rs, float* part, float* dh0_part,
                      int64_t B, int64_t L, int64_t H, void* stream);
 
 /* ---- blocks around the BD-LRU (RecurrentLayer / FeedForward / embedding) ---- */

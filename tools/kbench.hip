@@ -9,6 +9,8 @@
 #include "../datamining_recblr_amd/csrc/conv_silu.hip"
 #include "../datamining_recblr_amd/csrc/gate_scan.hip"
 #include "../datamining_recblr_amd/csrc/scan_rows.hip"
+#include "../datamining_recblr_amd/csrc/rownorm.hip"
+#include "../datamining_recblr_amd/csrc/embedding.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -50,25 +52,29 @@ static float* dalloc(int64_t n, uint32_t seed, float lo = -1.f, float hi = 1.f) 
   return p;
 }
 
+struct GateBufs {
+  float *rg, *xc, *z, *y, *car, *dy, *drg, *dxc, *dz, *part, *dh0, *lam;
+  int rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs;
+};
+
 template <int VEC, int Q, int TC, bool PF = false>
-void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, float* rg, float* xc,
-              float* z, float* lam, float* y, float* car, float* dy, float* drg, float* dxc,
-              float* dz, float* part, float* dh0, double N) {
+void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBufs g, double N) {
   constexpr int G = 64 / Q;
   const int ncw = (H + G * VEC - 1) / (G * VEC);
   const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
   char* f = (char*)malloc(64);
   snprintf(f, 64, "gate_fwd %s", nm);
   cs.push_back({f, 5 * N * 4, [=] {
-    hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
-                       xc, H, z, 2 * H, lam, nullptr, y, H, car, (int64_t)B, L, H, ncw);
+    hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, g.rg,
+                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, nullptr, g.y, H, g.car,
+                       (int64_t)B, L, H, ncw);
   }, {}});
   char* f2 = (char*)malloc(64);
   snprintf(f2, 64, "gate_bwd %s", nm);
   cs.push_back({f2, 9 * N * 4, [=] {
-    hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, rg, 2 * H,
-                       xc, H, z, 2 * H, lam, car, dy, drg, 2 * H, dxc, dz, 2 * H, part, dh0,
-                       (int64_t)B, L, H, ncw);
+    hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, g.rg,
+                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, g.car, g.dy, g.drg, g.drg_rs,
+                       g.dxc, g.dxc_rs, g.dz, g.dz_rs, g.part, g.dh0, (int64_t)B, L, H, ncw);
   }, {}});
 }
 
@@ -176,14 +182,18 @@ int main(int argc, char** argv) {
   CK(hipDeviceSynchronize());
 
   std::vector<Case> cs;
-#define GATE(V, Q, TC, PF, NM) add_gate<V, Q, TC, PF>(cs, NM, B, L, H, rg, xc, xz + H, lam, y, car, dy, drg, dxc, dz + H, part, dh0, N)
-  GATE(4, 4, 4, false, "v4 q4 tc4");
-  GATE(4, 4, 4, true, "v4 q4 tc4 pf");
-  GATE(2, 4, 4, false, "v2 q4 tc4");
-  GATE(2, 4, 4, true, "v2 q4 tc4 pf");
-  GATE(4, 8, 2, false, "v4 q8 tc2");
-  GATE(4, 8, 2, true, "v4 q8 tc2 pf");
-  GATE(2, 2, 8, true, "v2 q2 tc8 pf");
+  GateBufs sep{rg, xc, xz + H, y, car, dy, drg, dxc, dz + H, part, dh0, lam,
+               2 * H, H, 2 * H, 2 * H, H, 2 * H};
+  float* P = dalloc(3 * n, 31, -1, 1);   // [r | i | xc] rows
+  float* Qb = dalloc(3 * n, 32);          // [dr | di | dxc] rows
+  GateBufs comb{P, P + 2 * H, xz + H, y, car, dy, Qb, Qb + 2 * H, dz + H, part, dh0, lam,
+                3 * H, 3 * H, 2 * H, 3 * H, 3 * H, 2 * H};
+  add_gate<2, 4, 4, true>(cs, "v2 q4 tc4 pf  sep", B, L, H, sep, N);
+  add_gate<4, 8, 2, false>(cs, "v4 q8 tc2     sep", B, L, H, sep, N);
+  add_gate<2, 4, 4, true>(cs, "v2 q4 tc4 pf  comb", B, L, H, comb, N);
+  add_gate<4, 8, 2, false>(cs, "v4 q8 tc2     comb", B, L, H, comb, N);
+  add_gate<4, 4, 4, true>(cs, "v4 q4 tc4 pf  comb", B, L, H, comb, N);
+  add_gate<2, 8, 2, false>(cs, "v2 q8 tc2     comb", B, L, H, comb, N);
   add_conv<4, 4, 4, 8>(cs, "v4 q4 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
   add_conv<4, 4, 4, 4>(cs, "v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
   add_conv<4, 2, 4, 4>(cs, "v2 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
