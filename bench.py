@@ -22,6 +22,7 @@ import sys
 import time
 
 import torch
+import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -29,6 +30,7 @@ sys.path.insert(0, ROOT)
 from datamining_recblr_amd import kernels  # noqa: E402
 from datamining_recblr_amd.distributed import (barrier, init_from_env, max_over_ranks,  # noqa: E402
                                                synthetic_interaction, wrap_ddp)
+from datamining_recblr_amd.gemm_tuning import tuned_gemms_active  # noqa: E402
 from datamining_recblr_amd.model import RecBLR  # noqa: E402
 from datamining_recblr_amd.recbole_compat import SyntheticDataset  # noqa: E402
 
@@ -191,7 +193,8 @@ def main():
                     "ms_per_step": round(g["ms"] / args.steps, 3),
                     "gemms_per_step": g["launches"] / args.steps,
                     "flops_per_step": int(g["bytes"] / args.steps),
-                    "library": "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)"}
+                    "library": "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)",
+                    "tuned_table": tuned_gemms_active()}
         kernels_report = {}
         for name, d in summ.items():
             gbs = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
@@ -242,6 +245,9 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if dist.is_initialized():
+        barrier(env)
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

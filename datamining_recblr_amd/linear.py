@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import torch
 
-from . import kernels
+from . import gemm_tuning, kernels
 
 __all__ = ["linear", "wgrad", "LinearFn"]
 
@@ -83,4 +83,14 @@ class LinearFn(torch.autograd.Function):
 
 def linear(x: torch.Tensor, module: torch.nn.Linear) -> torch.Tensor:
     """module(x) with the split-K weight gradient."""
+    if _tuned is None and x.is_cuda:
+        _load_tuned()
     return LinearFn.apply(x, module.weight, module.bias)
+
+
+_tuned = None
+
+
+def _load_tuned():
+    global _tuned
+    _tuned = gemm_tuning.use_tuned_gemms()

@@ -142,3 +142,22 @@ def test_oracle_scan_reverse_matches_autograd_of_loop():
     torch.stack(outs, -1).backward(gy)
     torch.testing.assert_close(g.grad, g2.grad)
     torch.testing.assert_close(x.grad, x2.grad)
+
+
+def test_tuned_gemm_table_covers_bench_shapes():
+    """The shipped TunableOp table is well-formed and lists the C2 projection
+    GEMMs (B*L = 409,600 rows; K, N in {128, 256, 512})."""
+    import csv
+
+    from datamining_recblr_amd import gemm_tuning
+
+    rows = list(csv.reader(open(gemm_tuning.TABLE_PATH)))
+    validators = {r[1]: r[2] for r in rows if r[0] == "Validator"}
+    assert validators["GCN_ARCH_NAME"].startswith("gfx950")
+    assert "PT_VERSION" in validators and "HIPBLASLT_VERSION" in validators
+    entries = [r for r in rows if r[0] != "Validator"]
+    assert entries and all(len(r) == 4 and float(r[3]) > 0 for r in entries)
+    keys = " ".join(r[1] for r in entries)
+    for shape in ("512_409600_128", "512_409600_256", "128_409600_256", "128_409600_512"):
+        assert shape in keys
+    assert gemm_tuning.use_tuned_gemms() is False or torch.cuda.is_available()
