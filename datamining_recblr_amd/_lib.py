@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 5
+ABI_VERSION = 7
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -49,6 +49,16 @@ SIGNATURES = {
     "rb_dropout_mask": (ctypes.c_int, [_u64, _f32, _fp, _i64, _fp]),
     "rb_embedding_bwd_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
     "rb_embedding_bwd": (ctypes.c_int, [_fp, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp]),
+    "rb_item_ce_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
+    "rb_item_ce_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp, _i64, _fp]),
+    "rb_item_ce_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
+                                      _i64, _fp]),
+    "rb_item_rank_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
+    "rb_item_rank": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _i64,
+                                    _fp]),
+    "rb_item_ce_probs": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _i64, _fp, _i64,
+                                        _fp]),
+    "rb_item_scores": (ctypes.c_int, [_fp, _fp, _i64, _i64, _i64, _fp, _fp]),
 }
 
 

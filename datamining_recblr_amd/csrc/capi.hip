@@ -56,11 +56,11 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 5; }
+int rb_version(void) { return 7; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
-int rb_num_kernels(void) { return 12; }
+int rb_num_kernels(void) { return 20; }
 
 int rb_scan_fwd(const float* gates, const float* tokens, float* states, int64_t B, int64_t C,
                 int64_t T, void* stream) {
@@ -216,6 +216,75 @@ int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d
     return fail("rb_embedding_bwd: M or V too large");
   return launch_embedding_bwd(idx, grad, M, d, V, padding_idx, dweight, workspace,
                               workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+namespace {
+int check_items(const char* fn, const float* seq, const float* items, int64_t B, int64_t V,
+                int64_t d) {
+  (void)fn;
+  if (!seq || !items) return fail("item scores: null pointer");
+  if (B <= 0 || V <= 0) return fail("item scores: B and V must be positive");
+  if (d != 16 && d != 32 && d != 64 && d != 128 && d != 256)
+    return fail("item scores: d must be 16, 32, 64, 128 or 256");
+  if (!aligned16(seq) || !aligned16(items)) return fail("item scores: operands must be 16-B aligned");
+  if (B >= (int64_t(1) << 31) || V >= (int64_t(1) << 31)) return fail("item scores: B or V too large");
+  return 0;
+}
+}  // namespace
+
+int64_t rb_item_ce_workspace(int64_t B, int64_t V, int64_t d) {
+  if (B <= 0 || V <= 0 || d <= 0) return 0;
+  return item_ce_workspace_bytes(B, V, d);
+}
+
+int rb_item_ce_fwd(const float* seq, const float* items, const int64_t* target, int64_t B,
+                   int64_t V, int64_t d, float* lse, float* loss, void* workspace,
+                   int64_t workspace_bytes, void* stream) {
+  if (int rc = check_items("rb_item_ce_fwd", seq, items, B, V, d)) return rc;
+  if (!target || !lse || !loss || !workspace) return fail("rb_item_ce_fwd: null pointer");
+  return launch_item_ce_fwd(seq, items, target, B, V, d, lse, loss, workspace, workspace_bytes,
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_ce_bwd(const float* seq, const float* items, const int64_t* target, const float* lse,
+                   const float* dloss, int64_t B, int64_t V, int64_t d, float* dseq,
+                   float* ditems, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (int rc = check_items("rb_item_ce_bwd", seq, items, B, V, d)) return rc;
+  if (!target || !lse || !dloss || !workspace) return fail("rb_item_ce_bwd: null pointer");
+  return launch_item_ce_bwd(seq, items, target, lse, dloss, B, V, d, dseq, ditems, workspace,
+                            workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int64_t rb_item_rank_workspace(int64_t B, int64_t V, int64_t d) {
+  if (B <= 0 || V <= 0 || d <= 0) return 0;
+  return item_rank_workspace_bytes(B, V);
+}
+
+int rb_item_rank(const float* seq, const float* items, const int64_t* target, int64_t B,
+                 int64_t V, int64_t d, int64_t first_item, int64_t* n_greater, int64_t* n_equal,
+                 void* workspace, int64_t workspace_bytes, void* stream) {
+  if (int rc = check_items("rb_item_rank", seq, items, B, V, d)) return rc;
+  if (!target || !n_greater || !workspace) return fail("rb_item_rank: null pointer");
+  if (first_item < 0) return fail("rb_item_rank: first_item must be >= 0");
+  return launch_item_rank(seq, items, target, B, V, d, first_item, n_greater, n_equal, workspace,
+                          workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_ce_probs(const float* seq, const float* items, const int64_t* target,
+                     const float* lse, const float* dloss, int64_t B, int64_t V, int64_t d,
+                     int64_t item_offset, float* probs, int64_t ld, void* stream) {
+  if (int rc = check_items("rb_item_ce_probs", seq, items, B, V, d)) return rc;
+  if (!target || !lse || !dloss || !probs) return fail("rb_item_ce_probs: null pointer");
+  if (ld < V) return fail("rb_item_ce_probs: ld < V");
+  return launch_item_ce_probs(seq, items, target, lse, dloss, B, V, d, item_offset, V, probs, ld,
+                              reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,
+                   float* scores, void* stream) {
+  if (int rc = check_items("rb_item_scores", seq, items, B, V, d)) return rc;
+  if (!scores) return fail("rb_item_scores: null pointer");
+  return launch_item_scores(seq, items, B, V, d, scores, reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

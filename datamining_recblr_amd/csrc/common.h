@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 
@@ -162,6 +163,22 @@ int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
 int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
                          int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
                          hipStream_t st);
+int64_t item_ce_workspace_bytes(int64_t B, int64_t V, int64_t D);
+int64_t item_rank_workspace_bytes(int64_t B, int64_t V);
+int launch_item_ce_fwd(const float* E, const float* W, const int64_t* tgt, int64_t B, int64_t V,
+                       int64_t D, float* lse, float* loss, void* ws, int64_t ws_bytes,
+                       hipStream_t st);
+int launch_item_ce_bwd(const float* E, const float* W, const int64_t* tgt, const float* lse,
+                       const float* dloss, int64_t B, int64_t V, int64_t D, float* dE, float* dW,
+                       void* ws, int64_t ws_bytes, hipStream_t st);
+int launch_item_rank(const float* E, const float* W, const int64_t* tgt, int64_t B, int64_t V,
+                     int64_t D, int64_t first, int64_t* n_gt, int64_t* n_eq, void* ws,
+                     int64_t ws_bytes, hipStream_t st);
+int launch_item_ce_probs(const float* E, const float* W, const int64_t* tgt, const float* lse,
+                         const float* dloss, int64_t B, int64_t V, int64_t D, int64_t v_off,
+                         int64_t n_total, float* out, int64_t ld, hipStream_t st);
+int launch_item_scores(const float* E, const float* W, int64_t B, int64_t V, int64_t D,
+                       float* out, hipStream_t st);
 int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,
                     int64_t T, hipStream_t st);
 int launch_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,

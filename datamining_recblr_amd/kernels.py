@@ -17,6 +17,7 @@ from ._lib import RB_TILE, RecBLRNativeError
 __all__ = [
     "scan_fwd", "scan_bwd", "conv_silu_fwd", "conv_silu_bwd", "gate_scan_fwd",
     "gate_scan_bwd", "num_tiles", "RecBLRNativeError", "kernel_timing", "KernelTimer",
+    "item_ce_fwd", "item_ce_bwd", "item_ce_probs", "item_rank", "item_scores",
 ]
 
 
@@ -401,3 +402,114 @@ def embedding_bwd(idx, grad, num_rows, padding_idx=0):
     _launch("rb_embedding_bwd", 4 * M * d + 4 * num_rows * d, idx.data_ptr(), grad.data_ptr(), M,
             d, num_rows, pad, dw.data_ptr(), ws.data_ptr(), ws_bytes, _stream(grad))
     return dw
+
+
+# ---- item scoring (fp32 MFMA, no [B, V] logits) ------------------------------------
+# Launches timed in FLOPs rather than bytes (bench.py reports them against the
+# MFMA roofline).
+FLOP_KERNELS = frozenset({"rb_item_ce_fwd", "rb_item_ce_bwd", "rb_item_ce_probs", "rb_item_rank",
+                          "rb_item_scores"})
+ITEM_DIMS = (16, 32, 64, 128, 256)
+
+
+def _item_operands(seq, items, target=None):
+    _check(seq, "seq_output")
+    _check(items, "item table")
+    if seq.dim() != 2 or items.dim() != 2 or seq.shape[1] != items.shape[1]:
+        raise ValueError(f"seq [B, d] and items [V, d] required, got {tuple(seq.shape)} and "
+                         f"{tuple(items.shape)}")
+    if seq.shape[1] not in ITEM_DIMS:
+        raise ValueError(f"d = {seq.shape[1]} not in {ITEM_DIMS}")
+    seq = seq.contiguous()
+    items = items.contiguous()
+    if target is not None:
+        if target.dtype != torch.int64 or target.shape != (seq.shape[0],):
+            raise ValueError("target must be int64 [B]")
+        if target.device != seq.device:
+            raise ValueError("target must be on the same device")
+        target = target.contiguous()
+    return seq, items, target
+
+
+def item_ce_fwd(seq, items, target):
+    """(loss, lse): mean softmax cross-entropy of seq @ items^T against target."""
+    seq, items, target = _item_operands(seq, items, target)
+    B, d = seq.shape
+    V = items.shape[0]
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_item_ce_workspace(B, V, d))
+    ws = torch.empty((ws_bytes,), device=seq.device, dtype=torch.uint8)
+    lse = torch.empty((B,), device=seq.device, dtype=torch.float32)
+    loss = torch.empty((), device=seq.device, dtype=torch.float32)
+    _launch("rb_item_ce_fwd", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), target.data_ptr(),
+            B, V, d, lse.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws_bytes, _stream(seq))
+    return loss, lse
+
+
+def item_ce_bwd(seq, items, target, lse, dloss, want_seq=True, want_items=True):
+    """(dseq, ditems) of item_ce_fwd for the scalar upstream gradient dloss."""
+    seq, items, target = _item_operands(seq, items, target)
+    _check(lse, "lse")
+    _check(dloss, "dloss")
+    B, d = seq.shape
+    V = items.shape[0]
+    dloss = dloss.reshape(1).contiguous()
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_item_ce_workspace(B, V, d))
+    ws = torch.empty((ws_bytes,), device=seq.device, dtype=torch.uint8)
+    dseq = torch.empty_like(seq) if want_seq else None
+    ditems = torch.empty_like(items) if want_items else None
+    flops = 2 * B * V * d * (int(want_seq) + int(want_items))
+    _launch("rb_item_ce_bwd", flops, seq.data_ptr(), items.data_ptr(), target.data_ptr(),
+            lse.contiguous().data_ptr(), dloss.data_ptr(), B, V, d,
+            dseq.data_ptr() if dseq is not None else None,
+            ditems.data_ptr() if ditems is not None else None, ws.data_ptr(), ws_bytes,
+            _stream(seq))
+    return dseq, ditems
+
+
+def item_ce_probs(seq, items, target, lse, dloss, item_offset=0, out=None):
+    """P = (softmax - onehot) * dloss / B for the item rows `items` =
+    table[item_offset : item_offset + V] ([B, V], row stride of `out`)."""
+    seq, items, target = _item_operands(seq, items, target)
+    _check(lse, "lse")
+    _check(dloss, "dloss")
+    B, d = seq.shape
+    V = items.shape[0]
+    if out is None:
+        out = torch.empty((B, V), device=seq.device, dtype=torch.float32)
+    _check(out, "probs")
+    if out.shape != (B, V) or out.stride(1) != 1:
+        raise ValueError("probs must be [B, V] with unit column stride")
+    _launch("rb_item_ce_probs", 2 * B * V * d, seq.data_ptr(), items.data_ptr(),
+            target.data_ptr(), lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(),
+            B, V, d, int(item_offset), out.data_ptr(), out.stride(0), _stream(seq))
+    return out
+
+
+def item_rank(seq, items, target, first_item=1, want_equal=True):
+    """(n_greater, n_equal) int64 [B]: items in [first_item, V) other than the
+    target scoring above / equal to it (-1 for an out-of-range target)."""
+    seq, items, target = _item_operands(seq, items, target)
+    B, d = seq.shape
+    V = items.shape[0]
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_item_rank_workspace(B, V, d))
+    ws = torch.empty((ws_bytes,), device=seq.device, dtype=torch.uint8)
+    gt = torch.empty((B,), device=seq.device, dtype=torch.int64)
+    eq = torch.empty((B,), device=seq.device, dtype=torch.int64) if want_equal else None
+    _launch("rb_item_rank", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), target.data_ptr(),
+            B, V, d, int(first_item), gt.data_ptr(), eq.data_ptr() if eq is not None else None,
+            ws.data_ptr(), ws_bytes, _stream(seq))
+    return gt, eq
+
+
+def item_scores(seq, items):
+    """scores [B, V] = seq @ items^T on the same fma chain as the CE / rank kernels."""
+    seq, items, _ = _item_operands(seq, items)
+    B, d = seq.shape
+    V = items.shape[0]
+    out = torch.empty((B, V), device=seq.device, dtype=torch.float32)
+    _launch("rb_item_scores", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), B, V, d,
+            out.data_ptr(), _stream(seq))
+    return out

@@ -39,15 +39,15 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.T
     return out
 
 
-def _timed(kind, flops, fn, *args):
+def _timed(kind, flops, fn, *args, **kw):
     """Run a GEMM, bracketed by HIP events when bench.py's kernel timer is on."""
     t = kernels._timer
     if t is None:
-        return fn(*args)
+        return fn(*args, **kw)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    out = fn(*args)
+    out = fn(*args, **kw)
     e1.record()
     t.records.append((kind, flops, e0, e1))
     return out

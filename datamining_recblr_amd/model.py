@@ -31,6 +31,7 @@ from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, feed_forwa
 from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len
+from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
 __all__ = ["RecBLR", "RecurrentLayer", "GatedRecurrentLayer", "FeedForward",
            "softplus_inverse", "lambda_init_range"]
@@ -176,7 +177,7 @@ class RecBLR(SequentialRecommender):
         return self.gather_indexes(h, item_seq_len - 1)
 
     def _scores_all(self, seq_output):
-        return seq_output @ self.item_embedding.weight.t()
+        return full_sort_scores(seq_output, self.item_embedding.weight)
 
     def calculate_loss(self, interaction):
         seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
@@ -186,7 +187,8 @@ class RecBLR(SequentialRecommender):
             pos_score = (seq_output * self.item_embedding(pos_items)).sum(-1)
             neg_score = (seq_output * self.item_embedding(neg_items)).sum(-1)
             return self.loss_fct(pos_score, neg_score)
-        return self.loss_fct(self._scores_all(seq_output), pos_items)
+        # logits + nn.CrossEntropyLoss fused on MFMA, [B, n_items] never stored
+        return item_cross_entropy(seq_output, self.item_embedding.weight, pos_items)
 
     def predict(self, interaction):
         seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
@@ -195,3 +197,12 @@ class RecBLR(SequentialRecommender):
     def full_sort_predict(self, interaction):
         seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
         return self._scores_all(seq_output)
+
+    def full_sort_rank(self, interaction, first_item: int = 1):
+        """Rank of each row's target (POS_ITEM_ID) under full_sort_predict's
+        scores without materialising them: (n_greater, n_equal) over items
+        [first_item, n_items) (item 0 is RecBole's padding id, masked to -inf
+        by its full-sort evaluator)."""
+        seq_output = self.forward(interaction[self.ITEM_SEQ], interaction[self.ITEM_SEQ_LEN])
+        return target_ranks(seq_output, self.item_embedding.weight,
+                            interaction[self.POS_ITEM_ID], first_item)

@@ -1,0 +1,140 @@
+"""Scoring sequence representations against the whole item table.
+
+RecBLR.calculate_loss with loss_type "CE" (RecBLR.py:100-102) multiplies the
+[B, d] sequence representations by the [V, d] item table and applies
+nn.CrossEntropyLoss; full_sort_predict (RecBLR.py:114-122) returns the same
+[B, V] score matrix, which RecBole's evaluator (and run_with_unseen.py:229-265)
+reduces to the rank of each row's target item.  Here both run on the fp32
+MFMA kernels of csrc/item_scores.hip without materialising [B, V]:
+
+  * item_cross_entropy: forward computes the per-row log-sum-exp tile by
+    tile; backward recomputes the logits and forms dseq = P W and
+    ditems = P^T seq from P = softmax - onehot in registers;
+  * target_ranks: per row, the number of items scoring above / equal to the
+    target, from which Hit@k, MRR@k and NDCG@k follow exactly;
+  * full_sort_scores: the score matrix itself when a caller needs it.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn.functional as F
+
+from . import kernels
+
+__all__ = ["item_cross_entropy", "full_sort_scores", "target_ranks", "rank_metrics",
+           "supported"]
+
+
+def supported(seq: torch.Tensor, table: torch.Tensor) -> bool:
+    return (seq.is_cuda and seq.dtype == torch.float32 and table.dtype == torch.float32
+            and seq.dim() == 2 and seq.shape[-1] in kernels.ITEM_DIMS)
+
+
+# Backward strategy: "slices" writes the logits' gradient P one item slice at
+# a time (rb_item_ce_probs, at most PROBS_SLICE_BYTES) and runs dseq += P W,
+# ditems = P^T seq as library GEMMs; "fused" (rb_item_ce_bwd) recomputes the
+# logits inside the MFMA kernels and needs no [B, V] buffer at all.
+CE_BACKWARD = os.environ.get("RECBLR_CE_BACKWARD", "slices")
+PROBS_SLICE_BYTES = 1 << 30
+
+
+def _bwd_slices(seq, table, target, lse, dloss, want_seq, want_items):
+    from .linear import _timed
+
+    B, d = seq.shape
+    V = table.shape[0]
+    vc = max(32, min(V, PROBS_SLICE_BYTES // (4 * B)))
+    dseq = dtable = None
+    if want_items:
+        dtable = torch.empty_like(table)
+    for v0 in range(0, V, vc):
+        rows = table[v0:v0 + vc]
+        p = kernels.item_ce_probs(seq, rows, target, lse, dloss, item_offset=v0)
+        fl = 2 * B * rows.shape[0] * d
+        if want_seq:   # slices accumulate in a fixed order
+            dseq = (_timed("gemm", fl, torch.mm, p, rows) if dseq is None
+                    else _timed("gemm", fl, dseq.addmm_, p, rows))
+        if want_items:
+            _timed("gemm", fl, torch.mm, p.t(), seq, out=dtable[v0:v0 + vc])
+    return dseq, dtable
+
+
+class _ItemCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, seq, table, target):
+        seq, table = seq.contiguous(), table.contiguous()
+        loss, lse = kernels.item_ce_fwd(seq, table, target)
+        ctx.save_for_backward(seq, table, target, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dloss):
+        seq, table, target, lse = ctx.saved_tensors
+        want_seq, want_items = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        if CE_BACKWARD == "fused":
+            dseq, dtable = kernels.item_ce_bwd(seq, table, target, lse, dloss.float(),
+                                               want_seq=want_seq, want_items=want_items)
+        else:
+            dseq, dtable = _bwd_slices(seq, table, target, lse, dloss.float(), want_seq,
+                                       want_items)
+        return dseq, dtable, None
+
+
+def item_cross_entropy(seq: torch.Tensor, table: torch.Tensor,
+                       target: torch.Tensor) -> torch.Tensor:
+    """nn.CrossEntropyLoss()(seq @ table.T, target) without the [B, V] logits."""
+    if not supported(seq, table):
+        return F.cross_entropy(seq @ table.t(), target)
+    return _ItemCE.apply(seq, table, target)
+
+
+def full_sort_scores(seq: torch.Tensor, table: torch.Tensor) -> torch.Tensor:
+    """seq @ table.T ([B, V]); the MFMA kernel when no gradient is needed."""
+    if supported(seq, table) and not (torch.is_grad_enabled()
+                                      and (seq.requires_grad or table.requires_grad)):
+        return kernels.item_scores(seq, table)
+    return seq @ table.t()
+
+
+def target_ranks(seq: torch.Tensor, table: torch.Tensor, target: torch.Tensor,
+                 first_item: int = 1):
+    """(n_greater, n_equal) over items [first_item, V) other than the target.
+
+    first_item = 1 excludes the padding item 0, as RecBole's full-sort
+    evaluation does (scores[:, 0] = -inf) and as run_with_unseen.py:237 does
+    (scores[1:])."""
+    if not supported(seq, table):
+        raise kernels.RecBLRNativeError("target_ranks needs fp32 CUDA tensors with d in "
+                                        f"{kernels.ITEM_DIMS}")
+    return kernels.item_rank(seq.detach(), table.detach(), target, first_item=first_item)
+
+
+def rank_metrics(n_greater: torch.Tensor, n_equal: torch.Tensor | None = None,
+                 topk=(10, 20), ties: str = "optimistic") -> dict:
+    """Mean Hit@k, MRR@k and NDCG@k of single-target rows from their ranks.
+
+    ties="optimistic": rank = n_greater (the target placed first among equal
+    scores).  ties="average": the gain averaged over the positions the tied
+    group spans, as sklearn.metrics.ndcg_score(ignore_ties=False) does
+    (run_with_unseen.py:247); Hit/MRR then use the same averaging.
+    Rows with a negative rank (invalid target) are dropped."""
+    g = n_greater.double()
+    e = (n_equal.double() if n_equal is not None and ties == "average"
+         else torch.zeros_like(g))
+    keep = g >= 0
+    g, e = g[keep], e[keep]
+    out = {}
+    if g.numel() == 0:
+        for k in topk:
+            out[f"hit@{k}"] = out[f"mrr@{k}"] = out[f"ndcg@{k}"] = 0.0
+        return out
+    cnt = e + 1.0
+    for k in topk:
+        pos = torch.arange(k, dtype=torch.float64, device=g.device)[None, :]
+        hit = ((pos >= g[:, None]) & (pos <= (g + e)[:, None])).double()  # positions < k only
+        out[f"hit@{k}"] = float((hit.sum(1) / cnt).mean())
+        out[f"mrr@{k}"] = float(((hit / (pos + 1.0)).sum(1) / cnt).mean())
+        out[f"ndcg@{k}"] = float(((hit / torch.log2(pos + 2.0)).sum(1) / cnt).mean())
+    return out

@@ -180,6 +180,64 @@ int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d
                      int64_t V, int64_t padding_idx, float* dweight,
                      void* workspace, int64_t workspace_bytes, void* stream);
 
+/* ---- item scoring (RecBLR.py:86-122), fp32 MFMA, no [B, V] logits ----
+ * seq: [B, d] sequence representations (RecBLR.forward's output), items:
+ * [V, d] item table (item_embedding.weight), both contiguous and 16-B
+ * aligned; target: [B] int64 item ids.  d must be 16, 32, 64, 128 or 256.
+ * Deterministic (per-split partials summed in a fixed order). */
+
+/* Workspace bytes of rb_item_ce_fwd / rb_item_ce_bwd (one size serves both). */
+int64_t rb_item_ce_workspace(int64_t B, int64_t V, int64_t d);
+
+/* Softmax cross-entropy over all V items, mean over the batch
+ * (RecBLR.py:100-102: logits = seq @ items^T; nn.CrossEntropyLoss()):
+ *   lse[b] = log sum_v exp(seq[b] . items[v]),
+ *   loss[0] = mean_b (lse[b] - seq[b] . items[target[b]]).
+ * An out-of-range target makes loss NaN. */
+int rb_item_ce_fwd(const float* seq, const float* items, const int64_t* target, int64_t B,
+                   int64_t V, int64_t d, float* lse, float* loss, void* workspace,
+                   int64_t workspace_bytes, void* stream);
+
+/* Backward of rb_item_ce_fwd for the upstream gradient dloss[0] (a device
+ * scalar): with P[b][v] = (softmax_v(seq[b] . items) - [v == target[b]]) *
+ * dloss / B, dseq = P items and ditems = P^T seq.  The logits are recomputed
+ * tile by tile; either output may be NULL. */
+int rb_item_ce_bwd(const float* seq, const float* items, const int64_t* target, const float* lse,
+                   const float* dloss, int64_t B, int64_t V, int64_t d, float* dseq,
+                   float* ditems, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* The logits' gradient of rb_item_ce_fwd for a slice of the item table:
+ * items points at rows [item_offset, item_offset + V) of the table,
+ *   probs[b][v] = (softmax(seq[b] . table)[item_offset + v]
+ *                  - [item_offset + v == target[b]]) * dloss / B
+ * written with row stride ld >= V (lse from rb_item_ce_fwd).  With it the
+ * backward is two GEMMs, dseq += probs items and ditems = probs^T seq, at
+ * library speed; the slice bounds the [B, V] buffer for large tables.  The
+ * fully fused rb_item_ce_bwd needs no such buffer. */
+int rb_item_ce_probs(const float* seq, const float* items, const int64_t* target,
+                     const float* lse, const float* dloss, int64_t B, int64_t V, int64_t d,
+                     int64_t item_offset, float* probs, int64_t ld, void* stream);
+
+/* Workspace bytes of rb_item_rank. */
+int64_t rb_item_rank_workspace(int64_t B, int64_t V, int64_t d);
+
+/* Full-sort ranking of each row's target (the full_sort_predict evaluation,
+ * RecBLR.py:114-122 with RecBole's scores[:, 0] = -inf, and
+ * run_with_unseen.py:229-265): over items v in [first_item, V), v != target,
+ *   n_greater[b] = #{score(b, v) > score(b, target)},
+ *   n_equal[b]   = #{score(b, v) == score(b, target)}   (n_equal may be NULL).
+ * Hit@k = n_greater < k; NDCG@k and MRR follow from the rank.  The target's
+ * score is bit-identical to the tile's score for it.  -1 for an out-of-range
+ * target. */
+int rb_item_rank(const float* seq, const float* items, const int64_t* target, int64_t B,
+                 int64_t V, int64_t d, int64_t first_item, int64_t* n_greater, int64_t* n_equal,
+                 void* workspace, int64_t workspace_bytes, void* stream);
+
+/* scores[b][v] = seq[b] . items[v] (full_sort_predict, RecBLR.py:114-122), same
+ * fma chain as the kernels above; scores [B, V] contiguous. */
+int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,
+                   float* scores, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -161,3 +161,39 @@ def test_tuned_gemm_table_covers_bench_shapes():
     for shape in ("512_409600_128", "512_409600_256", "128_409600_256", "128_409600_512"):
         assert shape in keys
     assert gemm_tuning.use_tuned_gemms() is False or torch.cuda.is_available()
+
+
+def test_rank_metrics_match_sklearn_and_recbole():
+    """rank_metrics from (n_greater, n_equal) equals sklearn's tie-averaged
+    ndcg_score (run_with_unseen.py:247) and RecBole-style top-k metrics on an
+    explicit score matrix with ties."""
+    from sklearn.metrics import ndcg_score
+
+    from datamining_recblr_amd.scoring import rank_metrics
+
+    g = torch.Generator().manual_seed(0)
+    B, V = 64, 40
+    scores = torch.randint(0, 12, (B, V), generator=g).double()  # many ties
+    tgt = torch.randint(0, V, (B,), generator=g)
+    ts = scores[torch.arange(B), tgt]
+    others = torch.ones(B, V, dtype=torch.bool)
+    others[torch.arange(B), tgt] = False
+    gt = ((scores > ts[:, None]) & others).sum(1)
+    eq = ((scores == ts[:, None]) & others).sum(1)
+    y = torch.zeros(B, V)
+    y[torch.arange(B), tgt] = 1
+    for k in (5, 10):
+        ref = ndcg_score(y.numpy(), scores.numpy(), k=k)
+        m = rank_metrics(gt, eq, topk=(k,), ties="average")
+        assert abs(m[f"ndcg@{k}"] - ref) < 1e-12
+    # optimistic ranks: exact RecBole metrics when the target wins its ties
+    order = torch.argsort(-(scores + 1e-6 * (~others).double()), dim=1, stable=True)
+    pos = (order == tgt[:, None]).double().argmax(1).double()
+    m = rank_metrics(gt, eq, topk=(10,))
+    assert abs(m["hit@10"] - (pos < 10).double().mean().item()) < 1e-12
+    assert abs(m["mrr@10"] - torch.where(pos < 10, 1 / (pos + 1.0), 0.0).mean().item()) < 1e-12
+    ndcg = torch.where(pos < 10, 1 / torch.log2(pos + 2.0), 0.0).mean().item()
+    assert abs(m["ndcg@10"] - ndcg) < 1e-12
+    # invalid rows (-1) are dropped
+    m2 = rank_metrics(torch.cat([gt, torch.tensor([-1])]), None, topk=(10,))
+    assert abs(m2["hit@10"] - m["hit@10"]) < 1e-12
