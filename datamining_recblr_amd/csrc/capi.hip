@@ -56,7 +56,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 7; }
+int rb_version(void) { return 8; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -105,15 +105,16 @@ int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w, const float* 
 }
 
 int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                     const float* z, int64_t z_rs, const float* lam, const float* h0, float* y,
-                     int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-                     void* stream) {
+                     const float* z, int64_t z_rs, const float* lam, const float* h0,
+                     int64_t h0_bs, float* y, int64_t y_rs, float* carries, int64_t B, int64_t L,
+                     int64_t H, void* stream) {
   if (!rg || !xc || !z || !lam || !y) return fail("rb_gate_scan_fwd: null pointer");
+  if (h0_bs != 0 && h0_bs < H) return fail("rb_gate_scan_fwd: h0 batch stride must be 0 or >= H");
   if (rg_rs < 2 * H || xc_rs < H || z_rs < H || y_rs < H)
     return fail("rb_gate_scan_fwd: row stride too small");
   if (int r = check_dims("rb_gate_scan_fwd", B, L, H, max4(rg_rs, xc_rs, z_rs, y_rs))) return r;
-  return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, y, y_rs, carries, B, L, H,
-                         reinterpret_cast<hipStream_t>(stream));
+  return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, h0_bs, y, y_rs, carries, B, L,
+                         H, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,

@@ -136,9 +136,9 @@ int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* b
                     const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
                     float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st);
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                    const float* z, int64_t z_rs, const float* lam, const float* h0, float* y,
-                    int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-                    hipStream_t st);
+                    const float* z, int64_t z_rs, const float* lam, const float* h0,
+                    int64_t h0_bs, float* y, int64_t y_rs, float* carries, int64_t B, int64_t L,
+                    int64_t H, hipStream_t st);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* carries,
                     const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,

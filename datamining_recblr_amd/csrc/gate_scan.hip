@@ -37,7 +37,7 @@ template <int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
                 const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
-                const float* __restrict__ h0, float* __restrict__ y, int y_rs,
+                const float* __restrict__ h0, int h0_bs, float* __restrict__ y, int y_rs,
                 float* __restrict__ carries, int64_t B, int L, int H, int ncw) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
@@ -62,7 +62,7 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
 #pragma unroll
   for (int v = 0; v < VEC; ++v) nsp[v] = -softplus_f(nsp[v]);
   if (h0 != nullptr) {
-    ldv(carry, h0 + cc);
+    ldv(carry, h0 + b * h0_bs + cc);
   } else {
 #pragma unroll
     for (int v = 0; v < VEC; ++v) carry[v] = 0.0f;
@@ -388,14 +388,14 @@ bool vec_ok(int64_t H, std::initializer_list<int64_t> strides,
 
 template <int V>
 int gate_fwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
-               int64_t z_rs, const float* lam, const float* h0, float* y, int64_t y_rs,
-               float* carries, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+               int64_t z_rs, const float* lam, const float* h0, int64_t h0_bs, float* y,
+               int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_fwd<V, kFwdQ, kFwdTC, true>), dim3((unsigned)blocks),
-                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, h0, y,
-                     (int)y_rs, carries, B, (int)L, (int)H, ncw);
+                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, h0,
+                     (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_fwd");
 }
 
@@ -417,15 +417,17 @@ int gate_bwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, c
 }  // namespace
 
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                    const float* z, int64_t z_rs, const float* lam, const float* h0, float* y,
-                    int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-                    hipStream_t st) {
-  const auto strides = {rg_rs, xc_rs, z_rs, y_rs};
+                    const float* z, int64_t z_rs, const float* lam, const float* h0,
+                    int64_t h0_bs, float* y, int64_t y_rs, float* carries, int64_t B, int64_t L,
+                    int64_t H, hipStream_t st) {
+  const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
   const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y,
                      (const void*)lam, (const void*)h0, (const void*)carries};
   if (vec_ok<2>(H, strides, ptrs))
-    return gate_fwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, y, y_rs, carries, B, L, H, st);
-  return gate_fwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, y, y_rs, carries, B, L, H, st);
+    return gate_fwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, h0_bs, y, y_rs, carries, B, L,
+                         H, st);
+  return gate_fwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, h0_bs, y, y_rs, carries, B, L, H,
+                       st);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,

@@ -175,7 +175,8 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx):
 def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True):
     """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
 
-    rg: [B, L, 2H]; xc, z: [B, L, H] views; lam: [H]; h0: [H] or None.
+    rg: [B, L, 2H]; xc, z: [B, L, H] views; lam: [H]; h0: [H] (shared by every
+    row), [B, H] (one initial state per row) or None.
     Returns (y [B, L, H], carries [B, nT, H] or None when not wanted)."""
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (lam, "Lambda")):
         _check(t, n)
@@ -187,25 +188,28 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True):
         raise ValueError("rg, xc, z batch/length mismatch")
     if lam.shape != (H,):
         raise ValueError(f"Lambda must be [{H}]")
+    h0_bs = 0
     if h0 is not None:
         _check(h0, "h0")
-        if h0.shape != (H,):
-            raise ValueError(f"h0 must be [{H}]")
+        if h0.shape not in ((H,), (B, H)):
+            raise ValueError(f"h0 must be [{H}] or [{B}, {H}]")
         h0 = h0.contiguous()
+        h0_bs = H if h0.dim() == 2 else 0
     if y is None:
         y = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
     y_rs = _row_stride(y, "y", H)
     carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
                if want_carries else None)
     _launch("rb_gate_scan_fwd", 5 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
-              lam.contiguous().data_ptr(), 0 if h0 is None else h0.data_ptr(), y.data_ptr(),
+              lam.contiguous().data_ptr(), 0 if h0 is None else h0.data_ptr(), h0_bs, y.data_ptr(),
               y_rs, 0 if carries is None else carries.data_ptr(), B, L, H, _stream(xc))
     return y, carries
 
 
-def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None):
+def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=False):
     """Backward of gate_scan_fwd.  Writes dz (a row-strided view) and returns
-    (drg [B, L, 2H], dxc [B, L, H], dlam [H], dgate_bias [2H], dh0 [H])."""
+    (drg [B, L, 2H], dxc [B, L, H], dlam [H], dgate_bias [2H], dh0), dh0 [H]
+    (summed over rows) or [B, H] when dh0_rows (a per-row h0)."""
     B, L, H = xc.shape
     _check(dy, "dy")
     _check(dz, "dz")
@@ -231,7 +235,8 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None):
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
             part.data_ptr(), dh0_part.data_ptr(), B, L, H, _stream(xc))
     sums = part.sum(1)
-    return drg, dxc, sums[0], torch.cat([sums[1], sums[2]]), dh0_part.sum(0)
+    return (drg, dxc, sums[0], torch.cat([sums[1], sums[2]]),
+            dh0_part if dh0_rows else dh0_part.sum(0))
 
 
 # ---------------------------------------------------------------- row blocks

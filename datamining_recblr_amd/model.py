@@ -30,7 +30,7 @@ from ._lib import RecBLRNativeError
 from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, feed_forward
 from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
-from .recurrence import bd_lru, pow2_pad_len
+from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
 __all__ = ["RecBLR", "RecurrentLayer", "GatedRecurrentLayer", "FeedForward",
@@ -71,14 +71,16 @@ class GatedRecurrentLayer(nn.Module):
         self.Lambda = nn.Parameter(torch.linspace(lo, hi, hidden))
         self.output = nn.Linear(hidden, d_model, bias=False)
 
-    def forward(self, x):
+    def forward(self, x, pad=None):
+        """pad: None (the reference's pow2 pad prefix for x's length) or an
+        int64 tensor [B] of per-row pad lengths (see recurrence.bd_lru)."""
         if x.device.type != "cuda":
             raise RecBLRNativeError(
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
                 "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
         xz = linear(x, self.input)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
-                   self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d)
+                   self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad)
         return linear(y, self.output)
 
     @staticmethod
@@ -115,8 +117,8 @@ class RecurrentLayer(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
         self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
 
-    def forward(self, input_tensor):
-        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor), input_tensor,
+    def forward(self, input_tensor, pad=None):
+        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad), input_tensor,
                                    self.dropout, self.layer_norm, self.training)
         return h if self.disable_ffn else self.ffn(h)
 
@@ -169,11 +171,17 @@ class RecBLR(SequentialRecommender):
         if isinstance(module, nn.Linear) and module.bias is not None:
             module.bias.data.zero_()
 
-    def forward(self, item_seq, item_seq_len):
+    def forward(self, item_seq, item_seq_len, exact_lengths: bool = False):
+        """RecBLR.py:75-84.  exact_lengths=True makes each row behave as the
+        batch-1 forward of its unpadded sequence item_seq[b, :len_b] (its own
+        pow2 pad prefix), so users of different lengths batch together
+        without changing results (run_with_unseen.py:222-225 runs them one
+        by one)."""
+        pad = row_pad_lens(item_seq_len) if exact_lengths else None
         h = embed_dropout_layer_norm(item_seq, self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
         for layer in self.recurrent_layers:
-            h = layer(h)
+            h = layer(h, pad)
         return self.gather_indexes(h, item_seq_len - 1)
 
     def _scores_all(self, seq_output):

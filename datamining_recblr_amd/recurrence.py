@@ -30,7 +30,7 @@ import torch.nn.functional as F
 from . import kernels
 from .linear import _timed, wgrad
 
-__all__ = ["pow2_pad_len", "pad_prefix_state", "BDLRUCore", "bd_lru"]
+__all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "BDLRUCore", "bd_lru"]
 
 
 def pow2_pad_len(seq_len: int) -> int:
@@ -38,11 +38,13 @@ def pow2_pad_len(seq_len: int) -> int:
     return (1 << (seq_len - 1).bit_length()) - seq_len
 
 
-def pad_prefix_state(conv_bias, gate_w, gate_b, lam, pad_len: int):
+def pad_prefix_state(conv_bias, gate_w, gate_b, lam, pad_len):
     """Recurrent state after the ``pad_len`` constant pad steps (see module doc).
 
-    All operands are ``[H]`` / ``[2H, H]`` parameters; the result is ``[H]`` and
-    differentiable w.r.t. every one of them."""
+    All operands are ``[H]`` / ``[2H, H]`` parameters.  ``pad_len`` is an int
+    (result ``[H]``) or an int64 tensor ``[B]`` of per-row pad lengths (result
+    ``[B, H]``, for rows that stand for sequences of different true lengths).
+    Differentiable w.r.t. every parameter."""
     xc_p = F.silu(conv_bias)
     r_p, i_p = F.linear(xc_p, gate_w, gate_b).chunk(2, dim=-1)
     s = F.softplus(lam) * torch.sigmoid(r_p)          # alpha_p = exp(-s)
@@ -50,6 +52,8 @@ def pad_prefix_state(conv_bias, gate_w, gate_b, lam, pad_len: int):
     beta = torch.sqrt(1 - alpha * alpha + 1e-8) * torch.sigmoid(i_p)
     b_p = beta * xc_p
     s = s.clamp_min(1e-20)
+    if torch.is_tensor(pad_len):
+        pad_len = pad_len.to(s.dtype)[:, None]
     # sum_{k<P} alpha^k = (1 - alpha^P) / (1 - alpha), cancellation-free
     return b_p * (torch.expm1(-pad_len * s) / torch.expm1(-s))
 
@@ -73,6 +77,7 @@ class BDLRUCore(torch.autograd.Function):
         y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train)
         ctx.use_conv = use_conv
         ctx.has_h0 = h0 is not None
+        ctx.h0_rows = h0 is not None and h0.dim() == 2
         ctx.save_for_backward(xz, xc if use_conv else None, rg, carries, conv_w, conv_b,
                               gate_w, lam)
         return y
@@ -88,7 +93,7 @@ class BDLRUCore(torch.autograd.Function):
         dy = dy.contiguous()
         dxz = torch.empty_like(xz)
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
-            rg, xc, z, lam, carries, dy, dxz[..., H:])
+            rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows)
         drg2 = drg.view(B * L, H2)
         gflops = 2 * B * L * H * H2
         dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(B * L, H))
@@ -104,9 +109,26 @@ class BDLRUCore(torch.autograd.Function):
                 dh0 if ctx.has_h0 else None, None)
 
 
-def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True):
-    """Everything between the in- and out-projections of RecBLR.py:170-207."""
-    L = xz.shape[1]
-    P = pow2_pad_len(L)
-    h0 = pad_prefix_state(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
+def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
+    """Per-row pow2 pad lengths pow2(n) - n of sequences of true lengths n."""
+    n = lengths.clamp_min(1).to(torch.int64)
+    p2 = torch.pow(2, torch.ceil(torch.log2(n.double()))).to(torch.int64)
+    p2 = torch.where(p2 < n, p2 * 2, p2)        # guard log2 rounding
+    p2 = torch.where(p2 // 2 >= n, p2 // 2, p2)
+    return p2 - n
+
+
+def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None):
+    """Everything between the in- and out-projections of RecBLR.py:170-207.
+
+    pad=None: the reference's pad prefix pow2(L) - L for the batch's L.
+    pad=int64 tensor [B]: row b behaves as a sequence whose forward ran with
+    its own pad prefix pad[b] (a row right-padded from its true length n_b
+    with pad[b] = pow2(n_b) - n_b reproduces a batch-1 forward on the
+    unpadded sequence, run_with_unseen.py:222-225)."""
+    if pad is None:
+        P = pow2_pad_len(xz.shape[1])
+        h0 = pad_prefix_state(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
+    else:
+        h0 = pad_prefix_state(conv_b, gate_w, gate_b, lam, pad) if use_conv else None
     return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv)

@@ -104,8 +104,8 @@ int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w,
  * may be NULL for inference (no checkpoints written). */
 int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t xc_rs, const float* z, int64_t z_rs,
-                     const float* lam, const float* h0, float* y, int64_t y_rs,
-                     float* carries, int64_t B, int64_t L, int64_t H,
+                     const float* lam, const float* h0, int64_t h0_bs, float* y,
+                     int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
                      void* stream);
 
 /* Backward of rb_gate_scan_fwd given dy = dL/dy ([B, L, H] contiguous).
