@@ -24,7 +24,7 @@ from . import kernels
 from ._lib import RecBLRNativeError
 from .linear import _timed, linear, wgrad
 
-__all__ = ["draw_seed", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
+__all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
            "feed_forward"]
 
 
@@ -44,15 +44,28 @@ def _require_gpu(t):
             "the RecBLR blocks run on the MI355X HIP path only (ROCm GPU tensors)")
 
 
+class ResidualGrad:
+    """Carries the residual branch's gradient of RecurrentLayer (RecBLR.py:142,
+    LN(dropout(GRL(x)) + x)) from the LayerNorm backward to the backward of
+    the GRL's input projection, whose dX GEMM adds it with beta = 1
+    (linear.LinearFn) instead of autograd summing two [B, L, d] gradients in
+    a separate pass.  The LayerNorm backward always runs first (the
+    projection's gradient depends on it)."""
+    __slots__ = ("ds",)
+
+    def __init__(self):
+        self.ds = None
+
+
 class _AddDropoutLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, r, gamma, beta, mask, seed, p, eps):
+    def forward(ctx, a, r, gamma, beta, mask, seed, p, eps, slot=None):
         d = a.shape[-1]
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a.reshape(-1, d).contiguous(),
                                               r.reshape(-1, d).contiguous(), gamma, beta, eps,
                                               mask=mask, seed=seed, p=p, save=save)
-        ctx.seed, ctx.p = seed, p
+        ctx.seed, ctx.p, ctx.slot = seed, p, slot
         ctx.save_for_backward(s, mean, rstd, gamma, mask)
         return y.view(a.shape)
 
@@ -64,8 +77,11 @@ class _AddDropoutLN(torch.autograd.Function):
                                                seed=ctx.seed, p=ctx.p, want_ds=need_r,
                                                want_da=need_a or not need_r)
         shape = dy.shape
+        if need_r and ctx.slot is not None:   # handed to the GRL input projection
+            ctx.slot.ds = ds
+            ds, need_r = None, False
         return (da.view(shape) if need_a else None, ds.view(shape) if need_r else None,
-                dg, db, None, None, None, None)
+                dg, db, None, None, None, None, None)
 
 
 class _EmbedDropoutLN(torch.autograd.Function):
@@ -136,19 +152,20 @@ class _FeedForward(torch.autograd.Function):
         du = _timed("gemm", f, torch.mm, da2, w2)
         dw2 = _timed("gemm", f, wgrad, da2, u)
         da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True)
-        dx = _timed("gemm", f, torch.addmm, ds, da1, w1)   # residual grad + W1^T path
+        dx = _timed("gemm", f, ds.addmm_, da1, w1)   # residual grad + W1^T path, in place
         dw1 = _timed("gemm", f, wgrad, da1, x2)
         return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None)
 
 
 def add_dropout_layer_norm(a, residual, dropout: torch.nn.Dropout, ln: torch.nn.LayerNorm,
-                           training: bool):
-    """ln(dropout(a) + residual) — RecBLR.py:142."""
+                           training: bool, slot: ResidualGrad | None = None):
+    """ln(dropout(a) + residual) — RecBLR.py:142.  With `slot`, the residual's
+    gradient is handed over instead of returned (see ResidualGrad)."""
     _require_gpu(a)
     if a.shape[-1] not in kernels.ROW_SIZES:
         return ln(dropout(a) + residual)
     p, seed = _drop(dropout, training)
-    return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, None, seed, p, ln.eps)
+    return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, None, seed, p, ln.eps, slot)
 
 
 def embed_dropout_layer_norm(idx, emb: torch.nn.Embedding, dropout: torch.nn.Dropout,

@@ -56,11 +56,11 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 8; }
+int rb_version(void) { return 10; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
-int rb_num_kernels(void) { return 20; }
+int rb_num_kernels(void) { return 24; }
 
 int rb_scan_fwd(const float* gates, const float* tokens, float* states, int64_t B, int64_t C,
                 int64_t T, void* stream) {
@@ -286,6 +286,38 @@ int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, i
   if (int rc = check_items("rb_item_scores", seq, items, B, V, d)) return rc;
   if (!scores) return fail("rb_item_scores: null pointer");
   return launch_item_scores(seq, items, B, V, d, scores, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gate_b,
+                      const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
+                      int64_t H, float* h0, void* stream) {
+  if (!conv_b || !gate_w || !gate_b || !lam || !h0) return fail("rb_pad_prefix_fwd: null pointer");
+  if (H <= 0 || H > 4096 || n_rows <= 0 || pad_len < 0)
+    return fail("rb_pad_prefix_fwd: need 0 < H <= 4096, n_rows > 0, pad_len >= 0");
+  return launch_pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad, pad_len, n_rows, H, h0,
+                               reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_pad_prefix_bwd(const float* conv_b, const float* gate_w, const float* gate_b,
+                      const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
+                      int64_t H, const float* dh0, float* dconv_b, float* dgate_w,
+                      float* dgate_b, float* dlam, void* stream) {
+  if (!conv_b || !gate_w || !gate_b || !lam || !dh0 || !dconv_b || !dgate_w || !dgate_b || !dlam)
+    return fail("rb_pad_prefix_bwd: null pointer");
+  if (H <= 0 || H > 4096 || n_rows <= 0 || pad_len < 0)
+    return fail("rb_pad_prefix_bwd: need 0 < H <= 4096, n_rows > 0, pad_len >= 0");
+  return launch_pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad, pad_len, n_rows, H, dh0,
+                               dconv_b, dgate_w, dgate_b, dlam,
+                               reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
+              float* out, void* stream) {
+  if (!in || !out) return fail("rb_colsum: null pointer");
+  if (M <= 0 || P <= 0 || C <= 0 || rs < C || (M > 1 && ms < P * rs))
+    return fail("rb_colsum: bad shape or strides");
+  if (M * ((C + 63) / 64) > 0x7fffffffLL) return fail("rb_colsum: grid too large");
+  return launch_colsum(in, M, P, C, rs, ms, out, reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

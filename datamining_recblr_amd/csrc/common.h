@@ -179,6 +179,15 @@ int launch_item_ce_probs(const float* E, const float* W, const int64_t* tgt, con
                          int64_t n_total, float* out, int64_t ld, hipStream_t st);
 int launch_item_scores(const float* E, const float* W, int64_t B, int64_t V, int64_t D,
                        float* out, hipStream_t st);
+int launch_pad_prefix_fwd(const float* conv_b, const float* gw, const float* gb,
+                          const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
+                          int64_t H, float* h0, hipStream_t st);
+int launch_pad_prefix_bwd(const float* conv_b, const float* gw, const float* gb,
+                          const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
+                          int64_t H, const float* dh0, float* dconv_b, float* dgw, float* dgb,
+                          float* dlam, hipStream_t st);
+int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
+                  float* out, hipStream_t st);
 int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,
                     int64_t T, hipStream_t st);
 int launch_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,

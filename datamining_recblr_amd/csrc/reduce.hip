@@ -1,0 +1,58 @@
+// reduce.hip — fixed-order column sums of per-block / per-split partials.
+//
+// Every backward kernel here writes partial sums (per batch row, per row
+// block, per split-K slice) instead of using atomics; this one launch turns
+// them into the final gradients.  It replaces torch's sum(0), which for
+// these shapes costs a hipMemset of a semaphore buffer plus a reduction
+// launch, and fixes the summation order independently of the device:
+//   out[m, c] = ((S_0 + S_1) + ...) + S_{RG-1},  S_g = sum_{p = g, g+RG, ...} in[m, p, c]
+// with RG = 4 (P <= 256) or 16 row groups, each S_g summed in increasing p.
+#include "common.h"
+
+namespace rb {
+namespace {
+
+template <int RG>
+__global__ __launch_bounds__(64 * RG) void k_colsum(const float* __restrict__ in, int64_t P,
+                                                    int64_t C, int64_t rs, int64_t ms,
+                                                    int64_t cblocks, float* __restrict__ out) {
+  __shared__ float red[RG][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t m = blockIdx.x / cblocks;
+  const int64_t c = (blockIdx.x - m * cblocks) * 64 + tx;
+  const float* base = in + m * ms + c;
+  float s = 0.0f;
+  if (c < C) {
+    int64_t p = ty;
+    for (; p + 3 * RG < P; p += 4 * RG) {   // 4 independent loads in flight, order kept
+      const float a = base[p * rs], b = base[(p + RG) * rs];
+      const float d = base[(p + 2 * RG) * rs], e = base[(p + 3 * RG) * rs];
+      s = (((s + a) + b) + d) + e;
+    }
+    for (; p < P; p += RG) s += base[p * rs];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    float t = red[0][tx];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) t += red[g][tx];
+    out[m * C + c] = t;
+  }
+}
+
+}  // namespace
+
+int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
+                  float* out, hipStream_t st) {
+  const int64_t cblocks = (C + 63) / 64;
+  const unsigned grid = (unsigned)(M * cblocks);
+  if (P <= 256)
+    hipLaunchKernelGGL(k_colsum<4>, dim3(grid), dim3(256), 0, st, in, P, C, rs, ms, cblocks, out);
+  else
+    hipLaunchKernelGGL(k_colsum<16>, dim3(grid), dim3(1024), 0, st, in, P, C, rs, ms, cblocks,
+                       out);
+  return launch_status("rb_colsum");
+}
+
+}  // namespace rb

@@ -68,6 +68,26 @@ def _launch(name: str, nbytes: int, *args) -> None:
     t.records.append((name, nbytes, e0, e1))
 
 
+def colsum(x: torch.Tensor) -> torch.Tensor:
+    """Fixed-order sum over dim -2 of a [P, C] or [M, P, C] tensor whose last
+    dim is unit-stride (rb_colsum; replaces torch's sum(-2), which needs a
+    semaphore memset and another launch at these shapes)."""
+    _check(x, "partials")
+    squeeze = x.dim() == 2
+    x3 = x[None] if squeeze else x
+    if x3.dim() != 3:
+        raise ValueError("colsum expects [P, C] or [M, P, C]")
+    if x3.stride(2) != 1:
+        x3 = x3.contiguous()
+    M, P, C = x3.shape
+    out = torch.empty((M, C), device=x.device, dtype=torch.float32)
+    if P == 0:
+        return out.zero_()[0] if squeeze else out.zero_()
+    _lib.call("rb_colsum", x3.data_ptr(), M, P, C, x3.stride(1), x3.stride(0) if M > 1 else P * C,
+              out.data_ptr(), _stream(x))
+    return out[0] if squeeze else out
+
+
 def num_tiles(L: int) -> int:
     return (L + RB_TILE - 1) // RB_TILE
 
@@ -169,7 +189,7 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx):
     _launch("rb_conv_silu_bwd", (3 if g2 is None else 4) * B * L * H * 4, x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
               g1.data_ptr(), 0 if g2 is None else g2.data_ptr(), dx.data_ptr(), dx_rs,
               dw_part.data_ptr(), db_part.data_ptr(), B, L, H, K, _stream(x))
-    return dw_part.sum(0).t().contiguous(), db_part.sum(0)
+    return colsum(dw_part.view(B, -1)).view(-1, H).t().contiguous(), colsum(db_part)
 
 
 def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True):
@@ -234,9 +254,9 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
             z.data_ptr(), z_rs, lam.contiguous().data_ptr(), carries.data_ptr(), dy.data_ptr(),
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
             part.data_ptr(), dh0_part.data_ptr(), B, L, H, _stream(xc))
-    sums = part.sum(1)
-    return (drg, dxc, sums[0], torch.cat([sums[1], sums[2]]),
-            dh0_part if dh0_rows else dh0_part.sum(0))
+    sums = colsum(part)
+    return (drg, dxc, sums[0], sums[1:].reshape(-1),
+            dh0_part if dh0_rows else colsum(dh0_part))
 
 
 # ---------------------------------------------------------------- row blocks
@@ -324,9 +344,9 @@ def add_ln_bwd(dy, s, gamma, mean, rstd, mask=None, seed=0, p=0.0, want_ds=True,
     _check_mask(mask, (rows, d))
     nparts = row_num_parts(rows, d)
     dev = s.device
-    dgp = torch.empty((nparts, d), device=dev, dtype=torch.float32)
-    dbp = torch.empty((nparts, d), device=dev, dtype=torch.float32)
-    dbias_p = torch.empty((nparts, d), device=dev, dtype=torch.float32) if want_dbias else None
+    parts = torch.empty((3 if want_dbias else 2, nparts, d), device=dev, dtype=torch.float32)
+    dgp, dbp = parts[0], parts[1]
+    dbias_p = parts[2] if want_dbias else None
     ds = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_ds else None
     da = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_da else None
     n = rows * d
@@ -335,7 +355,8 @@ def add_ln_bwd(dy, s, gamma, mean, rstd, mask=None, seed=0, p=0.0, want_ds=True,
             mean.data_ptr(), rstd.data_ptr(), _ptr(mask), int(seed), float(p), _ptr(ds),
             _ptr(da), dgp.data_ptr(), dbp.data_ptr(), _ptr(dbias_p), nparts, rows, d,
             _stream(dy))
-    return ds, da, dgp.sum(0), dbp.sum(0), (dbias_p.sum(0) if want_dbias else None)
+    sums = colsum(parts)
+    return ds, da, sums[0], sums[1], (sums[2] if want_dbias else None)
 
 
 def _rows_cols(a):
@@ -374,7 +395,7 @@ def silu_dropout_bwd(a, du, mask=None, seed=0, p=0.0, want_dbias=False):
     _launch("rb_silu_dropout_bwd", 12 * n + (n if mask is not None else 0), a.data_ptr(),
             _ptr(mask), int(seed), float(p), du.data_ptr(), da.data_ptr(), _ptr(dbias_p), nparts,
             rows, cols, _stream(a))
-    return da, (dbias_p.sum(0) if want_dbias else None)
+    return da, (colsum(dbias_p) if want_dbias else None)
 
 
 def dropout_mask(seed, p, shape, device):
@@ -518,3 +539,45 @@ def item_scores(seq, items):
     _launch("rb_item_scores", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), B, V, d,
             out.data_ptr(), _stream(seq))
     return out
+
+
+# ---- pad-prefix state (RecBLR.py:176-179) -------------------------------------------
+def _pad_args(pad_len, H, device):
+    if torch.is_tensor(pad_len):
+        pad = pad_len.to(device=device, dtype=torch.int64).contiguous()
+        return pad, 0, pad.numel()
+    return None, int(pad_len), 1
+
+
+def pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad_len):
+    """h0 [H] (int pad_len) or [B, H] (int64 tensor pad_len [B])."""
+    for t, n in ((conv_b, "conv bias"), (gate_w, "gates weight"), (gate_b, "gates bias"),
+                 (lam, "Lambda")):
+        _check(t, n)
+    H = lam.shape[0]
+    if gate_w.shape != (2 * H, H) or conv_b.shape != (H,) or gate_b.shape != (2 * H,):
+        raise ValueError("pad prefix: parameter shapes")
+    pad, plen, rows = _pad_args(pad_len, H, lam.device)
+    h0 = torch.empty((rows, H), device=lam.device, dtype=torch.float32)
+    _lib.call("rb_pad_prefix_fwd", conv_b.contiguous().data_ptr(), gate_w.contiguous().data_ptr(),
+              gate_b.contiguous().data_ptr(), lam.contiguous().data_ptr(),
+              pad.data_ptr() if pad is not None else None, plen, rows, H, h0.data_ptr(),
+              _stream(lam))
+    return h0 if pad is not None else h0[0]
+
+
+def pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad_len, dh0):
+    """(dconv_b, dgate_w, dgate_b, dlam) for dh0 shaped like pad_prefix_fwd's h0."""
+    _check(dh0, "dh0")
+    H = lam.shape[0]
+    pad, plen, rows = _pad_args(pad_len, H, lam.device)
+    dh0 = dh0.reshape(rows, H).contiguous()
+    dcb = torch.empty_like(conv_b)
+    dgw = torch.empty_like(gate_w)
+    dgb = torch.empty_like(gate_b)
+    dlam = torch.empty_like(lam)
+    _lib.call("rb_pad_prefix_bwd", conv_b.contiguous().data_ptr(), gate_w.contiguous().data_ptr(),
+              gate_b.contiguous().data_ptr(), lam.contiguous().data_ptr(),
+              pad.data_ptr() if pad is not None else None, plen, rows, H, dh0.data_ptr(),
+              dcb.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), dlam.data_ptr(), _stream(lam))
+    return dcb, dgw, dgb, dlam

@@ -33,7 +33,7 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.T
     main = mk * splits
     a = dy2[:main].unflatten(0, (splits, mk)).transpose(1, 2)
     b = x2[:main].unflatten(0, (splits, mk))
-    out = torch.bmm(a, b).sum(0)
+    out = kernels.colsum(torch.bmm(a, b).view(splits, -1)).view(a.shape[1], b.shape[2])
     if main < M:
         out += dy2[main:].t() @ x2[main:]
     return out
@@ -55,7 +55,7 @@ def _timed(kind, flops, fn, *args, **kw):
 
 class LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, slot=None):
         x2 = x.reshape(-1, x.shape[-1])
         flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
         if bias is not None:
@@ -64,6 +64,7 @@ class LinearFn(torch.autograd.Function):
             y = _timed("gemm", flops, torch.mm, x2, weight.t())
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
+        ctx.slot = slot
         return y.view(*x.shape[:-1], weight.shape[0])
 
     @staticmethod
@@ -73,19 +74,26 @@ class LinearFn(torch.autograd.Function):
         flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = _timed("gemm", flops, torch.mm, dy2, weight).view(*dy.shape[:-1], weight.shape[1])
+            slot = ctx.slot
+            if slot is not None and slot.ds is not None:   # + a handed-over residual gradient
+                dx = _timed("gemm", flops, slot.ds.view(-1, weight.shape[1]).addmm_, dy2, weight)
+                slot.ds = None
+            else:
+                dx = _timed("gemm", flops, torch.mm, dy2, weight)
+            dx = dx.view(*dy.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _timed("gemm", flops, wgrad, dy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy2.sum(0)
-        return dx, dw, db
+            db = kernels.colsum(dy2.contiguous())
+        return dx, dw, db, None
 
 
-def linear(x: torch.Tensor, module: torch.nn.Linear) -> torch.Tensor:
-    """module(x) with the split-K weight gradient."""
+def linear(x: torch.Tensor, module: torch.nn.Linear, slot=None) -> torch.Tensor:
+    """module(x) with the split-K weight gradient; `slot` (blocks.ResidualGrad)
+    adds a residual gradient inside the dX GEMM."""
     if _tuned is None and x.is_cuda:
         _load_tuned()
-    return LinearFn.apply(x, module.weight, module.bias)
+    return LinearFn.apply(x, module.weight, module.bias, slot)
 
 
 _tuned = None

@@ -27,7 +27,8 @@ import torch.nn.functional as F
 from torch import nn
 
 from ._lib import RecBLRNativeError
-from .blocks import add_dropout_layer_norm, embed_dropout_layer_norm, feed_forward
+from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
+                     feed_forward)
 from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
@@ -71,14 +72,15 @@ class GatedRecurrentLayer(nn.Module):
         self.Lambda = nn.Parameter(torch.linspace(lo, hi, hidden))
         self.output = nn.Linear(hidden, d_model, bias=False)
 
-    def forward(self, x, pad=None):
+    def forward(self, x, pad=None, slot=None):
         """pad: None (the reference's pow2 pad prefix for x's length) or an
-        int64 tensor [B] of per-row pad lengths (see recurrence.bd_lru)."""
+        int64 tensor [B] of per-row pad lengths (see recurrence.bd_lru).
+        slot: blocks.ResidualGrad of the enclosing RecurrentLayer."""
         if x.device.type != "cuda":
             raise RecBLRNativeError(
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
                 "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
-        xz = linear(x, self.input)
+        xz = linear(x, self.input, slot)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad)
         return linear(y, self.output)
@@ -118,8 +120,10 @@ class RecurrentLayer(nn.Module):
         self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
 
     def forward(self, input_tensor, pad=None):
-        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad), input_tensor,
-                                   self.dropout, self.layer_norm, self.training)
+        slot = (ResidualGrad() if torch.is_grad_enabled() and input_tensor.requires_grad
+                else None)
+        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad, slot), input_tensor,
+                                   self.dropout, self.layer_norm, self.training, slot)
         return h if self.disable_ffn else self.ffn(h)
 
 

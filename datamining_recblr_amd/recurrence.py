@@ -13,9 +13,9 @@ conv, so every pad step sees the same per-channel constants
 the recurrence holds ``h0 = b'_p (1 - alpha_p^P) / (1 - alpha_p)``, which seeds
 the scan over the L real steps; real steps never see pad inputs through the
 conv because the reference's causal conv already zero-pads the history.  The
-``[H]``-sized prefix stays in torch (it is differentiable there, so the
-parameter gradients through the pad steps come from autograd), and everything
-``[B, L, *]``-sized runs in the HIP kernels:
+``[H]``-sized prefix is one small HIP launch each way (rb_pad_prefix_fwd /
+_bwd; ``pad_prefix_state`` is the same math in torch, kept as the checked
+reference), and everything ``[B, L, *]``-sized runs in the HIP kernels:
 
     K1  rb_conv_silu_fwd    x -> xc                    (R x, W xc)
     G   torch addmm         xc @ W_g^T + b_g -> rg     (MFMA GEMM)
@@ -30,7 +30,8 @@ import torch.nn.functional as F
 from . import kernels
 from .linear import _timed, wgrad
 
-__all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "BDLRUCore", "bd_lru"]
+__all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDLRUCore",
+           "bd_lru"]
 
 
 def pow2_pad_len(seq_len: int) -> int:
@@ -56,6 +57,24 @@ def pad_prefix_state(conv_bias, gate_w, gate_b, lam, pad_len):
         pad_len = pad_len.to(s.dtype)[:, None]
     # sum_{k<P} alpha^k = (1 - alpha^P) / (1 - alpha), cancellation-free
     return b_p * (torch.expm1(-pad_len * s) / torch.expm1(-s))
+
+
+class PadPrefix(torch.autograd.Function):
+    """pad_prefix_state on the HIP path: one launch forward, one backward
+    (rb_pad_prefix_fwd / _bwd) instead of ~60 [H]-sized torch kernels."""
+
+    @staticmethod
+    def forward(ctx, conv_b, gate_w, gate_b, lam, pad_len):
+        ctx.pad_len = pad_len
+        ctx.save_for_backward(conv_b, gate_w, gate_b, lam)
+        return kernels.pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad_len)
+
+    @staticmethod
+    def backward(ctx, dh0):
+        conv_b, gate_w, gate_b, lam = ctx.saved_tensors
+        dcb, dgw, dgb, dlam = kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len,
+                                                     dh0.float())
+        return dcb, dgw, dgb, dlam, None
 
 
 class BDLRUCore(torch.autograd.Function):
@@ -128,7 +147,7 @@ def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None):
     unpadded sequence, run_with_unseen.py:222-225)."""
     if pad is None:
         P = pow2_pad_len(xz.shape[1])
-        h0 = pad_prefix_state(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
+        h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
     else:
-        h0 = pad_prefix_state(conv_b, gate_w, gate_b, lam, pad) if use_conv else None
+        h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, pad) if use_conv else None
     return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv)

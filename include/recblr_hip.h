@@ -120,6 +120,28 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
                      float* dz, int64_t dz_rs, float* part, float* dh0_part,
                      int64_t B, int64_t L, int64_t H, void* stream);
 
+/* The state the power-of-two left padding leaves in the recurrence
+ * (RecBLR.py:176-179: F.pad of x by P zero steps before conv + scan), without
+ * materialising the padding.  Pad steps see the per-channel constants
+ * xc_p = silu(conv_b), (r_p, i_p) = gate_w xc_p + gate_b,
+ * s = softplus(lam) sigmoid(r_p), alpha = exp(-s),
+ * b_p = sqrt(1 - alpha^2 + 1e-8) sigmoid(i_p) xc_p, so after P steps
+ *   h0 = b_p expm1(-P s) / expm1(-s)            (s clamped at 1e-20).
+ * gate_w: [2H, H] row-major; h0: [n_rows, H]; row b uses pad[b] (pad != NULL)
+ * or pad_len.  Feeds rb_gate_scan_fwd's h0 (h0_bs = 0 for one row, H for
+ * per-row pad lengths).  Single-workgroup launches; H <= 4096. */
+int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gate_b,
+                      const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
+                      int64_t H, float* h0, void* stream);
+
+/* Backward of rb_pad_prefix_fwd for dh0 [n_rows, H] (rows summed in order):
+ * writes dconv_b [H], dgate_w [2H, H], dgate_b [2H], dlam [H] (overwritten,
+ * the caller adds them to the other gradient contributions). */
+int rb_pad_prefix_bwd(const float* conv_b, const float* gate_w, const float* gate_b,
+                      const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
+                      int64_t H, const float* dh0, float* dconv_b, float* dgate_w,
+                      float* dgate_b, float* dlam, void* stream);
+
 /* ---- blocks around the BD-LRU (RecurrentLayer / FeedForward / embedding) ---- */
 
 /* Dropout in the row kernels (nn.Dropout(p), train mode): element e is kept
@@ -179,6 +201,14 @@ int64_t rb_embedding_bwd_workspace(int64_t M, int64_t V, int64_t d);
 int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d,
                      int64_t V, int64_t padding_idx, float* dweight,
                      void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Fixed-order column sums of partials: out[m*C + c] = sum over p < P of
+ * in[m*ms + p*rs + c] for m < M, summed as RG interleaved partials
+ * (p = g, g+RG, ... in increasing order; RG = 4 for P <= 256, else 16)
+ * combined in order g = 0..RG-1.  Turns the per-block / per-split partials
+ * the backward kernels write (no atomics) into gradients; deterministic. */
+int rb_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
+              float* out, void* stream);
 
 /* ---- item scoring (RecBLR.py:86-122), fp32 MFMA, no [B, V] logits ----
  * seq: [B, d] sequence representations (RecBLR.forward's output), items:

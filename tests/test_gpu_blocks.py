@@ -235,3 +235,54 @@ def test_split_k_weight_gradient(cuda, M):
     close(w.grad, ref, atol=1e-3, rtol=1e-5, what="dW")
     close(b.grad, br.grad, atol=1e-3, rtol=1e-5, what="db")
     assert torch.equal(wgrad(dy, x.detach()), wgrad(dy, x.detach()))
+
+
+@pytest.mark.parametrize("H,pads", [(256, 56), (128, 14), (512, 1), (64, [0, 3, 14, 56, 1000]),
+                                    (128, 0)])
+def test_pad_prefix_kernels_match_torch(cuda, H, pads):
+    """rb_pad_prefix_fwd/_bwd against the torch statement pad_prefix_state
+    and its autograd (shared and per-row pad lengths)."""
+    from datamining_recblr_amd.recurrence import PadPrefix, pad_prefix_state
+
+    g = torch.Generator(device="cpu").manual_seed(H)
+    cb = (0.5 * torch.randn(H, generator=g)).to(cuda)
+    gw = (0.1 * torch.randn(2 * H, H, generator=g)).to(cuda)
+    gb = (0.1 * torch.randn(2 * H, generator=g)).to(cuda)
+    lam = torch.linspace(-2.0, 1.0, H).to(cuda)
+    P = torch.tensor(pads, device=cuda) if isinstance(pads, list) else pads
+    a = [t.clone().requires_grad_() for t in (cb, gw, gb, lam)]
+    b = [t.clone().double().requires_grad_() for t in (cb, gw, gb, lam)]
+    h_k = PadPrefix.apply(*a, P)
+    h_t = pad_prefix_state(*b, P)
+    close(h_k, h_t, atol=1e-5, rtol=1e-5, what="h0")
+    dh = torch.randn(h_t.shape, generator=g).to(cuda)
+    (h_k * dh).sum().backward()
+    (h_t * dh.double()).sum().backward()
+    for x, y, n in zip(a, b, ("dconv_b", "dgate_w", "dgate_b", "dlam")):
+        err = (x.grad.double() - y.grad).norm() / max(y.grad.norm().item(), 1e-30)
+        assert err < 2e-5, (n, err.item())
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 131072), (1024, 128), (300, 65), (3, 2048, 256)])
+def test_colsum_fixed_order(cuda, shape):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator(device="cpu").manual_seed(sum(shape))
+    x = torch.randn(shape, generator=g).to(cuda)
+    out = kernels.colsum(x)
+    ref = x.double().sum(-2)
+    assert out.shape == ref.shape
+    close(out, ref, atol=1e-5, rtol=1e-5, what="colsum")
+    assert torch.equal(out, kernels.colsum(x))
+    # restated order: RG interleaved partials in increasing p, combined in order
+    P = shape[-2]
+    RG = 4 if P <= 256 else 16
+    xs = x.reshape(-1, P, shape[-1]).cpu()
+    exp = torch.zeros(xs.shape[0], shape[-1])
+    parts = [torch.zeros(xs.shape[0], shape[-1]) for _ in range(RG)]
+    for p in range(P):
+        parts[p % RG] = parts[p % RG] + xs[:, p]
+    exp = parts[0]
+    for q in parts[1:]:
+        exp = exp + q
+    assert torch.equal(out.cpu().reshape(exp.shape), exp)
