@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 10
+ABI_VERSION = 12
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -34,10 +34,11 @@ SIGNATURES = {
     "rb_conv_silu_fwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64, _i64, _fp]),
     "rb_conv_silu_bwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
                                         _i64, _i64, _i64, _i64, _fp]),
-    "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _fp, _i64,
-                                        _fp, _i64, _i64, _i64, _fp]),
-    "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _i64,
-                                        _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64, _fp]),
+    "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp,
+                                        _i64, _fp, _i64, _i64, _i64, _fp]),
+    "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
+                                        _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
+                                        _fp]),
     "rb_pad_prefix_fwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp]),
     "rb_pad_prefix_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
                                          _fp, _fp, _fp]),
@@ -46,9 +47,9 @@ SIGNATURES = {
     "rb_row_num_parts": (ctypes.c_int64, [_i64, _i64]),
     "rb_add_ln_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _u64, _f32, _fp, _fp, _fp, _fp,
                                      _fp, _i64, _i64, _i64, _fp]),
-    "rb_silu_dropout_fwd": (ctypes.c_int, [_fp, _fp, _u64, _f32, _fp, _i64, _i64, _fp]),
-    "rb_silu_dropout_bwd": (ctypes.c_int, [_fp, _fp, _u64, _f32, _fp, _fp, _fp, _i64, _i64, _i64,
-                                           _fp]),
+    "rb_silu_dropout_fwd": (ctypes.c_int, [_fp, _fp, _fp, _u64, _f32, _fp, _i64, _i64, _fp]),
+    "rb_silu_dropout_bwd": (ctypes.c_int, [_fp, _fp, _fp, _u64, _f32, _fp, _fp, _fp, _i64, _i64,
+                                           _i64, _fp]),
     "rb_dropout_mask": (ctypes.c_int, [_u64, _f32, _fp, _i64, _fp]),
     "rb_embedding_bwd_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
     "rb_embedding_bwd": (ctypes.c_int, [_fp, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp]),

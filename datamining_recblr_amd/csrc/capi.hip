@@ -56,7 +56,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 10; }
+int rb_version(void) { return 12; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -105,20 +105,21 @@ int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w, const float* 
 }
 
 int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                     const float* z, int64_t z_rs, const float* lam, const float* h0,
-                     int64_t h0_bs, float* y, int64_t y_rs, float* carries, int64_t B, int64_t L,
-                     int64_t H, void* stream) {
+                     const float* z, int64_t z_rs, const float* lam, const float* gate_b,
+                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
+                     int64_t B, int64_t L, int64_t H, void* stream) {
   if (!rg || !xc || !z || !lam || !y) return fail("rb_gate_scan_fwd: null pointer");
   if (h0_bs != 0 && h0_bs < H) return fail("rb_gate_scan_fwd: h0 batch stride must be 0 or >= H");
   if (rg_rs < 2 * H || xc_rs < H || z_rs < H || y_rs < H)
     return fail("rb_gate_scan_fwd: row stride too small");
   if (int r = check_dims("rb_gate_scan_fwd", B, L, H, max4(rg_rs, xc_rs, z_rs, y_rs))) return r;
-  return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, h0_bs, y, y_rs, carries, B, L,
-                         H, reinterpret_cast<hipStream_t>(stream));
+  return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, h0, h0_bs, y, y_rs, carries,
+                         B, L, H, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                     const float* z, int64_t z_rs, const float* lam, const float* carries,
+                     const float* z, int64_t z_rs, const float* lam, const float* gate_b,
+                     const float* carries,
                      const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
                      float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B,
                      int64_t L, int64_t H, void* stream) {
@@ -129,7 +130,7 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
   if (int r = check_dims("rb_gate_scan_bwd", B, L, H,
                          max4(max4(rg_rs, xc_rs, z_rs, drg_rs), dz_rs, dxc_rs, H)))
     return r;
-  return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+  return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, carries, dy, drg, drg_rs, dxc,
                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H,
                          reinterpret_cast<hipStream_t>(stream));
 }
@@ -168,21 +169,23 @@ int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma, const flo
                            reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, uint64_t seed, float p, float* u,
-                        int64_t rows, int64_t cols, void* stream) {
+int rb_silu_dropout_fwd(const float* a, const float* bias, const uint8_t* mask, uint64_t seed,
+                        float p, float* u, int64_t rows, int64_t cols, void* stream) {
   if (!a || !u) return fail("rb_silu_dropout_fwd: null pointer");
+  if (bias && !aligned16(bias)) return fail("rb_silu_dropout_fwd: misaligned bias");
   if (rows <= 0 || cols <= 0) return fail("rb_silu_dropout_fwd: rows and cols must be positive");
   if (!(p >= 0.0f && p < 1.0f)) return fail("rb_silu_dropout_fwd: dropout p must be in [0, 1)");
   if (!aligned16(a) || !aligned16(u) || (mask && (reinterpret_cast<uintptr_t>(mask) & 3)))
     return fail("rb_silu_dropout_fwd: misaligned buffer");
-  return launch_silu_dropout_fwd(a, make_drop(mask, seed, p), u, rows, cols,
+  return launch_silu_dropout_fwd(a, bias, make_drop(mask, seed, p), u, rows, cols,
                                  reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, uint64_t seed, float p,
-                        const float* du, float* da, float* dbias_part, int64_t n_parts,
+int rb_silu_dropout_bwd(const float* a, const float* bias, const uint8_t* mask, uint64_t seed,
+                        float p, const float* du, float* da, float* dbias_part, int64_t n_parts,
                         int64_t rows, int64_t cols, void* stream) {
   if (!a || !du || !da) return fail("rb_silu_dropout_bwd: null pointer");
+  if (bias && !aligned16(bias)) return fail("rb_silu_dropout_bwd: misaligned bias");
   if (rows <= 0 || cols <= 0) return fail("rb_silu_dropout_bwd: rows and cols must be positive");
   if (!(p >= 0.0f && p < 1.0f)) return fail("rb_silu_dropout_bwd: dropout p must be in [0, 1)");
   if (!aligned16(a) || !aligned16(du) || !aligned16(da) ||
@@ -190,7 +193,7 @@ int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, uint64_t seed, floa
     return fail("rb_silu_dropout_bwd: misaligned buffer");
   if (dbias_part && n_parts != ln_num_parts(rows, cols))
     return fail("rb_silu_dropout_bwd: n_parts != rb_row_num_parts");
-  return launch_silu_dropout_bwd(a, make_drop(mask, seed, p), du, da, dbias_part,
+  return launch_silu_dropout_bwd(a, bias, make_drop(mask, seed, p), du, da, dbias_part,
                                  ln_num_parts(rows, cols), rows, cols,
                                  reinterpret_cast<hipStream_t>(stream));
 }

@@ -136,14 +136,14 @@ int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* b
                     const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
                     float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st);
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                    const float* z, int64_t z_rs, const float* lam, const float* h0,
-                    int64_t h0_bs, float* y, int64_t y_rs, float* carries, int64_t B, int64_t L,
-                    int64_t H, hipStream_t st);
+                    const float* z, int64_t z_rs, const float* lam, const float* gb,
+                    const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
+                    int64_t B, int64_t L, int64_t H, hipStream_t st);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                    const float* z, int64_t z_rs, const float* lam, const float* carries,
-                    const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
-                    float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
-                    int64_t H, hipStream_t st);
+                    const float* z, int64_t z_rs, const float* lam, const float* gb,
+                    const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
+                    int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
+                    int64_t B, int64_t L, int64_t H, hipStream_t st);
 int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
                       const float* r, const float* gamma, const float* beta, float eps, float* y,
                       float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,
@@ -153,11 +153,11 @@ int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const
                       float* dbp, float* dbiasp, int64_t nparts, int64_t rows, int64_t d,
                       hipStream_t st);
 int64_t ln_num_parts(int64_t rows, int64_t d);
-int launch_silu_dropout_fwd(const float* a, const DropSpec& drop, float* u, int64_t rows,
-                            int64_t cols, hipStream_t st);
-int launch_silu_dropout_bwd(const float* a, const DropSpec& drop, const float* du, float* da,
-                            float* dbias_part, int64_t nparts, int64_t rows, int64_t cols,
-                            hipStream_t st);
+int launch_silu_dropout_fwd(const float* a, const float* bias, const DropSpec& drop, float* u,
+                            int64_t rows, int64_t cols, hipStream_t st);
+int launch_silu_dropout_bwd(const float* a, const float* bias, const DropSpec& drop,
+                            const float* du, float* da, float* dbias_part, int64_t nparts,
+                            int64_t rows, int64_t cols, hipStream_t st);
 int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
 int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,

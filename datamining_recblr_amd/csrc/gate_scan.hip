@@ -37,7 +37,8 @@ template <int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
                 const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
-                const float* __restrict__ h0, int h0_bs, float* __restrict__ y, int y_rs,
+                const float* __restrict__ gbias, const float* __restrict__ h0, int h0_bs,
+                float* __restrict__ y, int y_rs,
                 float* __restrict__ carries, int64_t B, int L, int H, int ncw) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
@@ -57,10 +58,17 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   const float* zb = z + row0 * z_rs + cc;
   float* yb = y + row0 * y_rs + cc;
 
-  float nsp[VEC], carry[VEC];
+  float nsp[VEC], carry[VEC], br[VEC], bi[VEC];
   ldv(nsp, lam + cc);
 #pragma unroll
   for (int v = 0; v < VEC; ++v) nsp[v] = -softplus_f(nsp[v]);
+  if (gbias != nullptr) {   // the gates GEMM's bias, added here instead of in its epilogue
+    ldv(br, gbias + cc);
+    ldv(bi, gbias + H + cc);
+  } else {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) br[v] = bi[v] = 0.0f;
+  }
   if (h0 != nullptr) {
     ldv(carry, h0 + b * h0_bs + cc);
   } else {
@@ -89,8 +97,8 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
       const bool ok = t0 + j < L;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
-        const float a = fexp(nsp[v] * fsigm(in.r[j][v]));
-        const float beta = fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v]);
+        const float a = fexp(nsp[v] * fsigm(in.r[j][v] + br[v]));
+        const float beta = fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v] + bi[v]);
         in.r[j][v] = ok ? a : 1.0f;
         in.x[j][v] = ok ? beta * in.x[j][v] : 0.0f;
       }
@@ -159,7 +167,8 @@ template <int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
                 const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
-                const float* __restrict__ carries, const float* __restrict__ dy,
+                const float* __restrict__ gbias, const float* __restrict__ carries,
+                const float* __restrict__ dy,
                 float* __restrict__ drg, int drg_rs, float* __restrict__ dxc, int dxc_rs,
                 float* __restrict__ dz, int dz_rs, float* __restrict__ part,
                 float* __restrict__ dh0_part, int64_t B, int L, int H, int ncw) {
@@ -184,10 +193,17 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   float* dxcb = dxc + row0 * dxc_rs + cc;
   float* dzb = dz + row0 * dz_rs + cc;
 
-  float lamv[VEC], nsp[VEC];
+  float lamv[VEC], nsp[VEC], br[VEC], bi[VEC];
   ldv(lamv, lam + cc);
 #pragma unroll
   for (int v = 0; v < VEC; ++v) nsp[v] = -softplus_f(lamv[v]);
+  if (gbias != nullptr) {
+    ldv(br, gbias + cc);
+    ldv(bi, gbias + H + cc);
+  } else {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) br[v] = bi[v] = 0.0f;
+  }
   float ecarry[VEC], acc_v[VEC], acc_r[VEC], acc_i[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) ecarry[v] = acc_v[v] = acc_r[v] = acc_i[v] = 0.0f;
@@ -207,6 +223,13 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   };
   auto process = [&](BwdIn<VEC, TC>& in, int tile) {
     const int t0 = tile * TILE + q * TC;
+#pragma unroll
+    for (int j = 0; j < TC; ++j)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        in.r[j][v] += br[v];
+        in.i[j][v] += bi[v];
+      }
     float hcar[VEC];
     ldv(hcar, carries + (b * nT + tile) * H + cc);
     float al[TC][VEC];
@@ -388,28 +411,30 @@ bool vec_ok(int64_t H, std::initializer_list<int64_t> strides,
 
 template <int V>
 int gate_fwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
-               int64_t z_rs, const float* lam, const float* h0, int64_t h0_bs, float* y,
+               int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
+               float* y,
                int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_fwd<V, kFwdQ, kFwdTC, true>), dim3((unsigned)blocks),
-                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, h0,
-                     (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw);
+                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
+                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_fwd");
 }
 
 template <int V>
 int gate_bwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
-               int64_t z_rs, const float* lam, const float* carries, const float* dy, float* drg,
+               int64_t z_rs, const float* lam, const float* gb, const float* carries,
+               const float* dy, float* drg,
                int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz, int64_t dz_rs, float* part,
                float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const int span = (kWave / kBwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_bwd<V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
-                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, carries,
-                     dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part, dh0_part, B,
+                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
+                     carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part, dh0_part, B,
                      (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_bwd");
 }
@@ -417,35 +442,36 @@ int gate_bwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, c
 }  // namespace
 
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                    const float* z, int64_t z_rs, const float* lam, const float* h0,
-                    int64_t h0_bs, float* y, int64_t y_rs, float* carries, int64_t B, int64_t L,
-                    int64_t H, hipStream_t st) {
+                    const float* z, int64_t z_rs, const float* lam, const float* gb,
+                    const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
+                    int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
   const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y,
-                     (const void*)lam, (const void*)h0, (const void*)carries};
+                     (const void*)lam, (const void*)gb, (const void*)h0, (const void*)carries};
   if (vec_ok<2>(H, strides, ptrs))
-    return gate_fwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, h0_bs, y, y_rs, carries, B, L,
-                         H, st);
-  return gate_fwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, h0, h0_bs, y, y_rs, carries, B, L, H,
-                       st);
+    return gate_fwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B,
+                         L, H, st);
+  return gate_fwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B, L,
+                       H, st);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                    const float* z, int64_t z_rs, const float* lam, const float* carries,
-                    const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
-                    float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B, int64_t L,
-                    int64_t H, hipStream_t st) {
+                    const float* z, int64_t z_rs, const float* lam, const float* gb,
+                    const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
+                    int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
+                    int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
   const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)lam,
-                     (const void*)carries, (const void*)dy, (const void*)drg, (const void*)dxc,
-                     (const void*)dz, (const void*)part, (const void*)dh0_part};
+                     (const void*)gb, (const void*)carries, (const void*)dy, (const void*)drg,
+                     (const void*)dxc, (const void*)dz, (const void*)part,
+                     (const void*)dh0_part};
   if (vec_ok<4>(H, strides, ptrs))
-    return gate_bwd_v<4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+    return gate_bwd_v<4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
   if (vec_ok<2>(H, strides, ptrs))
-    return gate_bwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+    return gate_bwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
-  return gate_bwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, carries, dy, drg, drg_rs, dxc,
+  return gate_bwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
                        dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
 }
 

@@ -211,13 +211,23 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
 // FFN inner activation on rows of C = LPR * NV * 4: u = silu(a) * keep * scale
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
-k_silu_dropout_fwd(const float* __restrict__ a, DropSpec drop, float* __restrict__ u,
-                   int64_t rows) {
+k_silu_dropout_fwd(const float* __restrict__ a, const float* __restrict__ bias, DropSpec drop,
+                   float* __restrict__ u, int64_t rows) {
   constexpr int C = LPR * NV * 4;
   constexpr int RPW = kWave / LPR;
   const int lane = threadIdx.x & (kWave - 1);
   const int sub = lane / LPR;
   const int l = lane - sub * LPR;
+  float bv[NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (bias) {
+      ldv(bv[k], bias + (l + k * LPR) * 4);
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) bv[k][v] = 0.0f;
+    }
+  }
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   for (int64_t row0 = wave * RPW; row0 < rows; row0 += nwaves * RPW) {
@@ -230,7 +240,7 @@ k_silu_dropout_fwd(const float* __restrict__ a, DropSpec drop, float* __restrict
       ldv(x, a + e);
       drop.get4(e, m);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) o[v] = fsilu(x[v]) * m[v];
+      for (int v = 0; v < 4; ++v) o[v] = fsilu(x[v] + bv[k][v]) * m[v];
       stv(u + e, o);
     }
   }
@@ -240,8 +250,9 @@ k_silu_dropout_fwd(const float* __restrict__ a, DropSpec drop, float* __restrict
 // gradient of the GEMM that produced a.
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
-k_silu_dropout_bwd(const float* __restrict__ a, DropSpec drop, const float* __restrict__ du,
-                   float* __restrict__ da, float* __restrict__ dbias_part, int64_t rows) {
+k_silu_dropout_bwd(const float* __restrict__ a, const float* __restrict__ bias, DropSpec drop,
+                   const float* __restrict__ du, float* __restrict__ da,
+                   float* __restrict__ dbias_part, int64_t rows) {
   constexpr int C = LPR * NV * 4;
   constexpr int RPW = kWave / LPR;
   __shared__ float red[4][C];
@@ -249,6 +260,16 @@ k_silu_dropout_bwd(const float* __restrict__ a, DropSpec drop, const float* __re
   const int wv = threadIdx.x >> 6;
   const int sub = lane / LPR;
   const int l = lane - sub * LPR;
+  float bv[NV][4];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    if (bias) {
+      ldv(bv[k], bias + (l + k * LPR) * 4);
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) bv[k][v] = 0.0f;
+    }
+  }
   const int64_t wave = (int64_t)blockIdx.x * 4 + wv;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   float acc[NV][4];
@@ -268,7 +289,7 @@ k_silu_dropout_bwd(const float* __restrict__ a, DropSpec drop, const float* __re
       drop.get4(e, m);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        o[v] = (g[v] * m[v]) * fdsilu(x[v]);
+        o[v] = (g[v] * m[v]) * fdsilu(x[v] + bv[k][v]);
         acc[k][v] += o[v];
       }
       stv(da + e, o);
@@ -329,17 +350,18 @@ int add_ln_bwd_t(const float* dy, const float* s, const float* gamma, const floa
 }
 
 template <int NV, int LPR>
-int silu_fwd_t(const float* a, const DropSpec& drop, float* u, int64_t rows, hipStream_t st) {
+int silu_fwd_t(const float* a, const float* bias, const DropSpec& drop, float* u, int64_t rows,
+               hipStream_t st) {
   hipLaunchKernelGGL((k_silu_dropout_fwd<NV, LPR>), dim3((unsigned)(2 * row_blocks<LPR>(rows))),
-                     dim3(256), 0, st, a, drop, u, rows);
+                     dim3(256), 0, st, a, bias, drop, u, rows);
   return launch_status("rb_silu_dropout_fwd");
 }
 
 template <int NV, int LPR>
-int silu_bwd_t(const float* a, const DropSpec& drop, const float* du, float* da,
+int silu_bwd_t(const float* a, const float* bias, const DropSpec& drop, const float* du, float* da,
                float* dbias_part, int64_t nparts, int64_t rows, hipStream_t st) {
   hipLaunchKernelGGL((k_silu_dropout_bwd<NV, LPR>), dim3((unsigned)nparts), dim3(256), 0, st, a,
-                     drop, du, da, dbias_part, rows);
+                     bias, drop, du, da, dbias_part, rows);
   return launch_status("rb_silu_dropout_bwd");
 }
 
@@ -385,15 +407,15 @@ int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const
                   nparts, rows, st)
 }
 
-int launch_silu_dropout_fwd(const float* a, const DropSpec& drop, float* u, int64_t rows,
-                            int64_t cols, hipStream_t st) {
-  RB_ROW_DISPATCH(cols, silu_fwd_t, a, drop, u, rows, st)
+int launch_silu_dropout_fwd(const float* a, const float* bias, const DropSpec& drop, float* u,
+                            int64_t rows, int64_t cols, hipStream_t st) {
+  RB_ROW_DISPATCH(cols, silu_fwd_t, a, bias, drop, u, rows, st)
 }
 
-int launch_silu_dropout_bwd(const float* a, const DropSpec& drop, const float* du, float* da,
-                            float* dbias_part, int64_t nparts, int64_t rows, int64_t cols,
-                            hipStream_t st) {
-  RB_ROW_DISPATCH(cols, silu_bwd_t, a, drop, du, da, dbias_part, nparts, rows, st)
+int launch_silu_dropout_bwd(const float* a, const float* bias, const DropSpec& drop,
+                            const float* du, float* da, float* dbias_part, int64_t nparts,
+                            int64_t rows, int64_t cols, hipStream_t st) {
+  RB_ROW_DISPATCH(cols, silu_bwd_t, a, bias, drop, du, da, dbias_part, nparts, rows, st)
 }
 
 int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st) {

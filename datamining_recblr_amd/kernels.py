@@ -192,11 +192,12 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx):
     return colsum(dw_part.view(B, -1)).view(-1, H).t().contiguous(), colsum(db_part)
 
 
-def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True):
+def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=None):
     """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
 
     rg: [B, L, 2H]; xc, z: [B, L, H] views; lam: [H]; h0: [H] (shared by every
-    row), [B, H] (one initial state per row) or None.
+    row), [B, H] (one initial state per row) or None; gate_b: [2H] bias added
+    to rg inside the kernel (or None).
     Returns (y [B, L, H], carries [B, nT, H] or None when not wanted)."""
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (lam, "Lambda")):
         _check(t, n)
@@ -221,12 +222,23 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True):
     carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
                if want_carries else None)
     _launch("rb_gate_scan_fwd", 5 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
-              lam.contiguous().data_ptr(), 0 if h0 is None else h0.data_ptr(), h0_bs, y.data_ptr(),
+              lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), 0 if h0 is None else h0.data_ptr(),
+              h0_bs, y.data_ptr(),
               y_rs, 0 if carries is None else carries.data_ptr(), B, L, H, _stream(xc))
     return y, carries
 
 
-def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=False):
+def _gb_ptr(gate_b, H):
+    if gate_b is None:
+        return None
+    _check(gate_b, "gates bias")
+    if gate_b.shape != (2 * H,) or not gate_b.is_contiguous():
+        raise ValueError(f"gates bias must be contiguous [{2 * H}]")
+    return gate_b.data_ptr()
+
+
+def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=False,
+                  gate_b=None):
     """Backward of gate_scan_fwd.  Writes dz (a row-strided view) and returns
     (drg [B, L, 2H], dxc [B, L, H], dlam [H], dgate_bias [2H], dh0), dh0 [H]
     (summed over rows) or [B, H] when dh0_rows (a per-row h0)."""
@@ -251,7 +263,8 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
     part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
     dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
     _launch("rb_gate_scan_bwd", 9 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs,
-            z.data_ptr(), z_rs, lam.contiguous().data_ptr(), carries.data_ptr(), dy.data_ptr(),
+            z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), carries.data_ptr(),
+            dy.data_ptr(),
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
             part.data_ptr(), dh0_part.data_ptr(), B, L, H, _stream(xc))
     sums = colsum(part)
@@ -366,7 +379,17 @@ def _rows_cols(a):
     return a.numel() // cols, cols
 
 
-def silu_dropout_fwd(a, mask=None, seed=0, p=0.0):
+def _bias_ptr(bias, cols):
+    if bias is None:
+        return None
+    _check(bias, "bias")
+    if bias.shape != (cols,) or not bias.is_contiguous():
+        raise ValueError(f"bias must be contiguous [{cols}]")
+    return bias.data_ptr()
+
+
+def silu_dropout_fwd(a, mask=None, seed=0, p=0.0, bias=None):
+    """u = dropout(silu(a + bias)) over rows of a (bias may be None)."""
     _check(a, "a")
     _check_p(p)
     if not a.is_contiguous():
@@ -376,12 +399,13 @@ def silu_dropout_fwd(a, mask=None, seed=0, p=0.0):
     u = torch.empty_like(a)
     n = a.numel()
     _launch("rb_silu_dropout_fwd", 8 * n + (n if mask is not None else 0), a.data_ptr(),
-            _ptr(mask), int(seed), float(p), u.data_ptr(), rows, cols, _stream(a))
+            _bias_ptr(bias, cols), _ptr(mask), int(seed), float(p), u.data_ptr(), rows, cols,
+            _stream(a))
     return u
 
 
-def silu_dropout_bwd(a, du, mask=None, seed=0, p=0.0, want_dbias=False):
-    """Returns (da, dbias or None)."""
+def silu_dropout_bwd(a, du, mask=None, seed=0, p=0.0, want_dbias=False, bias=None):
+    """Returns (da, dbias or None); bias as given to silu_dropout_fwd."""
     _check(du, "du")
     _check_p(p)
     du = du.contiguous()
@@ -393,8 +417,8 @@ def silu_dropout_bwd(a, du, mask=None, seed=0, p=0.0, want_dbias=False):
                if want_dbias else None)
     n = a.numel()
     _launch("rb_silu_dropout_bwd", 12 * n + (n if mask is not None else 0), a.data_ptr(),
-            _ptr(mask), int(seed), float(p), du.data_ptr(), da.data_ptr(), _ptr(dbias_p), nparts,
-            rows, cols, _stream(a))
+            _bias_ptr(bias, cols), _ptr(mask), int(seed), float(p), du.data_ptr(), da.data_ptr(),
+            _ptr(dbias_p), nparts, rows, cols, _stream(a))
     return da, (colsum(dbias_p) if want_dbias else None)
 
 

@@ -90,20 +90,20 @@ class BDLRUCore(torch.autograd.Function):
         else:
             xc = x
         gflops = 2 * B * L * H * H2
-        rg = _timed("gemm", gflops, torch.addmm, gate_b, xc.reshape(B * L, H),
-                    gate_w.t()).view(B, L, H2)
+        # gates GEMM without its bias: the gate kernels add gate_b on the fly
+        rg = _timed("gemm", gflops, torch.mm, xc.reshape(B * L, H), gate_w.t()).view(B, L, H2)
         train = any(ctx.needs_input_grad)
-        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train)
+        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b)
         ctx.use_conv = use_conv
         ctx.has_h0 = h0 is not None
         ctx.h0_rows = h0 is not None and h0.dim() == 2
         ctx.save_for_backward(xz, xc if use_conv else None, rg, carries, conv_w, conv_b,
-                              gate_w, lam)
+                              gate_w, gate_b, lam)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xz, xc, rg, carries, conv_w, conv_b, gate_w, lam = ctx.saved_tensors
+        xz, xc, rg, carries, conv_w, conv_b, gate_w, gate_b, lam = ctx.saved_tensors
         B, L, H2 = xz.shape
         H = H2 // 2
         x, z = xz[..., :H], xz[..., H:]
@@ -112,7 +112,7 @@ class BDLRUCore(torch.autograd.Function):
         dy = dy.contiguous()
         dxz = torch.empty_like(xz)
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
-            rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows)
+            rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows, gate_b=gate_b)
         drg2 = drg.view(B * L, H2)
         gflops = 2 * B * L * H * H2
         dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(B * L, H))

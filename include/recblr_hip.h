@@ -99,14 +99,15 @@ int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w,
  *   h_t   = alpha_t * h_{t-1} + beta_t * xc_t,   h_{-1} = h0[c] (0 if NULL),
  *   y     = silu(z) * h.
  * rg: [B, L, 2H] view (r = columns [0,H), i = columns [H,2H)), row stride
- * rg_rs; xc, z, y: [B, L, H] views with their own row strides; lam, h0: [H].
+ * rg_rs, to which gate_b [2H] is added when non-NULL (the gates bias, folded
+ * here rather than into the GEMM; drg is the gradient w.r.t. rg + gate_b); xc, z, y: [B, L, H] views with their own row strides; lam, h0: [H].
  * carries: B * ceil(L/RB_TILE) * H floats (written, consumed by the bwd);
  * may be NULL for inference (no checkpoints written). */
 int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t xc_rs, const float* z, int64_t z_rs,
-                     const float* lam, const float* h0, int64_t h0_bs, float* y,
-                     int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-                     void* stream);
+                     const float* lam, const float* gate_b, const float* h0,
+                     int64_t h0_bs, float* y, int64_t y_rs, float* carries,
+                     int64_t B, int64_t L, int64_t H, void* stream);
 
 /* Backward of rb_gate_scan_fwd given dy = dL/dy ([B, L, H] contiguous).
  * Writes drg ([B, L, 2H] view: dr | di, row stride drg_rs), dxc (the gate
@@ -115,7 +116,8 @@ int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
  * dh0_part[B, H] = dL/dh_{-1} per batch row (caller sums over b). */
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t xc_rs, const float* z, int64_t z_rs,
-                     const float* lam, const float* carries, const float* dy,
+                     const float* lam, const float* gate_b, const float* carries,
+                     const float* dy,
                      float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
                      float* dz, int64_t dz_rs, float* part, float* dh0_part,
                      int64_t B, int64_t L, int64_t H, void* stream);
@@ -178,13 +180,15 @@ int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma,
                   int64_t n_parts, int64_t rows, int64_t d, void* stream);
 
 /* FeedForward's inner activation (RecBLR.py:220-221) on [rows, cols]:
- * u = dropout(silu(a)); backward da = dropout-backward(du) * silu'(a) with
- * optional column partials of da (the w_1 bias gradient). */
-int rb_silu_dropout_fwd(const float* a, const uint8_t* mask, uint64_t seed,
-                        float p, float* u, int64_t rows, int64_t cols,
-                        void* stream);
-int rb_silu_dropout_bwd(const float* a, const uint8_t* mask, uint64_t seed,
-                        float p, const float* du, float* da,
+ * u = dropout(silu(a + bias)) (bias [cols] may be NULL: the w_1 bias folded
+ * in here instead of into the GEMM); backward
+ * da = dropout-backward(du) * silu'(a + bias) with optional column partials
+ * of da (the w_1 bias gradient). */
+int rb_silu_dropout_fwd(const float* a, const float* bias, const uint8_t* mask,
+                        uint64_t seed, float p, float* u, int64_t rows,
+                        int64_t cols, void* stream);
+int rb_silu_dropout_bwd(const float* a, const float* bias, const uint8_t* mask,
+                        uint64_t seed, float p, const float* du, float* da,
                         float* dbias_part, int64_t n_parts, int64_t rows,
                         int64_t cols, void* stream);
 

@@ -286,3 +286,20 @@ def test_colsum_fixed_order(cuda, shape):
     for q in parts[1:]:
         exp = exp + q
     assert torch.equal(out.cpu().reshape(exp.shape), exp)
+
+
+def test_silu_dropout_with_folded_bias(cuda):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator(device="cpu").manual_seed(4)
+    a = torch.randn(65, 256, generator=g).to(cuda)
+    b = torch.randn(256, generator=g).to(cuda)
+    du = torch.randn(65, 256, generator=g).to(cuda)
+    u = kernels.silu_dropout_fwd(a, seed=9, p=0.25, bias=b)
+    keep = kernels.dropout_mask(9, 0.25, (65, 256), cuda).float() / 0.75
+    close(u, F.silu(a + b) * keep, what="u")
+    da, db = kernels.silu_dropout_bwd(a, du, seed=9, p=0.25, want_dbias=True, bias=b)
+    ar = (a + b).requires_grad_()
+    (F.silu(ar) * keep).backward(du)
+    close(da, ar.grad, what="da")
+    close(db, ar.grad.double().sum(0), what="db")

@@ -66,14 +66,14 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
   snprintf(f, 64, "gate_fwd %s", nm);
   cs.push_back({f, 5 * N * 4, [=] {
     hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, g.rg,
-                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, nullptr, 0, g.y, H, g.car,
+                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, nullptr, nullptr, 0, g.y, H, g.car,
                        (int64_t)B, L, H, ncw);
   }, {}});
   char* f2 = (char*)malloc(64);
   snprintf(f2, 64, "gate_bwd %s", nm);
   cs.push_back({f2, 9 * N * 4, [=] {
     hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, g.rg,
-                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, g.car, g.dy, g.drg, g.drg_rs,
+                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, nullptr, g.car, g.dy, g.drg, g.drg_rs,
                        g.dxc, g.dxc_rs, g.dz, g.dz_rs, g.part, g.dh0, (int64_t)B, L, H, ncw);
   }, {}});
 }
