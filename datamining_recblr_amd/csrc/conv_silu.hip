@@ -241,14 +241,14 @@ int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* b
   const bool vec = H % 4 == 0 && x_rs % 4 == 0 && xc_rs % 4 == 0 && aligned16(x) &&
                    aligned16(xc) && aligned16(bias);
   switch (K) {
-    case 1: return conv_fwd_t<1, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 2: return conv_fwd_t<2, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 3: return conv_fwd_t<3, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 4: return conv_fwd_t<4, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 5: return conv_fwd_t<5, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 6: return conv_fwd_t<6, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 7: return conv_fwd_t<7, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 8: return conv_fwd_t<8, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 1: return conv_fwd_t<1, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 2: return conv_fwd_t<2, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 3: return conv_fwd_t<3, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 4: return conv_fwd_t<4, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 5: return conv_fwd_t<5, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 6: return conv_fwd_t<6, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 7: return conv_fwd_t<7, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 8: return conv_fwd_t<8, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
     default: return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
   }
 }

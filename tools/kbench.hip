@@ -11,6 +11,9 @@
 #include "../datamining_recblr_amd/csrc/scan_rows.hip"
 #include "../datamining_recblr_amd/csrc/rownorm.hip"
 #include "../datamining_recblr_amd/csrc/embedding.hip"
+#include "../datamining_recblr_amd/csrc/item_scores.hip"
+#include "../datamining_recblr_amd/csrc/pad_prefix.hip"
+#include "../datamining_recblr_amd/csrc/reduce.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -98,6 +101,13 @@ void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float*
     hipLaunchKernelGGL((k_conv_silu_bwd<K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, x, 2 * H,
                        w, bias, g1, nullptr, dx, 2 * H, dwp, dbp, (int64_t)B, L, H, ncw);
   }, {}});
+}
+
+// pure 1R+1W float4 copy (the guide's copy ceiling)
+__global__ void copy4(const float4* a, float4* o, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = a[i];
 }
 
 // pure data movement: 4 reads + 1 write per element, flat float4 grid-stride
@@ -220,6 +230,30 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL((pattern4to1<1, 16>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0, rg,
                        2 * H, xc, H, xz + H, 2 * H, y, H, (int64_t)B, L, H, ncw);
   }, {}});
+  cs.push_back({"copy4 (1R+1W float4)", 2 * N * 4, [=] {
+    hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)xc, (float4*)dxc, n / 4);
+  }, {}});
+  // the same gate kernels with the operand arrays staggered inside one pool
+  // (tests whether equal 2 MB alignment of the streams costs channel balance)
+  {
+    const int64_t pool_f = 8 * n + (1 << 22);
+    float* pool = dalloc(pool_f, 40);
+    const int64_t offs[3][6] = {{0, 2304, 4608, 6912, 9216, 11520},            // 9 KB steps
+                                {0, 16448, 32896, 49344, 65792, 82240},        // 64 KB + 64 B
+                                {0, 262208, 524416, 786624, 1048832, 1311040}}; // 1 MB + 256 B
+    for (int k = 0; k < 3; ++k) {
+      const int64_t* o = offs[k];
+      float* rg2 = pool + o[0];
+      float* xz2 = rg2 + 2 * n + o[1];
+      float* xc2 = xz2 + 2 * n + o[2];
+      float* y2 = xc2 + n + o[3];
+      GateBufs st{rg2, xc2, xz2 + H, y2, car, dy, drg, dxc, dz + H, part, dh0, lam,
+                  2 * H, H, 2 * H, 2 * H, H, 2 * H};
+      char* nm = (char*)malloc(64);
+      snprintf(nm, 64, "v2 q4 tc4 pf stag%d", k);
+      add_gate<2, 4, 4, true>(cs, nm, B, L, H, st, N);
+    }
+  }
   cs.push_back({"hipMemcpy d2d (R+W)", 2 * N * 4, [=] {
     CK(hipMemcpyAsync(dxc, xc, n * sizeof(float), hipMemcpyDeviceToDevice, 0));
   }, {}});
