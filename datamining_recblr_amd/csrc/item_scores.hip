@@ -37,13 +37,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kWaves = 4;            // waves per workgroup
 constexpr int kThreads = kWaves * 64;
 constexpr int kTile = 32;            // rows (items or sequences) per wave tile
-#ifndef RB_ITEM_NACC
-#define RB_ITEM_NACC 1
-#endif
-#ifndef RB_ITEM_WGS
-#define RB_ITEM_WGS 512
-#endif
-constexpr int64_t kTargetWgs = RB_ITEM_WGS;  // ~2 workgroups per CU over 256 CUs
+constexpr int64_t kTargetWgs = 512;  // ~2 workgroups per CU over 256 CUs
 
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -56,26 +50,6 @@ __device__ __forceinline__ void ld_half(float (&o)[KH], const float* row, int h)
     const float4 t = p[q];
     o[4 * q] = t.x; o[4 * q + 1] = t.y; o[4 * q + 2] = t.z; o[4 * q + 3] = t.w;
   }
-}
-
-// X[i][j] = sum_k A[i][k] B[k][j]; lane supplies row i = lane&31 of A and
-// column j = lane&31 of B through its k-half.
-template <int KH>
-__device__ __forceinline__ f32x16 mfma_dot(const float (&a)[KH], const float (&b)[KH]) {
-#if RB_ITEM_NACC == 2
-  f32x16 acc = {}, acc1 = {};
-#pragma unroll
-  for (int s = 0; s < KH; s += 2) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s + 1], b[s + 1], acc1, 0, 0, 0);
-  }
-  return acc + acc1;
-#else
-  f32x16 acc = {};
-#pragma unroll
-  for (int s = 0; s < KH; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], acc, 0, 0, 0);
-  return acc;
-#endif
 }
 
 // ---- the streamed operand: 32-row tiles through double-buffered LDS ---------------
@@ -258,17 +232,6 @@ __global__ __launch_bounds__(256) void k_target_dot(const float* __restrict__ E,
   ld_half<KH>(e1, E + b * D, 1);
   ld_half<KH>(w0, W + t * D, 0);
   ld_half<KH>(w1, W + t * D, 1);
-#if RB_ITEM_NACC == 2
-  float acc = 0.0f, acc1 = 0.0f;
-#pragma unroll
-  for (int s = 0; s < KH; s += 2) {
-    acc = fmaf(w0[s], e0[s], acc);
-    acc = fmaf(w1[s], e1[s], acc);
-    acc1 = fmaf(w0[s + 1], e0[s + 1], acc1);
-    acc1 = fmaf(w1[s + 1], e1[s + 1], acc1);
-  }
-  ts[b] = acc + acc1;
-#else
   float acc = 0.0f;
 #pragma unroll
   for (int s = 0; s < KH; ++s) {
@@ -276,7 +239,6 @@ __global__ __launch_bounds__(256) void k_target_dot(const float* __restrict__ E,
     acc = fmaf(w1[s], e1[s], acc);
   }
   ts[b] = acc;
-#endif
 }
 
 #ifdef RB_ITEM_PROF

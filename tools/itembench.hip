@@ -1,6 +1,6 @@
 // itembench.hip — timing of the item-scoring kernels (csrc/item_scores.hip)
-// at the benchmark's CE shape (B=2048, V=10544, d=128 by default); compile
-// variants with -DRB_ITEM_NACC=... -DRB_ITEM_WGS=...
+// at the benchmark's CE shape (B=2048, V=10544, d=128 by default), plus a
+// pure-MFMA issue-rate probe; -DRB_ITEM_PROF adds per-wave cycle counts.
 //
 //   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 -I include \
 //       tools/itembench.hip -o tools/itembench && tools/itembench [B V d]
@@ -95,8 +95,7 @@ int main(int argc, char** argv) {
   auto rep = [&](const char* n, float us, double gflop) {
     printf("%-10s %9.2f us  %7.1f TF/s (algorithmic)\n", n, us, gflop / us * 1e3);
   };
-  printf("B=%ld V=%ld d=%ld NACC=%d WGS=%d\n", (long)B, (long)V, (long)d, RB_ITEM_NACC,
-         RB_ITEM_WGS);
+  printf("B=%ld V=%ld d=%ld\n", (long)B, (long)V, (long)d);
   rep("ce_fwd", time_us([&] { rb_item_ce_fwd(E, W, tgt, B, V, d, lse, loss, ws, ws_b, 0); }), gf);
   rep("ce_bwd", time_us([&] { rb_item_ce_bwd(E, W, tgt, lse, dl, B, V, d, dE, dW, ws, ws_b, 0); }),
       2 * gf);
