@@ -11,6 +11,8 @@
 #include "../datamining_recblr_amd/csrc/rownorm.hip"
 #include "../datamining_recblr_amd/csrc/embedding.hip"
 #include "../datamining_recblr_amd/csrc/item_scores.hip"
+#include "../datamining_recblr_amd/csrc/pad_prefix.hip"
+#include "../datamining_recblr_amd/csrc/reduce.hip"
 
 #include <algorithm>
 #include <cstdio>
