@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -53,6 +53,8 @@ SIGNATURES = {
     "rb_dropout_mask": (ctypes.c_int, [_u64, _f32, _fp, _i64, _fp]),
     "rb_embedding_bwd_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
     "rb_embedding_bwd": (ctypes.c_int, [_fp, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp]),
+    "rb_embedding_bwd_plan": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp]),
+    "rb_embedding_bwd_apply": (ctypes.c_int, [_fp, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp]),
     "rb_colsum": (ctypes.c_int, [_fp, _i64, _i64, _i64, _i64, _i64, _fp, _fp]),
     "rb_item_ce_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
     "rb_item_ce_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp, _i64, _fp]),

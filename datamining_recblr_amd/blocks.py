@@ -84,15 +84,37 @@ class _AddDropoutLN(torch.autograd.Function):
                 dg, db, None, None, None, None, None)
 
 
+_side_streams = {}
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    s = _side_streams.get(device)
+    if s is None:
+        s = _side_streams[device] = torch.cuda.Stream(device=device)
+    return s
+
+
 class _EmbedDropoutLN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, table, idx, gamma, beta, mask, seed, p, eps, padding_idx):
         save = any(ctx.needs_input_grad)
         flat = idx.reshape(-1).contiguous()
+        plan = event = None
+        if ctx.needs_input_grad[0]:
+            # the embedding backward's sort depends on the ids only: run it now on
+            # a side stream, overlapped with the forward, and only wait in backward
+            side = _side_stream(table.device)
+            side.wait_stream(torch.cuda.current_stream(table.device))
+            with torch.cuda.stream(side):
+                plan = kernels.embedding_plan(flat, table.shape[0], table.shape[1], stream=side)
+                event = torch.cuda.Event()
+                event.record(side)
+            flat.record_stream(side)
         y, s, mean, rstd = kernels.add_ln_fwd(table, None, gamma, beta, eps, mask=mask,
                                               seed=seed, p=p, idx=flat, save=save)
         ctx.seed, ctx.p = seed, p
         ctx.padding_idx, ctx.num_rows = padding_idx, table.shape[0]
+        ctx.plan, ctx.event = plan, event
         ctx.save_for_backward(s, mean, rstd, gamma, mask, flat)
         return y.view(*idx.shape, table.shape[1])
 
@@ -102,8 +124,15 @@ class _EmbedDropoutLN(torch.autograd.Function):
         _, da, dg, db, _ = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask=mask,
                                               seed=ctx.seed, p=ctx.p, want_ds=False,
                                               want_da=True)
-        dtable = (kernels.embedding_bwd(flat, da, ctx.num_rows, ctx.padding_idx)
-                  if ctx.needs_input_grad[0] else None)
+        dtable = None
+        if ctx.needs_input_grad[0]:
+            if ctx.event is not None:
+                torch.cuda.current_stream(da.device).wait_event(ctx.event)
+            dtable = kernels.embedding_bwd(flat, da, ctx.num_rows, ctx.padding_idx,
+                                           plan=ctx.plan)
+            if ctx.plan is not None:   # allocated on the side stream, last used here
+                ctx.plan.record_stream(torch.cuda.current_stream(da.device))
+            ctx.plan = ctx.event = None
         return dtable, None, dg, db, None, None, None, None, None
 
 

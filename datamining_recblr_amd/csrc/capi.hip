@@ -56,7 +56,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 12; }
+int rb_version(void) { return 13; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -209,6 +209,27 @@ int rb_dropout_mask(uint64_t seed, float p, uint8_t* out, int64_t n, void* strea
 int64_t rb_embedding_bwd_workspace(int64_t M, int64_t V, int64_t d) {
   if (M <= 0 || V <= 0 || d <= 0) return 0;
   return emb_workspace_bytes(M, V, d);
+}
+
+int rb_embedding_bwd_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, void* workspace,
+                          int64_t workspace_bytes, void* stream) {
+  if (!idx || !workspace) return fail("rb_embedding_bwd_plan: null pointer");
+  if (M <= 0 || d <= 0 || V <= 0) return fail("rb_embedding_bwd_plan: M, d, V must be positive");
+  if (M >= (int64_t(1) << 31) || V >= (int64_t(1) << 30))
+    return fail("rb_embedding_bwd_plan: M or V too large");
+  return launch_embedding_plan(idx, M, d, V, workspace, workspace_bytes,
+                               reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_embedding_bwd_apply(const float* grad, int64_t M, int64_t d, int64_t V,
+                           int64_t padding_idx, float* dweight, void* workspace,
+                           int64_t workspace_bytes, void* stream) {
+  if (!grad || !dweight || !workspace) return fail("rb_embedding_bwd_apply: null pointer");
+  if (M <= 0 || d <= 0 || V <= 0) return fail("rb_embedding_bwd_apply: M, d, V must be positive");
+  if (M >= (int64_t(1) << 31) || V >= (int64_t(1) << 30))
+    return fail("rb_embedding_bwd_apply: M or V too large");
+  return launch_embedding_apply(grad, M, d, V, padding_idx, dweight, workspace, workspace_bytes,
+                                reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,

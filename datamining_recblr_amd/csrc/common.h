@@ -160,6 +160,11 @@ int launch_silu_dropout_bwd(const float* a, const float* bias, const DropSpec& d
                             int64_t rows, int64_t cols, hipStream_t st);
 int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
+int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, void* workspace,
+                          int64_t ws_bytes, hipStream_t st);
+int launch_embedding_apply(const float* grad, int64_t M, int64_t d, int64_t V,
+                           int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
+                           hipStream_t st);
 int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
                          int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
                          hipStream_t st);

@@ -207,9 +207,8 @@ int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d) {
   return (int64_t)emb_layout(M, V, d).total;
 }
 
-int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
-                         int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
-                         hipStream_t st) {
+int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, void* workspace,
+                          int64_t ws_bytes, hipStream_t st) {
   const EmbWs w = emb_layout(M, V, d);
   if (ws_bytes < (int64_t)w.total) return fail("rb_embedding_bwd: workspace too small");
   char* ws = static_cast<char*>(workspace);
@@ -234,11 +233,27 @@ int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64
   if (rocprim::exclusive_scan(ws + w.scan_tmp, scb, nch, choff, 0, (size_t)(V + 1),
                               rocprim::plus<int>(), st) != hipSuccess)
     return fail("rb_embedding_bwd: scan failed");
+  return launch_status("rb_embedding_plan");
+}
+
+int launch_embedding_apply(const float* grad, int64_t M, int64_t d, int64_t V,
+                           int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
+                           hipStream_t st) {
+  const EmbWs w = emb_layout(M, V, d);
+  if (ws_bytes < (int64_t)w.total) return fail("rb_embedding_bwd: workspace too small");
+  char* ws = static_cast<char*>(workspace);
   if (d <= 64) return emb_sums<1>(w, ws, grad, M, d, V, padding_idx, dw, st);
   if (d <= 128) return emb_sums<2>(w, ws, grad, M, d, V, padding_idx, dw, st);
   if (d <= 256) return emb_sums<4>(w, ws, grad, M, d, V, padding_idx, dw, st);
   if (d <= 512) return emb_sums<8>(w, ws, grad, M, d, V, padding_idx, dw, st);
   return fail("rb_embedding_bwd: d must be <= 512");
+}
+
+int launch_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d, int64_t V,
+                         int64_t padding_idx, float* dw, void* workspace, int64_t ws_bytes,
+                         hipStream_t st) {
+  if (int rc = launch_embedding_plan(idx, M, d, V, workspace, ws_bytes, st)) return rc;
+  return launch_embedding_apply(grad, M, d, V, padding_idx, dw, workspace, ws_bytes, st);
 }
 
 }  // namespace rb

@@ -18,6 +18,7 @@ __all__ = [
     "scan_fwd", "scan_bwd", "conv_silu_fwd", "conv_silu_bwd", "gate_scan_fwd",
     "gate_scan_bwd", "num_tiles", "RecBLRNativeError", "kernel_timing", "KernelTimer",
     "item_ce_fwd", "item_ce_bwd", "item_ce_probs", "item_rank", "item_scores",
+    "embedding_bwd", "embedding_plan",
 ]
 
 
@@ -55,15 +56,16 @@ def kernel_timing():
         _timer = prev
 
 
-def _launch(name: str, nbytes: int, *args) -> None:
+def _launch(name: str, nbytes: int, *args, _fn: str | None = None) -> None:
+    """Call C-ABI entry point `_fn or name`; timed under `name` in bench runs."""
     t = _timer
     if t is None:
-        _lib.call(name, *args)
+        _lib.call(_fn or name, *args)
         return
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    _lib.call(name, *args)
+    _lib.call(_fn or name, *args)
     e1.record()
     t.records.append((name, nbytes, e0, e1))
 
@@ -434,24 +436,40 @@ def dropout_mask(seed, p, shape, device):
     return out
 
 
-def embedding_bwd(idx, grad, num_rows, padding_idx=0):
-    """dW[v] = sum_{p: idx[p] == v} grad[p] (dW[padding_idx] = 0), deterministic."""
+def embedding_bwd(idx, grad, num_rows, padding_idx=0, plan=None):
+    """dW[v] = sum_{p: idx[p] == v} grad[p] (dW[padding_idx] = 0), deterministic.
+    plan: the workspace returned by embedding_plan for the same idx (skips the
+    sort), or None."""
     _check(grad, "grad")
     M = idx.numel()
     d = grad.shape[-1]
-    if idx.dtype != torch.int64 or not idx.is_contiguous():
-        raise ValueError("idx must be contiguous int64")
     grad = grad.reshape(M, d)
     if not grad.is_contiguous():
         grad = grad.contiguous()
-    lib = _lib.load()
-    ws_bytes = int(lib.rb_embedding_bwd_workspace(M, num_rows, d))
-    ws = torch.empty((ws_bytes,), device=grad.device, dtype=torch.uint8)
+    if plan is None:
+        plan = embedding_plan(idx, num_rows, d)
+    ws_bytes = plan.numel()
     dw = torch.empty((num_rows, d), device=grad.device, dtype=torch.float32)
     pad = -1 if padding_idx is None else int(padding_idx)
-    _launch("rb_embedding_bwd", 4 * M * d + 4 * num_rows * d, idx.data_ptr(), grad.data_ptr(), M,
-            d, num_rows, pad, dw.data_ptr(), ws.data_ptr(), ws_bytes, _stream(grad))
+    _launch("rb_embedding_bwd", 4 * M * d + 4 * num_rows * d, grad.data_ptr(), M, d, num_rows,
+            pad, dw.data_ptr(), plan.data_ptr(), ws_bytes, _stream(grad), _fn="rb_embedding_bwd_apply")
     return dw
+
+
+def embedding_plan(idx, num_rows, d, stream=None):
+    """Sort + segment the ids for embedding_bwd (index work only; may run on a
+    side stream during the forward).  Returns the uint8 workspace."""
+    M = idx.numel()
+    if idx.dtype != torch.int64 or not idx.is_contiguous():
+        raise ValueError("idx must be contiguous int64")
+    if idx.device.type != "cuda":
+        raise RecBLRNativeError("embedding_plan needs a GPU tensor")
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_embedding_bwd_workspace(M, num_rows, d))
+    ws = torch.empty((ws_bytes,), device=idx.device, dtype=torch.uint8)
+    st = stream.cuda_stream if stream is not None else _stream(idx)
+    _lib.call("rb_embedding_bwd_plan", idx.data_ptr(), M, d, num_rows, ws.data_ptr(), ws_bytes, st)
+    return ws
 
 
 # ---- item scoring (fp32 MFMA, no [B, V] logits) ------------------------------------

@@ -206,6 +206,16 @@ int rb_embedding_bwd(const int64_t* idx, const float* grad, int64_t M, int64_t d
                      int64_t V, int64_t padding_idx, float* dweight,
                      void* workspace, int64_t workspace_bytes, void* stream);
 
+/* rb_embedding_bwd in two halves: the plan (stable sort of the ids, segment
+ * and chunk offsets; depends on idx only, so it can run during the forward on
+ * another stream) and the apply (fixed-order segment sums of grad).  Same
+ * workspace, untouched between the two calls. */
+int rb_embedding_bwd_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V,
+                          void* workspace, int64_t workspace_bytes, void* stream);
+int rb_embedding_bwd_apply(const float* grad, int64_t M, int64_t d, int64_t V,
+                           int64_t padding_idx, float* dweight, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+
 /* Fixed-order column sums of partials: out[m*C + c] = sum over p < P of
  * in[m*ms + p*rs + c] for m < M, summed as RG interleaved partials
  * (p = g, g+RG, ... in increasing order; RG = 4 for P <= 256, else 16)
