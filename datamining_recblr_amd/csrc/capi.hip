@@ -56,7 +56,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 13; }
+int rb_version(void) { return 14; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -314,24 +314,26 @@ int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, i
 
 int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gate_b,
                       const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
-                      int64_t H, float* h0, void* stream) {
-  if (!conv_b || !gate_w || !gate_b || !lam || !h0) return fail("rb_pad_prefix_fwd: null pointer");
+                      int64_t H, float* h0, float* workspace, void* stream) {
+  if (!conv_b || !gate_w || !gate_b || !lam || !h0 || !workspace)
+    return fail("rb_pad_prefix_fwd: null pointer");
   if (H <= 0 || H > 4096 || n_rows <= 0 || pad_len < 0)
     return fail("rb_pad_prefix_fwd: need 0 < H <= 4096, n_rows > 0, pad_len >= 0");
   return launch_pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad, pad_len, n_rows, H, h0,
-                               reinterpret_cast<hipStream_t>(stream));
+                               workspace, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_pad_prefix_bwd(const float* conv_b, const float* gate_w, const float* gate_b,
                       const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                       int64_t H, const float* dh0, float* dconv_b, float* dgate_w,
-                      float* dgate_b, float* dlam, void* stream) {
-  if (!conv_b || !gate_w || !gate_b || !lam || !dh0 || !dconv_b || !dgate_w || !dgate_b || !dlam)
+                      float* dgate_b, float* dlam, float* workspace, void* stream) {
+  if (!conv_b || !gate_w || !gate_b || !lam || !dh0 || !dconv_b || !dgate_w || !dgate_b || !dlam ||
+      !workspace)
     return fail("rb_pad_prefix_bwd: null pointer");
   if (H <= 0 || H > 4096 || n_rows <= 0 || pad_len < 0)
     return fail("rb_pad_prefix_bwd: need 0 < H <= 4096, n_rows > 0, pad_len >= 0");
   return launch_pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad, pad_len, n_rows, H, dh0,
-                               dconv_b, dgate_w, dgate_b, dlam,
+                               dconv_b, dgate_w, dgate_b, dlam, workspace,
                                reinterpret_cast<hipStream_t>(stream));
 }
 

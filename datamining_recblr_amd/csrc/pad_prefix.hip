@@ -1,6 +1,6 @@
 // pad_prefix.hip — the recurrent state the reference's power-of-two left
-// padding leaves behind (RecBLR.py:176-179), forward and backward, each as
-// one single-workgroup launch.
+// padding leaves behind (RecBLR.py:176-179), forward (2 small launches) and
+// backward (4).
 //
 // Pad positions carry zeros into the causal conv, so every pad step sees the
 // per-channel constants xc_p = silu(conv.bias), (r_p, i_p) = W_g xc_p + b_g,
@@ -12,15 +12,14 @@
 // separate ~5 us launch at these sizes.
 //
 // Rows: h0 has n_rows rows; row b uses pad length pad[b] (pad != NULL) or
-// pad_len.  The backward sums the per-row gradients in row order.
+// pad_len.  The backward sums the per-row gradients in row order.  ws: 5H
+// floats of caller scratch (rg, drg, dxb).
 #include <cmath>
 
 #include "common.h"
 
 namespace rb {
 namespace {
-
-constexpr int kPT = 1024;  // threads of the single workgroup
 
 struct PadConsts {
   float xc, sg_r, sg_i, sp, s, alpha, q, beta, b;
@@ -37,11 +36,11 @@ __device__ __forceinline__ float expm1_ratio_ds(float P, float s) {
   return (-P * expf(-P * s) * d + expm1f(-P * s) * expf(-s)) / (d * d);
 }
 
-// per-channel constants from the gate pre-activations rg (LDS)
-__device__ __forceinline__ PadConsts consts(int c, int H, const float* xc, const float* rg,
+// per-channel constants from the gate pre-activations rg
+__device__ __forceinline__ PadConsts consts(int c, int H, float xc, const float* rg,
                                             const float* lam) {
   PadConsts k;
-  k.xc = xc[c];
+  k.xc = xc;
   k.sg_r = sigm(rg[c]);
   k.sg_i = sigm(rg[H + c]);
   k.sp = softplus_f(lam[c]);
@@ -55,89 +54,107 @@ __device__ __forceinline__ PadConsts consts(int c, int H, const float* xc, const
   return k;
 }
 
-// xc_p into LDS, then rg = W_g xc_p + b_g: one wave per output row, lanes
-// along the row (coalesced), fixed-order butterfly reduction
-__device__ void gates_of_pad(const float* conv_b, const float* gw, const float* gb, int H,
-                             float* xc, float* rg) {
-  for (int c = threadIdx.x; c < H; c += kPT) xc[c] = silu_f(conv_b[c]);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int o = wave; o < 2 * H; o += kPT / 64) {
-    const float* w = gw + (int64_t)o * H;
-    float acc = 0.0f;
-    for (int k = lane; k < H; k += 64) acc = fmaf(w[k], xc[k], acc);
+// rg = W_g silu(conv_b) + b_g: one wave per output row, lanes along the row
+// (coalesced), fixed-order butterfly; many workgroups so the 2H row reads
+// are in flight together (a single workgroup is load-latency bound).
+__global__ __launch_bounds__(256) void k_pad_gates(const float* __restrict__ conv_b,
+                                                   const float* __restrict__ gw,
+                                                   const float* __restrict__ gb, int H,
+                                                   float* __restrict__ rg) {
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (o >= 2 * H) return;
+  const float* w = gw + (int64_t)o * H;
+  float acc = 0.0f;
+  for (int k = lane; k < H; k += 64) acc = fmaf(w[k], silu_f(conv_b[k]), acc);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) rg[o] = acc + gb[o];
-  }
-  __syncthreads();
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (lane == 0) rg[o] = acc + gb[o];
 }
 
-__global__ __launch_bounds__(kPT) void k_pad_prefix_fwd(const float* __restrict__ conv_b,
-                                                        const float* __restrict__ gw,
-                                                        const float* __restrict__ gb,
+__global__ __launch_bounds__(256) void k_pad_prefix_fwd(const float* __restrict__ conv_b,
+                                                        const float* __restrict__ rg,
                                                         const float* __restrict__ lam,
                                                         const int64_t* __restrict__ pad,
                                                         int64_t pad_len, int64_t n_rows, int H,
                                                         float* __restrict__ h0) {
-  extern __shared__ float sh[];
-  float* xc = sh;
-  float* rg = sh + H;
-  gates_of_pad(conv_b, gw, gb, H, xc, rg);
-  for (int c = threadIdx.x; c < H; c += kPT) {
-    const PadConsts k = consts(c, H, xc, rg, lam);
-    for (int64_t r = 0; r < n_rows; ++r) {
-      const float P = (float)(pad ? pad[r] : pad_len);
-      h0[r * H + c] = k.b * expm1_ratio(P, k.s);
-    }
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= H) return;
+  const float xc = silu_f(conv_b[c]);
+  const PadConsts k = consts(c, H, xc, rg, lam);
+  for (int64_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
+    const float P = (float)(pad ? pad[r] : pad_len);
+    h0[r * H + c] = k.b * expm1_ratio(P, k.s);
   }
 }
 
-__global__ __launch_bounds__(kPT) void k_pad_prefix_bwd(
-    const float* __restrict__ conv_b, const float* __restrict__ gw, const float* __restrict__ gb,
-    const float* __restrict__ lam, const int64_t* __restrict__ pad, int64_t pad_len,
-    int64_t n_rows, int H, const float* __restrict__ dh0, float* __restrict__ dconv_b,
-    float* __restrict__ dgw, float* __restrict__ dgb, float* __restrict__ dlam) {
-  extern __shared__ float sh[];
-  float* xc = sh;
-  float* rg = sh + H;
-  float* drg = sh + 3 * H;    // [2H]
-  float* dxb = sh + 5 * H;    // [H] d xc_p through b_p
-  gates_of_pad(conv_b, gw, gb, H, xc, rg);
-  for (int c = threadIdx.x; c < H; c += kPT) {
-    const PadConsts k = consts(c, H, xc, rg, lam);
-    float gb_ = 0.0f, gs = 0.0f;   // dL/db_p, dL/ds
-    for (int64_t r = 0; r < n_rows; ++r) {
-      const float P = (float)(pad ? pad[r] : pad_len);
-      const float g = dh0[r * H + c];
-      gb_ = fmaf(g, expm1_ratio(P, k.s), gb_);
-      gs = fmaf(g * k.b, expm1_ratio_ds(P, k.s), gs);
-    }
-    if (k.clamped) gs = 0.0f;                        // clamp_min(1e-20) passes no gradient
-    // b = beta xc; beta = q sg_i; q = sqrt(1 - alpha^2 + 1e-8); alpha = exp(-s)
-    const float dbeta = gb_ * k.xc;
-    dxb[c] = gb_ * k.beta;
-    const float dq = dbeta * k.sg_i;
-    const float dsg_i = dbeta * k.q;
-    const float dalpha = dq * (-k.alpha / k.q);
-    // alpha = exp(-s_raw) (the unclamped s, as torch computes alpha)
-    const float ds = gs + dalpha * (-k.alpha);
-    // s = sp * sg_r
-    dlam[c] = ds * k.sg_r * dsoftplus_f(lam[c]);
-    const float dsg_r = ds * k.sp;
-    drg[c] = dsg_r * k.sg_r * (1.0f - k.sg_r);
-    drg[H + c] = dsg_i * k.sg_i * (1.0f - k.sg_i);
+// per-channel part of the backward: drg [2H], dlam, dgate_b, and the part of
+// d xc_p that flows through b_p (dxb)
+__global__ __launch_bounds__(256) void k_pad_prefix_bwd1(
+    const float* __restrict__ conv_b, const float* __restrict__ rg, const float* __restrict__ lam,
+    const int64_t* __restrict__ pad, int64_t pad_len, int64_t n_rows, int H,
+    const float* __restrict__ dh0, float* __restrict__ drg, float* __restrict__ dxb,
+    float* __restrict__ dgb, float* __restrict__ dlam) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= H) return;
+  const float xc = silu_f(conv_b[c]);
+  const PadConsts k = consts(c, H, xc, rg, lam);
+  float gb_ = 0.0f, gs = 0.0f;   // dL/db_p, dL/ds, rows in order
+  for (int64_t r = 0; r < n_rows; ++r) {
+    const float P = (float)(pad ? pad[r] : pad_len);
+    const float g = dh0[r * H + c];
+    gb_ = fmaf(g, expm1_ratio(P, k.s), gb_);
+    gs = fmaf(g * k.b, expm1_ratio_ds(P, k.s), gs);
   }
+  if (k.clamped) gs = 0.0f;                        // clamp_min(1e-20) passes no gradient
+  // b = beta xc; beta = q sg_i; q = sqrt(1 - alpha^2 + 1e-8); alpha = exp(-s_raw)
+  const float dbeta = gb_ * k.xc;
+  dxb[c] = gb_ * k.beta;
+  const float dq = dbeta * k.sg_i;
+  const float dsg_i = dbeta * k.q;
+  const float dalpha = dq * (-k.alpha / k.q);
+  const float ds = gs + dalpha * (-k.alpha);
+  dlam[c] = ds * k.sg_r * dsoftplus_f(lam[c]);     // s = softplus(lam) sg_r
+  const float dr = ds * k.sp * k.sg_r * (1.0f - k.sg_r);
+  const float di = dsg_i * k.sg_i * (1.0f - k.sg_i);
+  drg[c] = dr;
+  drg[H + c] = di;
+  dgb[c] = dr;
+  dgb[H + c] = di;
+}
+
+// dW_g = drg (x) xc_p, grid-stride over the [2H, H] rows (coalesced)
+__global__ __launch_bounds__(256) void k_pad_prefix_bwd2(const float* __restrict__ conv_b, int H,
+                                                         const float* __restrict__ drg,
+                                                         float* __restrict__ dgw) {
+  const int64_t n = 2 * (int64_t)H * H;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * 256) {
+    const int64_t o = e / H, c = e - o * H;
+    dgw[e] = drg[o] * silu_f(conv_b[c]);
+  }
+}
+
+// dconv_b = (W_g^T drg + dxb) silu'(conv_b): 64 columns per workgroup, 16
+// row groups (o = g, g+16, ... in order) combined in order g = 0..15
+__global__ __launch_bounds__(1024) void k_pad_prefix_bwd3(const float* __restrict__ conv_b,
+                                                          const float* __restrict__ gw, int H,
+                                                          const float* __restrict__ drg,
+                                                          const float* __restrict__ dxb,
+                                                          float* __restrict__ dconv_b) {
+  __shared__ float red[16][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float acc = 0.0f;
+  if (c < H)
+    for (int o = ty; o < 2 * H; o += 16) acc = fmaf(gw[(int64_t)o * H + c], drg[o], acc);
+  red[ty][tx] = acc;
   __syncthreads();
-  for (int o = threadIdx.x; o < 2 * H; o += kPT) dgb[o] = drg[o];
-  // dW_g = drg (x) xc_p, written row by row (threads along the row)
-  for (int o = 0; o < 2 * H; ++o)
-    for (int c = threadIdx.x; c < H; c += kPT) dgw[(int64_t)o * H + c] = drg[o] * xc[c];
-  // d xc_p = W_g^T drg + (through b_p), then silu'
-  for (int c = threadIdx.x; c < H; c += kPT) {
-    float acc = 0.0f;
-    for (int o = 0; o < 2 * H; ++o) acc = fmaf(gw[(int64_t)o * H + c], drg[o], acc);
-    dconv_b[c] = (acc + dxb[c]) * dsilu_f(conv_b[c]);
+  if (ty == 0 && c < H) {
+    float t = red[0][tx];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) t += red[g][tx];
+    dconv_b[c] = (t + dxb[c]) * dsilu_f(conv_b[c]);
   }
 }
 
@@ -145,19 +162,31 @@ __global__ __launch_bounds__(kPT) void k_pad_prefix_bwd(
 
 int launch_pad_prefix_fwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
-                          int64_t H, float* h0, hipStream_t st) {
-  hipLaunchKernelGGL(k_pad_prefix_fwd, dim3(1), dim3(kPT), (size_t)3 * H * sizeof(float), st,
-                     conv_b, gw, gb, lam, pad, pad_len, n_rows, (int)H, h0);
+                          int64_t H, float* h0, float* ws, hipStream_t st) {
+  float* rg = ws;
+  hipLaunchKernelGGL(k_pad_gates, dim3((unsigned)((2 * H + 3) / 4)), dim3(256), 0, st, conv_b, gw,
+                     gb, (int)H, rg);
+  const unsigned ry = (unsigned)std::min<int64_t>(n_rows, 1024);
+  hipLaunchKernelGGL(k_pad_prefix_fwd, dim3((unsigned)((H + 255) / 256), ry), dim3(256), 0, st,
+                     conv_b, rg, lam, pad, pad_len, n_rows, (int)H, h0);
   return launch_status("rb_pad_prefix_fwd");
 }
 
 int launch_pad_prefix_bwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                           int64_t H, const float* dh0, float* dconv_b, float* dgw, float* dgb,
-                          float* dlam, hipStream_t st) {
-  hipLaunchKernelGGL(k_pad_prefix_bwd, dim3(1), dim3(kPT), (size_t)6 * H * sizeof(float), st,
-                     conv_b, gw, gb, lam, pad, pad_len, n_rows, (int)H, dh0, dconv_b, dgw, dgb,
-                     dlam);
+                          float* dlam, float* ws, hipStream_t st) {
+  float* rg = ws;
+  float* drg = ws + 2 * H;
+  float* dxb = ws + 4 * H;
+  hipLaunchKernelGGL(k_pad_gates, dim3((unsigned)((2 * H + 3) / 4)), dim3(256), 0, st, conv_b, gw,
+                     gb, (int)H, rg);
+  hipLaunchKernelGGL(k_pad_prefix_bwd1, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, st,
+                     conv_b, rg, lam, pad, pad_len, n_rows, (int)H, dh0, drg, dxb, dgb, dlam);
+  const unsigned nb = (unsigned)std::min<int64_t>(1024, (2 * H * H + 255) / 256);
+  hipLaunchKernelGGL(k_pad_prefix_bwd2, dim3(nb), dim3(256), 0, st, conv_b, (int)H, drg, dgw);
+  hipLaunchKernelGGL(k_pad_prefix_bwd3, dim3((unsigned)((H + 63) / 64)), dim3(1024), 0, st, conv_b,
+                     gw, (int)H, drg, dxb, dconv_b);
   return launch_status("rb_pad_prefix_bwd");
 }
 

@@ -601,10 +601,11 @@ def pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad_len):
         raise ValueError("pad prefix: parameter shapes")
     pad, plen, rows = _pad_args(pad_len, H, lam.device)
     h0 = torch.empty((rows, H), device=lam.device, dtype=torch.float32)
+    ws = torch.empty((5 * H,), device=lam.device, dtype=torch.float32)
     _lib.call("rb_pad_prefix_fwd", conv_b.contiguous().data_ptr(), gate_w.contiguous().data_ptr(),
               gate_b.contiguous().data_ptr(), lam.contiguous().data_ptr(),
               pad.data_ptr() if pad is not None else None, plen, rows, H, h0.data_ptr(),
-              _stream(lam))
+              ws.data_ptr(), _stream(lam))
     return h0 if pad is not None else h0[0]
 
 
@@ -618,8 +619,10 @@ def pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad_len, dh0):
     dgw = torch.empty_like(gate_w)
     dgb = torch.empty_like(gate_b)
     dlam = torch.empty_like(lam)
+    ws = torch.empty((5 * H,), device=lam.device, dtype=torch.float32)
     _lib.call("rb_pad_prefix_bwd", conv_b.contiguous().data_ptr(), gate_w.contiguous().data_ptr(),
               gate_b.contiguous().data_ptr(), lam.contiguous().data_ptr(),
               pad.data_ptr() if pad is not None else None, plen, rows, H, dh0.data_ptr(),
-              dcb.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), dlam.data_ptr(), _stream(lam))
+              dcb.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), dlam.data_ptr(), ws.data_ptr(),
+              _stream(lam))
     return dcb, dgw, dgb, dlam

@@ -131,10 +131,10 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
  *   h0 = b_p expm1(-P s) / expm1(-s)            (s clamped at 1e-20).
  * gate_w: [2H, H] row-major; h0: [n_rows, H]; row b uses pad[b] (pad != NULL)
  * or pad_len.  Feeds rb_gate_scan_fwd's h0 (h0_bs = 0 for one row, H for
- * per-row pad lengths).  Single-workgroup launches; H <= 4096. */
+ * per-row pad lengths).  workspace: 5H floats of scratch; H <= 4096. */
 int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gate_b,
                       const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
-                      int64_t H, float* h0, void* stream);
+                      int64_t H, float* h0, float* workspace, void* stream);
 
 /* Backward of rb_pad_prefix_fwd for dh0 [n_rows, H] (rows summed in order):
  * writes dconv_b [H], dgate_w [2H, H], dgate_b [2H], dlam [H] (overwritten,
@@ -142,7 +142,7 @@ int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gat
 int rb_pad_prefix_bwd(const float* conv_b, const float* gate_w, const float* gate_b,
                       const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                       int64_t H, const float* dh0, float* dconv_b, float* dgate_w,
-                      float* dgate_b, float* dlam, void* stream);
+                      float* dgate_b, float* dlam, float* workspace, void* stream);
 
 /* ---- blocks around the BD-LRU (RecurrentLayer / FeedForward / embedding) ---- */
 
