@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-full-tail", action="store_true",
+                    help="skip the comparison run that evaluates the last layer's "
+                         "position-wise tail at every position")
     args = ap.parse_args()
 
     env = init_from_env()
@@ -178,6 +181,30 @@ def main():
     value = env.world_size * args.batch * args.steps / elapsed
     if not torch.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
+
+    # Same step with the last layer's position-wise tail at every position (as
+    # the reference computes it; results identical) for comparison.
+    full_tail = None
+    if not args.no_full_tail:
+        model.gather_last_layer = False
+        for i in range(2):
+            step(i)
+        torch.cuda.synchronize()
+        barrier(env)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        torch.cuda.synchronize()
+        barrier(env)
+        torch.cuda.synchronize()
+        el = max_over_ranks(time.perf_counter() - t1, env, dev)
+        model.gather_last_layer = True
+        full_tail = {"value": round(env.world_size * args.batch * args.steps / el, 1),
+                     "ms_per_step": round(1000.0 * el / args.steps, 3),
+                     "note": "last layer's out-proj/LN/FFN at all B*L positions (the "
+                             "reference's arithmetic); loss and gradients identical to "
+                             "the gathered run (tests/test_gpu_eval.py)"}
 
     roofline = None
     kernels_report = None
@@ -252,6 +279,7 @@ def main():
             "data": "synthetic RecBole-shaped batches (ids ~U{1..n_items-1}, lengths ~U{1..L}, "
                     "right-padded), reference init (seed 2020), resident in HBM",
             "config": {"workload": "RecBLR train step: calculate_loss(CE)+backward+Adam",
+                       "last_layer_tail": "gathered positions (gather_indexes rows only)",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * env.world_size,
                        "seq_len": args.seq_len, "hidden_size": args.hidden, "inner_H": H,
                        "num_layers": args.layers, "n_items": args.n_items,
@@ -259,6 +287,7 @@ def main():
             "roofline": roofline,
             "gemm": gemm,
             "kernels": kernels_report,
+            "all_positions_tail": full_tail,
             "scan_fwd_only": scan,
             "cpu_baseline": cpu,
         }

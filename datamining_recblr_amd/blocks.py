@@ -50,11 +50,14 @@ class ResidualGrad:
     the GRL's input projection, whose dX GEMM adds it with beta = 1
     (linear.LinearFn) instead of autograd summing two [B, L, d] gradients in
     a separate pass.  The LayerNorm backward always runs first (the
-    projection's gradient depends on it)."""
-    __slots__ = ("ds",)
+    projection's gradient depends on it).  ``rows``: when the LayerNorm ran
+    on a gathered subset of the positions (the last layer, see
+    RecBLR.forward), the flat [B*L] rows its residual came from."""
+    __slots__ = ("ds", "rows")
 
-    def __init__(self):
+    def __init__(self, rows=None):
         self.ds = None
+        self.rows = rows
 
 
 class _AddDropoutLN(torch.autograd.Function):

@@ -75,11 +75,15 @@ class LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             slot = ctx.slot
-            if slot is not None and slot.ds is not None:   # + a handed-over residual gradient
+            if slot is not None and slot.ds is not None and slot.rows is None:
+                # + a handed-over residual gradient, inside the GEMM (beta = 1)
                 dx = _timed("gemm", flops, slot.ds.view(-1, weight.shape[1]).addmm_, dy2, weight)
                 slot.ds = None
             else:
                 dx = _timed("gemm", flops, torch.mm, dy2, weight)
+                if slot is not None and slot.ds is not None:   # residual of gathered rows
+                    dx.index_add_(0, slot.rows, slot.ds.view(-1, weight.shape[1]))
+                    slot.ds = None
             dx = dx.view(*dy.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _timed("gemm", flops, wgrad, dy2, x2)

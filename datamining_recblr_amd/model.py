@@ -21,6 +21,7 @@ Everything needs a ROCm GPU; there is no CPU fallback.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -72,10 +73,13 @@ class GatedRecurrentLayer(nn.Module):
         self.Lambda = nn.Parameter(torch.linspace(lo, hi, hidden))
         self.output = nn.Linear(hidden, d_model, bias=False)
 
-    def forward(self, x, pad=None, slot=None):
+    def forward(self, x, pad=None, slot=None, rows=None):
         """pad: None (the reference's pow2 pad prefix for x's length) or an
         int64 tensor [B] of per-row pad lengths (see recurrence.bd_lru).
-        slot: blocks.ResidualGrad of the enclosing RecurrentLayer."""
+        slot: blocks.ResidualGrad of the enclosing RecurrentLayer.
+        rows: flat [B*L] positions at which the output is needed (the
+        out-projection is position-wise, so only those rows are projected;
+        returns [len(rows), d])."""
         if x.device.type != "cuda":
             raise RecBLRNativeError(
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
@@ -83,6 +87,8 @@ class GatedRecurrentLayer(nn.Module):
         xz = linear(x, self.input, slot)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad)
+        if rows is not None:
+            y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
         return linear(y, self.output)
 
     @staticmethod
@@ -119,10 +125,15 @@ class RecurrentLayer(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
         self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
 
-    def forward(self, input_tensor, pad=None):
-        slot = (ResidualGrad() if torch.is_grad_enabled() and input_tensor.requires_grad
+    def forward(self, input_tensor, pad=None, rows=None):
+        """rows: evaluate the position-wise tail (out-projection, residual
+        LayerNorm, FFN) only at these flat [B*L] positions -> [len(rows), d]."""
+        slot = (ResidualGrad(rows) if torch.is_grad_enabled() and input_tensor.requires_grad
                 else None)
-        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad, slot), input_tensor,
+        residual = input_tensor
+        if rows is not None:
+            residual = input_tensor.reshape(-1, input_tensor.shape[-1]).index_select(0, rows)
+        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad, slot, rows), residual,
                                    self.dropout, self.layer_norm, self.training, slot)
         return h if self.disable_ffn else self.ffn(h)
 
@@ -144,6 +155,9 @@ class RecBLR(SequentialRecommender):
         if self.bd_lru_only:  # RecBLR.py:33-35
             self.disable_conv1d = True
             self.disable_ffn = True
+        # evaluate the last layer's position-wise tail only where gather_indexes
+        # reads it (RECBLR_FULL_LAST_LAYER=1: every position, as the reference)
+        self.gather_last_layer = os.environ.get("RECBLR_FULL_LAST_LAYER", "0") != "1"
 
         self.item_embedding = nn.Embedding(self.n_items, self.hidden_size, padding_idx=0)
         self.layer_norm = nn.LayerNorm(self.hidden_size, eps=1e-12)
@@ -184,7 +198,15 @@ class RecBLR(SequentialRecommender):
         pad = row_pad_lens(item_seq_len) if exact_lengths else None
         h = embed_dropout_layer_norm(item_seq, self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
-        for layer in self.recurrent_layers:
+        n = len(self.recurrent_layers)
+        for i, layer in enumerate(self.recurrent_layers):
+            if i == n - 1 and self.gather_last_layer:
+                # Everything after the last layer's scan is position-wise and only
+                # the positions gather_indexes picks reach the output: evaluate
+                # that tail at those B positions (identical results).
+                B, L = item_seq.shape
+                rows = torch.arange(B, device=item_seq.device) * L + (item_seq_len - 1)
+                return layer(h, pad, rows)
             h = layer(h, pad)
         return self.gather_indexes(h, item_seq_len - 1)
 

@@ -116,3 +116,28 @@ def test_full_sort_metrics_recbole(cuda):
             top = sc.topk(20, dim=1).indices
             hits.append((top == inter["item_id"][:, None]).any(1).double())
     assert abs(m["hit@20"] - torch.cat(hits).mean().item()) < 1e-9
+
+
+@pytest.mark.parametrize("flags", [{}, {"disable_ffn": True}, {"num_layers": 1}])
+def test_gathered_last_layer_equals_full(cuda, flags):
+    """The last layer's position-wise tail evaluated only at the gathered
+    positions gives the reference's full-sequence results (loss and every
+    gradient), dropout off."""
+    from datamining_recblr_amd.distributed import synthetic_interaction
+
+    model = _model(cuda, n_items=600, **flags)
+    inter = synthetic_interaction(96, 50, 600, cuda, seed=11)
+    res = []
+    for gather in (True, False):
+        model.gather_last_layer = gather
+        model.zero_grad(set_to_none=True)
+        loss = model.calculate_loss(inter)
+        loss.backward()
+        res.append((loss.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                                    if p.grad is not None}))
+    (l1, g1), (l2, g2) = res
+    assert abs(l1.item() - l2.item()) < 1e-5
+    assert g1.keys() == g2.keys()
+    for n in g1:
+        err = (g1[n].double() - g2[n].double()).norm() / max(g2[n].double().norm().item(), 1e-12)
+        assert err < 1e-5, (n, err.item())
