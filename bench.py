@@ -31,6 +31,7 @@ from datamining_recblr_amd import kernels  # noqa: E402
 from datamining_recblr_amd.distributed import (barrier, init_from_env, max_over_ranks,  # noqa: E402
                                                synthetic_interaction, wrap_ddp)
 from datamining_recblr_amd.gemm_tuning import tuned_gemms_active  # noqa: E402
+from datamining_recblr_amd.linear import split_gemm_enabled  # noqa: E402
 from datamining_recblr_amd.model import RecBLR  # noqa: E402
 from datamining_recblr_amd.recbole_compat import SyntheticDataset  # noqa: E402
 
@@ -220,8 +221,11 @@ def main():
                     "ms_per_step": round(g["ms"] / args.steps, 3),
                     "gemms_per_step": g["launches"] / args.steps,
                     "flops_per_step": int(g["bytes"] / args.steps),
-                    "library": "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)",
-                    "tuned_table": tuned_gemms_active()}
+                    "library": ("split-bf16 MFMA kernel (csrc/gemm_split.hip) for the [B*L] "
+                                "forward/input-gradient GEMMs, " if split_gemm_enabled() else "")
+                               + "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)",
+                    "tuned_table": tuned_gemms_active(),
+                    "by_shape": timer.gemm_detail(args.steps)}
         kernels_report = {}
         for name, d in summ.items():
             if name in kernels.FLOP_KERNELS:   # MFMA kernels: algorithmic FLOPs

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 
 from . import kernels
 from ._lib import RecBLRNativeError
-from .linear import _timed, linear, wgrad
+from .linear import _timed, linear, mm_nn, mm_nt, wgrad
 
 __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
            "feed_forward"]
@@ -165,9 +165,9 @@ class _FeedForward(torch.autograd.Function):
         f = 2 * M * d * inner
         # b1 is added inside the activation kernel (the bias epilogue of the
         # library GEMM costs more than the add on the fly)
-        a1 = _timed("gemm", f, torch.mm, x2, w1.t())
+        a1 = _timed("gemm", f, mm_nt, x2, w1)
         u = kernels.silu_dropout_fwd(a1, seed=seed1, p=p, bias=b1)
-        a2 = _timed("gemm", f, torch.addmm, b2, u, w2.t())
+        a2 = _timed("gemm", f, mm_nt, u, w2, b2)
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
                                               p=p, save=save)
@@ -183,11 +183,11 @@ class _FeedForward(torch.autograd.Function):
         ds, da2, dgamma, dbeta, db2 = kernels.add_ln_bwd(
             dy, s, gamma, mean, rstd, seed=ctx.seed2, p=ctx.p, want_ds=True, want_da=True,
             want_dbias=True)
-        du = _timed("gemm", f, torch.mm, da2, w2)
+        du = _timed("gemm", f, mm_nn, da2, w2)
         dw2 = _timed("gemm", f, wgrad, da2, u)
         da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True,
                                             bias=b1)
-        dx = _timed("gemm", f, ds.addmm_, da1, w1)   # residual grad + W1^T path, in place
+        dx = _timed("gemm", f, mm_nn, da1, w1, ds)   # residual grad + W1^T path, in place
         dw1 = _timed("gemm", f, wgrad, da1, x2)
         return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None)
 

@@ -2,6 +2,8 @@
 // argument validation, error reporting, dispatch to the kernel launchers.
 #include "common.h"
 
+#include <atomic>
+
 namespace rb {
 
 namespace {
@@ -11,6 +13,19 @@ thread_local std::string g_last_error;
 int fail(const char* msg) {
   g_last_error = msg;
   return RB_EINVAL;
+}
+
+int num_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n <= 0) {
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+  }
+  return n;
 }
 
 int launch_status(const char* what) {
@@ -56,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 14; }
+int rb_version(void) { return 15; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -344,6 +359,32 @@ int rb_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int6
     return fail("rb_colsum: bad shape or strides");
   if (M * ((C + 63) / 64) > 0x7fffffffLL) return fail("rb_colsum: grid too large");
   return launch_colsum(in, M, P, C, rs, ms, out, reinterpret_cast<hipStream_t>(stream));
+}
+
+int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R) { return C * R * 6; }
+
+int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
+                         void* Wf, void* stream) {
+  if (!W || !Wf) return fail("rb_gemm_split_weight: null pointer");
+  if (C <= 0 || R <= 0 || C % 32 || R % 16 || C > (1 << 20) || R > (1 << 20))
+    return fail("rb_gemm_split_weight: C must be a multiple of 32 and R of 16");
+  if (ldw < (transpose ? C : R)) return fail("rb_gemm_split_weight: bad row stride");
+  if (!aligned16(Wf)) return fail("rb_gemm_split_weight: Wf must be 16-byte aligned");
+  return launch_split_weight(W, ldw, (int)C, (int)R, transpose, Wf,
+                             reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+               const float* bias, float* out, int64_t ldo, int accumulate, void* stream) {
+  if (!A || !Wf || !out) return fail("rb_gemm_nt: null pointer");
+  if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt: empty shape");
+  if (R % 32 || C % 128 || R > (1 << 16) || C > (1 << 16))
+    return fail("rb_gemm_nt: R must be a multiple of 32 and C of 128");
+  if (lda < R || lda % 4 || ldo < C) return fail("rb_gemm_nt: bad row strides");
+  if (!aligned16(A) || !aligned16(Wf)) return fail("rb_gemm_nt: A and Wf must be 16-byte aligned");
+  if ((M + 127) / 128 * (C / 128) > 0x7fffffffLL) return fail("rb_gemm_nt: grid too large");
+  return launch_gemm_nt(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate,
+                        reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

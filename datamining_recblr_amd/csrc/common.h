@@ -16,6 +16,8 @@ constexpr int kWave = 64;
 // ---- error reporting (host) -------------------------------------------------
 int fail(const char* msg);
 int launch_status(const char* what);
+// compute units of the current device (cached per device)
+int num_cus();
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
@@ -159,6 +161,10 @@ int launch_silu_dropout_bwd(const float* a, const float* bias, const DropSpec& d
                             const float* du, float* da, float* dbias_part, int64_t nparts,
                             int64_t rows, int64_t cols, hipStream_t st);
 int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st);
+int launch_split_weight(const float* W, int64_t ldw, int C, int R, int transpose, void* Wf,
+                        hipStream_t st);
+int launch_gemm_nt(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                   const float* bias, float* out, int64_t ldo, int accumulate, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
 int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, void* workspace,
                           int64_t ws_bytes, hipStream_t st);

@@ -28,6 +28,20 @@ class KernelTimer:
 
     def __init__(self):
         self.records = []   # (name, algorithmic bytes, start event, end event)
+        self.detail = []    # GEMMs by shape: (label, flops, start event, end event)
+
+    def gemm_detail(self, steps: int):
+        """Per-shape GEMM times: label -> launches/step, avg us, TFLOP/s."""
+        torch.cuda.synchronize()
+        out = {}
+        for label, flops, e0, e1 in self.detail:
+            d = out.setdefault(label, {"n": 0, "ms": 0.0, "flops": 0})
+            d["n"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += flops
+        return {k: {"per_step": d["n"] / steps, "avg_us": round(d["ms"] * 1e3 / d["n"], 1),
+                    "tflops": round(d["flops"] / d["ms"] / 1e9, 1)}
+                for k, d in sorted(out.items(), key=lambda kv: -kv[1]["ms"])}
 
     def summary(self):
         torch.cuda.synchronize()
@@ -626,3 +640,41 @@ def pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad_len, dh0):
               dcb.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), dlam.data_ptr(), ws.data_ptr(),
               _stream(lam))
     return dcb, dgw, dgb, dlam
+
+
+# ---- projection GEMMs on the bf16 MFMA pipe (exact 3-way split, fp32-accurate) ----
+
+def gemm_split_weight(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """Fragment-ordered bf16 split image of Bm = w (transpose=False, w [C, R])
+    or Bm = w^T (w [R, C]) for gemm_nt (rb_gemm_split_weight)."""
+    _check(w, "weight")
+    if w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("weight must be a 2-D row-major tensor")
+    R, C = (w.shape[0], w.shape[1]) if transpose else (w.shape[1], w.shape[0])
+    nbytes = _lib.load().rb_gemm_split_weight_bytes(C, R)
+    wf = torch.empty(nbytes // 2, device=w.device, dtype=torch.bfloat16)
+    _lib.call("rb_gemm_split_weight", w.data_ptr(), w.stride(0), C, R, int(transpose),
+              wf.data_ptr(), _stream(w))
+    return wf
+
+
+def gemm_nt(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None = None,
+            out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
+    """out[M, C] (+)= a[M, R] @ Bm^T (+ bias) with Bm's split image wf
+    (rb_gemm_nt).  a: 2-D, unit inner stride, row stride a multiple of 4."""
+    _check(a, "a")
+    if a.dim() != 2 or a.stride(1) != 1:
+        raise ValueError("a must be a 2-D tensor with unit inner stride")
+    M, R = a.shape
+    if out is None:
+        if accumulate:
+            raise ValueError("accumulate needs out")
+        out = torch.empty((M, C), device=a.device, dtype=torch.float32)
+    elif out.shape != (M, C) or out.stride(1) != 1:
+        raise ValueError("out must be [M, C] with unit inner stride")
+    if bias is not None:
+        _check(bias, "bias")
+    _lib.call("rb_gemm_nt", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
+              0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0),
+              int(accumulate), _stream(a))
+    return out

@@ -9,16 +9,58 @@ MFMA peak 157).  Splitting the reduction into S row blocks as one batched GEMM
 ([S, N, M/S] x [S, M/S, K], ~1000 tiles) and summing the S partials in a fixed
 order runs 2-4.5x faster (tools/gemm_probe.py) and is deterministic.
 
-All GEMMs run on hipBLASLt/rocBLAS MFMA kernels through torch; the math is
-exactly nn.Linear's (RecBLR.py:162,165,167,213,214).
+With RECBLR_SPLIT_GEMM=1 the forward and input-gradient GEMMs of the
+[B*L, *] projections run on the split-bf16 MFMA kernel (csrc/gemm_split.hip,
+``mm_nt`` / ``mm_nn``): fp32 operands split exactly into three bf16 parts, six
+partial products, fp32 accumulation — fp32-level accuracy on the bf16 pipe
+(2.67x the fp32 MFMA peak on paper).  Measured inside the training step it
+runs at 120-156 TFLOP/s against 128-149 for the tuned hipBLASLt fp32 kernels
+(DESIGN.md §4), so it is off by default.  Shapes it does not cover (and small
+M) always stay on hipBLASLt/rocBLAS through torch.  The math is exactly
+nn.Linear's (RecBLR.py:162,165,167,213,214).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from . import gemm_tuning, kernels
 
-__all__ = ["linear", "wgrad", "LinearFn"]
+__all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled"]
+
+SPLIT_MIN_ROWS = 4096
+_split_on = os.environ.get("RECBLR_SPLIT_GEMM", "0") == "1"
+
+
+def split_gemm_enabled() -> bool:
+    return _split_on
+
+
+def _split_ok(a: torch.Tensor, C: int, R: int) -> bool:
+    return (_split_on and a.is_cuda and a.dim() == 2 and a.shape[0] >= SPLIT_MIN_ROWS
+            and C % 128 == 0 and R % 32 == 0 and a.stride(1) == 1 and a.stride(0) % 4 == 0
+            and a.data_ptr() % 16 == 0 and a.dtype == torch.float32)
+
+
+def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+    """a [M, K] @ w[N, K]^T (+ bias): F.linear's forward GEMM."""
+    N, K = w.shape
+    if _split_ok(a, N, K):
+        return kernels.gemm_nt(a, kernels.gemm_split_weight(w), N, bias=bias)
+    return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
+
+
+def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """dy [M, N] @ w [N, K] (the input gradient of F.linear); with `out`,
+    accumulated into it in place (out += dy @ w)."""
+    N, K = w.shape
+    if _split_ok(dy, K, N) and (out is None or (out.stride(1) == 1 and out.shape == (dy.shape[0], K))):
+        return kernels.gemm_nt(dy, kernels.gemm_split_weight(w, transpose=True), K, out=out,
+                               accumulate=out is not None)
+    if out is not None:
+        return out.addmm_(dy, w)
+    return torch.mm(dy, w)
 
 SPLIT_K = 64
 MIN_ROWS_FOR_SPLIT = 16384
@@ -39,6 +81,18 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.T
     return out
 
 
+def _label(fn, args) -> str:
+    """GEMM label for the bench's per-shape breakdown: op[M x K -> N]."""
+    name = getattr(fn, "__name__", "gemm")
+    if name in ("mm_nt", "mm_nn") and len(args) >= 2:
+        a, w = args[0], args[1]
+        n_out = w.shape[0] if name == "mm_nt" else w.shape[1]
+        return f"{name}[{a.shape[0]}x{a.shape[1]}->{n_out}]"
+    if name == "wgrad" and len(args) >= 2:
+        return f"wgrad[{args[0].shape[0]}:{args[0].shape[1]}x{args[1].shape[1]}]"
+    return name
+
+
 def _timed(kind, flops, fn, *args, **kw):
     """Run a GEMM, bracketed by HIP events when bench.py's kernel timer is on."""
     t = kernels._timer
@@ -50,6 +104,7 @@ def _timed(kind, flops, fn, *args, **kw):
     out = fn(*args, **kw)
     e1.record()
     t.records.append((kind, flops, e0, e1))
+    t.detail.append((_label(fn, args), flops, e0, e1))
     return out
 
 
@@ -58,10 +113,7 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, slot=None):
         x2 = x.reshape(-1, x.shape[-1])
         flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
-        if bias is not None:
-            y = _timed("gemm", flops, torch.addmm, bias, x2, weight.t())
-        else:
-            y = _timed("gemm", flops, torch.mm, x2, weight.t())
+        y = _timed("gemm", flops, mm_nt, x2, weight, bias)
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         ctx.slot = slot
@@ -77,10 +129,10 @@ class LinearFn(torch.autograd.Function):
             slot = ctx.slot
             if slot is not None and slot.ds is not None and slot.rows is None:
                 # + a handed-over residual gradient, inside the GEMM (beta = 1)
-                dx = _timed("gemm", flops, slot.ds.view(-1, weight.shape[1]).addmm_, dy2, weight)
+                dx = _timed("gemm", flops, mm_nn, dy2, weight, slot.ds.view(-1, weight.shape[1]))
                 slot.ds = None
             else:
-                dx = _timed("gemm", flops, torch.mm, dy2, weight)
+                dx = _timed("gemm", flops, mm_nn, dy2, weight)
                 if slot is not None and slot.ds is not None:   # residual of gathered rows
                     dx.index_add_(0, slot.rows, slot.ds.view(-1, weight.shape[1]))
                     slot.ds = None

@@ -28,7 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from . import kernels
-from .linear import _timed, wgrad
+from .linear import _timed, mm_nn, mm_nt, wgrad
 
 __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDLRUCore",
            "bd_lru"]
@@ -91,7 +91,7 @@ class BDLRUCore(torch.autograd.Function):
             xc = x
         gflops = 2 * B * L * H * H2
         # gates GEMM without its bias: the gate kernels add gate_b on the fly
-        rg = _timed("gemm", gflops, torch.mm, xc.reshape(B * L, H), gate_w.t()).view(B, L, H2)
+        rg = _timed("gemm", gflops, mm_nt, xc.reshape(B * L, H), gate_w).view(B, L, H2)
         train = any(ctx.needs_input_grad)
         y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b)
         ctx.use_conv = use_conv
@@ -117,7 +117,7 @@ class BDLRUCore(torch.autograd.Function):
         gflops = 2 * B * L * H * H2
         dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(B * L, H))
         # + dL/dxc through the gates GEMM, accumulated in place (beta = 1)
-        _timed("gemm", gflops, dxc.view(B * L, H).addmm_, drg2, gate_w)
+        _timed("gemm", gflops, mm_nn, drg2, gate_w, dxc.view(B * L, H))
         dconv_w = dconv_b = None
         if ctx.use_conv:
             dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, None, dxz[..., :H])

@@ -282,6 +282,30 @@ int rb_item_rank(const float* seq, const float* items, const int64_t* target, in
 int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,
                    float* scores, void* stream);
 
+/* ---- projection GEMMs (RecBLR.py:162,165,167,213,214: nn.Linear, fp32) ----
+ * fp32 GEMMs on the bf16 MFMA pipe: every fp32 operand is split exactly into
+ * three bf16 parts and the six partial products of weight >= 2^-18 are
+ * accumulated in fp32 (fp32-level accuracy; csrc/gemm_split.hip).
+ *
+ * Bytes of the pre-split weight image of Bm [C, R]. */
+int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R);
+
+/* Split Bm into the fragment-ordered bf16 image Wf consumed by rb_gemm_nt:
+ * Bm = W (transpose = 0; W [C, R], row stride ldw) or Bm = W^T (transpose = 1;
+ * W [R, C]).  C % 32 == 0, R % 16 == 0; Wf 16-B aligned,
+ * rb_gemm_split_weight_bytes(C, R) bytes.  Replaces the weight operand of
+ * F.linear (forward: Bm = W) and of its input gradient (Bm = W^T). */
+int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
+                         void* Wf, void* stream);
+
+/* out[m, c] = sum_r A[m, r] Bm[c, r] (+ bias[c] if bias) (+ out[m, c] if
+ * accumulate), m < M, c < C: F.linear's forward (A = x, Bm = W) and input
+ * gradient (A = dy, Bm = W^T, accumulate adds a residual gradient in place).
+ * A row stride lda (multiple of 4, A 16-B aligned), out row stride ldo;
+ * R % 32 == 0, C % 128 == 0. */
+int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+               const float* bias, float* out, int64_t ldo, int accumulate, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
