@@ -96,6 +96,23 @@ def pmc_traffic(args, kernel_prefix):
     return None, None
 
 
+def pmc_mfma(args):
+    """MFMA busy fraction of the projection GEMMs (>= 20 GFLOP per launch) from
+    the newest committed PMC summary (profiles/*_pmc_mfma.json,
+    tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs))."""
+    if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_mfma.json")))
+    if not files:
+        return None
+    data = json.load(open(files[-1]))
+    utils = [k["mfma_util"] for k in data.get("kernels", {}).values()
+             if k.get("mfma_util") and k["mfma_flops_f32_per_dispatch"] >= 2e10]
+    if not utils:
+        return None
+    return {"min": min(utils), "max": max(utils), "source": os.path.relpath(files[-1], ROOT)}
+
+
 def scan_microbench(args, dev, reps=20):
     """BASELINE configs[1]: forward-only parallel_scan at B=2048, C=H=256,
     T=L=200 on the reference layout [B, C, T] (the reference pads T to 256;
@@ -225,6 +242,7 @@ def main():
                                 "forward/input-gradient GEMMs, " if split_gemm_enabled() else "")
                                + "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)",
                     "tuned_table": tuned_gemms_active(),
+                    "mfma_busy": pmc_mfma(args),
                     "by_shape": timer.gemm_detail(args.steps)}
         kernels_report = {}
         for name, d in summ.items():
