@@ -138,6 +138,61 @@ def scan_microbench(args, dev, reps=20):
             "sequences_per_sec": round(B / (ms * 1e-3), 1)}
 
 
+def long_seq_c5(args, env, dev, steps=3, warmup=1):
+    """BASELINE configs[4]: long-sequence stress, L = 2048, d = 256, B = 1024
+    per GPU, bf16 activations (fp32 recurrence arithmetic, bf16 MFMA GEMMs
+    with fp32 accumulation, fp32 parameters and gradients).  One step = one
+    GatedRecurrentLayer (the fused conv + gate + scan path with its in/gate/out
+    projections) forward + backward on synthetic input; sequences/s over all
+    ranks (weak scaling, max-over-ranks time).  The HBM fraction is that of
+    the bf16 conv + gate-scan kernels (algorithmic bytes 20*N*2 per step,
+    N = B*L*H)."""
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    B, L, d = args.c5_batch, 2048, 256
+    torch.manual_seed(2020)
+    layer = GatedRecurrentLayer(d_model=d).to(dev)
+    g = torch.Generator(device=dev).manual_seed(env.rank)
+    x = torch.randn(B, L, d, device=dev, generator=g).to(torch.bfloat16).requires_grad_()
+    gy = torch.randn(B, L, d, device=dev, generator=g).to(torch.bfloat16)
+
+    def one():
+        layer.zero_grad(set_to_none=True)
+        x.grad = None
+        layer(x).backward(gy)
+
+    for _ in range(warmup):
+        one()
+    torch.cuda.synchronize()
+    barrier(env)
+    with kernels.kernel_timing() as t:
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            one()
+        torch.cuda.synchronize()
+        barrier(env)
+        el = max_over_ranks(time.perf_counter() - t0, env, dev)
+    summ = t.summary()
+    path = [summ[n] for n in ("rb_conv_silu_fwd_bf16", "rb_conv_silu_bwd_bf16",
+                              "rb_gate_scan_fwd_bf16", "rb_gate_scan_bwd_bf16") if n in summ]
+    pb, pms = sum(p["bytes"] for p in path), sum(p["ms"] for p in path)
+    gbs = pb / (pms * 1e-3) / 1e9 if pms else None
+    kern = {n: {"avg_us": round(summ[n]["avg_ms"] * 1e3, 1),
+                "frac": round(summ[n]["avg_bytes"] / (summ[n]["avg_ms"] * 1e-3) / 1e9
+                              / HBM_PEAK_GBS, 4)}
+            for n in ("rb_conv_silu_fwd_bf16", "rb_conv_silu_bwd_bf16",
+                      "rb_gate_scan_fwd_bf16", "rb_gate_scan_bwd_bf16") if n in summ}
+    return {"workload": "GatedRecurrentLayer fwd+bwd (BASELINE configs[4])",
+            "batch_per_gpu": B, "seq_len": L, "hidden_size": d, "inner_H": 2 * d,
+            "dtype": "bf16 storage, fp32 recurrence math", "steps": steps,
+            "value": round(env.world_size * B * steps / el, 1), "unit": "sequences/sec",
+            "ms_per_step": round(1000.0 * el / steps, 3),
+            "scan_conv_gate_path": {"ms_per_step": round(pms / steps, 3),
+                                    "achieved_gbs": round(gbs, 1) if gbs else None,
+                                    "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
+                                    "kernels": kern}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,6 +207,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--c5-batch", type=int, default=1024,
+                    help="sequences per GPU of the long-sequence bf16 run (configs[4])")
+    ap.add_argument("--no-c5", action="store_true", help="skip the configs[4] run")
     ap.add_argument("--no-full-tail", action="store_true",
                     help="skip the comparison run that evaluates the last layer's "
                          "position-wise tail at every position")
@@ -287,6 +345,7 @@ def main():
             "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
     scan = scan_microbench(args, dev) if env.rank == 0 else None
+    c5 = None if args.no_c5 else long_seq_c5(args, env, dev)   # every rank (weak scaling)
     cpu = None
     if env.rank == 0 and env.world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, model.state_dict())
@@ -311,6 +370,7 @@ def main():
             "kernels": kernels_report,
             "all_positions_tail": full_tail,
             "scan_fwd_only": scan,
+            "long_seq_bf16": c5,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

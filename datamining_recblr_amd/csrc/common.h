@@ -78,6 +78,51 @@ __device__ __forceinline__ void stv(float* p, const float (&o)[V]) {
   }
 }
 
+// ---- bf16 storage (fp32 arithmetic): VEC bf16 per lane, RNE on store ---------
+typedef __bf16 bf16_t;
+typedef __bf16 rb_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float rb_f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void unpack2(uint32_t u, float& a, float& b) {
+  a = __uint_as_float(u << 16);
+  b = __uint_as_float(u & 0xffff0000u);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(rb_f32x2{a, b}, rb_bf16x2));
+}
+
+template <int V>
+__device__ __forceinline__ void ldv(float (&o)[V], const bf16_t* p) {
+  if constexpr (V == 8) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    unpack2(t.x, o[0], o[1]); unpack2(t.y, o[2], o[3]);
+    unpack2(t.z, o[4], o[5]); unpack2(t.w, o[6], o[7]);
+  } else if constexpr (V == 4) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    unpack2(t.x, o[0], o[1]); unpack2(t.y, o[2], o[3]);
+  } else if constexpr (V == 2) {
+    unpack2(*reinterpret_cast<const uint32_t*>(p), o[0], o[1]);
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) o[v] = (float)p[v];
+  }
+}
+
+template <int V>
+__device__ __forceinline__ void stv(bf16_t* p, const float (&o)[V]) {
+  if constexpr (V == 8) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]),
+                                              pack2(o[4], o[5]), pack2(o[6], o[7]));
+  } else if constexpr (V == 4) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+  } else if constexpr (V == 2) {
+    *reinterpret_cast<uint32_t*>(p) = pack2(o[0], o[1]);
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) p[v] = (bf16_t)o[v];
+  }
+}
+
 // ---- dropout keep-flags ------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11): counter = element index / 4, key =
 // 64-bit seed, 4 uniform u32 per call -> keep flags of 4 consecutive elements.
@@ -146,6 +191,27 @@ int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
                     int64_t B, int64_t L, int64_t H, hipStream_t st);
+int launch_scan_fwd_bf16(const bf16_t* gates, const bf16_t* tokens, bf16_t* states,
+                         int64_t rows, int64_t T, hipStream_t st);
+int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t* grad,
+                         bf16_t* d_gates, bf16_t* d_tokens, int64_t rows, int64_t T,
+                         hipStream_t st);
+int launch_conv_fwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
+                         bf16_t* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
+                         hipStream_t st);
+int launch_conv_bwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
+                         const bf16_t* g1, const bf16_t* g2, bf16_t* dx, int64_t dx_rs,
+                         float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
+                         int64_t K, hipStream_t st);
+int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
+                         const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
+                         const float* h0, int64_t h0_bs, bf16_t* y, int64_t y_rs, float* carries,
+                         int64_t B, int64_t L, int64_t H, hipStream_t st);
+int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
+                         const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
+                         const float* carries, const bf16_t* dy, bf16_t* drg, int64_t drg_rs,
+                         bf16_t* dxc, int64_t dxc_rs, bf16_t* dz, int64_t dz_rs, float* part,
+                         float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st);
 int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
                       const float* r, const float* gamma, const float* beta, float eps, float* y,
                       float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,

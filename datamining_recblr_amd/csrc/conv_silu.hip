@@ -9,10 +9,10 @@
 namespace rb {
 namespace {
 
-template <int K, int VEC, int Q, int TC>
+template <typename T, int K, int VEC, int Q, int TC>
 __global__ void __launch_bounds__(256)
-k_conv_silu_fwd(const float* __restrict__ x, int x_rs, const float* __restrict__ w,
-                const float* __restrict__ bias, float* __restrict__ xc, int xc_rs, int64_t B,
+k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
+                const float* __restrict__ bias, T* __restrict__ xc, int xc_rs, int64_t B,
                 int L, int H, int ncw, int ntile) {
   constexpr int G = kWave / Q;
   constexpr int NX = TC + K - 1;
@@ -28,8 +28,8 @@ k_conv_silu_fwd(const float* __restrict__ x, int x_rs, const float* __restrict__
   const int c0 = cw * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
-  const float* xb = x + b * L * x_rs + cc;
-  float* ob = xc + b * L * xc_rs + cc;
+  const T* xb = x + b * L * x_rs + cc;
+  T* ob = xc + b * L * xc_rs + cc;
   float wk[K][VEC], bi[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -68,11 +68,11 @@ k_conv_silu_fwd(const float* __restrict__ x, int x_rs, const float* __restrict__
 // over b by the caller: deterministic, no atomics).  Tiles are walked from the
 // end; the K-1 "look-ahead" du values a chunk needs come from the next chunk's
 // lane by shuffle, or from the previous (later) tile for the last chunk.
-template <int K, int VEC, int Q, int TC>
+template <typename T, int K, int VEC, int Q, int TC>
 __global__ void __launch_bounds__(256)
-k_conv_silu_bwd(const float* __restrict__ x, int x_rs, const float* __restrict__ w,
-                const float* __restrict__ bias, const float* __restrict__ g1,
-                const float* __restrict__ g2, float* __restrict__ dx, int dx_rs,
+k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
+                const float* __restrict__ bias, const T* __restrict__ g1,
+                const T* __restrict__ g2, T* __restrict__ dx, int dx_rs,
                 float* __restrict__ dw_part, float* __restrict__ db_part, int64_t B, int L,
                 int H, int ncw) {
   constexpr int G = kWave / Q;
@@ -88,10 +88,10 @@ k_conv_silu_bwd(const float* __restrict__ x, int x_rs, const float* __restrict__
   const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
-  const float* xb = x + b * L * x_rs + cc;
-  const float* g1b = g1 + b * L * H + cc;
-  const float* g2b = g2 ? g2 + b * L * H + cc : nullptr;
-  float* dxb = dx + b * L * dx_rs + cc;
+  const T* xb = x + b * L * x_rs + cc;
+  const T* g1b = g1 + b * L * H + cc;
+  const T* g2b = g2 ? g2 + b * L * H + cc : nullptr;
+  T* dxb = dx + b * L * dx_rs + cc;
   float wk[K][VEC], bi[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -196,8 +196,8 @@ k_conv_silu_bwd(const float* __restrict__ x, int x_rs, const float* __restrict__
 
 constexpr int kConvQ = 4;
 
-template <int K, int TC>
-int conv_fwd_t(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
+template <typename T, int K, int TC>
+int conv_fwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, T* xc,
                int64_t xc_rs, int64_t B, int64_t L, int64_t H, bool vec, hipStream_t st) {
   const int V = vec ? 4 : 1;
   const int span = (kWave / kConvQ) * V;
@@ -207,69 +207,102 @@ int conv_fwd_t(const float* x, int64_t x_rs, const float* w, const float* bias, 
   const int64_t blocks = (waves + 3) / 4;
   if (blocks > 0x7fffffffLL) return fail("rb_conv_silu_fwd: grid too large");
   if (vec)
-    hipLaunchKernelGGL((k_conv_silu_fwd<K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
+    hipLaunchKernelGGL((k_conv_silu_fwd<T, K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
+                       0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
   else
-    hipLaunchKernelGGL((k_conv_silu_fwd<K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
+    hipLaunchKernelGGL((k_conv_silu_fwd<T, K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
+                       0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
   return launch_status("rb_conv_silu_fwd");
 }
 
-template <int K, int TC>
-int conv_bwd_t(const float* x, int64_t x_rs, const float* w, const float* bias, const float* g1,
-               const float* g2, float* dx, int64_t dx_rs, float* dw_part, float* db_part,
+template <typename T, int K, int TC>
+int conv_bwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, const T* g1,
+               const T* g2, T* dx, int64_t dx_rs, float* dw_part, float* db_part,
                int64_t B, int64_t L, int64_t H, bool vec, hipStream_t st) {
   const int V = vec ? 4 : 1;
   const int span = (kWave / kConvQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   if (vec)
-    hipLaunchKernelGGL((k_conv_silu_bwd<K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
+    hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
+                       0, st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
                        (int)L, (int)H, ncw);
   else
-    hipLaunchKernelGGL((k_conv_silu_bwd<K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256), 0,
-                       st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
+    hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
+                       0, st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
                        (int)L, (int)H, ncw);
   return launch_status("rb_conv_silu_bwd");
+}
+
+// 4 channels per lane: 16-B (fp32) or 8-B (bf16) accesses
+template <typename T>
+bool al4(const void* p) {
+  return p == nullptr || reinterpret_cast<uintptr_t>(p) % (4 * sizeof(T)) == 0;
+}
+
+template <typename T>
+int conv_fwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, T* xc, int64_t xc_rs,
+               int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
+  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && xc_rs % 4 == 0 && al4<T>(x) && al4<T>(xc) &&
+                   aligned16(bias);
+  switch (K) {
+    case 1: return conv_fwd_t<T, 1, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 2: return conv_fwd_t<T, 2, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 3: return conv_fwd_t<T, 3, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 4: return conv_fwd_t<T, 4, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 5: return conv_fwd_t<T, 5, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 6: return conv_fwd_t<T, 6, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 7: return conv_fwd_t<T, 7, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 8: return conv_fwd_t<T, 8, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    default: return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
+  }
+}
+
+template <typename T>
+int conv_bwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, const T* g1,
+               const T* g2, T* dx, int64_t dx_rs, float* dw_part, float* db_part, int64_t B,
+               int64_t L, int64_t H, int64_t K, hipStream_t st) {
+  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && dx_rs % 4 == 0 && al4<T>(x) && al4<T>(g1) &&
+                   al4<T>(g2) && al4<T>(dx) && aligned16(dw_part) && aligned16(db_part) &&
+                   aligned16(bias);
+  switch (K) {
+    case 1: return conv_bwd_t<T, 1, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 2: return conv_bwd_t<T, 2, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 3: return conv_bwd_t<T, 3, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 4: return conv_bwd_t<T, 4, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 5: return conv_bwd_t<T, 5, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 6: return conv_bwd_t<T, 6, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 7: return conv_bwd_t<T, 7, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 8: return conv_bwd_t<T, 8, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    default: return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
+  }
 }
 
 }  // namespace
 
 int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
-  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && xc_rs % 4 == 0 && aligned16(x) &&
-                   aligned16(xc) && aligned16(bias);
-  switch (K) {
-    case 1: return conv_fwd_t<1, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 2: return conv_fwd_t<2, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 3: return conv_fwd_t<3, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 4: return conv_fwd_t<4, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 5: return conv_fwd_t<5, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 6: return conv_fwd_t<6, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 7: return conv_fwd_t<7, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 8: return conv_fwd_t<8, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    default: return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
-  }
+  return conv_fwd_k<float>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, st);
+}
+
+int launch_conv_fwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
+                         bf16_t* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
+                         hipStream_t st) {
+  return conv_fwd_k<bf16_t>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, st);
 }
 
 int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
                     const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
                     float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
-  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && dx_rs % 4 == 0 && aligned16(x) &&
-                   aligned16(g1) && (g2 == nullptr || aligned16(g2)) && aligned16(dx) &&
-                   aligned16(dw_part) && aligned16(db_part) && aligned16(bias);
-  switch (K) {
-    case 1: return conv_bwd_t<1, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 2: return conv_bwd_t<2, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 3: return conv_bwd_t<3, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 4: return conv_bwd_t<4, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 5: return conv_bwd_t<5, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 6: return conv_bwd_t<6, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 7: return conv_bwd_t<7, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 8: return conv_bwd_t<8, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    default: return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
-  }
+  return conv_bwd_k<float>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K, st);
+}
+
+int launch_conv_bwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
+                         const bf16_t* g1, const bf16_t* g2, bf16_t* dx, int64_t dx_rs,
+                         float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
+                         int64_t K, hipStream_t st) {
+  return conv_bwd_k<bf16_t>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K,
+                            st);
 }
 
 }  // namespace rb

@@ -33,12 +33,12 @@ struct BwdIn {
 // PF: software-prefetch the next tile's operands before computing this one
 // (two register buffers), so a wave keeps its loads in flight across the
 // shuffle/compute/store phase of the previous tile.
-template <int VEC, int Q, int TC, bool PF>
+template <typename T, int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
-k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
-                const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
+k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, int xc_rs,
+                const T* __restrict__ z, int z_rs, const float* __restrict__ lam,
                 const float* __restrict__ gbias, const float* __restrict__ h0, int h0_bs,
-                float* __restrict__ y, int y_rs,
+                T* __restrict__ y, int y_rs,
                 float* __restrict__ carries, int64_t B, int L, int H, int ncw) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
@@ -53,10 +53,10 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
   const int64_t row0 = b * L;
-  const float* rgb = rg + row0 * rg_rs + cc;
-  const float* xcb = xc + row0 * xc_rs + cc;
-  const float* zb = z + row0 * z_rs + cc;
-  float* yb = y + row0 * y_rs + cc;
+  const T* rgb = rg + row0 * rg_rs + cc;
+  const T* xcb = xc + row0 * xc_rs + cc;
+  const T* zb = z + row0 * z_rs + cc;
+  T* yb = y + row0 * y_rs + cc;
 
   float nsp[VEC], carry[VEC], br[VEC], bi[VEC];
   ldv(nsp, lam + cc);
@@ -163,14 +163,14 @@ k_gate_scan_fwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   }
 }
 
-template <int VEC, int Q, int TC, bool PF>
+template <typename T, int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
-k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict__ xc, int xc_rs,
-                const float* __restrict__ z, int z_rs, const float* __restrict__ lam,
+k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, int xc_rs,
+                const T* __restrict__ z, int z_rs, const float* __restrict__ lam,
                 const float* __restrict__ gbias, const float* __restrict__ carries,
-                const float* __restrict__ dy,
-                float* __restrict__ drg, int drg_rs, float* __restrict__ dxc, int dxc_rs,
-                float* __restrict__ dz, int dz_rs, float* __restrict__ part,
+                const T* __restrict__ dy,
+                T* __restrict__ drg, int drg_rs, T* __restrict__ dxc, int dxc_rs,
+                T* __restrict__ dz, int dz_rs, float* __restrict__ part,
                 float* __restrict__ dh0_part, int64_t B, int L, int H, int ncw) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
@@ -185,13 +185,13 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
   const int64_t row0 = b * L;
-  const float* rgb = rg + row0 * rg_rs + cc;
-  const float* xcb = xc + row0 * xc_rs + cc;
-  const float* zb = z + row0 * z_rs + cc;
-  const float* dyb = dy + row0 * H + cc;
-  float* drgb = drg + row0 * drg_rs + cc;
-  float* dxcb = dxc + row0 * dxc_rs + cc;
-  float* dzb = dz + row0 * dz_rs + cc;
+  const T* rgb = rg + row0 * rg_rs + cc;
+  const T* xcb = xc + row0 * xc_rs + cc;
+  const T* zb = z + row0 * z_rs + cc;
+  const T* dyb = dy + row0 * H + cc;
+  T* drgb = drg + row0 * drg_rs + cc;
+  T* dxcb = dxc + row0 * dxc_rs + cc;
+  T* dzb = dz + row0 * dz_rs + cc;
 
   float lamv[VEC], nsp[VEC], br[VEC], bi[VEC];
   ldv(lamv, lam + cc);
@@ -398,45 +398,90 @@ k_gate_scan_bwd(const float* __restrict__ rg, int rg_rs, const float* __restrict
 constexpr int kFwdQ = 4, kFwdTC = RB_TILE / kFwdQ;
 constexpr int kBwdQ = 8, kBwdTC = RB_TILE / kBwdQ;
 
-template <int V>
+// alignment/stride check for VEC-wide access: activation pointers (T) need
+// sizeof(T)*V-byte alignment, the fp32 per-channel vectors 4*V
+template <typename T, int V>
 bool vec_ok(int64_t H, std::initializer_list<int64_t> strides,
-            std::initializer_list<const void*> ptrs) {
+            std::initializer_list<const void*> act, std::initializer_list<const void*> f32) {
   if (H % V) return false;
   for (int64_t s : strides)
     if (s % V) return false;
-  for (const void* p : ptrs)
+  for (const void* p : act)
+    if (p != nullptr && (reinterpret_cast<uintptr_t>(p) % (sizeof(T) * V))) return false;
+  for (const void* p : f32)
     if (p != nullptr && (reinterpret_cast<uintptr_t>(p) % (4 * V))) return false;
   return true;
 }
 
-template <int V>
-int gate_fwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
+template <typename T, int V>
+int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
-               float* y,
-               int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+               T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
+               hipStream_t st) {
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
-  hipLaunchKernelGGL((k_gate_scan_fwd<V, kFwdQ, kFwdTC, true>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_gate_scan_fwd<T, V, kFwdQ, kFwdTC, true>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_fwd");
 }
 
-template <int V>
-int gate_bwd_v(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs, const float* z,
+template <typename T, int V>
+int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
-               const float* dy, float* drg,
-               int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz, int64_t dz_rs, float* part,
-               float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+               const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
+               float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
   const int span = (kWave / kBwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
-  hipLaunchKernelGGL((k_gate_scan_bwd<V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
-                     carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part, dh0_part, B,
-                     (int)L, (int)H, ncw);
+                     carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
+                     dh0_part, B, (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_bwd");
+}
+
+// widest vector the layout allows: fp32 fwd 2 / bwd 4 channels per lane
+// (8 / 16 B); bf16 4 / 4 channels (8 / 8 B)
+template <typename T>
+int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
+               int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
+               T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
+               hipStream_t st) {
+  constexpr int VW = sizeof(T) == 2 ? 4 : 2;
+  const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
+  const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y};
+  const auto f32 = {(const void*)lam, (const void*)gb, (const void*)h0, (const void*)carries};
+  if (vec_ok<T, VW>(H, strides, act, f32))
+    return gate_fwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs,
+                             carries, B, L, H, st);
+  if (vec_ok<T, 2>(H, strides, act, f32))
+    return gate_fwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
+                            B, L, H, st);
+  return gate_fwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B,
+                          L, H, st);
+}
+
+template <typename T>
+int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
+               int64_t z_rs, const float* lam, const float* gb, const float* carries,
+               const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
+               float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+  constexpr int VW = 4;  // bf16 at 8 channels per lane spills (256 VGPRs)
+  const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
+  const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)dy,
+                    (const void*)drg, (const void*)dxc, (const void*)dz};
+  const auto f32 = {(const void*)lam, (const void*)gb, (const void*)carries, (const void*)part,
+                    (const void*)dh0_part};
+  if (vec_ok<T, VW>(H, strides, act, f32))
+    return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
+                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+  if (vec_ok<T, 2>(H, strides, act, f32))
+    return gate_bwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+  return gate_bwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
+                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
 }
 
 }  // namespace
@@ -445,14 +490,16 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
                     int64_t B, int64_t L, int64_t H, hipStream_t st) {
-  const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
-  const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y,
-                     (const void*)lam, (const void*)gb, (const void*)h0, (const void*)carries};
-  if (vec_ok<2>(H, strides, ptrs))
-    return gate_fwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B,
-                         L, H, st);
-  return gate_fwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B, L,
-                       H, st);
+  return gate_fwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
+                           B, L, H, st);
+}
+
+int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
+                         const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
+                         const float* h0, int64_t h0_bs, bf16_t* y, int64_t y_rs, float* carries,
+                         int64_t B, int64_t L, int64_t H, hipStream_t st) {
+  return gate_fwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
+                            B, L, H, st);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
@@ -460,19 +507,17 @@ int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
                     int64_t B, int64_t L, int64_t H, hipStream_t st) {
-  const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
-  const auto ptrs = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)lam,
-                     (const void*)gb, (const void*)carries, (const void*)dy, (const void*)drg,
-                     (const void*)dxc, (const void*)dz, (const void*)part,
-                     (const void*)dh0_part};
-  if (vec_ok<4>(H, strides, ptrs))
-    return gate_bwd_v<4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                         dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
-  if (vec_ok<2>(H, strides, ptrs))
-    return gate_bwd_v<2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                         dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
-  return gate_bwd_v<1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                       dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+  return gate_bwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
+                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+}
+
+int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
+                         const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
+                         const float* carries, const bf16_t* dy, bf16_t* drg, int64_t drg_rs,
+                         bf16_t* dxc, int64_t dxc_rs, bf16_t* dz, int64_t dz_rs, float* part,
+                         float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+  return gate_bwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
 }
 
 }  // namespace rb

@@ -12,31 +12,29 @@
 namespace rb {
 namespace {
 
-template <bool VEC4>
+template <typename TS, bool VEC4>
 __global__ void __launch_bounds__(256)
-k_scan_rows_fwd(const float* __restrict__ gates, const float* __restrict__ tokens,
-                float* __restrict__ out, int64_t rows, int64_t T) {
+k_scan_rows_fwd(const TS* __restrict__ gates, const TS* __restrict__ tokens,
+                TS* __restrict__ out, int64_t rows, int64_t T) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;  // wave-uniform
-  const float* g = gates + row * T;
-  const float* x = tokens + row * T;
-  float* o = out + row * T;
+  const TS* g = gates + row * T;
+  const TS* x = tokens + row * T;
+  TS* o = out + row * T;
   float carry = 0.0f;
   for (int64_t t0 = 0; t0 < T; t0 += 4 * kWave) {
     const int64_t t = t0 + 4 * lane;
     float a[4], v[4];
     if (VEC4 && t + 3 < T) {
-      const float4 ga = *reinterpret_cast<const float4*>(g + t);
-      const float4 xa = *reinterpret_cast<const float4*>(x + t);
-      a[0] = ga.x; a[1] = ga.y; a[2] = ga.z; a[3] = ga.w;
-      v[0] = xa.x; v[1] = xa.y; v[2] = xa.z; v[3] = xa.w;
+      ldv(a, g + t);
+      ldv(v, x + t);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool ok = t + j < T;
-        a[j] = ok ? g[t + j] : 1.0f;  // identity element (x=0, f=1)
-        v[j] = ok ? x[t + j] : 0.0f;
+        a[j] = ok ? (float)g[t + j] : 1.0f;  // identity element (x=0, f=1)
+        v[j] = ok ? (float)x[t + j] : 0.0f;
       }
     }
     // upsweep inside the lane
@@ -71,11 +69,11 @@ k_scan_rows_fwd(const float* __restrict__ gates, const float* __restrict__ token
       res[j] = h;
     }
     if (VEC4 && t + 3 < T) {
-      *reinterpret_cast<float4*>(o + t) = make_float4(res[0], res[1], res[2], res[3]);
+      stv(o + t, res);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (t + j < T) o[t + j] = res[j];
+        if (t + j < T) o[t + j] = (TS)res[j];
     }
     const float A63 = __shfl(A, kWave - 1, kWave);
     const float X63 = __shfl(X, kWave - 1, kWave);
@@ -85,19 +83,19 @@ k_scan_rows_fwd(const float* __restrict__ gates, const float* __restrict__ token
 
 // Reverse scan with shifted gates (parallel_scan.py:106-113):
 //   d_t = d_{t+1} * a_{t+1} + grad_t, d_gates_t = h_{t-1} d_t, d_tokens = d.
-template <bool VEC4>
+template <typename TS, bool VEC4>
 __global__ void __launch_bounds__(256)
-k_scan_rows_bwd(const float* __restrict__ gates, const float* __restrict__ states,
-                const float* __restrict__ grad, float* __restrict__ d_gates,
-                float* __restrict__ d_tokens, int64_t rows, int64_t T) {
+k_scan_rows_bwd(const TS* __restrict__ gates, const TS* __restrict__ states,
+                const TS* __restrict__ grad, TS* __restrict__ d_gates,
+                TS* __restrict__ d_tokens, int64_t rows, int64_t T) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* g = gates + row * T;
-  const float* s = states + row * T;
-  const float* gr = grad + row * T;
-  float* dg = d_gates + row * T;
-  float* dt = d_tokens + row * T;
+  const TS* g = gates + row * T;
+  const TS* s = states + row * T;
+  const TS* gr = grad + row * T;
+  TS* dg = d_gates + row * T;
+  TS* dt = d_tokens + row * T;
   const int64_t nblk = (T + 4 * kWave - 1) / (4 * kWave);
   float carry = 0.0f;     // d at the first step after the block
   float a_next = 1.0f;    // gates at the first step after the block
@@ -106,19 +104,16 @@ k_scan_rows_bwd(const float* __restrict__ gates, const float* __restrict__ state
     const int64_t t = t0 + 4 * lane;
     float a[4], y[4], hs[4];
     if (VEC4 && t + 3 < T) {
-      const float4 ga = *reinterpret_cast<const float4*>(g + t);
-      const float4 ya = *reinterpret_cast<const float4*>(gr + t);
-      const float4 sa = *reinterpret_cast<const float4*>(s + t);
-      a[0] = ga.x; a[1] = ga.y; a[2] = ga.z; a[3] = ga.w;
-      y[0] = ya.x; y[1] = ya.y; y[2] = ya.z; y[3] = ya.w;
-      hs[0] = sa.x; hs[1] = sa.y; hs[2] = sa.z; hs[3] = sa.w;
+      ldv(a, g + t);
+      ldv(y, gr + t);
+      ldv(hs, s + t);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const bool ok = t + j < T;
-        a[j] = ok ? g[t + j] : 1.0f;
-        y[j] = ok ? gr[t + j] : 0.0f;
-        hs[j] = ok ? s[t + j] : 0.0f;
+        a[j] = ok ? (float)g[t + j] : 1.0f;
+        y[j] = ok ? (float)gr[t + j] : 0.0f;
+        hs[j] = ok ? (float)s[t + j] : 0.0f;
       }
     }
     // shifted gates: as[j] = a_{t+j+1}
@@ -158,7 +153,7 @@ k_scan_rows_bwd(const float* __restrict__ gates, const float* __restrict__ state
     float d = carry * Ae + De;
     // h_{t-1} for the lane's first element
     float hprev0 = __shfl_up(hs[3], 1, kWave);
-    if (lane == 0) hprev0 = (t0 > 0) ? s[t0 - 1] : 0.0f;
+    if (lane == 0) hprev0 = (t0 > 0) ? (float)s[t0 - 1] : 0.0f;
     float dres[4], gres[4];
 #pragma unroll
     for (int j = 3; j >= 0; --j) {
@@ -168,14 +163,14 @@ k_scan_rows_bwd(const float* __restrict__ gates, const float* __restrict__ state
       gres[j] = hp * d;
     }
     if (VEC4 && t + 3 < T) {
-      *reinterpret_cast<float4*>(dt + t) = make_float4(dres[0], dres[1], dres[2], dres[3]);
-      *reinterpret_cast<float4*>(dg + t) = make_float4(gres[0], gres[1], gres[2], gres[3]);
+      stv(dt + t, dres);
+      stv(dg + t, gres);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (t + j < T) {
-          dt[t + j] = dres[j];
-          dg[t + j] = gres[j];
+          dt[t + j] = (TS)dres[j];
+          dg[t + j] = (TS)gres[j];
         }
     }
     const float A0 = __shfl(A, 0, kWave);
@@ -185,33 +180,59 @@ k_scan_rows_bwd(const float* __restrict__ gates, const float* __restrict__ state
   }
 }
 
+template <typename TS>
+bool al4s(const void* p) { return reinterpret_cast<uintptr_t>(p) % (4 * sizeof(TS)) == 0; }
+
+template <typename TS>
+int scan_fwd_t(const TS* gates, const TS* tokens, TS* states, int64_t rows, int64_t T,
+               hipStream_t st) {
+  const int64_t blocks = (rows + 3) / 4;
+  const bool vec = (T % 4 == 0) && al4s<TS>(gates) && al4s<TS>(tokens) && al4s<TS>(states);
+  if (vec)
+    hipLaunchKernelGGL((k_scan_rows_fwd<TS, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       gates, tokens, states, rows, T);
+  else
+    hipLaunchKernelGGL((k_scan_rows_fwd<TS, false>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       gates, tokens, states, rows, T);
+  return launch_status("rb_scan_fwd");
+}
+
+template <typename TS>
+int scan_bwd_t(const TS* gates, const TS* states, const TS* grad, TS* d_gates, TS* d_tokens,
+               int64_t rows, int64_t T, hipStream_t st) {
+  const int64_t blocks = (rows + 3) / 4;
+  const bool vec = (T % 4 == 0) && al4s<TS>(gates) && al4s<TS>(states) && al4s<TS>(grad) &&
+                   al4s<TS>(d_gates) && al4s<TS>(d_tokens);
+  if (vec)
+    hipLaunchKernelGGL((k_scan_rows_bwd<TS, true>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       gates, states, grad, d_gates, d_tokens, rows, T);
+  else
+    hipLaunchKernelGGL((k_scan_rows_bwd<TS, false>), dim3((unsigned)blocks), dim3(256), 0, st,
+                       gates, states, grad, d_gates, d_tokens, rows, T);
+  return launch_status("rb_scan_bwd");
+}
+
 }  // namespace
 
 int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,
                     int64_t T, hipStream_t st) {
-  const int64_t blocks = (rows + 3) / 4;
-  const bool vec = (T % 4 == 0) && aligned16(gates) && aligned16(tokens) && aligned16(states);
-  if (vec)
-    hipLaunchKernelGGL(k_scan_rows_fwd<true>, dim3((unsigned)blocks), dim3(256), 0, st, gates,
-                       tokens, states, rows, T);
-  else
-    hipLaunchKernelGGL(k_scan_rows_fwd<false>, dim3((unsigned)blocks), dim3(256), 0, st, gates,
-                       tokens, states, rows, T);
-  return launch_status("rb_scan_fwd");
+  return scan_fwd_t<float>(gates, tokens, states, rows, T, st);
+}
+
+int launch_scan_fwd_bf16(const bf16_t* gates, const bf16_t* tokens, bf16_t* states,
+                         int64_t rows, int64_t T, hipStream_t st) {
+  return scan_fwd_t<bf16_t>(gates, tokens, states, rows, T, st);
 }
 
 int launch_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,
                     float* d_tokens, int64_t rows, int64_t T, hipStream_t st) {
-  const int64_t blocks = (rows + 3) / 4;
-  const bool vec = (T % 4 == 0) && aligned16(gates) && aligned16(states) && aligned16(grad) &&
-                   aligned16(d_gates) && aligned16(d_tokens);
-  if (vec)
-    hipLaunchKernelGGL(k_scan_rows_bwd<true>, dim3((unsigned)blocks), dim3(256), 0, st, gates,
-                       states, grad, d_gates, d_tokens, rows, T);
-  else
-    hipLaunchKernelGGL(k_scan_rows_bwd<false>, dim3((unsigned)blocks), dim3(256), 0, st, gates,
-                       states, grad, d_gates, d_tokens, rows, T);
-  return launch_status("rb_scan_bwd");
+  return scan_bwd_t<float>(gates, states, grad, d_gates, d_tokens, rows, T, st);
+}
+
+int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t* grad,
+                         bf16_t* d_gates, bf16_t* d_tokens, int64_t rows, int64_t T,
+                         hipStream_t st) {
+  return scan_bwd_t<bf16_t>(gates, states, grad, d_gates, d_tokens, rows, T, st);
 }
 
 }  // namespace rb

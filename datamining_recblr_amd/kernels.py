@@ -112,15 +112,31 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def _check(t: torch.Tensor, name: str) -> None:
+def _check(t: torch.Tensor, name: str, dtype: torch.dtype = torch.float32) -> None:
     if not isinstance(t, torch.Tensor):
         raise TypeError(f"{name} must be a torch.Tensor")
     if t.device.type != "cuda":
         raise RecBLRNativeError(
             f"{name} is on {t.device}; the RecBLR HIP path needs a ROCm GPU tensor "
             "(there is no CPU fallback)")
-    if t.dtype != torch.float32:
-        raise TypeError(f"{name} must be float32, got {t.dtype}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+
+
+ACT_DTYPES = (torch.float32, torch.bfloat16)
+
+
+def _act_dtype(t: torch.Tensor, name: str) -> torch.dtype:
+    """Storage dtype of the [B, L, *] activations of a recurrence kernel:
+    fp32 (the reference's) or bf16 (BASELINE config 5; fp32 arithmetic)."""
+    if isinstance(t, torch.Tensor) and t.dtype in ACT_DTYPES:
+        return t.dtype
+    _check(t, name)
+    return torch.float32
+
+
+def _sfx(dt: torch.dtype) -> str:
+    return "_bf16" if dt == torch.bfloat16 else ""
 
 
 def _row_stride(t: torch.Tensor, name: str, H: int) -> int:
@@ -139,8 +155,9 @@ def _row_stride(t: torch.Tensor, name: str, H: int) -> int:
 
 
 def scan_fwd(gates: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
-    _check(gates, "gates")
-    _check(tokens, "tokens")
+    dt = _act_dtype(gates, "gates")
+    _check(gates, "gates", dt)
+    _check(tokens, "tokens", dt)
     if gates.dim() != 3 or tokens.shape != gates.shape:
         raise ValueError("gates and tokens must both be [B, C, T] of equal shape")
     if not (gates.is_contiguous() and tokens.is_contiguous()):
@@ -148,14 +165,15 @@ def scan_fwd(gates: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
     B, C, T = gates.shape
     states = torch.empty_like(tokens)
     if states.numel():
-        _launch("rb_scan_fwd", 3 * gates.numel() * 4, gates.data_ptr(), tokens.data_ptr(), states.data_ptr(),
-                  B, C, T, _stream(gates))
+        _launch("rb_scan_fwd" + _sfx(dt), 3 * gates.numel() * gates.element_size(),
+                gates.data_ptr(), tokens.data_ptr(), states.data_ptr(), B, C, T, _stream(gates))
     return states
 
 
 def scan_bwd(gates: torch.Tensor, states: torch.Tensor, grad: torch.Tensor):
+    dt = _act_dtype(gates, "gates")
     for t, n in ((gates, "gates"), (states, "states"), (grad, "grad")):
-        _check(t, n)
+        _check(t, n, dt)
         if not t.is_contiguous():
             raise ValueError(f"{n} must be contiguous")
     if states.shape != gates.shape or grad.shape != gates.shape:
@@ -164,45 +182,50 @@ def scan_bwd(gates: torch.Tensor, states: torch.Tensor, grad: torch.Tensor):
     d_gates = torch.empty_like(gates)
     d_tokens = torch.empty_like(gates)
     if gates.numel():
-        _launch("rb_scan_bwd", 5 * gates.numel() * 4, gates.data_ptr(), states.data_ptr(), grad.data_ptr(),
-                  d_gates.data_ptr(), d_tokens.data_ptr(), B, C, T, _stream(gates))
+        _launch("rb_scan_bwd" + _sfx(dt), 5 * gates.numel() * gates.element_size(),
+                gates.data_ptr(), states.data_ptr(), grad.data_ptr(), d_gates.data_ptr(),
+                d_tokens.data_ptr(), B, C, T, _stream(gates))
     return d_gates, d_tokens
 
 
 def conv_silu_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-    """x: [B, L, H] (row-strided view ok); weight: [H, K]; bias: [H] -> xc [B, L, H]."""
-    _check(x, "x")
+    """x: [B, L, H] (row-strided view ok, fp32 or bf16); weight: [H, K]; bias:
+    [H] (fp32) -> xc [B, L, H] in x's dtype."""
+    dt = _act_dtype(x, "x")
+    _check(x, "x", dt)
     _check(weight, "conv weight")
     _check(bias, "conv bias")
     B, L, H = x.shape
     x_rs = _row_stride(x, "x", H)
     w = weight.reshape(H, -1).contiguous()
     K = w.shape[1]
-    xc = torch.empty((B, L, H), device=x.device, dtype=torch.float32)
-    _launch("rb_conv_silu_fwd", 2 * B * L * H * 4, x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
-              xc.data_ptr(), H, B, L, H, K, _stream(x))
+    xc = torch.empty((B, L, H), device=x.device, dtype=dt)
+    _launch("rb_conv_silu_fwd" + _sfx(dt), 2 * B * L * H * x.element_size(), x.data_ptr(), x_rs,
+            w.data_ptr(), bias.contiguous().data_ptr(), xc.data_ptr(), H, B, L, H, K, _stream(x))
     return xc
 
 
 def conv_silu_bwd(x, weight, bias, g1, g2, dx):
     """Writes dx (a [B, L, H] row-strided view) and returns (dweight [H, K], dbias [H])."""
-    _check(x, "x")
-    _check(g1, "g1")
-    _check(dx, "dx")
+    dt = _act_dtype(x, "x")
+    _check(x, "x", dt)
+    _check(g1, "g1", dt)
+    _check(dx, "dx", dt)
     B, L, H = x.shape
     x_rs = _row_stride(x, "x", H)
     dx_rs = _row_stride(dx, "dx", H)
     if not g1.is_contiguous() or g1.shape != (B, L, H):
         raise ValueError("g1 must be contiguous [B, L, H]")
     if g2 is not None:
-        _check(g2, "g2")
+        _check(g2, "g2", dt)
         if not g2.is_contiguous() or g2.shape != (B, L, H):
             raise ValueError("g2 must be contiguous [B, L, H]")
     w = weight.reshape(H, -1).contiguous()
     K = w.shape[1]
     dw_part = torch.empty((B, K, H), device=x.device, dtype=torch.float32)
     db_part = torch.empty((B, H), device=x.device, dtype=torch.float32)
-    _launch("rb_conv_silu_bwd", (3 if g2 is None else 4) * B * L * H * 4, x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
+    _launch("rb_conv_silu_bwd" + _sfx(dt), (3 if g2 is None else 4) * B * L * H * x.element_size(),
+            x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
               g1.data_ptr(), 0 if g2 is None else g2.data_ptr(), dx.data_ptr(), dx_rs,
               dw_part.data_ptr(), db_part.data_ptr(), B, L, H, K, _stream(x))
     return colsum(dw_part.view(B, -1)).view(-1, H).t().contiguous(), colsum(db_part)
@@ -215,8 +238,10 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
     row), [B, H] (one initial state per row) or None; gate_b: [2H] bias added
     to rg inside the kernel (or None).
     Returns (y [B, L, H], carries [B, nT, H] or None when not wanted)."""
-    for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (lam, "Lambda")):
-        _check(t, n)
+    dt = _act_dtype(xc, "xc")
+    for t, n in ((rg, "rg"), (xc, "xc"), (z, "z")):
+        _check(t, n, dt)
+    _check(lam, "Lambda")
     B, L, H = xc.shape
     rg_rs = _row_stride(rg, "rg", 2 * H)
     xc_rs = _row_stride(xc, "xc", H)
@@ -233,11 +258,13 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
         h0 = h0.contiguous()
         h0_bs = H if h0.dim() == 2 else 0
     if y is None:
-        y = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
+        y = torch.empty((B, L, H), device=xc.device, dtype=dt)
+    _check(y, "y", dt)
     y_rs = _row_stride(y, "y", H)
     carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
                if want_carries else None)
-    _launch("rb_gate_scan_fwd", 5 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
+    _launch("rb_gate_scan_fwd" + _sfx(dt), 5 * B * L * H * xc.element_size(), rg.data_ptr(), rg_rs,
+            xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
               lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), 0 if h0 is None else h0.data_ptr(),
               h0_bs, y.data_ptr(),
               y_rs, 0 if carries is None else carries.data_ptr(), B, L, H, _stream(xc))
@@ -259,8 +286,9 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
     (drg [B, L, 2H], dxc [B, L, H], dlam [H], dgate_bias [2H], dh0), dh0 [H]
     (summed over rows) or [B, H] when dh0_rows (a per-row h0)."""
     B, L, H = xc.shape
-    _check(dy, "dy")
-    _check(dz, "dz")
+    dt = _act_dtype(xc, "xc")
+    for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (dy, "dy"), (dz, "dz")):
+        _check(t, n, dt)
     _check(carries, "carries")
     if not dy.is_contiguous() or dy.shape != (B, L, H):
         raise ValueError("dy must be contiguous [B, L, H]")
@@ -271,14 +299,17 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
     z_rs = _row_stride(z, "z", H)
     dz_rs = _row_stride(dz, "dz", H)
     if drg is None:
-        drg = torch.empty((B, L, 2 * H), device=xc.device, dtype=torch.float32)
+        drg = torch.empty((B, L, 2 * H), device=xc.device, dtype=dt)
     drg_rs = _row_stride(drg, "drg", 2 * H)
     if dxc is None:
-        dxc = torch.empty((B, L, H), device=xc.device, dtype=torch.float32)
+        dxc = torch.empty((B, L, H), device=xc.device, dtype=dt)
+    _check(drg, "drg", dt)
+    _check(dxc, "dxc", dt)
     dxc_rs = _row_stride(dxc, "dxc", H)
     part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
     dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
-    _launch("rb_gate_scan_bwd", 9 * B * L * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(), xc_rs,
+    _launch("rb_gate_scan_bwd" + _sfx(dt), 9 * B * L * H * xc.element_size(), rg.data_ptr(), rg_rs,
+            xc.data_ptr(), xc_rs,
             z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), carries.data_ptr(),
             dy.data_ptr(),
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,

@@ -44,7 +44,12 @@ def _split_ok(a: torch.Tensor, C: int, R: int) -> bool:
 
 
 def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
-    """a [M, K] @ w[N, K]^T (+ bias): F.linear's forward GEMM."""
+    """a [M, K] @ w[N, K]^T (+ bias): F.linear's forward GEMM.  bf16
+    activations (config 5) use the weight rounded to bf16 (bf16 MFMA, fp32
+    accumulation, bf16 output)."""
+    if a.dtype != w.dtype:
+        wb = w.to(a.dtype)
+        return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
     N, K = w.shape
     if _split_ok(a, N, K):
         return kernels.gemm_nt(a, kernels.gemm_split_weight(w), N, bias=bias)
@@ -54,6 +59,9 @@ def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) ->
 def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
     """dy [M, N] @ w [N, K] (the input gradient of F.linear); with `out`,
     accumulated into it in place (out += dy @ w)."""
+    if dy.dtype != w.dtype:
+        wb = w.to(dy.dtype)
+        return out.addmm_(dy, wb) if out is not None else dy @ wb
     N, K = w.shape
     if _split_ok(dy, K, N) and (out is None or (out.stride(1) == 1 and out.shape == (dy.shape[0], K))):
         return kernels.gemm_nt(dy, kernels.gemm_split_weight(w, transpose=True), K, out=out,
@@ -67,17 +75,19 @@ MIN_ROWS_FOR_SPLIT = 16384
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.Tensor:
-    """dW = dy2^T @ x2 for dy2 [M, N], x2 [M, K] (row-strided views allowed)."""
+    """dW = dy2^T @ x2 for dy2 [M, N], x2 [M, K] (row-strided views allowed).
+    bf16 activations (config 5): bf16 MFMA partials, summed in fp32; the
+    result is fp32 like the parameter."""
     M = dy2.shape[0]
     if M < MIN_ROWS_FOR_SPLIT or splits <= 1:
-        return dy2.t() @ x2
+        return (dy2.t() @ x2).float()
     mk = M // splits
     main = mk * splits
     a = dy2[:main].unflatten(0, (splits, mk)).transpose(1, 2)
     b = x2[:main].unflatten(0, (splits, mk))
-    out = kernels.colsum(torch.bmm(a, b).view(splits, -1)).view(a.shape[1], b.shape[2])
+    out = kernels.colsum(torch.bmm(a, b).float().view(splits, -1)).view(a.shape[1], b.shape[2])
     if main < M:
-        out += dy2[main:].t() @ x2[main:]
+        out += (dy2[main:].t() @ x2[main:]).float()
     return out
 
 
@@ -140,7 +150,8 @@ class LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = _timed("gemm", flops, wgrad, dy2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = kernels.colsum(dy2.contiguous())
+            db = (kernels.colsum(dy2.contiguous()) if dy2.dtype == torch.float32
+                  else dy2.sum(0, dtype=torch.float32))
         return dx, dw, db, None
 
 

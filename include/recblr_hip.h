@@ -44,6 +44,9 @@ extern "C" {
 
 #define RB_EINVAL (-1)
 
+/* bf16 activation storage (raw bits); kernels compute in fp32. */
+typedef uint16_t rb_bf16;
+
 /* Time-tile length of the fused gate/scan kernels: rb_gate_scan_fwd writes one
  * carry (the recurrent state entering the tile) per (b, tile, c) and
  * rb_gate_scan_bwd reads them back.  carries has B * ceil(L / RB_TILE) * H
@@ -281,6 +284,37 @@ int rb_item_rank(const float* seq, const float* items, const int64_t* target, in
  * fma chain as the kernels above; scores [B, V] contiguous. */
 int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,
                    float* scores, void* stream);
+
+/* ---- bf16 storage variants (BASELINE config 5: L = 2048, d = 256, bf16) ----
+ * Same semantics, arguments and checks as the fp32 entry points above, with
+ * the [B, L, *] / [B, C, T] activations stored as bf16 (loaded to fp32,
+ * every recurrence, gate and accumulation in fp32 registers, the outputs
+ * rounded to bf16 once, RNE); per-channel parameters (w, bias, lam, gate_b),
+ * the carry checkpoint, h0 and all partial sums stay fp32.  alpha is never
+ * stored (alpha ~ 0.9995 would round to 1 in bf16: SURVEY §7).  The reference
+ * has no bf16 scan (parallel_scan.py:19,27-28 are fp32-only); these replace
+ * the same interfaces as their fp32 forms. */
+int rb_scan_fwd_bf16(const rb_bf16* gates, const rb_bf16* tokens, rb_bf16* states, int64_t B,
+                     int64_t C, int64_t T, void* stream);
+int rb_scan_bwd_bf16(const rb_bf16* gates, const rb_bf16* states, const rb_bf16* grad,
+                     rb_bf16* d_gates, rb_bf16* d_tokens, int64_t B, int64_t C, int64_t T,
+                     void* stream);
+int rb_conv_silu_fwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
+                          rb_bf16* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
+                          void* stream);
+int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
+                          const rb_bf16* g1, const rb_bf16* g2, rb_bf16* dx, int64_t dx_rs,
+                          float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
+                          int64_t K, void* stream);
+int rb_gate_scan_fwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, int64_t xc_rs,
+                          const rb_bf16* z, int64_t z_rs, const float* lam, const float* gate_b,
+                          const float* h0, int64_t h0_bs, rb_bf16* y, int64_t y_rs,
+                          float* carries, int64_t B, int64_t L, int64_t H, void* stream);
+int rb_gate_scan_bwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, int64_t xc_rs,
+                          const rb_bf16* z, int64_t z_rs, const float* lam, const float* gate_b,
+                          const float* carries, const rb_bf16* dy, rb_bf16* drg, int64_t drg_rs,
+                          rb_bf16* dxc, int64_t dxc_rs, rb_bf16* dz, int64_t dz_rs, float* part,
+                          float* dh0_part, int64_t B, int64_t L, int64_t H, void* stream);
 
 /* ---- projection GEMMs (RecBLR.py:162,165,167,213,214: nn.Linear, fp32) ----
  * fp32 GEMMs on the bf16 MFMA pipe: every fp32 operand is split exactly into

@@ -1,0 +1,145 @@
+"""bf16-storage recurrence kernels (BASELINE config 5: L = 2048, d = 256, bf16).
+
+The reference is fp32-only (parallel_scan.py:19,27-28), so parity is stated
+against fp32 computations fed the SAME bf16-rounded inputs:
+* kernel level — the bf16 kernels run the fp32 kernels' arithmetic on
+  bf16-loaded values and round each output once, so every bf16 output equals
+  the fp32 kernel's output on the rounded inputs, rounded to bf16 (RNE):
+  asserted bit for bit; the fp32 partial sums (dW, dbias, dLambda, dh0) are
+  asserted equal to the fp32 kernel's to 1e-5 relative (identical order, only
+  the vector width of a lane differs);
+* layer level — GatedRecurrentLayer on bf16 activations (bf16 MFMA GEMMs with
+  fp32 accumulation) against the CPU oracle (oracle/recblr_oracle.py, fp32)
+  on the same bf16-rounded input: within 3e-2 of max|ref|, the expected bf16
+  storage error (2^-8 relative per rounding, a few roundings deep)."""
+import pytest
+import torch
+
+from oracle import recblr_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+
+
+def _rb(t):
+    """round to bf16 and back (the value a bf16 tensor holds)."""
+    return t.to(BF).float()
+
+
+def _bits_equal(a_bf16, ref_fp32, what):
+    exp = ref_fp32.to(BF)
+    diff = (a_bf16.view(torch.int16) != exp.view(torch.int16))
+    assert not diff.any(), (f"{what}: {int(diff.sum())} of {diff.numel()} elements differ; "
+                            f"max |d| {(a_bf16.float() - exp.float()).abs().max().item():.3e}")
+
+
+def _close(a, b, rtol=1e-5, what=""):
+    err = (a - b).abs().max().item()
+    assert err <= rtol * max(b.abs().max().item(), 1e-30) + 1e-7, f"{what}: {err:.3e}"
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 8), (3, 16, 256), (1, 5, 2048), (2, 4, 2051)])
+def test_scan_bf16_equals_rounded_fp32_kernel(cuda, shape):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(sum(shape))
+    gates = _rb(torch.rand(shape, generator=g) * 0.2 + 0.8).to(cuda)
+    tokens = _rb(torch.randn(shape, generator=g)).to(cuda)
+    grad = _rb(torch.randn(shape, generator=g)).to(cuda)
+    h32 = kernels.scan_fwd(gates, tokens)
+    h16 = kernels.scan_fwd(gates.to(BF), tokens.to(BF))
+    assert h16.dtype == BF
+    _bits_equal(h16, h32, "states")
+    # oracle (serial fp32 scan) on the same rounded inputs
+    ref = orc.serial_scan(gates.cpu(), tokens.cpu())
+    assert (h16.float().cpu() - ref).abs().max() <= 2 ** -8 * ref.abs().max() + 1e-5
+    # backward with the bf16 states the forward stored
+    dg32, dt32 = kernels.scan_bwd(gates, h16.float(), grad)
+    dg16, dt16 = kernels.scan_bwd(gates.to(BF), h16, grad.to(BF))
+    _bits_equal(dg16, dg32, "d_gates")
+    _bits_equal(dt16, dt32, "d_tokens")
+
+
+@pytest.mark.parametrize("B,L,H,K", [(2, 50, 64, 4), (3, 2048, 512, 4), (2, 33, 20, 3)])
+def test_conv_bf16_equals_rounded_fp32_kernel(cuda, B, L, H, K):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(B * L + H)
+    x = _rb(torch.randn(B, L, H, generator=g)).to(cuda)
+    w = (torch.randn(H, 1, K, generator=g) * 0.3).to(cuda)
+    b = (torch.randn(H, generator=g) * 0.1).to(cuda)
+    gy = _rb(torch.randn(B, L, H, generator=g)).to(cuda)
+    y32 = kernels.conv_silu_fwd(x, w, b)
+    y16 = kernels.conv_silu_fwd(x.to(BF), w, b)
+    _bits_equal(y16, y32, "xc")
+    dx32 = torch.empty_like(x)
+    dw32, db32 = kernels.conv_silu_bwd(x, w, b, gy, None, dx32)
+    dx16 = torch.empty_like(x, dtype=BF)
+    dw16, db16 = kernels.conv_silu_bwd(x.to(BF), w, b, gy.to(BF), None, dx16)
+    _bits_equal(dx16, dx32, "dx")
+    _close(dw16, dw32, what="dw")
+    _close(db16, db32, what="dbias")
+
+
+@pytest.mark.parametrize("B,L,H,h0", [(2, 50, 64, "shared"), (3, 2048, 512, None),
+                                      (2, 37, 96, "rows"), (1, 16, 256, None)])
+def test_gate_scan_bf16_equals_rounded_fp32_kernel(cuda, B, L, H, h0):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(B + L + H)
+    rg = _rb(torch.randn(B, L, 2 * H, generator=g)).to(cuda)
+    xc = _rb(torch.randn(B, L, H, generator=g)).to(cuda)
+    z = _rb(torch.randn(B, L, H, generator=g)).to(cuda)
+    dy = _rb(torch.randn(B, L, H, generator=g)).to(cuda)
+    lam = torch.linspace(-2.2, -6.9, H).to(cuda)
+    gb = (0.1 * torch.randn(2 * H, generator=g)).to(cuda)
+    h = None
+    if h0 == "shared":
+        h = torch.randn(H, generator=g).to(cuda)
+    elif h0 == "rows":
+        h = torch.randn(B, H, generator=g).to(cuda)
+    y32, c32 = kernels.gate_scan_fwd(rg, xc, z, lam, h, gate_b=gb)
+    y16, c16 = kernels.gate_scan_fwd(rg.to(BF), xc.to(BF), z.to(BF), lam, h, gate_b=gb)
+    _bits_equal(y16, y32, "y")
+    assert torch.equal(c16, c32), "carries (fp32) differ"
+    dz32 = torch.empty_like(z)
+    r32 = kernels.gate_scan_bwd(rg, xc, z, lam, c32, dy, dz32, dh0_rows=h0 == "rows", gate_b=gb)
+    dz16 = torch.empty_like(z, dtype=BF)
+    r16 = kernels.gate_scan_bwd(rg.to(BF), xc.to(BF), z.to(BF), lam, c16, dy.to(BF), dz16,
+                                dh0_rows=h0 == "rows", gate_b=gb)
+    _bits_equal(dz16, dz32, "dz")
+    _bits_equal(r16[0], r32[0], "drg")
+    _bits_equal(r16[1], r32[1], "dxc")
+    for k, n in ((2, "dLambda"), (3, "dgate_b"), (4, "dh0")):
+        _close(r16[k], r32[k], what=n)
+
+
+@pytest.mark.parametrize("B,L,d", [(3, 50, 64), (2, 2048, 256)])
+def test_grl_bf16_vs_oracle(cuda, B, L, d):
+    """GatedRecurrentLayer on bf16 activations (C5 when L = 2048, d = 256)
+    against the fp32 CPU oracle on the same bf16-rounded input."""
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    torch.manual_seed(5)
+    layer = GatedRecurrentLayer(d_model=d).to(cuda)
+    g = torch.Generator().manual_seed(11)
+    x32 = _rb(torch.randn(B, L, d, generator=g))
+    gy = _rb(torch.randn(B, L, d, generator=g))
+    x = x32.to(cuda).to(BF).requires_grad_()
+    y = layer(x)
+    assert y.dtype == BF
+    (y.float() * gy.to(cuda)).sum().backward()
+    params = {k: v.detach().cpu().requires_grad_() for k, v in layer.state_dict().items()}
+    xs = x32.clone().requires_grad_()
+    ys = orc.grl_forward(params, "", xs)
+    (ys * gy).sum().backward()
+
+    def rel(a, b):
+        return ((a.float().cpu() - b).abs().max() / b.abs().max()).item()
+
+    assert rel(y.detach(), ys.detach()) < 3e-2
+    assert rel(x.grad, xs.grad) < 3e-2
+    for n, p in layer.named_parameters():
+        assert p.grad.dtype == torch.float32
+        assert rel(p.grad, params[n].grad) < 5e-2, n
