@@ -413,7 +413,7 @@ bool vec_ok(int64_t H, std::initializer_list<int64_t> strides,
   return true;
 }
 
-template <typename T, int V>
+template <typename T, int V, bool PF = true>
 int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
@@ -421,7 +421,7 @@ int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
-  hipLaunchKernelGGL((k_gate_scan_fwd<T, V, kFwdQ, kFwdTC, true>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_gate_scan_fwd<T, V, kFwdQ, kFwdTC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw);
   return launch_status("rb_gate_scan_fwd");
@@ -453,9 +453,10 @@ int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y};
   const auto f32 = {(const void*)lam, (const void*)gb, (const void*)h0, (const void*)carries};
+  // bf16: no register prefetch (measured 3% faster at config 5, tools/kbench.hip)
   if (vec_ok<T, VW>(H, strides, act, f32))
-    return gate_fwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs,
-                             carries, B, L, H, st);
+    return gate_fwd_v<T, VW, sizeof(T) == 4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs,
+                                             y, y_rs, carries, B, L, H, st);
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_fwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
                             B, L, H, st);

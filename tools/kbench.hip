@@ -14,6 +14,7 @@
 #include "../datamining_recblr_amd/csrc/item_scores.hip"
 #include "../datamining_recblr_amd/csrc/pad_prefix.hip"
 #include "../datamining_recblr_amd/csrc/reduce.hip"
+#include "../datamining_recblr_amd/csrc/gemm_split.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -60,47 +61,65 @@ struct GateBufs {
   int rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs;
 };
 
-template <int VEC, int Q, int TC, bool PF = false>
-void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBufs g, double N) {
+// T: activation storage (float, or bf16_t reading the same buffers as bf16
+// for timing); which = 1 fwd, 2 bwd, 3 both
+template <typename T, int VEC, int Q, int TC, bool PF = false>
+void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBufs g, double N,
+              int which = 3) {
   constexpr int G = 64 / Q;
   const int ncw = (H + G * VEC - 1) / (G * VEC);
   const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
-  char* f = (char*)malloc(64);
-  snprintf(f, 64, "gate_fwd %s", nm);
-  cs.push_back({f, 5 * N * 4, [=] {
-    hipLaunchKernelGGL((k_gate_scan_fwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, g.rg,
-                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, nullptr, nullptr, 0, g.y, H, g.car,
-                       (int64_t)B, L, H, ncw);
-  }, {}});
-  char* f2 = (char*)malloc(64);
-  snprintf(f2, 64, "gate_bwd %s", nm);
-  cs.push_back({f2, 9 * N * 4, [=] {
-    hipLaunchKernelGGL((k_gate_scan_bwd<VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0, g.rg,
-                       g.rg_rs, g.xc, g.xc_rs, g.z, g.z_rs, g.lam, nullptr, g.car, g.dy, g.drg, g.drg_rs,
-                       g.dxc, g.dxc_rs, g.dz, g.dz_rs, g.part, g.dh0, (int64_t)B, L, H, ncw);
-  }, {}});
+  const double es = sizeof(T);
+  auto A = [](float* p) { return reinterpret_cast<T*>(p); };
+  if (which & 1) {
+    char* f = (char*)malloc(64);
+    snprintf(f, 64, "gate_fwd %s", nm);
+    cs.push_back({f, 5 * N * es, [=] {
+      hipLaunchKernelGGL((k_gate_scan_fwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
+                         A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr,
+                         nullptr, 0, A(g.y), H, g.car, (int64_t)B, L, H, ncw);
+    }, {}});
+  }
+  if (which & 2) {
+    char* f2 = (char*)malloc(64);
+    snprintf(f2, 64, "gate_bwd %s", nm);
+    cs.push_back({f2, 9 * N * es, [=] {
+      hipLaunchKernelGGL((k_gate_scan_bwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
+                         A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr, g.car,
+                         A(g.dy), A(g.drg), g.drg_rs, A(g.dxc), g.dxc_rs, A(g.dz), g.dz_rs, g.part,
+                         g.dh0, (int64_t)B, L, H, ncw);
+    }, {}});
+  }
 }
 
-template <int K, int VEC, int Q, int TC>
+template <typename T, int K, int VEC, int Q, int TC>
 void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float* x, float* w,
-              float* bias, float* xc, float* g1, float* dx, float* dwp, float* dbp, double N) {
+              float* bias, float* xc, float* g1, float* dx, float* dwp, float* dbp, double N,
+              int which = 3) {
   constexpr int G = 64 / Q;
   const int ncw = (H + G * VEC - 1) / (G * VEC);
   const int ntile = (L + Q * TC - 1) / (Q * TC);
-  char* f = (char*)malloc(64);
-  snprintf(f, 64, "conv_fwd %s", nm);
-  cs.push_back({f, 2 * N * 4, [=] {
-    const int64_t blocks = ((int64_t)B * ncw * ntile + 3) / 4;
-    hipLaunchKernelGGL((k_conv_silu_fwd<K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, x, 2 * H,
-                       w, bias, xc, H, (int64_t)B, L, H, ncw, ntile);
-  }, {}});
-  char* f2 = (char*)malloc(64);
-  snprintf(f2, 64, "conv_bwd %s", nm);
-  cs.push_back({f2, 3 * N * 4, [=] {
-    const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
-    hipLaunchKernelGGL((k_conv_silu_bwd<K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0, x, 2 * H,
-                       w, bias, g1, nullptr, dx, 2 * H, dwp, dbp, (int64_t)B, L, H, ncw);
-  }, {}});
+  const double es = sizeof(T);
+  auto A = [](float* p) { return reinterpret_cast<T*>(p); };
+  if (which & 1) {
+    char* f = (char*)malloc(64);
+    snprintf(f, 64, "conv_fwd %s", nm);
+    cs.push_back({f, 2 * N * es, [=] {
+      const int64_t blocks = ((int64_t)B * ncw * ntile + 3) / 4;
+      hipLaunchKernelGGL((k_conv_silu_fwd<T, K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0,
+                         A(x), 2 * H, w, bias, A(xc), H, (int64_t)B, L, H, ncw, ntile);
+    }, {}});
+  }
+  if (which & 2) {
+    char* f2 = (char*)malloc(64);
+    snprintf(f2, 64, "conv_bwd %s", nm);
+    cs.push_back({f2, 3 * N * es, [=] {
+      const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
+      hipLaunchKernelGGL((k_conv_silu_bwd<T, K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0,
+                         A(x), 2 * H, w, bias, A(g1), (const T*)nullptr, A(dx), 2 * H, dwp, dbp,
+                         (int64_t)B, L, H, ncw);
+    }, {}});
+  }
 }
 
 // pure 1R+1W float4 copy (the guide's copy ceiling)
@@ -164,6 +183,7 @@ int main(int argc, char** argv) {
   const int L = argc > 2 ? atoi(argv[2]) : 200;
   const int H = argc > 3 ? atoi(argv[3]) : 256;
   const int rounds = argc > 4 ? atoi(argv[4]) : 15;
+  const bool bf16_only = argc > 5 && atoi(argv[5]) == 1;   // the config-5 bf16 sweep only
   const double N = (double)B * L * H;
   const int64_t n = (int64_t)B * L * H;
   const int nT = (L + RB_TILE - 1) / RB_TILE;
@@ -198,18 +218,41 @@ int main(int argc, char** argv) {
   float* Qb = dalloc(3 * n, 32);          // [dr | di | dxc] rows
   GateBufs comb{P, P + 2 * H, xz + H, y, car, dy, Qb, Qb + 2 * H, dz + H, part, dh0, lam,
                 3 * H, 3 * H, 2 * H, 3 * H, 3 * H, 2 * H};
-  add_gate<2, 4, 4, true>(cs, "v2 q4 tc4 pf  sep", B, L, H, sep, N);
-  add_gate<4, 8, 2, false>(cs, "v4 q8 tc2     sep", B, L, H, sep, N);
-  add_gate<2, 4, 4, true>(cs, "v2 q4 tc4 pf  comb", B, L, H, comb, N);
-  add_gate<4, 8, 2, false>(cs, "v4 q8 tc2     comb", B, L, H, comb, N);
-  add_gate<4, 4, 4, true>(cs, "v4 q4 tc4 pf  comb", B, L, H, comb, N);
-  add_gate<2, 8, 2, false>(cs, "v2 q8 tc2     comb", B, L, H, comb, N);
-  add_conv<4, 4, 4, 8>(cs, "v4 q4 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
-  add_conv<4, 4, 4, 4>(cs, "v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
-  add_conv<4, 2, 4, 4>(cs, "v2 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
-  add_conv<4, 4, 2, 8>(cs, "v4 q2 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
-  add_conv<4, 2, 2, 8>(cs, "v2 q2 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
-  add_conv<4, 4, 8, 4>(cs, "v4 q8 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  if (bf16_only) {
+    add_gate<bf16_t, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 8, 8, 2, false>(cs, "bf16 v8 q8 tc2", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 8, 4, 4, false>(cs, "bf16 v8 q4 tc4", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 2, 4, 4, true>(cs, "bf16 v2 q4 tc4 pf", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 4, 8, 2, false>(cs, "bf16 v4 q8 tc2", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 8, 8, 2, false>(cs, "bf16 v8 q8 tc2", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 8, 16, 1, false>(cs, "bf16 v8 q16 tc1", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 4, 16, 1, false>(cs, "bf16 v4 q16 tc1", B, L, H, sep, N, 2);
+    add_gate<float, 4, 8, 2, false>(cs, "f32 v4 q8 tc2", B, L, H, sep, N, 2);
+    add_gate<float, 2, 4, 4, true>(cs, "f32 v2 q4 tc4 pf", B, L, H, sep, N, 1);
+    add_conv<bf16_t, 4, 4, 4, 4>(cs, "bf16 v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+    add_conv<bf16_t, 4, 8, 4, 4>(cs, "bf16 v8 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+    add_conv<bf16_t, 4, 8, 4, 8>(cs, "bf16 v8 q4 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+    add_conv<bf16_t, 4, 8, 8, 4>(cs, "bf16 v8 q8 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+    add_conv<bf16_t, 4, 4, 8, 4>(cs, "bf16 v4 q8 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+    add_conv<float, 4, 4, 4, 4>(cs, "f32 v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+    cs.push_back({"copy4 (1R+1W float4)", 2 * N * 4, [=] {
+      hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)xc, (float4*)dxc, n / 4);
+    }, {}});
+  } else {
+  add_gate<float, 2, 4, 4, true>(cs, "v2 q4 tc4 pf  sep", B, L, H, sep, N);
+  add_gate<float, 4, 8, 2, false>(cs, "v4 q8 tc2     sep", B, L, H, sep, N);
+  add_gate<float, 2, 4, 4, true>(cs, "v2 q4 tc4 pf  comb", B, L, H, comb, N);
+  add_gate<float, 4, 8, 2, false>(cs, "v4 q8 tc2     comb", B, L, H, comb, N);
+  add_gate<float, 4, 4, 4, true>(cs, "v4 q4 tc4 pf  comb", B, L, H, comb, N);
+  add_gate<float, 2, 8, 2, false>(cs, "v2 q8 tc2     comb", B, L, H, comb, N);
+  add_conv<float, 4, 4, 4, 8>(cs, "v4 q4 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<float, 4, 4, 4, 4>(cs, "v4 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<float, 4, 2, 4, 4>(cs, "v2 q4 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<float, 4, 4, 2, 8>(cs, "v4 q2 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<float, 4, 2, 2, 8>(cs, "v2 q2 tc8", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
+  add_conv<float, 4, 4, 8, 4>(cs, "v4 q8 tc4", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N);
   cs.push_back({"scan_rows_fwd [B,H,L]", 3 * N * 4, [=] {
     launch_scan_fwd(sg, sx, so, (int64_t)B * H, L, 0);
   }, {}});
@@ -251,12 +294,13 @@ int main(int argc, char** argv) {
                   2 * H, H, 2 * H, 2 * H, H, 2 * H};
       char* nm = (char*)malloc(64);
       snprintf(nm, 64, "v2 q4 tc4 pf stag%d", k);
-      add_gate<2, 4, 4, true>(cs, nm, B, L, H, st, N);
+      add_gate<float, 2, 4, 4, true>(cs, nm, B, L, H, st, N);
     }
   }
   cs.push_back({"hipMemcpy d2d (R+W)", 2 * N * 4, [=] {
     CK(hipMemcpyAsync(dxc, xc, n * sizeof(float), hipMemcpyDeviceToDevice, 0));
   }, {}});
+  }
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
