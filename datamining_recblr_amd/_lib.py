@@ -17,7 +17,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -31,14 +31,14 @@ SIGNATURES = {
     "rb_num_kernels": (ctypes.c_int, []),
     "rb_scan_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp]),
     "rb_scan_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp]),
-    "rb_conv_silu_fwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64, _i64, _fp]),
+    "rb_conv_silu_fwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64, _i64, _fp, _fp]),
     "rb_conv_silu_bwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
-                                        _i64, _i64, _i64, _i64, _fp]),
+                                        _i64, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp,
-                                        _i64, _fp, _i64, _i64, _i64, _fp]),
+                                        _i64, _fp, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
                                         _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
-                                        _fp]),
+                                        _fp, _fp]),
     "rb_pad_prefix_fwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp]),
     "rb_pad_prefix_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
                                          _fp, _fp, _fp, _fp]),
@@ -69,14 +69,14 @@ SIGNATURES = {
     "rb_scan_fwd_bf16": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp]),
     "rb_scan_bwd_bf16": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp]),
     "rb_conv_silu_fwd_bf16": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64,
-                                             _i64, _fp]),
+                                             _i64, _fp, _fp]),
     "rb_conv_silu_bwd_bf16": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
-                                             _i64, _i64, _i64, _i64, _fp]),
+                                             _i64, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_fwd_bf16": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp,
-                                             _i64, _fp, _i64, _fp, _i64, _i64, _i64, _fp]),
+                                             _i64, _fp, _i64, _fp, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_bwd_bf16": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp,
                                              _fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64,
-                                             _i64, _i64, _fp]),
+                                             _i64, _i64, _fp, _fp]),
     "rb_gemm_split_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
     "rb_gemm_split_weight": (ctypes.c_int, [_fp, _i64, _i64, _i64, ctypes.c_int, _fp, _fp]),
     "rb_gemm_nt": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 16; }
+int rb_version(void) { return 17; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -98,38 +98,38 @@ int rb_scan_bwd(const float* gates, const float* states, const float* grad, floa
 }
 
 int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
-                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, void* stream) {
+                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* seq_offsets, void* stream) {
   if (!x || !w || !bias || !xc) return fail("rb_conv_silu_fwd: null pointer");
   if (K < 1 || K > 8) return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
   if (x_rs < H || xc_rs < H) return fail("rb_conv_silu_fwd: row stride < H");
   if (int r = check_dims("rb_conv_silu_fwd", B, L, H, max4(x_rs, xc_rs))) return r;
   return launch_conv_fwd(x, x_rs, w, bias, xc, xc_rs, B, L, H, K,
-                         reinterpret_cast<hipStream_t>(stream));
+                         seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
                      const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
-                     float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, void* stream) {
+                     float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* seq_offsets, void* stream) {
   if (!x || !w || !bias || !g1 || !dx || !dw_part || !db_part)
     return fail("rb_conv_silu_bwd: null pointer");
   if (K < 1 || K > 8) return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
   if (x_rs < H || dx_rs < H) return fail("rb_conv_silu_bwd: row stride < H");
   if (int r = check_dims("rb_conv_silu_bwd", B, L, H, max4(x_rs, dx_rs, H))) return r;
   return launch_conv_bwd(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K,
-                         reinterpret_cast<hipStream_t>(stream));
+                         seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                      const float* z, int64_t z_rs, const float* lam, const float* gate_b,
                      const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
-                     int64_t B, int64_t L, int64_t H, void* stream) {
+                     int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream) {
   if (!rg || !xc || !z || !lam || !y) return fail("rb_gate_scan_fwd: null pointer");
   if (h0_bs != 0 && h0_bs < H) return fail("rb_gate_scan_fwd: h0 batch stride must be 0 or >= H");
   if (rg_rs < 2 * H || xc_rs < H || z_rs < H || y_rs < H)
     return fail("rb_gate_scan_fwd: row stride too small");
   if (int r = check_dims("rb_gate_scan_fwd", B, L, H, max4(rg_rs, xc_rs, z_rs, y_rs))) return r;
   return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, h0, h0_bs, y, y_rs, carries,
-                         B, L, H, reinterpret_cast<hipStream_t>(stream));
+                         B, L, H, seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
@@ -137,7 +137,7 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
                      const float* carries,
                      const float* dy, float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
                      float* dz, int64_t dz_rs, float* part, float* dh0_part, int64_t B,
-                     int64_t L, int64_t H, void* stream) {
+                     int64_t L, int64_t H, const int64_t* seq_offsets, void* stream) {
   if (!rg || !xc || !z || !lam || !carries || !dy || !drg || !dxc || !dz || !part || !dh0_part)
     return fail("rb_gate_scan_bwd: null pointer");
   if (rg_rs < 2 * H || xc_rs < H || z_rs < H || drg_rs < 2 * H || dxc_rs < H || dz_rs < H)
@@ -147,7 +147,7 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
     return r;
   return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, carries, dy, drg, drg_rs, dxc,
                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H,
-                         reinterpret_cast<hipStream_t>(stream));
+                         seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 // ---- bf16 storage variants (fp32 arithmetic; same checks as the fp32 forms) ----
@@ -178,19 +178,19 @@ int rb_scan_bwd_bf16(const rb_bf16* gates, const rb_bf16* states, const rb_bf16*
 
 int rb_conv_silu_fwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
                           rb_bf16* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
-                          void* stream) {
+                          const int64_t* seq_offsets, void* stream) {
   if (!x || !w || !bias || !xc) return fail("rb_conv_silu_fwd_bf16: null pointer");
   if (K < 1 || K > 8) return fail("rb_conv_silu_fwd_bf16: kernel size K must be in [1, 8]");
   if (x_rs < H || xc_rs < H) return fail("rb_conv_silu_fwd_bf16: row stride < H");
   if (int r = check_dims("rb_conv_silu_fwd_bf16", B, L, H, max4(x_rs, xc_rs))) return r;
   return launch_conv_fwd_bf16(BF(x), x_rs, w, bias, BFW(xc), xc_rs, B, L, H, K,
-                              reinterpret_cast<hipStream_t>(stream));
+                              seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
                           const rb_bf16* g1, const rb_bf16* g2, rb_bf16* dx, int64_t dx_rs,
                           float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
-                          int64_t K, void* stream) {
+                          int64_t K, const int64_t* seq_offsets, void* stream) {
   if (!x || !w || !bias || !g1 || !dx || !dw_part || !db_part)
     return fail("rb_conv_silu_bwd_bf16: null pointer");
   if (K < 1 || K > 8) return fail("rb_conv_silu_bwd_bf16: kernel size K must be in [1, 8]");
@@ -198,13 +198,13 @@ int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const 
   if (int r = check_dims("rb_conv_silu_bwd_bf16", B, L, H, max4(x_rs, dx_rs, H))) return r;
   return launch_conv_bwd_bf16(BF(x), x_rs, w, bias, BF(g1), g2 ? BF(g2) : nullptr, BFW(dx),
                               dx_rs, dw_part, db_part, B, L, H, K,
-                              reinterpret_cast<hipStream_t>(stream));
+                              seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gate_scan_fwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, int64_t xc_rs,
                           const rb_bf16* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* h0, int64_t h0_bs, rb_bf16* y, int64_t y_rs,
-                          float* carries, int64_t B, int64_t L, int64_t H, void* stream) {
+                          float* carries, int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream) {
   if (!rg || !xc || !z || !lam || !y) return fail("rb_gate_scan_fwd_bf16: null pointer");
   if (h0_bs != 0 && h0_bs < H)
     return fail("rb_gate_scan_fwd_bf16: h0 batch stride must be 0 or >= H");
@@ -214,14 +214,14 @@ int rb_gate_scan_fwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, i
     return r;
   return launch_gate_fwd_bf16(BF(rg), rg_rs, BF(xc), xc_rs, BF(z), z_rs, lam, gate_b, h0, h0_bs,
                               BFW(y), y_rs, carries, B, L, H,
-                              reinterpret_cast<hipStream_t>(stream));
+                              seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gate_scan_bwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, int64_t xc_rs,
                           const rb_bf16* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* carries, const rb_bf16* dy, rb_bf16* drg, int64_t drg_rs,
                           rb_bf16* dxc, int64_t dxc_rs, rb_bf16* dz, int64_t dz_rs, float* part,
-                          float* dh0_part, int64_t B, int64_t L, int64_t H, void* stream) {
+                          float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream) {
   if (!rg || !xc || !z || !lam || !carries || !dy || !drg || !dxc || !dz || !part || !dh0_part)
     return fail("rb_gate_scan_bwd_bf16: null pointer");
   if (rg_rs < 2 * H || xc_rs < H || z_rs < H || drg_rs < 2 * H || dxc_rs < H || dz_rs < H)
@@ -231,7 +231,7 @@ int rb_gate_scan_bwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, i
     return r;
   return launch_gate_bwd_bf16(BF(rg), rg_rs, BF(xc), xc_rs, BF(z), z_rs, lam, gate_b, carries,
                               BF(dy), BFW(drg), drg_rs, BFW(dxc), dxc_rs, BFW(dz), dz_rs, part,
-                              dh0_part, B, L, H, reinterpret_cast<hipStream_t>(stream));
+                              dh0_part, B, L, H, seq_offsets, reinterpret_cast<hipStream_t>(stream));
 }
 
 #undef BF

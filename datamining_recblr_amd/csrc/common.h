@@ -178,19 +178,19 @@ DropSpec make_drop(const uint8_t* mask, uint64_t seed, float p);
 
 // host launch helpers (defined in the .hip files)
 int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
-                    int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st);
+                    int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st);
 int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
                     const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
-                    float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st);
+                    float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st);
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
-                    int64_t B, int64_t L, int64_t H, hipStream_t st);
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
-                    int64_t B, int64_t L, int64_t H, hipStream_t st);
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st);
 int launch_scan_fwd_bf16(const bf16_t* gates, const bf16_t* tokens, bf16_t* states,
                          int64_t rows, int64_t T, hipStream_t st);
 int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t* grad,
@@ -198,20 +198,20 @@ int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t
                          hipStream_t st);
 int launch_conv_fwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
                          bf16_t* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
-                         hipStream_t st);
+                         const int64_t* offs, hipStream_t st);
 int launch_conv_bwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
                          const bf16_t* g1, const bf16_t* g2, bf16_t* dx, int64_t dx_rs,
                          float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
-                         int64_t K, hipStream_t st);
+                         int64_t K, const int64_t* offs, hipStream_t st);
 int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
                          const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
                          const float* h0, int64_t h0_bs, bf16_t* y, int64_t y_rs, float* carries,
-                         int64_t B, int64_t L, int64_t H, hipStream_t st);
+                         int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st);
 int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
                          const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
                          const float* carries, const bf16_t* dy, bf16_t* drg, int64_t drg_rs,
                          bf16_t* dxc, int64_t dxc_rs, bf16_t* dz, int64_t dz_rs, float* part,
-                         float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st);
+                         float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st);
 int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
                       const float* r, const float* gamma, const float* beta, float eps, float* y,
                       float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,

@@ -13,7 +13,7 @@ template <typename T, int K, int VEC, int Q, int TC>
 __global__ void __launch_bounds__(256)
 k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
                 const float* __restrict__ bias, T* __restrict__ xc, int xc_rs, int64_t B,
-                int L, int H, int ncw, int ntile) {
+                int Lmax, int H, int ncw, int ntile, const int64_t* __restrict__ offs) {
   constexpr int G = kWave / Q;
   constexpr int NX = TC + K - 1;
   const int lane = threadIdx.x & (kWave - 1);
@@ -28,8 +28,20 @@ k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
   const int c0 = cw * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
-  const T* xb = x + b * L * x_rs + cc;
-  T* ob = xc + b * L * xc_rs + cc;
+  // dense rows (b, t) at b * Lmax + t, or packed variable-length sequences:
+  // sequence b at rows offs[b] .. offs[b+1] (wave-uniform)
+  int64_t row0;
+  int L;
+  if (offs != nullptr) {
+    row0 = offs[b];
+    L = (int)(offs[b + 1] - row0);
+  } else {
+    row0 = b * Lmax;
+    L = Lmax;
+  }
+  if (tile * (Q * TC) >= L) return;   // past this sequence's end (wave-uniform)
+  const T* xb = x + row0 * x_rs + cc;
+  T* ob = xc + row0 * xc_rs + cc;
   float wk[K][VEC], bi[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -73,8 +85,8 @@ __global__ void __launch_bounds__(256)
 k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
                 const float* __restrict__ bias, const T* __restrict__ g1,
                 const T* __restrict__ g2, T* __restrict__ dx, int dx_rs,
-                float* __restrict__ dw_part, float* __restrict__ db_part, int64_t B, int L,
-                int H, int ncw) {
+                float* __restrict__ dw_part, float* __restrict__ db_part, int64_t B, int Lmax,
+                int H, int ncw, const int64_t* __restrict__ offs) {
   constexpr int G = kWave / Q;
   constexpr int NX = TC + K - 1;
   constexpr int KH = K > 1 ? K - 1 : 1;
@@ -88,10 +100,21 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
   const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
-  const T* xb = x + b * L * x_rs + cc;
-  const T* g1b = g1 + b * L * H + cc;
-  const T* g2b = g2 ? g2 + b * L * H + cc : nullptr;
-  T* dxb = dx + b * L * dx_rs + cc;
+  // dense rows (b, t) at b * Lmax + t, or packed variable-length sequences:
+  // sequence b at rows offs[b] .. offs[b+1] (wave-uniform)
+  int64_t row0;
+  int L;
+  if (offs != nullptr) {
+    row0 = offs[b];
+    L = (int)(offs[b + 1] - row0);
+  } else {
+    row0 = b * Lmax;
+    L = Lmax;
+  }
+  const T* xb = x + row0 * x_rs + cc;
+  const T* g1b = g1 + row0 * H + cc;
+  const T* g2b = g2 ? g2 + row0 * H + cc : nullptr;
+  T* dxb = dx + row0 * dx_rs + cc;
   float wk[K][VEC], bi[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -198,7 +221,8 @@ constexpr int kConvQ = 4;
 
 template <typename T, int K, int TC, int VW = 4>
 int conv_fwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, T* xc,
-               int64_t xc_rs, int64_t B, int64_t L, int64_t H, bool vec, hipStream_t st) {
+               int64_t xc_rs, int64_t B, int64_t L, int64_t H, bool vec, const int64_t* offs,
+               hipStream_t st) {
   const int V = vec ? VW : 1;
   const int span = (kWave / kConvQ) * V;
   const int ncw = (int)((H + span - 1) / span);
@@ -208,17 +232,17 @@ int conv_fwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, T* x
   if (blocks > 0x7fffffffLL) return fail("rb_conv_silu_fwd: grid too large");
   if (vec)
     hipLaunchKernelGGL((k_conv_silu_fwd<T, K, VW, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
-                       0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
+                       0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile, offs);
   else
     hipLaunchKernelGGL((k_conv_silu_fwd<T, K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
-                       0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile);
+                       0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, B, (int)L, (int)H, ncw, ntile, offs);
   return launch_status("rb_conv_silu_fwd");
 }
 
 template <typename T, int K, int TC>
 int conv_bwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, const T* g1,
                const T* g2, T* dx, int64_t dx_rs, float* dw_part, float* db_part,
-               int64_t B, int64_t L, int64_t H, bool vec, hipStream_t st) {
+               int64_t B, int64_t L, int64_t H, bool vec, const int64_t* offs, hipStream_t st) {
   const int V = vec ? 4 : 1;
   const int span = (kWave / kConvQ) * V;
   const int ncw = (int)((H + span - 1) / span);
@@ -226,11 +250,11 @@ int conv_bwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, cons
   if (vec)
     hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
                        0, st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
-                       (int)L, (int)H, ncw);
+                       (int)L, (int)H, ncw, offs);
   else
     hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
                        0, st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
-                       (int)L, (int)H, ncw);
+                       (int)L, (int)H, ncw, offs);
   return launch_status("rb_conv_silu_bwd");
 }
 
@@ -242,23 +266,23 @@ bool al4(const void* p) {
 
 template <typename T>
 int conv_fwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, T* xc, int64_t xc_rs,
-               int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
+               int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st) {
   const bool vec = H % 4 == 0 && x_rs % 4 == 0 && xc_rs % 4 == 0 && al4<T>(x) && al4<T>(xc) &&
                    aligned16(bias);
   // bf16 at K = 4: 8 channels (16 B) per lane, 8-step chunks (tools/kbench.hip: 6% faster
   // at config 5)
   if (sizeof(T) == 2 && K == 4 && vec && H % 8 == 0 && x_rs % 8 == 0 && xc_rs % 8 == 0 &&
       aligned16(x) && aligned16(xc) && aligned16(bias) && aligned16(w))
-    return conv_fwd_t<T, 4, 8, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, true, st);
+    return conv_fwd_t<T, 4, 8, 8>(x, x_rs, w, bias, xc, xc_rs, B, L, H, true, offs, st);
   switch (K) {
-    case 1: return conv_fwd_t<T, 1, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 2: return conv_fwd_t<T, 2, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 3: return conv_fwd_t<T, 3, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 4: return conv_fwd_t<T, 4, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 5: return conv_fwd_t<T, 5, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 6: return conv_fwd_t<T, 6, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 7: return conv_fwd_t<T, 7, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
-    case 8: return conv_fwd_t<T, 8, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, st);
+    case 1: return conv_fwd_t<T, 1, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 2: return conv_fwd_t<T, 2, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 3: return conv_fwd_t<T, 3, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 4: return conv_fwd_t<T, 4, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 5: return conv_fwd_t<T, 5, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 6: return conv_fwd_t<T, 6, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 7: return conv_fwd_t<T, 7, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
+    case 8: return conv_fwd_t<T, 8, 4>(x, x_rs, w, bias, xc, xc_rs, B, L, H, vec, offs, st);
     default: return fail("rb_conv_silu_fwd: kernel size K must be in [1, 8]");
   }
 }
@@ -266,19 +290,19 @@ int conv_fwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, T* x
 template <typename T>
 int conv_bwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, const T* g1,
                const T* g2, T* dx, int64_t dx_rs, float* dw_part, float* db_part, int64_t B,
-               int64_t L, int64_t H, int64_t K, hipStream_t st) {
+               int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st) {
   const bool vec = H % 4 == 0 && x_rs % 4 == 0 && dx_rs % 4 == 0 && al4<T>(x) && al4<T>(g1) &&
                    al4<T>(g2) && al4<T>(dx) && aligned16(dw_part) && aligned16(db_part) &&
                    aligned16(bias);
   switch (K) {
-    case 1: return conv_bwd_t<T, 1, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 2: return conv_bwd_t<T, 2, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 3: return conv_bwd_t<T, 3, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 4: return conv_bwd_t<T, 4, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 5: return conv_bwd_t<T, 5, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 6: return conv_bwd_t<T, 6, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 7: return conv_bwd_t<T, 7, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
-    case 8: return conv_bwd_t<T, 8, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, st);
+    case 1: return conv_bwd_t<T, 1, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 2: return conv_bwd_t<T, 2, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 3: return conv_bwd_t<T, 3, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 4: return conv_bwd_t<T, 4, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 5: return conv_bwd_t<T, 5, 4>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 6: return conv_bwd_t<T, 6, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 7: return conv_bwd_t<T, 7, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
+    case 8: return conv_bwd_t<T, 8, 8>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, vec, offs, st);
     default: return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
   }
 }
@@ -286,28 +310,31 @@ int conv_bwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, cons
 }  // namespace
 
 int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
-                    int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
-  return conv_fwd_k<float>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, st);
+                    int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
+                    const int64_t* offs, hipStream_t st) {
+  return conv_fwd_k<float>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, offs, st);
 }
 
 int launch_conv_fwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
                          bf16_t* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
-                         hipStream_t st) {
-  return conv_fwd_k<bf16_t>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, st);
+                         const int64_t* offs, hipStream_t st) {
+  return conv_fwd_k<bf16_t>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, offs, st);
 }
 
 int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
                     const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
-                    float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, hipStream_t st) {
-  return conv_bwd_k<float>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K, st);
+                    float* db_part, int64_t B, int64_t L, int64_t H, int64_t K,
+                    const int64_t* offs, hipStream_t st) {
+  return conv_bwd_k<float>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K,
+                           offs, st);
 }
 
 int launch_conv_bwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
                          const bf16_t* g1, const bf16_t* g2, bf16_t* dx, int64_t dx_rs,
                          float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
-                         int64_t K, hipStream_t st) {
+                         int64_t K, const int64_t* offs, hipStream_t st) {
   return conv_bwd_k<bf16_t>(x, x_rs, w, bias, g1, g2, dx, dx_rs, dw_part, db_part, B, L, H, K,
-                            st);
+                            offs, st);
 }
 
 }  // namespace rb

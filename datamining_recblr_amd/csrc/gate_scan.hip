@@ -39,7 +39,8 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 const T* __restrict__ z, int z_rs, const float* __restrict__ lam,
                 const float* __restrict__ gbias, const float* __restrict__ h0, int h0_bs,
                 T* __restrict__ y, int y_rs,
-                float* __restrict__ carries, int64_t B, int L, int H, int ncw) {
+                float* __restrict__ carries, int64_t B, int Lmax, int H, int ncw,
+                const int64_t* __restrict__ offs) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -52,7 +53,17 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
-  const int64_t row0 = b * L;
+  // dense rows (b, t) at b * Lmax + t, or packed variable-length sequences:
+  // sequence b at rows offs[b] .. offs[b+1] (wave-uniform)
+  int64_t row0;
+  int L;
+  if (offs != nullptr) {
+    row0 = offs[b];
+    L = (int)(offs[b + 1] - row0);
+  } else {
+    row0 = b * Lmax;
+    L = Lmax;
+  }
   const T* rgb = rg + row0 * rg_rs + cc;
   const T* xcb = xc + row0 * xc_rs + cc;
   const T* zb = z + row0 * z_rs + cc;
@@ -75,7 +86,8 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
 #pragma unroll
     for (int v = 0; v < VEC; ++v) carry[v] = 0.0f;
   }
-  const int nT = (L + TILE - 1) / TILE;
+  const int nT = (L + TILE - 1) / TILE;          // tiles of this row
+  const int nTc = (Lmax + TILE - 1) / TILE;      // carries row stride
 
   auto load = [&](FwdIn<VEC, TC>& in, int tile) {
     const int t0 = tile * TILE + q * TC;
@@ -89,7 +101,7 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
     }
   };
   auto process = [&](FwdIn<VEC, TC>& in, int tile) {
-    if (carries != nullptr && q == 0 && cv) stv(carries + (b * nT + tile) * H + c0, carry);
+    if (carries != nullptr && q == 0 && cv) stv(carries + (b * nTc + tile) * H + c0, carry);
     const int t0 = tile * TILE + q * TC;
     // in.r <- alpha, in.x <- b' = beta * xc
 #pragma unroll
@@ -171,7 +183,8 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 const T* __restrict__ dy,
                 T* __restrict__ drg, int drg_rs, T* __restrict__ dxc, int dxc_rs,
                 T* __restrict__ dz, int dz_rs, float* __restrict__ part,
-                float* __restrict__ dh0_part, int64_t B, int L, int H, int ncw) {
+                float* __restrict__ dh0_part, int64_t B, int Lmax, int H, int ncw,
+                const int64_t* __restrict__ offs) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -184,7 +197,17 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
-  const int64_t row0 = b * L;
+  // dense rows (b, t) at b * Lmax + t, or packed variable-length sequences:
+  // sequence b at rows offs[b] .. offs[b+1] (wave-uniform)
+  int64_t row0;
+  int L;
+  if (offs != nullptr) {
+    row0 = offs[b];
+    L = (int)(offs[b + 1] - row0);
+  } else {
+    row0 = b * Lmax;
+    L = Lmax;
+  }
   const T* rgb = rg + row0 * rg_rs + cc;
   const T* xcb = xc + row0 * xc_rs + cc;
   const T* zb = z + row0 * z_rs + cc;
@@ -207,7 +230,8 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   float ecarry[VEC], acc_v[VEC], acc_r[VEC], acc_i[VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) ecarry[v] = acc_v[v] = acc_r[v] = acc_i[v] = 0.0f;
-  const int nT = (L + TILE - 1) / TILE;
+  const int nT = (L + TILE - 1) / TILE;          // tiles of this row
+  const int nTc = (Lmax + TILE - 1) / TILE;      // carries row stride
 
   auto load = [&](BwdIn<VEC, TC>& in, int tile) {
     const int t0 = tile * TILE + q * TC;
@@ -231,7 +255,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
         in.i[j][v] += bi[v];
       }
     float hcar[VEC];
-    ldv(hcar, carries + (b * nT + tile) * H + cc);
+    ldv(hcar, carries + (b * nTc + tile) * H + cc);
     float al[TC][VEC];
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
@@ -370,6 +394,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
       process(bufA, tile);
     }
   }
+  if (nT == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ecarry);   // empty row: zeros
   // per-channel partial sums: butterfly over the Q lanes sharing the channels
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -417,13 +442,13 @@ template <typename T, int V, bool PF = true>
 int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-               hipStream_t st) {
+               const int64_t* offs, hipStream_t st) {
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_fwd<T, V, kFwdQ, kFwdTC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
-                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw);
+                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw, offs);
   return launch_status("rb_gate_scan_fwd");
 }
 
@@ -431,14 +456,15 @@ template <typename T, int V>
 int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
-               float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+               float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
+               hipStream_t st) {
   const int span = (kWave / kBwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_bwd<T, V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
-                     dh0_part, B, (int)L, (int)H, ncw);
+                     dh0_part, B, (int)L, (int)H, ncw, offs);
   return launch_status("rb_gate_scan_bwd");
 }
 
@@ -448,7 +474,7 @@ template <typename T>
 int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-               hipStream_t st) {
+               const int64_t* offs, hipStream_t st) {
   constexpr int VW = sizeof(T) == 2 ? 4 : 2;
   const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y};
@@ -456,19 +482,20 @@ int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   // bf16: no register prefetch (measured 3% faster at config 5, tools/kbench.hip)
   if (vec_ok<T, VW>(H, strides, act, f32))
     return gate_fwd_v<T, VW, sizeof(T) == 4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs,
-                                             y, y_rs, carries, B, L, H, st);
+                                             y, y_rs, carries, B, L, H, offs, st);
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_fwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                            B, L, H, st);
+                            B, L, H, offs, st);
   return gate_fwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B,
-                          L, H, st);
+                          L, H, offs, st);
 }
 
 template <typename T>
 int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
-               float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+               float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
+               hipStream_t st) {
   constexpr int VW = 4;  // bf16 at 8 channels per lane spills (256 VGPRs)
   const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)dy,
@@ -477,12 +504,12 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                     (const void*)dh0_part};
   if (vec_ok<T, VW>(H, strides, act, f32))
     return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_bwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
   return gate_bwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
 }
 
 }  // namespace
@@ -490,35 +517,36 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
-                    int64_t B, int64_t L, int64_t H, hipStream_t st) {
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
   return gate_fwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                           B, L, H, st);
+                           B, L, H, offs, st);
 }
 
 int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
                          const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
                          const float* h0, int64_t h0_bs, bf16_t* y, int64_t y_rs, float* carries,
-                         int64_t B, int64_t L, int64_t H, hipStream_t st) {
+                         int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
   return gate_fwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                            B, L, H, st);
+                            B, L, H, offs, st);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
-                    int64_t B, int64_t L, int64_t H, hipStream_t st) {
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
   return gate_bwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
 }
 
 int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
                          const bf16_t* z, int64_t z_rs, const float* lam, const float* gb,
                          const float* carries, const bf16_t* dy, bf16_t* drg, int64_t drg_rs,
                          bf16_t* dxc, int64_t dxc_rs, bf16_t* dz, int64_t dz_rs, float* part,
-                         float* dh0_part, int64_t B, int64_t L, int64_t H, hipStream_t st) {
+                         float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
+                         hipStream_t st) {
   return gate_bwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, st);
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
 }
 
 }  // namespace rb

@@ -154,6 +154,34 @@ def _row_stride(t: torch.Tensor, name: str, H: int) -> int:
     return rs
 
 
+class Packed:
+    """Packed variable-length sequences: sequence b occupies rows
+    offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
+    right-padded batch without the padding; include/recblr_hip.h)."""
+    __slots__ = ("offsets", "B", "L", "ntok")
+
+    def __init__(self, offsets: torch.Tensor, L: int, ntok: int):
+        if offsets.dtype != torch.int64 or offsets.dim() != 1 or not offsets.is_contiguous():
+            raise ValueError("offsets must be a contiguous int64 [B + 1] tensor")
+        self.offsets, self.B, self.L, self.ntok = offsets, offsets.numel() - 1, int(L), int(ntok)
+
+
+def _layout(t: torch.Tensor, name: str, C: int, seq: "Packed | None"):
+    """(B, L, row stride, offsets pointer) of a dense [B, L, C] view or a
+    packed [ntok, C] view."""
+    if seq is None:
+        rs = _row_stride(t, name, C)
+        return t.shape[0], t.shape[1], rs, 0
+    if t.dim() != 2 or t.shape != (seq.ntok, C) or (C > 1 and t.stride(1) != 1):
+        raise ValueError(f"{name} must be a [{seq.ntok}, {C}] view with unit channel stride")
+    rs = t.stride(0) if seq.ntok > 1 else C
+    if rs < C:
+        raise ValueError(f"{name}: row stride {rs} < {C}")
+    if seq.offsets.device != t.device:
+        raise ValueError("offsets must live on the activations' device")
+    return seq.B, seq.L, rs, seq.offsets.data_ptr()
+
+
 def scan_fwd(gates: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
     dt = _act_dtype(gates, "gates")
     _check(gates, "gates", dt)
@@ -188,65 +216,72 @@ def scan_bwd(gates: torch.Tensor, states: torch.Tensor, grad: torch.Tensor):
     return d_gates, d_tokens
 
 
-def conv_silu_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
-    """x: [B, L, H] (row-strided view ok, fp32 or bf16); weight: [H, K]; bias:
-    [H] (fp32) -> xc [B, L, H] in x's dtype."""
+def conv_silu_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor,
+                  seq: Packed | None = None) -> torch.Tensor:
+    """x: [B, L, H] (row-strided view ok, fp32 or bf16) or packed [ntok, H]
+    with `seq`; weight: [H, K]; bias: [H] (fp32) -> xc in x's layout and dtype."""
     dt = _act_dtype(x, "x")
     _check(x, "x", dt)
     _check(weight, "conv weight")
     _check(bias, "conv bias")
-    B, L, H = x.shape
-    x_rs = _row_stride(x, "x", H)
+    H = x.shape[-1]
+    B, L, x_rs, offs = _layout(x, "x", H, seq)
     w = weight.reshape(H, -1).contiguous()
     K = w.shape[1]
-    xc = torch.empty((B, L, H), device=x.device, dtype=dt)
-    _launch("rb_conv_silu_fwd" + _sfx(dt), 2 * B * L * H * x.element_size(), x.data_ptr(), x_rs,
-            w.data_ptr(), bias.contiguous().data_ptr(), xc.data_ptr(), H, B, L, H, K, _stream(x))
+    xc = torch.empty(x.shape[:-1] + (H,), device=x.device, dtype=dt)
+    n = x.numel() // max(H, 1) * H
+    _launch("rb_conv_silu_fwd" + _sfx(dt), 2 * n * x.element_size(), x.data_ptr(), x_rs,
+            w.data_ptr(), bias.contiguous().data_ptr(), xc.data_ptr(), H, B, L, H, K, offs,
+            _stream(x))
     return xc
 
 
-def conv_silu_bwd(x, weight, bias, g1, g2, dx):
-    """Writes dx (a [B, L, H] row-strided view) and returns (dweight [H, K], dbias [H])."""
+def conv_silu_bwd(x, weight, bias, g1, g2, dx, seq: Packed | None = None):
+    """Writes dx (x's layout, row-strided view ok) and returns (dweight [H, K],
+    dbias [H]).  g1, g2: contiguous, x's shape."""
     dt = _act_dtype(x, "x")
     _check(x, "x", dt)
     _check(g1, "g1", dt)
     _check(dx, "dx", dt)
-    B, L, H = x.shape
-    x_rs = _row_stride(x, "x", H)
-    dx_rs = _row_stride(dx, "dx", H)
-    if not g1.is_contiguous() or g1.shape != (B, L, H):
-        raise ValueError("g1 must be contiguous [B, L, H]")
+    H = x.shape[-1]
+    B, L, x_rs, offs = _layout(x, "x", H, seq)
+    dx_rs = _layout(dx, "dx", H, seq)[2]
+    if not g1.is_contiguous() or g1.shape != x.shape:
+        raise ValueError("g1 must be contiguous, shaped like x")
     if g2 is not None:
         _check(g2, "g2", dt)
-        if not g2.is_contiguous() or g2.shape != (B, L, H):
-            raise ValueError("g2 must be contiguous [B, L, H]")
+        if not g2.is_contiguous() or g2.shape != x.shape:
+            raise ValueError("g2 must be contiguous, shaped like x")
     w = weight.reshape(H, -1).contiguous()
     K = w.shape[1]
     dw_part = torch.empty((B, K, H), device=x.device, dtype=torch.float32)
     db_part = torch.empty((B, H), device=x.device, dtype=torch.float32)
-    _launch("rb_conv_silu_bwd" + _sfx(dt), (3 if g2 is None else 4) * B * L * H * x.element_size(),
+    n = x.numel()
+    _launch("rb_conv_silu_bwd" + _sfx(dt), (3 if g2 is None else 4) * n * x.element_size(),
             x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
-              g1.data_ptr(), 0 if g2 is None else g2.data_ptr(), dx.data_ptr(), dx_rs,
-              dw_part.data_ptr(), db_part.data_ptr(), B, L, H, K, _stream(x))
+            g1.data_ptr(), 0 if g2 is None else g2.data_ptr(), dx.data_ptr(), dx_rs,
+            dw_part.data_ptr(), db_part.data_ptr(), B, L, H, K, offs, _stream(x))
     return colsum(dw_part.view(B, -1)).view(-1, H).t().contiguous(), colsum(db_part)
 
 
-def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=None):
+def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=None,
+                  seq: Packed | None = None):
     """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
 
-    rg: [B, L, 2H]; xc, z: [B, L, H] views; lam: [H]; h0: [H] (shared by every
-    row), [B, H] (one initial state per row) or None; gate_b: [2H] bias added
-    to rg inside the kernel (or None).
-    Returns (y [B, L, H], carries [B, nT, H] or None when not wanted)."""
+    rg: [B, L, 2H]; xc, z: [B, L, H] views (or packed [ntok, 2H] / [ntok, H]
+    with `seq`); lam: [H]; h0: [H] (shared by every row), [B, H] (one initial
+    state per row) or None; gate_b: [2H] bias added to rg inside the kernel
+    (or None).  Returns (y in xc's layout, carries [B, nT, H] or None when not
+    wanted)."""
     dt = _act_dtype(xc, "xc")
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z")):
         _check(t, n, dt)
     _check(lam, "Lambda")
-    B, L, H = xc.shape
-    rg_rs = _row_stride(rg, "rg", 2 * H)
-    xc_rs = _row_stride(xc, "xc", H)
-    z_rs = _row_stride(z, "z", H)
-    if z.shape[:2] != (B, L) or rg.shape[:2] != (B, L):
+    H = xc.shape[-1]
+    B, L, xc_rs, offs = _layout(xc, "xc", H, seq)
+    rg_rs = _layout(rg, "rg", 2 * H, seq)[2]
+    z_rs = _layout(z, "z", H, seq)[2]
+    if seq is None and (z.shape[:2] != (B, L) or rg.shape[:2] != (B, L)):
         raise ValueError("rg, xc, z batch/length mismatch")
     if lam.shape != (H,):
         raise ValueError(f"Lambda must be [{H}]")
@@ -258,16 +293,17 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
         h0 = h0.contiguous()
         h0_bs = H if h0.dim() == 2 else 0
     if y is None:
-        y = torch.empty((B, L, H), device=xc.device, dtype=dt)
+        y = torch.empty(xc.shape[:-1] + (H,), device=xc.device, dtype=dt)
     _check(y, "y", dt)
-    y_rs = _row_stride(y, "y", H)
+    y_rs = _layout(y, "y", H, seq)[2]
     carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
                if want_carries else None)
-    _launch("rb_gate_scan_fwd" + _sfx(dt), 5 * B * L * H * xc.element_size(), rg.data_ptr(), rg_rs,
+    n = xc.numel()
+    _launch("rb_gate_scan_fwd" + _sfx(dt), 5 * n * xc.element_size(), rg.data_ptr(), rg_rs,
             xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
-              lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), 0 if h0 is None else h0.data_ptr(),
-              h0_bs, y.data_ptr(),
-              y_rs, 0 if carries is None else carries.data_ptr(), B, L, H, _stream(xc))
+            lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), 0 if h0 is None else h0.data_ptr(),
+            h0_bs, y.data_ptr(), y_rs, 0 if carries is None else carries.data_ptr(), B, L, H,
+            offs, _stream(xc))
     return y, carries
 
 
@@ -281,39 +317,40 @@ def _gb_ptr(gate_b, H):
 
 
 def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=False,
-                  gate_b=None):
+                  gate_b=None, seq: Packed | None = None):
     """Backward of gate_scan_fwd.  Writes dz (a row-strided view) and returns
-    (drg [B, L, 2H], dxc [B, L, H], dlam [H], dgate_bias [2H], dh0), dh0 [H]
-    (summed over rows) or [B, H] when dh0_rows (a per-row h0)."""
-    B, L, H = xc.shape
+    (drg, dxc, dlam [H], dgate_bias [2H], dh0), dh0 [H] (summed over rows) or
+    [B, H] when dh0_rows (a per-row h0).  Layouts as in gate_scan_fwd."""
+    H = xc.shape[-1]
     dt = _act_dtype(xc, "xc")
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (dy, "dy"), (dz, "dz")):
         _check(t, n, dt)
     _check(carries, "carries")
-    if not dy.is_contiguous() or dy.shape != (B, L, H):
-        raise ValueError("dy must be contiguous [B, L, H]")
+    B, L, xc_rs, offs = _layout(xc, "xc", H, seq)
+    if not dy.is_contiguous() or dy.shape != xc.shape:
+        raise ValueError("dy must be contiguous, shaped like xc")
     if carries.shape != (B, num_tiles(L), H) or not carries.is_contiguous():
         raise ValueError("carries shape mismatch")
-    rg_rs = _row_stride(rg, "rg", 2 * H)
-    xc_rs = _row_stride(xc, "xc", H)
-    z_rs = _row_stride(z, "z", H)
-    dz_rs = _row_stride(dz, "dz", H)
+    rg_rs = _layout(rg, "rg", 2 * H, seq)[2]
+    z_rs = _layout(z, "z", H, seq)[2]
+    dz_rs = _layout(dz, "dz", H, seq)[2]
     if drg is None:
-        drg = torch.empty((B, L, 2 * H), device=xc.device, dtype=dt)
-    drg_rs = _row_stride(drg, "drg", 2 * H)
+        drg = torch.empty(xc.shape[:-1] + (2 * H,), device=xc.device, dtype=dt)
+    drg_rs = _layout(drg, "drg", 2 * H, seq)[2]
     if dxc is None:
-        dxc = torch.empty((B, L, H), device=xc.device, dtype=dt)
+        dxc = torch.empty(xc.shape[:-1] + (H,), device=xc.device, dtype=dt)
     _check(drg, "drg", dt)
     _check(dxc, "dxc", dt)
-    dxc_rs = _row_stride(dxc, "dxc", H)
+    dxc_rs = _layout(dxc, "dxc", H, seq)[2]
     part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
     dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
-    _launch("rb_gate_scan_bwd" + _sfx(dt), 9 * B * L * H * xc.element_size(), rg.data_ptr(), rg_rs,
+    n = xc.numel()
+    _launch("rb_gate_scan_bwd" + _sfx(dt), 9 * n * xc.element_size(), rg.data_ptr(), rg_rs,
             xc.data_ptr(), xc_rs,
             z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), carries.data_ptr(),
             dy.data_ptr(),
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
-            part.data_ptr(), dh0_part.data_ptr(), B, L, H, _stream(xc))
+            part.data_ptr(), dh0_part.data_ptr(), B, L, H, offs, _stream(xc))
     sums = colsum(part)
     return (drg, dxc, sums[0], sums[1:].reshape(-1),
             dh0_part if dh0_rows else colsum(dh0_part))

@@ -9,14 +9,15 @@ MFMA peak 157).  Splitting the reduction into S row blocks as one batched GEMM
 ([S, N, M/S] x [S, M/S, K], ~1000 tiles) and summing the S partials in a fixed
 order runs 2-4.5x faster (tools/gemm_probe.py) and is deterministic.
 
-With RECBLR_SPLIT_GEMM=1 the forward and input-gradient GEMMs of the
-[B*L, *] projections run on the split-bf16 MFMA kernel (csrc/gemm_split.hip,
-``mm_nt`` / ``mm_nn``): fp32 operands split exactly into three bf16 parts, six
-partial products, fp32 accumulation — fp32-level accuracy on the bf16 pipe
-(2.67x the fp32 MFMA peak on paper).  Measured inside the training step it
-runs at 120-156 TFLOP/s against 128-149 for the tuned hipBLASLt fp32 kernels
-(DESIGN.md §4), so it is off by default.  Shapes it does not cover (and small
-M) always stay on hipBLASLt/rocBLAS through torch.  The math is exactly
+The forward and input-gradient GEMMs of the packed [ntok, *] projections run
+on the split-bf16 MFMA kernel (csrc/gemm_split.hip, ``mm_nt`` / ``mm_nn``):
+fp32 operands split exactly into three bf16 parts, six partial products, fp32
+accumulation — fp32-level accuracy on the bf16 pipe.  Its speed does not
+depend on the row count, which changes every batch once the sequences are
+packed (RecBLR._forward_packed): there hipBLASLt's untuned heuristic picks
+run at 86-117 TFLOP/s, this kernel at 120-156.  Shapes it does
+not cover (and small M) stay on hipBLASLt/rocBLAS through torch;
+RECBLR_SPLIT_GEMM=0 routes everything through torch.  The math is exactly
 nn.Linear's (RecBLR.py:162,165,167,213,214).
 """
 from __future__ import annotations
@@ -30,7 +31,7 @@ from . import gemm_tuning, kernels
 __all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled"]
 
 SPLIT_MIN_ROWS = 4096
-_split_on = os.environ.get("RECBLR_SPLIT_GEMM", "0") == "1"
+_split_on = os.environ.get("RECBLR_SPLIT_GEMM", "1") != "0"
 
 
 def split_gemm_enabled() -> bool:

@@ -30,6 +30,7 @@ from torch import nn
 from ._lib import RecBLRNativeError
 from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
                      feed_forward)
+from .kernels import Packed
 from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
@@ -73,20 +74,23 @@ class GatedRecurrentLayer(nn.Module):
         self.Lambda = nn.Parameter(torch.linspace(lo, hi, hidden))
         self.output = nn.Linear(hidden, d_model, bias=False)
 
-    def forward(self, x, pad=None, slot=None, rows=None):
+    def forward(self, x, pad=None, slot=None, rows=None, seq=None):
         """pad: None (the reference's pow2 pad prefix for x's length) or an
         int64 tensor [B] of per-row pad lengths (see recurrence.bd_lru).
         slot: blocks.ResidualGrad of the enclosing RecurrentLayer.
-        rows: flat [B*L] positions at which the output is needed (the
+        rows: flat positions at which the output is needed (the
         out-projection is position-wise, so only those rows are projected;
-        returns [len(rows), d])."""
+        returns [len(rows), d]).
+        seq: kernels.Packed — x is [ntok, d], the sequences' valid positions
+        packed back to back (RecBLR.forward)."""
         if x.device.type != "cuda":
             raise RecBLRNativeError(
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
                 "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
         xz = linear(x, self.input, slot)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
-                   self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad)
+                   self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad,
+                   seq=seq)
         if rows is not None:
             y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
         return linear(y, self.output)
@@ -125,15 +129,17 @@ class RecurrentLayer(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
         self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
 
-    def forward(self, input_tensor, pad=None, rows=None):
+    def forward(self, input_tensor, pad=None, rows=None, seq=None):
         """rows: evaluate the position-wise tail (out-projection, residual
-        LayerNorm, FFN) only at these flat [B*L] positions -> [len(rows), d]."""
+        LayerNorm, FFN) only at these flat positions -> [len(rows), d].
+        seq: kernels.Packed (input_tensor is [ntok, d])."""
         slot = (ResidualGrad(rows) if torch.is_grad_enabled() and input_tensor.requires_grad
                 else None)
         residual = input_tensor
         if rows is not None:
             residual = input_tensor.reshape(-1, input_tensor.shape[-1]).index_select(0, rows)
-        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad, slot, rows), residual,
+        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad, slot, rows, seq),
+                                   residual,
                                    self.dropout, self.layer_norm, self.training, slot)
         return h if self.disable_ffn else self.ffn(h)
 
@@ -158,6 +164,10 @@ class RecBLR(SequentialRecommender):
         # evaluate the last layer's position-wise tail only where gather_indexes
         # reads it (RECBLR_FULL_LAST_LAYER=1: every position, as the reference)
         self.gather_last_layer = os.environ.get("RECBLR_FULL_LAST_LAYER", "0") != "1"
+        # run the encoder on each sequence's first item_seq_len positions only,
+        # packed back to back (RECBLR_PACKED=0: the dense [B, L] batch, as the
+        # reference); identical outputs and gradients, see DESIGN.md
+        self.pack_sequences = os.environ.get("RECBLR_PACKED", "1") != "0"
 
         self.item_embedding = nn.Embedding(self.n_items, self.hidden_size, padding_idx=0)
         self.layer_norm = nn.LayerNorm(self.hidden_size, eps=1e-12)
@@ -196,6 +206,8 @@ class RecBLR(SequentialRecommender):
         without changing results (run_with_unseen.py:222-225 runs them one
         by one)."""
         pad = row_pad_lens(item_seq_len) if exact_lengths else None
+        if self.pack_sequences:
+            return self._forward_packed(item_seq, item_seq_len, pad)
         h = embed_dropout_layer_norm(item_seq, self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
         n = len(self.recurrent_layers)
@@ -209,6 +221,34 @@ class RecBLR(SequentialRecommender):
                 return layer(h, pad, rows)
             h = layer(h, pad)
         return self.gather_indexes(h, item_seq_len - 1)
+
+    def _forward_packed(self, item_seq, item_seq_len, pad):
+        """forward() on the valid positions only.  RecBole right-pads every
+        sequence to L; the encoder is causal (causal conv, forward scan,
+        position-wise projections / LayerNorms / FFN), so position t of row b
+        influences only positions >= t of that row, and forward() returns
+        position len_b - 1 (gather_indexes, RecBLR.py:84).  Positions >= len_b
+        therefore never reach the output or any gradient; they are dropped
+        before the embedding and the sequences run packed back to back
+        ([ntok, d], ntok = sum of lengths; the recurrence kernels take the
+        per-sequence offsets).  The pow2 pad prefix still uses the batch's L."""
+        B, L = item_seq.shape
+        dev = item_seq.device
+        lens = item_seq_len.to(torch.int64).clamp(1, L)
+        offsets = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(lens, 0, out=offsets[1:])
+        flat = (torch.arange(L, device=dev) < lens[:, None]).reshape(-1).nonzero().squeeze(1)
+        seq = Packed(offsets, L, flat.numel())
+        h = embed_dropout_layer_norm(item_seq.reshape(-1).index_select(0, flat),
+                                     self.item_embedding, self.dropout, self.layer_norm,
+                                     self.training)
+        last = offsets[1:] - 1
+        n = len(self.recurrent_layers)
+        for i, layer in enumerate(self.recurrent_layers):
+            if i == n - 1 and self.gather_last_layer:
+                return layer(h, pad, last, seq)
+            h = layer(h, pad, seq=seq)
+        return h.index_select(0, last)
 
     def _scores_all(self, seq_output):
         return full_sort_scores(seq_output, self.item_embedding.weight)

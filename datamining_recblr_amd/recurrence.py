@@ -78,25 +78,30 @@ class PadPrefix(torch.autograd.Function):
 
 
 class BDLRUCore(torch.autograd.Function):
-    """xz [B, L, 2H] -> y = silu(z) * BD-LRU(conv_silu(x)) [B, L, H]."""
+    """xz [B, L, 2H] (or packed [ntok, 2H] with `seq`) -> y = silu(z) *
+    BD-LRU(conv_silu(x)), in xz's layout."""
 
     @staticmethod
-    def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv):
-        B, L, H2 = xz.shape
+    def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq=None):
+        H2 = xz.shape[-1]
         H = H2 // 2
         x, z = xz[..., :H], xz[..., H:]
         if use_conv:
-            xc = kernels.conv_silu_fwd(x, conv_w, conv_b)
+            xc = kernels.conv_silu_fwd(x, conv_w, conv_b, seq=seq)
         else:
             xc = x
-        gflops = 2 * B * L * H * H2
+        rows = xz.numel() // H2
+        gflops = 2 * rows * H * H2
         # gates GEMM without its bias: the gate kernels add gate_b on the fly
-        rg = _timed("gemm", gflops, mm_nt, xc.reshape(B * L, H), gate_w).view(B, L, H2)
+        rg = _timed("gemm", gflops, mm_nt, xc.reshape(rows, H), gate_w).view(
+            *xz.shape[:-1], H2)
         train = any(ctx.needs_input_grad)
-        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b)
+        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b,
+                                           seq=seq)
         ctx.use_conv = use_conv
         ctx.has_h0 = h0 is not None
         ctx.h0_rows = h0 is not None and h0.dim() == 2
+        ctx.seq = seq
         ctx.save_for_backward(xz, xc if use_conv else None, rg, carries, conv_w, conv_b,
                               gate_w, gate_b, lam)
         return y
@@ -104,28 +109,32 @@ class BDLRUCore(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         xz, xc, rg, carries, conv_w, conv_b, gate_w, gate_b, lam = ctx.saved_tensors
-        B, L, H2 = xz.shape
+        seq = ctx.seq
+        H2 = xz.shape[-1]
         H = H2 // 2
+        rows = xz.numel() // H2
         x, z = xz[..., :H], xz[..., H:]
         if xc is None:
             xc = x
         dy = dy.contiguous()
         dxz = torch.empty_like(xz)
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
-            rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows, gate_b=gate_b)
-        drg2 = drg.view(B * L, H2)
-        gflops = 2 * B * L * H * H2
-        dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(B * L, H))
+            rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows, gate_b=gate_b,
+            seq=seq)
+        drg2 = drg.view(rows, H2)
+        gflops = 2 * rows * H * H2
+        dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H))
         # + dL/dxc through the gates GEMM, accumulated in place (beta = 1)
-        _timed("gemm", gflops, mm_nn, drg2, gate_w, dxc.view(B * L, H))
+        _timed("gemm", gflops, mm_nn, drg2, gate_w, dxc.view(rows, H))
         dconv_w = dconv_b = None
         if ctx.use_conv:
-            dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, None, dxz[..., :H])
+            dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, None, dxz[..., :H],
+                                                seq=seq)
             dconv_w = dw.view_as(conv_w)
         else:
             dxz[..., :H].copy_(dxc)
         return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
-                dh0 if ctx.has_h0 else None, None)
+                dh0 if ctx.has_h0 else None, None, None)
 
 
 def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
@@ -137,17 +146,19 @@ def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
     return p2 - n
 
 
-def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None):
+def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq=None):
     """Everything between the in- and out-projections of RecBLR.py:170-207.
 
     pad=None: the reference's pad prefix pow2(L) - L for the batch's L.
     pad=int64 tensor [B]: row b behaves as a sequence whose forward ran with
     its own pad prefix pad[b] (a row right-padded from its true length n_b
     with pad[b] = pow2(n_b) - n_b reproduces a batch-1 forward on the
-    unpadded sequence, run_with_unseen.py:222-225)."""
+    unpadded sequence, run_with_unseen.py:222-225).
+    seq: kernels.Packed — xz holds only each sequence's first len_b positions
+    ([ntok, 2H]); the batch's L (for the pad prefix) is seq.L."""
     if pad is None:
-        P = pow2_pad_len(xz.shape[1])
+        P = pow2_pad_len(seq.L if seq is not None else xz.shape[1])
         h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
     else:
         h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, pad) if use_conv else None
-    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv)
+    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq)

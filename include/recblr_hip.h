@@ -31,6 +31,16 @@
  * Layout (channel-last, "rows" = (batch, time) pairs):
  *   element (b, t, c) of a [B, L, *] activation lives at
  *   ptr[(b * L + t) * row_stride + c]; row_stride >= H.
+ *
+ * Packed variable-length sequences (seq_offsets != NULL; the conv and gate
+ * scan entry points): seq_offsets is a device int64 array [B + 1]; sequence b
+ * occupies rows seq_offsets[b] .. seq_offsets[b+1] - 1 (length in [0, L]), so
+ * element (b, t, c) lives at ptr[(seq_offsets[b] + t) * row_stride + c]; L is
+ * the maximum length (it sizes the carry checkpoint [B, ceil(L/RB_TILE), H]
+ * and the grid).  This is RecBole's right-padded batch without its padding:
+ * the recurrence is causal, so positions past a sequence's length never reach
+ * RecBLR.forward's output (gather_indexes at len - 1, RecBLR.py:84).
+ * seq_offsets = NULL: the dense layout above.
  */
 #ifndef RECBLR_HIP_H
 #define RECBLR_HIP_H
@@ -84,7 +94,7 @@ int rb_scan_bwd(const float* gates, const float* states, const float* grad,
  * with row stride xc_rs.  1 <= K <= 8. */
 int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w,
                      const float* bias, float* xc, int64_t xc_rs,
-                     int64_t B, int64_t L, int64_t H, int64_t K, void* stream);
+                     int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* seq_offsets, void* stream);
 
 /* Backward of rb_conv_silu_fwd.  dxc = g1 + g2 (g2 may be NULL), both
  * [B, L, H] contiguous.  Writes dx (row stride dx_rs) and per-batch partial
@@ -93,7 +103,7 @@ int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w,
 int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w,
                      const float* bias, const float* g1, const float* g2,
                      float* dx, int64_t dx_rs, float* dw_part, float* db_part,
-                     int64_t B, int64_t L, int64_t H, int64_t K, void* stream);
+                     int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* seq_offsets, void* stream);
 
 /* Fused BD-LRU forward (everything between the gates GEMM and the output
  * GEMM):
@@ -110,7 +120,7 @@ int rb_gate_scan_fwd(const float* rg, int64_t rg_rs, const float* xc,
                      int64_t xc_rs, const float* z, int64_t z_rs,
                      const float* lam, const float* gate_b, const float* h0,
                      int64_t h0_bs, float* y, int64_t y_rs, float* carries,
-                     int64_t B, int64_t L, int64_t H, void* stream);
+                     int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream);
 
 /* Backward of rb_gate_scan_fwd given dy = dL/dy ([B, L, H] contiguous).
  * Writes drg ([B, L, 2H] view: dr | di, row stride drg_rs), dxc (the gate
@@ -123,7 +133,7 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
                      const float* dy,
                      float* drg, int64_t drg_rs, float* dxc, int64_t dxc_rs,
                      float* dz, int64_t dz_rs, float* part, float* dh0_part,
-                     int64_t B, int64_t L, int64_t H, void* stream);
+                     int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream);
 
 /* The state the power-of-two left padding leaves in the recurrence
  * (RecBLR.py:176-179: F.pad of x by P zero steps before conv + scan), without
@@ -301,20 +311,20 @@ int rb_scan_bwd_bf16(const rb_bf16* gates, const rb_bf16* states, const rb_bf16*
                      void* stream);
 int rb_conv_silu_fwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
                           rb_bf16* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
-                          void* stream);
+                          const int64_t* seq_offsets, void* stream);
 int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
                           const rb_bf16* g1, const rb_bf16* g2, rb_bf16* dx, int64_t dx_rs,
                           float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
-                          int64_t K, void* stream);
+                          int64_t K, const int64_t* seq_offsets, void* stream);
 int rb_gate_scan_fwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, int64_t xc_rs,
                           const rb_bf16* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* h0, int64_t h0_bs, rb_bf16* y, int64_t y_rs,
-                          float* carries, int64_t B, int64_t L, int64_t H, void* stream);
+                          float* carries, int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream);
 int rb_gate_scan_bwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, int64_t xc_rs,
                           const rb_bf16* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* carries, const rb_bf16* dy, rb_bf16* drg, int64_t drg_rs,
                           rb_bf16* dxc, int64_t dxc_rs, rb_bf16* dz, int64_t dz_rs, float* part,
-                          float* dh0_part, int64_t B, int64_t L, int64_t H, void* stream);
+                          float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream);
 
 /* ---- projection GEMMs (RecBLR.py:162,165,167,213,214: nn.Linear, fp32) ----
  * fp32 GEMMs on the bf16 MFMA pipe: every fp32 operand is split exactly into

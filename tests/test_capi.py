@@ -42,8 +42,8 @@ def test_argument_errors_are_reported_without_touching_the_gpu():
     rc = lib.rb_scan_fwd(None, None, None, 1, 1, 1, None)
     assert rc == _lib.RB_EINVAL
     assert b"null" in lib.rb_last_error_string()
-    rc = lib.rb_conv_silu_fwd(1, 4, 1, 1, 1, 4, 1, 1, 4, 9, None)
+    rc = lib.rb_conv_silu_fwd(1, 4, 1, 1, 1, 4, 1, 1, 4, 9, None, None)
     assert rc == _lib.RB_EINVAL
     assert b"K must be" in lib.rb_last_error_string()
-    rc = lib.rb_gate_scan_fwd(1, 3, 1, 4, 1, 4, 1, 0, 0, 0, 1, 4, 1, 1, 1, 4, None)
+    rc = lib.rb_gate_scan_fwd(1, 3, 1, 4, 1, 4, 1, 0, 0, 0, 1, 4, 1, 1, 1, 4, None, None)
     assert rc == _lib.RB_EINVAL   # rg row stride < 2H

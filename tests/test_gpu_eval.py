@@ -141,3 +141,63 @@ def test_gathered_last_layer_equals_full(cuda, flags):
     for n in g1:
         err = (g1[n].double() - g2[n].double()).norm() / max(g2[n].double().norm().item(), 1e-12)
         assert err < 1e-5, (n, err.item())
+
+
+@pytest.mark.parametrize("flags", [{}, {"disable_ffn": True}, {"disable_conv1d": True},
+                                   {"num_layers": 1}])
+@pytest.mark.parametrize("gather", [True, False])
+def test_packed_sequences_equal_dense(cuda, flags, gather):
+    """Running each sequence's first item_seq_len positions packed back to
+    back (RecBLR._forward_packed) gives the dense [B, L] batch's loss and every
+    gradient: the dropped right-padding positions never reach the output
+    (causal encoder, gather_indexes at len - 1).  Dropout off."""
+    from datamining_recblr_amd.distributed import synthetic_interaction
+
+    model = _model(cuda, n_items=600, **flags)
+    model.gather_last_layer = gather
+    inter = synthetic_interaction(96, 50, 600, cuda, seed=21)
+    res = []
+    for packed in (True, False):
+        model.pack_sequences = packed
+        model.zero_grad(set_to_none=True)
+        loss = model.calculate_loss(inter)
+        loss.backward()
+        res.append((loss.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                                    if p.grad is not None}))
+    (l1, g1), (l2, g2) = res
+    assert abs(l1.item() - l2.item()) < 1e-5
+    assert g1.keys() == g2.keys()
+    for n in g1:
+        err = (g1[n].double() - g2[n].double()).norm() / max(g2[n].double().norm().item(), 1e-12)
+        assert err < 1e-5, (n, err.item())
+
+
+def test_packed_full_size_and_eval_paths(cuda):
+    """C2 shape (B = 2048, L = 200, d = 128): packed vs dense loss/gradients,
+    and forward(exact_lengths=True) / full_sort_predict in eval mode."""
+    from datamining_recblr_amd.distributed import synthetic_interaction
+
+    model = _model(cuda, n_items=2000, hidden_size=128, MAX_ITEM_LIST_LENGTH=200)
+    inter = synthetic_interaction(2048, 200, 2000, cuda, seed=5)
+    res = []
+    for packed in (True, False):
+        model.pack_sequences = packed
+        model.zero_grad(set_to_none=True)
+        loss = model.calculate_loss(inter)
+        loss.backward()
+        res.append((loss.item(), {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                                  if p.grad is not None}))
+    assert abs(res[0][0] - res[1][0]) < 1e-5
+    for n in res[0][1]:
+        a, b = res[0][1][n].double(), res[1][1][n].double()
+        assert (a - b).norm() / max(b.norm().item(), 1e-12) < 1e-5, n
+    model.eval()
+    seq, lens = inter["item_id_list"][:64], inter["item_length"][:64]
+    with torch.no_grad():
+        outs = []
+        for packed in (True, False):
+            model.pack_sequences = packed
+            outs.append((model(seq, lens, exact_lengths=True),
+                         model.full_sort_predict({"item_id_list": seq, "item_length": lens})))
+    assert (outs[0][0] - outs[1][0]).abs().max().item() < 1e-5
+    assert (outs[0][1] - outs[1][1]).abs().max().item() < 1e-4

@@ -77,7 +77,7 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
     cs.push_back({f, 5 * N * es, [=] {
       hipLaunchKernelGGL((k_gate_scan_fwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
                          A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr,
-                         nullptr, 0, A(g.y), H, g.car, (int64_t)B, L, H, ncw);
+                         nullptr, 0, A(g.y), H, g.car, (int64_t)B, L, H, ncw, nullptr);
     }, {}});
   }
   if (which & 2) {
@@ -87,7 +87,7 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
       hipLaunchKernelGGL((k_gate_scan_bwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
                          A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr, g.car,
                          A(g.dy), A(g.drg), g.drg_rs, A(g.dxc), g.dxc_rs, A(g.dz), g.dz_rs, g.part,
-                         g.dh0, (int64_t)B, L, H, ncw);
+                         g.dh0, (int64_t)B, L, H, ncw, nullptr);
     }, {}});
   }
 }
@@ -107,7 +107,7 @@ void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float*
     cs.push_back({f, 2 * N * es, [=] {
       const int64_t blocks = ((int64_t)B * ncw * ntile + 3) / 4;
       hipLaunchKernelGGL((k_conv_silu_fwd<T, K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0,
-                         A(x), 2 * H, w, bias, A(xc), H, (int64_t)B, L, H, ncw, ntile);
+                         A(x), 2 * H, w, bias, A(xc), H, (int64_t)B, L, H, ncw, ntile, nullptr);
     }, {}});
   }
   if (which & 2) {
@@ -117,7 +117,7 @@ void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float*
       const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
       hipLaunchKernelGGL((k_conv_silu_bwd<T, K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0,
                          A(x), 2 * H, w, bias, A(g1), (const T*)nullptr, A(dx), 2 * H, dwp, dbp,
-                         (int64_t)B, L, H, ncw);
+                         (int64_t)B, L, H, ncw, nullptr);
     }, {}});
   }
 }
