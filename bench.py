@@ -258,11 +258,12 @@ def main():
     if not torch.isfinite(loss):
         raise RuntimeError(f"non-finite loss {loss}")
 
-    # Same step with the last layer's position-wise tail at every position (as
-    # the reference computes it; results identical) for comparison.
-    full_tail = None
-    if not args.no_full_tail:
-        model.gather_last_layer = False
+    # The same step in the reference's shapes, for comparison (results identical,
+    # tests/test_gpu_eval.py): the dense [B, L] batch with the gathered tail,
+    # and the dense batch with the last layer's tail at every position (the
+    # reference's arithmetic position for position).
+    def timed_variant(packed, gather):
+        model.pack_sequences, model.gather_last_layer = packed, gather
         for i in range(2):
             step(i)
         torch.cuda.synchronize()
@@ -275,12 +276,18 @@ def main():
         barrier(env)
         torch.cuda.synchronize()
         el = max_over_ranks(time.perf_counter() - t1, env, dev)
-        model.gather_last_layer = True
-        full_tail = {"value": round(env.world_size * args.batch * args.steps / el, 1),
-                     "ms_per_step": round(1000.0 * el / args.steps, 3),
-                     "note": "last layer's out-proj/LN/FFN at all B*L positions (the "
-                             "reference's arithmetic); loss and gradients identical to "
-                             "the gathered run (tests/test_gpu_eval.py)"}
+        model.pack_sequences, model.gather_last_layer = True, True
+        return {"value": round(env.world_size * args.batch * args.steps / el, 1),
+                "ms_per_step": round(1000.0 * el / args.steps, 3)}
+
+    dense = full_tail = None
+    if not args.no_full_tail:
+        dense = timed_variant(False, True)
+        dense["note"] = ("dense [B, L] batch (right padding computed, RECBLR_PACKED=0), "
+                         "last layer's tail at the gathered positions")
+        full_tail = timed_variant(False, False)
+        full_tail["note"] = ("dense [B, L] batch and the last layer's out-proj/LN/FFN at all "
+                             "B*L positions: the reference's arithmetic")
 
     roofline = None
     kernels_report = None
@@ -360,6 +367,8 @@ def main():
             "data": "synthetic RecBole-shaped batches (ids ~U{1..n_items-1}, lengths ~U{1..L}, "
                     "right-padded), reference init (seed 2020), resident in HBM",
             "config": {"workload": "RecBLR train step: calculate_loss(CE)+backward+Adam",
+                       "sequences": "packed: each sequence's first item_seq_len positions "
+                                    "(right padding, which never reaches the output, dropped)",
                        "last_layer_tail": "gathered positions (gather_indexes rows only)",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * env.world_size,
                        "seq_len": args.seq_len, "hidden_size": args.hidden, "inner_H": H,
@@ -368,6 +377,7 @@ def main():
             "roofline": roofline,
             "gemm": gemm,
             "kernels": kernels_report,
+            "dense_batch": dense,
             "all_positions_tail": full_tail,
             "scan_fwd_only": scan,
             "long_seq_bf16": c5,

@@ -155,6 +155,14 @@ __device__ __forceinline__ void split8(f32x4 x0, f32x4 x1, bf16x8 (&a)[3]) {
   }
 }
 
+// the deferred epilogue's prefetched old outputs (accumulate mode only)
+template <bool ACC>
+struct OldVals {
+  f32x2 v[8];
+};
+template <>
+struct OldVals<false> {};
+
 template <bool BIAS, bool ACC>
 __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float* __restrict__ A, int64_t lda,
                                                     int64_t M, int R,
@@ -253,6 +261,25 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
   f32x16 pend[2][2];
   int pend_mt = -1, pend_ct = 0, pend_q = 4;
   bool stored_prev = false;  // step u-1 issued 8 stores after its DMAs
+  // ACC: the old output values of the next quarter, loaded one phase ahead
+  // (before the step's DMAs, so waiting for them never drains those)
+  OldVals<ACC> oldb;
+  auto load_old = [&]() {
+    if constexpr (ACC) {
+      f32x2 (&oldv)[8] = oldb.v;
+      const int m = pend_q & 1, n = pend_q >> 1;
+      const bool full = (int64_t)pend_mt * G_BM + G_BM <= M;
+      const bool odd = lane & 1;
+      const int col = pend_ct * G_BN + wn * 64 + n * 32 + (ccol & ~1);
+      const int64_t rbase = (int64_t)pend_mt * G_BM + wm * 64 + m * 32 + 4 * (lane >> 5);
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const int64_t r = rbase + (e & 3) + 8 * (e >> 2) + (odd ? 1 : 0);
+        oldv[e >> 1] = (full || r < M) ? *reinterpret_cast<const f32x2*>(out + r * ldo + col)
+                                       : f32x2{0.0f, 0.0f};
+      }
+    }
+  };
   auto store_block = [&](const f32x16& blk, int m, int n) {
     const bool full = (int64_t)pend_mt * G_BM + G_BM <= M;
     const bool odd = lane & 1;
@@ -275,9 +302,9 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
 #endif
         f32x2* o = reinterpret_cast<f32x2*>(out + r * ldo + col);
         if (BIAS) { v0 += b0; v1 += b1; }
-        if (ACC) {
-          const f32x2 old = *o;
-          v0 += old[0]; v1 += old[1];
+        if constexpr (ACC) {
+          v0 += oldb.v[e >> 1][0];
+          v1 += oldb.v[e >> 1][1];
         }
         __builtin_nontemporal_store(f32x2{v0, v1}, o);
       }
@@ -352,6 +379,7 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
 #endif
           }
     };
+    if (pend_mt >= 0 && pend_q < 4) load_old();
     substep(0);
 #ifndef GS_NO_DMA
     if (u + 1 < U) issueB(u + 1);
@@ -371,7 +399,10 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
       tile_of(i, mt, ct);
       // tiles shorter than 4 steps: finish the previous tile first (extra
       // stores only make the next vmcnt waits stricter)
-      while (pend_mt >= 0 && pend_q < 4) store_quarter();
+      while (pend_mt >= 0 && pend_q < 4) {
+        load_old();
+        store_quarter();
+      }
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -389,7 +420,10 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
       ++kt;
     }
   }
-  while (pend_mt >= 0 && pend_q < 4) store_quarter();
+  while (pend_mt >= 0 && pend_q < 4) {
+    load_old();
+    store_quarter();
+  }
 }
 
 template <bool BIAS, bool ACC>
