@@ -205,11 +205,20 @@ class SequentialLoader:
         return n // self.batch_size if self.drop_last else -(-n // self.batch_size)
 
     def __iter__(self):
-        idx = self._indices().to(self.desc.device)
+        from .model import attach_host_lengths
+        idx_h = self._indices()
+        idx = idx_h.to(self.desc.device)
+        desc_h = self.desc.cpu()
         nb = len(self)
         for b in range(nb):
             sel = idx[b * self.batch_size:(b + 1) * self.batch_size]
-            yield build_batch(self.data, self.desc[sel])
+            batch = build_batch(self.data, self.desc[sel])
+            # the same lengths on the host: the packed forward sizes its buffers
+            # from them without a device sync
+            dh = desc_h[idx_h[b * self.batch_size:(b + 1) * self.batch_size]]
+            attach_host_lengths(batch["item_length"],
+                                torch.clamp(dh[:, 1] - dh[:, 0], max=self.data.max_len))
+            yield batch
 
 
 def from_atomic_file(path: str, max_len: int = 200, min_user: int = 5,

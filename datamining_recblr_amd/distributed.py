@@ -86,7 +86,10 @@ def synthetic_interaction(batch: int, seq_len: int, n_items: int, device, seed: 
              "item_id": torch.randint(1, n_items, (batch,), generator=g)}
     if with_neg:
         inter["neg_item_id"] = torch.randint(1, n_items, (batch,), generator=g)
-    return {k: v.to(device) for k, v in inter.items()}
+    out = {k: v.to(device) for k, v in inter.items()}
+    from .model import attach_host_lengths
+    attach_host_lengths(out["item_length"], lengths)
+    return out
 
 
 def shard_range(global_batch: int, rank: int, world: int):

@@ -26,7 +26,8 @@ class KernelTimer:
     """HIP-event timing of every C-ABI launch, recorded on the stream the
     kernel is launched on (torch's current stream).  Used by bench.py."""
 
-    def __init__(self):
+    def __init__(self, only=None):
+        self.only = None if only is None else frozenset(only)   # names to time (None: all)
         self.records = []   # (name, algorithmic bytes, start event, end event)
         self.detail = []    # GEMMs by shape: (label, flops, start event, end event)
 
@@ -61,9 +62,11 @@ _timer: KernelTimer | None = None
 
 
 @contextlib.contextmanager
-def kernel_timing():
+def kernel_timing(only=None):
+    """Time C-ABI launches with HIP events; `only`: the entry point names to
+    time (the rest run untimed, so the timer barely perturbs the step)."""
     global _timer
-    prev, _timer = _timer, KernelTimer()
+    prev, _timer = _timer, KernelTimer(only)
     try:
         yield _timer
     finally:
@@ -73,7 +76,7 @@ def kernel_timing():
 def _launch(name: str, nbytes: int, *args, _fn: str | None = None) -> None:
     """Call C-ABI entry point `_fn or name`; timed under `name` in bench runs."""
     t = _timer
-    if t is None:
+    if t is None or (t.only is not None and name not in t.only):
         _lib.call(_fn or name, *args)
         return
     e0 = torch.cuda.Event(enable_timing=True)

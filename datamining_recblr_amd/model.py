@@ -144,6 +144,17 @@ class RecurrentLayer(nn.Module):
         return h if self.disable_ffn else self.ffn(h)
 
 
+# Attribute a data path may set on the item_seq_len device tensor: the same
+# lengths as a CPU tensor, so the packed forward needs no device sync to size
+# its buffers (distributed.synthetic_interaction, data.SequentialLoader).
+HOST_LENGTHS = "_recblr_host_lengths"
+
+
+def attach_host_lengths(lengths_dev: torch.Tensor, lengths_cpu: torch.Tensor) -> torch.Tensor:
+    setattr(lengths_dev, HOST_LENGTHS, lengths_cpu.detach().to("cpu"))
+    return lengths_dev
+
+
 class RecBLR(SequentialRecommender):
     """RecBole sequential recommender with the BD-LRU encoder (RecBLR.py:18-122)."""
 
@@ -235,10 +246,22 @@ class RecBLR(SequentialRecommender):
         B, L = item_seq.shape
         dev = item_seq.device
         lens = item_seq_len.to(torch.int64).clamp(1, L)
-        offsets = torch.zeros(B + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(lens, 0, out=offsets[1:])
-        flat = (torch.arange(L, device=dev) < lens[:, None]).reshape(-1).nonzero().squeeze(1)
-        seq = Packed(offsets, L, flat.numel())
+        host = getattr(item_seq_len, HOST_LENGTHS, None)
+        if host is not None and host.shape == item_seq_len.shape:
+            # lengths known on the host (the data path attaches them): no device sync
+            lens_h = host.to(torch.int64).clamp(1, L)
+            offs_h = torch.zeros(B + 1, dtype=torch.int64)
+            torch.cumsum(lens_h, 0, out=offs_h[1:])
+            ntok = int(offs_h[-1])
+            offsets = offs_h.pin_memory().to(dev, non_blocking=True)
+        else:
+            offsets = torch.zeros(B + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(lens, 0, out=offsets[1:])
+            ntok = int(offsets[-1])   # one device sync
+        # flat [B*L] position of every packed token
+        seq_of = torch.repeat_interleave(torch.arange(B, device=dev), lens, output_size=ntok)
+        flat = seq_of * L + (torch.arange(ntok, device=dev) - offsets[seq_of])
+        seq = Packed(offsets, L, ntok)
         h = embed_dropout_layer_norm(item_seq.reshape(-1).index_select(0, flat),
                                      self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
