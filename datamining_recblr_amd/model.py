@@ -246,26 +246,37 @@ class RecBLR(SequentialRecommender):
         B, L = item_seq.shape
         dev = item_seq.device
         lens = item_seq_len.to(torch.int64).clamp(1, L)
+        # sequences are packed longest first: the recurrence kernels give one
+        # wave per sequence, so the short ones fill in behind the long ones
         host = getattr(item_seq_len, HOST_LENGTHS, None)
         if host is not None and host.shape == item_seq_len.shape:
             # lengths known on the host (the data path attaches them): no device sync
             lens_h = host.to(torch.int64).clamp(1, L)
+            order_h = torch.argsort(lens_h, descending=True, stable=True)
             offs_h = torch.zeros(B + 1, dtype=torch.int64)
-            torch.cumsum(lens_h, 0, out=offs_h[1:])
+            torch.cumsum(lens_h[order_h], 0, out=offs_h[1:])
             ntok = int(offs_h[-1])
-            offsets = offs_h.pin_memory().to(dev, non_blocking=True)
+            both = torch.cat([offs_h, order_h]).pin_memory().to(dev, non_blocking=True)
+            offsets, order = both[:B + 1], both[B + 1:]
         else:
+            order = torch.argsort(lens, descending=True, stable=True)
             offsets = torch.zeros(B + 1, dtype=torch.int64, device=dev)
-            torch.cumsum(lens, 0, out=offsets[1:])
+            torch.cumsum(lens.index_select(0, order), 0, out=offsets[1:])
             ntok = int(offsets[-1])   # one device sync
-        # flat [B*L] position of every packed token
-        seq_of = torch.repeat_interleave(torch.arange(B, device=dev), lens, output_size=ntok)
-        flat = seq_of * L + (torch.arange(ntok, device=dev) - offsets[seq_of])
+        # token -> packed sequence -> batch row; flat [B*L] position of each token
+        seq_of = torch.repeat_interleave(torch.arange(B, device=dev), lens.index_select(0, order),
+                                         output_size=ntok)
+        flat = (order.index_select(0, seq_of) * L
+                + (torch.arange(ntok, device=dev) - offsets.index_select(0, seq_of)))
+        inv = torch.empty_like(order)
+        inv.scatter_(0, order, torch.arange(B, device=dev))
         seq = Packed(offsets, L, ntok)
+        if pad is not None:
+            pad = pad.index_select(0, order)
         h = embed_dropout_layer_norm(item_seq.reshape(-1).index_select(0, flat),
                                      self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
-        last = offsets[1:] - 1
+        last = offsets.index_select(0, inv + 1) - 1   # each batch row's last token
         n = len(self.recurrent_layers)
         for i, layer in enumerate(self.recurrent_layers):
             if i == n - 1 and self.gather_last_layer:
