@@ -120,11 +120,17 @@ def load(path: str | None = None) -> ctypes.CDLL:
         return lib
 
 
+_fns = {}
+
+
 def call(name: str, *args) -> None:
     """Invoke a C-ABI entry point and raise on a non-zero status."""
-    lib = load()
-    rc = getattr(lib, name)(*args)
+    fn = _fns.get(name)
+    if fn is None:
+        fn = _fns[name] = getattr(load(), name)
+    rc = fn(*args)
     if rc != 0:
+        lib = load()
         msg = lib.rb_last_error_string()
         msg = msg.decode() if msg else ""
         kind = "invalid argument" if rc == RB_EINVAL else f"hipError {rc}"

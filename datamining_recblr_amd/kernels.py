@@ -102,8 +102,21 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     out = torch.empty((M, C), device=x.device, dtype=torch.float32)
     if P == 0:
         return out.zero_()[0] if squeeze else out.zero_()
-    _lib.call("rb_colsum", x3.data_ptr(), M, P, C, x3.stride(1), x3.stride(0) if M > 1 else P * C,
-              out.data_ptr(), _stream(x))
+    rs, ms = x3.stride(1), (x3.stride(0) if M > 1 else P * x3.stride(1))
+    # Few columns, many rows (per-sequence partials [B, H]): one launch would
+    # have a handful of workgroups each walking thousands of rows.  Sum
+    # 64-row chunks first (many workgroups), then the chunk sums — two
+    # fixed-order passes, still deterministic.
+    CH = 64
+    if M * ((C + 63) // 64) < 64 and P >= 4 * CH and P % CH == 0 and ms == P * rs:
+        nch = P // CH
+        part = torch.empty((M * nch, C), device=x.device, dtype=torch.float32)
+        _lib.call("rb_colsum", x3.data_ptr(), M * nch, CH, C, rs, CH * rs, part.data_ptr(),
+                  _stream(x))
+        _lib.call("rb_colsum", part.data_ptr(), M, nch, C, C, nch * C, out.data_ptr(),
+                  _stream(x))
+        return out[0] if squeeze else out
+    _lib.call("rb_colsum", x3.data_ptr(), M, P, C, rs, ms, out.data_ptr(), _stream(x))
     return out[0] if squeeze else out
 
 
@@ -111,7 +124,14 @@ def num_tiles(L: int) -> int:
     return (L + RB_TILE - 1) // RB_TILE
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(t: torch.Tensor) -> int:
+    """hipStream_t (as int) of torch's current stream on t's device."""
+    if _raw_stream is not None:
+        return _raw_stream(t.device.index if t.device.index is not None
+                           else torch.cuda.current_device())
     return torch.cuda.current_stream(t.device).cuda_stream
 
 

@@ -263,7 +263,8 @@ def test_pad_prefix_kernels_match_torch(cuda, H, pads):
         assert err < 2e-5, (n, err.item())
 
 
-@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 131072), (1024, 128), (300, 65), (3, 2048, 256)])
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 131072), (1024, 128), (300, 65),
+                                   (3, 2048, 256), (2048, 1024), (2048, 256), (2000, 256)])
 def test_colsum_fixed_order(cuda, shape):
     from datamining_recblr_amd import kernels
 
@@ -275,16 +276,26 @@ def test_colsum_fixed_order(cuda, shape):
     close(out, ref, atol=1e-5, rtol=1e-5, what="colsum")
     assert torch.equal(out, kernels.colsum(x))
     # restated order: RG interleaved partials in increasing p, combined in order
-    P = shape[-2]
-    RG = 4 if P <= 256 else 16
-    xs = x.reshape(-1, P, shape[-1]).cpu()
-    exp = torch.zeros(xs.shape[0], shape[-1])
-    parts = [torch.zeros(xs.shape[0], shape[-1]) for _ in range(RG)]
-    for p in range(P):
-        parts[p % RG] = parts[p % RG] + xs[:, p]
-    exp = parts[0]
-    for q in parts[1:]:
-        exp = exp + q
+    # (RG = 4 for P <= 256, else 16); few columns with many rows: 64-row
+    # chunk sums first, then the chunk sums (kernels.colsum)
+    def one_pass(xs):
+        P = xs.shape[1]
+        RG = 4 if P <= 256 else 16
+        parts = [torch.zeros(xs.shape[0], xs.shape[2]) for _ in range(RG)]
+        for p in range(P):
+            parts[p % RG] = parts[p % RG] + xs[:, p]
+        exp = parts[0]
+        for q in parts[1:]:
+            exp = exp + q
+        return exp
+
+    P, C = shape[-2], shape[-1]
+    xs = x.reshape(-1, P, C).cpu()
+    M = xs.shape[0]
+    if M * ((C + 63) // 64) < 64 and P >= 256 and P % 64 == 0:
+        exp = one_pass(one_pass(xs.reshape(M * (P // 64), 64, C)).reshape(M, P // 64, C))
+    else:
+        exp = one_pass(xs)
     assert torch.equal(out.cpu().reshape(exp.shape), exp)
 
 
