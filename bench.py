@@ -198,6 +198,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-seconds", type=float, default=15.0,
+                    help="after the warmup, keep running untimed steps for about this long "
+                         "so the device clocks reach their sustained state (0: off); a fresh "
+                         "box runs the GEMMs ~15%% slower for its first seconds under load")
     ap.add_argument("--batch", type=int, default=2048, help="sequences per GPU")
     ap.add_argument("--seq-len", type=int, default=200)
     ap.add_argument("--hidden", type=int, default=128)
@@ -238,6 +242,19 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    # settle: untimed steps, sized from three timed ones (the same count on every rank)
+    settle_steps = 0
+    if args.settle_seconds > 0:
+        t1 = time.perf_counter()
+        for i in range(3):
+            step(i)
+        torch.cuda.synchronize()
+        per = max_over_ranks((time.perf_counter() - t1) / 3, env, dev)
+        settle_steps = int(args.settle_seconds / max(per, 1e-4))
+        for i in range(settle_steps):
+            step(i)
+        settle_steps += 3
+        torch.cuda.synchronize()
     barrier(env)
     torch.cuda.synchronize()
 
@@ -377,6 +394,7 @@ def main():
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "sequences/sec",
             "n_gpus": env.world_size, "steps": args.steps, "warmup": args.warmup,
+            "settle": {"seconds": args.settle_seconds, "steps": settle_steps},
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic RecBole-shaped batches (ids ~U{1..n_items-1}, lengths ~U{1..L}, "

@@ -12,7 +12,9 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libdmrecblr.so")
+# RECBLR_LIB points at an alternative build of the same sources (A/B timing
+# of compile-time variants, e.g. tools/ab_build.sh); the default is the in-tree build
+LIB_PATH = os.environ.get("RECBLR_LIB") or os.path.join(_HERE, "lib", "libdmrecblr.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1

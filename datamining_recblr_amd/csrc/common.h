@@ -52,31 +52,67 @@ __device__ __forceinline__ float fdsilu(float x) {
 }
 
 // ---- VEC-wide loads/stores (VEC = 4 -> one 16-B access per lane) -------------
-template <int V>
-__device__ __forceinline__ void ldv(float (&o)[V], const float* p) {
+// Every [B, L, H] stream is read or written once per kernel, so the accesses
+// carry the nontemporal hint (global_load/store ... nt): on this chip a plain
+// 1R+1W float4 copy runs at 0.76 of 8 TB/s with default-policy accesses and
+// 0.83 with nt ones (tools/copyprobe2.hip, profiles/r01_copyprobe2.log).
+#ifndef RB_STREAM_NT
+#define RB_STREAM_NT 1
+#endif
+typedef float rb_f32x4 __attribute__((ext_vector_type(4)));
+typedef float rb_f32x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t rb_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t rb_u32x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_pol(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_pol(T v, T* p) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+constexpr bool kNT = RB_STREAM_NT != 0;
+
+// ldv / stv: once-touched activation streams (nt); ldc / stc: default policy,
+// for small operands many workgroups re-read (parameters, carries) and for
+// inputs that neighbouring tiles re-read (the conv's halo rows).
+template <bool NT, int V>
+__device__ __forceinline__ void ld_f32(float (&o)[V], const float* p) {
   if constexpr (V == 4) {
-    const float4 t = *reinterpret_cast<const float4*>(p);
-    o[0] = t.x; o[1] = t.y; o[2] = t.z; o[3] = t.w;
+    const rb_f32x4 t = ld_pol<NT>(reinterpret_cast<const rb_f32x4*>(p));
+    o[0] = t[0]; o[1] = t[1]; o[2] = t[2]; o[3] = t[3];
   } else if constexpr (V == 2) {
-    const float2 t = *reinterpret_cast<const float2*>(p);
-    o[0] = t.x; o[1] = t.y;
+    const rb_f32x2v t = ld_pol<NT>(reinterpret_cast<const rb_f32x2v*>(p));
+    o[0] = t[0]; o[1] = t[1];
   } else {
 #pragma unroll
-    for (int v = 0; v < V; ++v) o[v] = p[v];
+    for (int v = 0; v < V; ++v) o[v] = ld_pol<NT>(p + v);
+  }
+}
+
+template <bool NT, int V>
+__device__ __forceinline__ void st_f32(float* p, const float (&o)[V]) {
+  if constexpr (V == 4) {
+    st_pol<NT>(rb_f32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<rb_f32x4*>(p));
+  } else if constexpr (V == 2) {
+    st_pol<NT>(rb_f32x2v{o[0], o[1]}, reinterpret_cast<rb_f32x2v*>(p));
+  } else {
+#pragma unroll
+    for (int v = 0; v < V; ++v) st_pol<NT>(o[v], p + v);
   }
 }
 
 template <int V>
-__device__ __forceinline__ void stv(float* p, const float (&o)[V]) {
-  if constexpr (V == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(o[0], o[1], o[2], o[3]);
-  } else if constexpr (V == 2) {
-    *reinterpret_cast<float2*>(p) = make_float2(o[0], o[1]);
-  } else {
-#pragma unroll
-    for (int v = 0; v < V; ++v) p[v] = o[v];
-  }
-}
+__device__ __forceinline__ void ldv(float (&o)[V], const float* p) { ld_f32<kNT>(o, p); }
+template <int V>
+__device__ __forceinline__ void stv(float* p, const float (&o)[V]) { st_f32<kNT>(p, o); }
+template <int V>
+__device__ __forceinline__ void ldc(float (&o)[V], const float* p) { ld_f32<false>(o, p); }
+template <int V>
+__device__ __forceinline__ void stc(float* p, const float (&o)[V]) { st_f32<false>(p, o); }
 
 // ---- bf16 storage (fp32 arithmetic): VEC bf16 per lane, RNE on store ---------
 typedef __bf16 bf16_t;
@@ -91,37 +127,46 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return __builtin_bit_cast(uint32_t, __builtin_convertvector(rb_f32x2{a, b}, rb_bf16x2));
 }
 
-template <int V>
-__device__ __forceinline__ void ldv(float (&o)[V], const bf16_t* p) {
+template <bool NT, int V>
+__device__ __forceinline__ void ld_b16(float (&o)[V], const bf16_t* p) {
   if constexpr (V == 8) {
-    const uint4 t = *reinterpret_cast<const uint4*>(p);
-    unpack2(t.x, o[0], o[1]); unpack2(t.y, o[2], o[3]);
-    unpack2(t.z, o[4], o[5]); unpack2(t.w, o[6], o[7]);
+    const rb_u32x4 t = ld_pol<NT>(reinterpret_cast<const rb_u32x4*>(p));
+    unpack2(t[0], o[0], o[1]); unpack2(t[1], o[2], o[3]);
+    unpack2(t[2], o[4], o[5]); unpack2(t[3], o[6], o[7]);
   } else if constexpr (V == 4) {
-    const uint2 t = *reinterpret_cast<const uint2*>(p);
-    unpack2(t.x, o[0], o[1]); unpack2(t.y, o[2], o[3]);
+    const rb_u32x2 t = ld_pol<NT>(reinterpret_cast<const rb_u32x2*>(p));
+    unpack2(t[0], o[0], o[1]); unpack2(t[1], o[2], o[3]);
   } else if constexpr (V == 2) {
-    unpack2(*reinterpret_cast<const uint32_t*>(p), o[0], o[1]);
+    unpack2(ld_pol<NT>(reinterpret_cast<const uint32_t*>(p)), o[0], o[1]);
   } else {
 #pragma unroll
     for (int v = 0; v < V; ++v) o[v] = (float)p[v];
   }
 }
 
-template <int V>
-__device__ __forceinline__ void stv(bf16_t* p, const float (&o)[V]) {
+template <bool NT, int V>
+__device__ __forceinline__ void st_b16(bf16_t* p, const float (&o)[V]) {
   if constexpr (V == 8) {
-    *reinterpret_cast<uint4*>(p) = make_uint4(pack2(o[0], o[1]), pack2(o[2], o[3]),
-                                              pack2(o[4], o[5]), pack2(o[6], o[7]));
+    st_pol<NT>(rb_u32x4{pack2(o[0], o[1]), pack2(o[2], o[3]), pack2(o[4], o[5]), pack2(o[6], o[7])},
+               reinterpret_cast<rb_u32x4*>(p));
   } else if constexpr (V == 4) {
-    *reinterpret_cast<uint2*>(p) = make_uint2(pack2(o[0], o[1]), pack2(o[2], o[3]));
+    st_pol<NT>(rb_u32x2{pack2(o[0], o[1]), pack2(o[2], o[3])}, reinterpret_cast<rb_u32x2*>(p));
   } else if constexpr (V == 2) {
-    *reinterpret_cast<uint32_t*>(p) = pack2(o[0], o[1]);
+    st_pol<NT>(pack2(o[0], o[1]), reinterpret_cast<uint32_t*>(p));
   } else {
 #pragma unroll
     for (int v = 0; v < V; ++v) p[v] = (bf16_t)o[v];
   }
 }
+
+template <int V>
+__device__ __forceinline__ void ldv(float (&o)[V], const bf16_t* p) { ld_b16<kNT>(o, p); }
+template <int V>
+__device__ __forceinline__ void stv(bf16_t* p, const float (&o)[V]) { st_b16<kNT>(p, o); }
+template <int V>
+__device__ __forceinline__ void ldc(float (&o)[V], const bf16_t* p) { ld_b16<false>(o, p); }
+template <int V>
+__device__ __forceinline__ void stc(bf16_t* p, const float (&o)[V]) { st_b16<false>(p, o); }
 
 // ---- dropout keep-flags ------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11): counter = element index / 4, key =

@@ -6,6 +6,17 @@
 // and one wave-instruction touches Q contiguous 256-B row segments.
 #include "common.h"
 
+// the input rows are re-read by the neighbouring time tile (K-1 halo rows), so
+// they keep the default cache policy unless RB_CONV_X_NT is set
+#ifndef RB_CONV_X_NT
+#define RB_CONV_X_NT 0
+#endif
+#if RB_CONV_X_NT
+#define RB_CONV_LDX ldv
+#else
+#define RB_CONV_LDX ldc
+#endif
+
 namespace rb {
 namespace {
 
@@ -48,14 +59,14 @@ k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
 #pragma unroll
     for (int k = 0; k < K; ++k) wk[k][v] = w[(cc + v) * K + k];
   }
-  ldv(bi, bias + cc);
+  ldc(bi, bias + cc);
   const int t0 = tile * (Q * TC) + q * TC;
   float xs[NX][VEC];   // x[t0-K+1 .. t0+TC-1]
 #pragma unroll
   for (int m = 0; m < NX; ++m) {
     const int t = t0 - (K - 1) + m;
     const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
-    ldv(xs[m], xb + tc * x_rs);
+    RB_CONV_LDX(xs[m], xb + tc * x_rs);
     if (t < 0) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) xs[m][v] = 0.0f;
@@ -121,7 +132,7 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
 #pragma unroll
     for (int k = 0; k < K; ++k) wk[k][v] = w[(cc + v) * K + k];
   }
-  ldv(bi, bias + cc);
+  ldc(bi, bias + cc);
   float accw[K][VEC], accb[VEC], halo[KH][VEC];
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -140,7 +151,7 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
     for (int m = 0; m < NX; ++m) {
       const int t = t0 - (K - 1) + m;
       const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
-      ldv(xs[m], xb + tc * x_rs);
+      RB_CONV_LDX(xs[m], xb + tc * x_rs);
       if (t < 0) {
 #pragma unroll
         for (int v = 0; v < VEC; ++v) xs[m][v] = 0.0f;

@@ -70,18 +70,18 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   T* yb = y + row0 * y_rs + cc;
 
   float nsp[VEC], carry[VEC], br[VEC], bi[VEC];
-  ldv(nsp, lam + cc);
+  ldc(nsp, lam + cc);
 #pragma unroll
   for (int v = 0; v < VEC; ++v) nsp[v] = -softplus_f(nsp[v]);
   if (gbias != nullptr) {   // the gates GEMM's bias, added here instead of in its epilogue
-    ldv(br, gbias + cc);
-    ldv(bi, gbias + H + cc);
+    ldc(br, gbias + cc);
+    ldc(bi, gbias + H + cc);
   } else {
 #pragma unroll
     for (int v = 0; v < VEC; ++v) br[v] = bi[v] = 0.0f;
   }
   if (h0 != nullptr) {
-    ldv(carry, h0 + b * h0_bs + cc);
+    ldc(carry, h0 + b * h0_bs + cc);
   } else {
 #pragma unroll
     for (int v = 0; v < VEC; ++v) carry[v] = 0.0f;
@@ -175,6 +175,55 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   }
 }
 
+// Cross-chunk scans of the backward: the Q time chunks of a channel group sit
+// on Q consecutive lanes, so "value of chunk q-k / q+k" is a DPP row shift
+// (VALU, no LDS round trip as with ds_bpermute) and "chunk 0's value" a
+// ds_swizzle broadcast.  Lanes whose source crosses a group edge get a wrong
+// value that the callers never use (they mask with q >= k / q + k < Q).
+template <int K>
+__device__ __forceinline__ float dpp_from_lower(float x) {   // lane i - K, K in 1..8
+  static_assert(K >= 1 && K <= 8, "row shift within a 16-lane DPP row");
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
+                                                    0x110 + K, 0xF, 0xF, false));
+}
+template <int K>
+__device__ __forceinline__ float dpp_from_upper(float x) {   // lane i + K
+  static_assert(K >= 1 && K <= 8, "row shift within a 16-lane DPP row");
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
+                                                    0x100 + K, 0xF, 0xF, false));
+}
+template <int Q>
+__device__ __forceinline__ float group_first(float x) {      // lane i & ~(Q - 1)
+  static_assert(Q >= 2 && Q <= 32 && (Q & (Q - 1)) == 0, "power-of-two groups within 32 lanes");
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), 0x1F & ~(Q - 1)));
+}
+// inclusive scans of (A, X) pairs over the Q chunk lanes: from lower chunks
+// (X = X_lower * A + X, A = A_lower * A) and from upper chunks (reverse)
+template <int Q, int K = 1>
+__device__ __forceinline__ void scan_from_lower(float& A, float& X, int q) {
+  if constexpr (K < Q) {
+    const float Ap = dpp_from_lower<K>(A);
+    const float Xp = dpp_from_lower<K>(X);
+    if (q >= K) {
+      X = Xp * A + X;
+      A = Ap * A;
+    }
+    scan_from_lower<Q, 2 * K>(A, X, q);
+  }
+}
+template <int Q, int K = 1>
+__device__ __forceinline__ void scan_from_upper(float& A, float& E, int q) {
+  if constexpr (K < Q) {
+    const float An = dpp_from_upper<K>(A);
+    const float En = dpp_from_upper<K>(E);
+    if (q + K < Q) {
+      E = En * A + E;
+      A = An * A;
+    }
+    scan_from_upper<Q, 2 * K>(A, E, q);
+  }
+}
+
 template <typename T, int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, int xc_rs,
@@ -189,8 +238,8 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
   const int lane = threadIdx.x & (kWave - 1);
-  const int q = lane / G;
-  const int g = lane - q * G;
+  const int q = lane & (Q - 1);   // time chunk on the low lane bits (scans: DPP)
+  const int g = lane / Q;
   const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t b = wid / ncw;
   if (b >= B) return;
@@ -217,12 +266,12 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   T* dzb = dz + row0 * dz_rs + cc;
 
   float lamv[VEC], nsp[VEC], br[VEC], bi[VEC];
-  ldv(lamv, lam + cc);
+  ldc(lamv, lam + cc);
 #pragma unroll
   for (int v = 0; v < VEC; ++v) nsp[v] = -softplus_f(lamv[v]);
   if (gbias != nullptr) {
-    ldv(br, gbias + cc);
-    ldv(bi, gbias + H + cc);
+    ldc(br, gbias + cc);
+    ldc(bi, gbias + H + cc);
   } else {
 #pragma unroll
     for (int v = 0; v < VEC; ++v) br[v] = bi[v] = 0.0f;
@@ -246,7 +295,8 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
     }
   };
   auto process = [&](BwdIn<VEC, TC>& in, int tile) {
-    const int t0 = tile * TILE + q * TC;
+    float hcar[VEC];
+    ldc(hcar, carries + (b * nTc + tile) * H + cc);
 #pragma unroll
     for (int j = 0; j < TC; ++j)
 #pragma unroll
@@ -254,78 +304,65 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
         in.r[j][v] += br[v];
         in.i[j][v] += bi[v];
       }
-    float hcar[VEC];
-    ldv(hcar, carries + (b * nTc + tile) * H + cc);
-    float al[TC][VEC];
+    const int t0 = tile * TILE + q * TC;
+    // per-step derived values, each transcendental evaluated once
+    float al[TC][VEC], sr[TC][VEC], si[TC][VEC], sq[TC][VEC], bp[TC][VEC], gs[TC][VEC],
+        dsz[TC][VEC];
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
       const bool ok = t0 + j < L;
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
-        const float a = fexp(nsp[v] * fsigm(in.r[j][v]));
-        al[j][v] = ok ? a : 1.0f;
-        if (!ok) in.g[j][v] = 0.0f;   // dy past the end contributes nothing
+        sr[j][v] = fsigm(in.r[j][v]);
+        const float a = ok ? fexp(nsp[v] * sr[j][v]) : 1.0f;
+        al[j][v] = a;
+        si[j][v] = fsigm(in.i[j][v]);
+        sq[j][v] = fsqrt(1.0f - a * a + 1e-8f);
+        bp[j][v] = ok ? sq[j][v] * si[j][v] * in.x[j][v] : 0.0f;
+        const float zz = in.z[j][v];
+        const float sz = fsigm(zz);
+        const float g = ok ? in.g[j][v] : 0.0f;   // dy past the end contributes nothing
+        in.g[j][v] = g;
+        gs[j][v] = g * (zz * sz);
+        dsz[j][v] = sz * (1.0f + zz * (1.0f - sz));
       }
     }
     float cin[VEC], ein[VEC];
 #pragma unroll
     for (int v = 0; v < VEC; ++v) {
-      // chunk summaries: forward (A, X) and reverse (A, E)
       float A = 1.0f, X = 0.0f, E = 0.0f;
 #pragma unroll
       for (int j = 0; j < TC; ++j) {
-        const float a = al[j][v];
-        const float bpj = (t0 + j < L)
-            ? fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v]) * in.x[j][v] : 0.0f;
-        X = X * a + bpj;
-        A = A * a;
+        X = X * al[j][v] + bp[j][v];
+        A = A * al[j][v];
       }
 #pragma unroll
       for (int j = TC - 1; j >= 0; --j) {
-        const float d = E + in.g[j][v] * fsilu(in.z[j][v]);
+        const float d = E + gs[j][v];
         E = d * al[j][v];
       }
-      // forward scan over earlier chunks -> carry into this chunk
       float Af = A, Xf = X;
-#pragma unroll
-      for (int k = 1; k < Q; k <<= 1) {
-        const float Ap = __shfl_up(Af, k * G, kWave);
-        const float Xp = __shfl_up(Xf, k * G, kWave);
-        if (q >= k) {
-          Xf = Xp * Af + Xf;
-          Af = Ap * Af;
-        }
-      }
-      float Ae = __shfl_up(Af, G, kWave);
-      float Xe = __shfl_up(Xf, G, kWave);
+      scan_from_lower<Q>(Af, Xf, q);
+      float Ae = dpp_from_lower<1>(Af);
+      float Xe = dpp_from_lower<1>(Xf);
       if (q == 0) {
         Ae = 1.0f;
         Xe = 0.0f;
       }
       cin[v] = hcar[v] * Ae + Xe;
-      // reverse scan over later chunks -> adjoint flowing into this chunk
       float Ab = A, Eb = E;
-#pragma unroll
-      for (int k = 1; k < Q; k <<= 1) {
-        const float An = __shfl_down(Ab, k * G, kWave);
-        const float En = __shfl_down(Eb, k * G, kWave);
-        if (q + k < Q) {
-          Eb = En * Ab + Eb;
-          Ab = An * Ab;
-        }
-      }
-      float Ase = __shfl_down(Ab, G, kWave);
-      float Ese = __shfl_down(Eb, G, kWave);
+      scan_from_upper<Q>(Ab, Eb, q);
+      float Ase = dpp_from_upper<1>(Ab);
+      float Ese = dpp_from_upper<1>(Eb);
       if (q == Q - 1) {
         Ase = 1.0f;
         Ese = 0.0f;
       }
       ein[v] = ecarry[v] * Ase + Ese;
-      const float At = __shfl(Ab, g, kWave);
-      const float Et = __shfl(Eb, g, kWave);
+      const float At = group_first<Q>(Ab);
+      const float Et = group_first<Q>(Eb);
       ecarry[v] = ecarry[v] * At + Et;
     }
-    // recompute h (h_{t-1} for the scan gradient, h_t for dz)
     float hp[TC][VEC];
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
@@ -333,12 +370,9 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
       float dzo[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
-        const float a = al[j][v];
-        const float bpj =
-            ok ? fsqrt(1.0f - a * a + 1e-8f) * fsigm(in.i[j][v]) * in.x[j][v] : 0.0f;
         hp[j][v] = cin[v];
-        cin[v] = cin[v] * a + bpj;
-        dzo[v] = (in.g[j][v] * cin[v]) * fdsilu(in.z[j][v]);
+        cin[v] = cin[v] * al[j][v] + bp[j][v];
+        dzo[v] = (in.g[j][v] * cin[v]) * dsz[j][v];
       }
       if (cv && ok) stv(dzb + (t0 + j) * dz_rs, dzo);
     }
@@ -349,22 +383,17 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
 #pragma unroll
       for (int v = 0; v < VEC; ++v) {
         const float a = al[j][v];
-        const float d = ein[v] + in.g[j][v] * fsilu(in.z[j][v]);   // dL/dh_t
-        const float sr = fsigm(in.r[j][v]);
-        const float si = fsigm(in.i[j][v]);
-        const float sq = fsqrt(1.0f - a * a + 1e-8f);
+        const float d = ein[v] + gs[j][v];   // dL/dh_t
         const float dbeta = d * in.x[j][v];
-        const float du = (dbeta * si) * (0.5f * frcp(sq));
+        const float du = (dbeta * si[j][v]) * (0.5f * frcp(sq[j][v]));
         const float da = hp[j][v] * d + (-du) * (2.0f * a);
         const float dv = da * a;
-        dro[v] = (dv * nsp[v]) * ((1.0f - sr) * sr);
-        dio[v] = (dbeta * sq) * ((1.0f - si) * si);
-        dxo[v] = d * (sq * si);
-        if (ok) {
-          acc_v[v] = acc_v[v] + dv * sr;
-          acc_r[v] = acc_r[v] + dro[v];
-          acc_i[v] = acc_i[v] + dio[v];
-        }
+        dro[v] = (dv * nsp[v]) * ((1.0f - sr[j][v]) * sr[j][v]);
+        dio[v] = (dbeta * sq[j][v]) * ((1.0f - si[j][v]) * si[j][v]);
+        dxo[v] = d * (sq[j][v] * si[j][v]);
+        acc_v[v] = acc_v[v] + (ok ? dv * sr[j][v] : 0.0f);
+        acc_r[v] = acc_r[v] + (ok ? dro[v] : 0.0f);
+        acc_i[v] = acc_i[v] + (ok ? dio[v] : 0.0f);
         ein[v] = d * a;
       }
       if (cv && ok) {
@@ -399,7 +428,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
 #pragma unroll
-    for (int k = G; k < kWave; k <<= 1) {
+    for (int k = 1; k < Q; k <<= 1) {   // the Q chunk lanes of this channel group
       acc_v[v] += __shfl_xor(acc_v[v], k, kWave);
       acc_r[v] += __shfl_xor(acc_r[v], k, kWave);
       acc_i[v] += __shfl_xor(acc_i[v], k, kWave);
@@ -502,9 +531,10 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                     (const void*)drg, (const void*)dxc, (const void*)dz};
   const auto f32 = {(const void*)lam, (const void*)gb, (const void*)carries, (const void*)part,
                     (const void*)dh0_part};
-  if (vec_ok<T, VW>(H, strides, act, f32))
+  if (vec_ok<T, VW>(H, strides, act, f32)) {
     return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
                              dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
+  }
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_bwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);

@@ -184,6 +184,7 @@ int main(int argc, char** argv) {
   const int H = argc > 3 ? atoi(argv[3]) : 256;
   const int rounds = argc > 4 ? atoi(argv[4]) : 15;
   const bool bf16_only = argc > 5 && atoi(argv[5]) == 1;   // the config-5 bf16 sweep only
+  const bool packed_only = argc > 5 && atoi(argv[5]) == 2; // gate bwd: dense vs packed lengths
   const double N = (double)B * L * H;
   const int64_t n = (int64_t)B * L * H;
   const int nT = (L + RB_TILE - 1) / RB_TILE;
@@ -218,7 +219,53 @@ int main(int argc, char** argv) {
   float* Qb = dalloc(3 * n, 32);          // [dr | di | dxc] rows
   GateBufs comb{P, P + 2 * H, xz + H, y, car, dy, Qb, Qb + 2 * H, dz + H, part, dh0, lam,
                 3 * H, 3 * H, 2 * H, 3 * H, 3 * H, 2 * H};
-  if (bf16_only) {
+  if (packed_only) {
+    // the bench's packed batch: lengths uniform in 1..L, sequences longest
+    // first, rows concatenated (ntok ~ B * L / 2); bytes = 9 streams x ntok x H
+    std::vector<int64_t> lens(B), offs_h(B + 1, 0);
+    uint64_t st = 12345;
+    for (int i = 0; i < B; ++i) {
+      st = st * 6364136223846793005ULL + 1442695040888963407ULL;
+      lens[i] = 1 + (int64_t)((st >> 33) % L);
+    }
+    std::vector<int64_t> unsorted = lens;
+    std::sort(lens.begin(), lens.end(), [](int64_t a, int64_t b) { return a > b; });
+    auto mk_offs = [&](const std::vector<int64_t>& ls) {
+      std::vector<int64_t> o(B + 1, 0);
+      for (int i = 0; i < B; ++i) o[i + 1] = o[i] + ls[i];
+      int64_t* d;
+      CK(hipMalloc(&d, (B + 1) * 8));
+      CK(hipMemcpy(d, o.data(), (B + 1) * 8, hipMemcpyHostToDevice));
+      return std::make_pair(d, o[B]);
+    };
+    auto [offs_sorted, ntok] = mk_offs(lens);
+    auto [offs_unsorted, ntok2] = mk_offs(unsorted);
+    (void)ntok2;
+    const double NP = (double)ntok * H;
+    auto bwd = [=](const char* nm, const int64_t* offs, bool dma, double bytes) {
+      return Case{nm, bytes, [=] {
+        if (dma)
+          launch_gate_bwd(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, car, dy, drg, 2 * H, dxc,
+                          H, dz + H, 2 * H, part, dh0, B, L, H, offs, 0);
+        else
+          gate_bwd_v<float, 4>(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, car, dy, drg, 2 * H,
+                               dxc, H, dz + H, 2 * H, part, dh0, B, L, H, offs, 0);
+      }, {}};
+    };
+    cs.push_back(bwd("bwd dense regs", nullptr, false, 9 * N * 4));
+    cs.push_back(bwd("bwd dense dma", nullptr, true, 9 * N * 4));
+    cs.push_back(bwd("bwd packed regs", offs_sorted, false, 9 * NP * 4));
+    cs.push_back(bwd("bwd packed dma", offs_sorted, true, 9 * NP * 4));
+    cs.push_back(bwd("bwd packed-unsorted dma", offs_unsorted, true, 9 * NP * 4));
+    cs.push_back({"gate_fwd packed", 5 * NP * 4, [=] {
+      launch_gate_fwd(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, nullptr, 0, y, H, car, B, L,
+                      H, offs_sorted, 0);
+    }, {}});
+    cs.push_back({"gate_fwd dense", 5 * N * 4, [=] {
+      launch_gate_fwd(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, nullptr, 0, y, H, car, B, L,
+                      H, nullptr, 0);
+    }, {}});
+  } else if (bf16_only) {
     add_gate<bf16_t, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, sep, N, 1);
     add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 1);
     add_gate<bf16_t, 8, 8, 2, false>(cs, "bf16 v8 q8 tc2", B, L, H, sep, N, 1);
@@ -307,15 +354,17 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   for (auto& c : cs) c.run();  // warm-up
   CK(hipDeviceSynchronize());
+  // KB_REPS=k: k back-to-back launches per timed sample (per-launch time shown)
+  const int reps = getenv("KB_REPS") ? std::max(1, atoi(getenv("KB_REPS"))) : 1;
   for (int r = 0; r < rounds; ++r) {
     for (auto& c : cs) {
       CK(hipEventRecord(e0, 0));
-      c.run();
+      for (int k = 0; k < reps; ++k) c.run();
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
-      c.ms.push_back(ms);
+      c.ms.push_back(ms / reps);
     }
   }
   CK(hipGetLastError());
