@@ -168,6 +168,53 @@ __device__ __forceinline__ void ldc(float (&o)[V], const bf16_t* p) { ld_b16<fal
 template <int V>
 __device__ __forceinline__ void stc(bf16_t* p, const float (&o)[V]) { st_b16<false>(p, o); }
 
+// raw (storage-format) register image of V elements: fp32 as is, bf16 as
+// packed pairs, unpacked to fp32 only when used (prefetch buffers)
+template <typename T, int V>
+struct RawVec {
+  float w[V];
+};
+template <int V>
+struct RawVec<bf16_t, V> {
+  static_assert(V % 2 == 0, "packed bf16 needs an even width");
+  uint32_t w[V / 2];
+};
+template <>
+struct RawVec<bf16_t, 1> {
+  float w[1];
+};
+
+template <bool NT = kNT, int V>
+__device__ __forceinline__ void ld_raw(RawVec<float, V>& o, const float* p) { ld_f32<NT>(o.w, p); }
+template <int V>
+__device__ __forceinline__ void unpack_raw(float (&o)[V], const RawVec<float, V>& r) {
+#pragma unroll
+  for (int v = 0; v < V; ++v) o[v] = r.w[v];
+}
+template <bool NT = kNT, int V>
+__device__ __forceinline__ void ld_raw(RawVec<bf16_t, V>& o, const bf16_t* p) {
+  if constexpr (V == 8) {
+    const rb_u32x4 t = ld_pol<NT>(reinterpret_cast<const rb_u32x4*>(p));
+    o.w[0] = t[0]; o.w[1] = t[1]; o.w[2] = t[2]; o.w[3] = t[3];
+  } else if constexpr (V == 4) {
+    const rb_u32x2 t = ld_pol<NT>(reinterpret_cast<const rb_u32x2*>(p));
+    o.w[0] = t[0]; o.w[1] = t[1];
+  } else if constexpr (V == 2) {
+    o.w[0] = ld_pol<NT>(reinterpret_cast<const uint32_t*>(p));
+  } else {
+    o.w[0] = (float)p[0];
+  }
+}
+template <int V>
+__device__ __forceinline__ void unpack_raw(float (&o)[V], const RawVec<bf16_t, V>& r) {
+  if constexpr (V == 1) {
+    o[0] = r.w[0];
+  } else {
+#pragma unroll
+    for (int k = 0; k < V / 2; ++k) unpack2(r.w[k], o[2 * k], o[2 * k + 1]);
+  }
+}
+
 // ---- dropout keep-flags ------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11): counter = element index / 4, key =
 // 64-bit seed, 4 uniform u32 per call -> keep flags of 4 consecutive elements.

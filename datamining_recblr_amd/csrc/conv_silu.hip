@@ -91,7 +91,16 @@ k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
 // over b by the caller: deterministic, no atomics).  Tiles are walked from the
 // end; the K-1 "look-ahead" du values a chunk needs come from the next chunk's
 // lane by shuffle, or from the previous (later) tile for the last chunk.
-template <typename T, int K, int VEC, int Q, int TC>
+// PF: the next (earlier) tile's rows are loaded, in storage format, before the
+// current tile is computed, so a wave keeps two tiles of loads in flight —
+// what long sequences (configs[4], L = 2048: 128 tiles walked by one wave)
+// need to cover HBM latency.
+template <typename T, int VEC, int NX, int TC>
+struct ConvBwdIn {
+  RawVec<T, VEC> xs[NX], g1[TC], g2[TC];
+};
+
+template <typename T, int K, int VEC, int Q, int TC, bool PF = false>
 __global__ void __launch_bounds__(256)
 k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
                 const float* __restrict__ bias, const T* __restrict__ g1,
@@ -144,26 +153,39 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
   }
   constexpr int TILE = Q * TC;
   const int nT = (L + TILE - 1) / TILE;
-  for (int tile = nT - 1; tile >= 0; --tile) {
+  using In = ConvBwdIn<T, VEC, NX, TC>;
+  auto load = [&](In& in, int tile) {
     const int t0 = tile * TILE + q * TC;
-    float xs[NX][VEC], du[TC][VEC];
 #pragma unroll
     for (int m = 0; m < NX; ++m) {
       const int t = t0 - (K - 1) + m;
       const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
-      RB_CONV_LDX(xs[m], xb + tc * x_rs);
-      if (t < 0) {
+      ld_raw<RB_CONV_X_NT != 0>(in.xs[m], xb + tc * x_rs);
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int tc = min(t0 + j, L - 1);
+      ld_raw(in.g1[j], g1b + tc * H);
+      if (g2b != nullptr) ld_raw(in.g2[j], g2b + tc * H);
+    }
+  };
+  auto process = [&](const In& in, int tile) {
+    const int t0 = tile * TILE + q * TC;
+    float xs[NX][VEC], du[TC][VEC];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) {
+      unpack_raw(xs[m], in.xs[m]);
+      if (t0 - (K - 1) + m < 0) {
 #pragma unroll
         for (int v = 0; v < VEC; ++v) xs[m][v] = 0.0f;
       }
     }
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
-      const int tc = min(t0 + j, L - 1);
-      ldv(du[j], g1b + tc * H);
+      unpack_raw(du[j], in.g1[j]);
       if (g2b != nullptr) {
         float t2[VEC];
-        ldv(t2, g2b + tc * H);
+        unpack_raw(t2, in.g2[j]);
 #pragma unroll
         for (int v = 0; v < VEC; ++v) du[j][v] = du[j][v] + t2[v];
       }
@@ -211,6 +233,23 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
       }
       if (cv && t0 + j < L) stv(dxb + (t0 + j) * dx_rs, out);
     }
+  };
+  In bufA, bufB;
+  if constexpr (PF) {
+    if (nT > 0) load(bufA, nT - 1);
+    for (int tile = nT - 1; tile >= 0; tile -= 2) {
+      if (tile - 1 >= 0) load(bufB, tile - 1);
+      process(bufA, tile);
+      if (tile - 1 >= 0) {
+        if (tile - 2 >= 0) load(bufA, tile - 2);
+        process(bufB, tile - 1);
+      }
+    }
+  } else {
+    for (int tile = nT - 1; tile >= 0; --tile) {
+      load(bufA, tile);
+      process(bufA, tile);
+    }
   }
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -250,20 +289,27 @@ int conv_fwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, T* x
   return launch_status("rb_conv_silu_fwd");
 }
 
+// backward chunks per tile: 4 x 4 steps (8 x 4 is 3% faster on dense L = 200
+// rows in tools/kbench.hip but 2% slower on the bench's packed sequences; bf16
+// at configs[4]: 0.59 of 8 TB/s with 4 chunks, 0.38 with 8)
+template <typename T>
+constexpr int conv_bwd_q() { return 4; }
+
 template <typename T, int K, int TC>
 int conv_bwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, const T* g1,
                const T* g2, T* dx, int64_t dx_rs, float* dw_part, float* db_part,
                int64_t B, int64_t L, int64_t H, bool vec, const int64_t* offs, hipStream_t st) {
+  constexpr int kQ = conv_bwd_q<T>();
   const int V = vec ? 4 : 1;
-  const int span = (kWave / kConvQ) * V;
+  const int span = (kWave / kQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   if (vec)
-    hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 4, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
+    hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 4, kQ, TC>), dim3((unsigned)blocks), dim3(256),
                        0, st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
                        (int)L, (int)H, ncw, offs);
   else
-    hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 1, kConvQ, TC>), dim3((unsigned)blocks), dim3(256),
+    hipLaunchKernelGGL((k_conv_silu_bwd<T, K, 1, kQ, TC>), dim3((unsigned)blocks), dim3(256),
                        0, st, x, (int)x_rs, w, bias, g1, g2, dx, (int)dx_rs, dw_part, db_part, B,
                        (int)L, (int)H, ncw, offs);
   return launch_status("rb_conv_silu_bwd");

@@ -25,9 +25,11 @@ struct FwdIn {
   float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC];
 };
 
-template <int VEC, int TC>
+// backward operands as loaded: raw storage words (bf16 stays packed until the
+// tile is processed, so a prefetched tile costs half the registers)
+template <typename T, int VEC, int TC>
 struct BwdIn {
-  float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC], g[TC][VEC];
+  RawVec<T, VEC> r[TC], i[TC], x[TC], z[TC], g[TC];
 };
 
 // PF: software-prefetch the next tile's operands before computing this one
@@ -282,21 +284,32 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   const int nT = (L + TILE - 1) / TILE;          // tiles of this row
   const int nTc = (Lmax + TILE - 1) / TILE;      // carries row stride
 
-  auto load = [&](BwdIn<VEC, TC>& in, int tile) {
+  auto load = [&](BwdIn<T, VEC, TC>& in, int tile) {
     const int t0 = tile * TILE + q * TC;
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
       const int t = min(t0 + j, L - 1);
-      ldv(in.r[j], rgb + t * rg_rs);
-      ldv(in.i[j], rgb + t * rg_rs + H);
-      ldv(in.x[j], xcb + t * xc_rs);
-      ldv(in.z[j], zb + t * z_rs);
-      ldv(in.g[j], dyb + t * H);
+      ld_raw(in.r[j], rgb + t * rg_rs);
+      ld_raw(in.i[j], rgb + t * rg_rs + H);
+      ld_raw(in.x[j], xcb + t * xc_rs);
+      ld_raw(in.z[j], zb + t * z_rs);
+      ld_raw(in.g[j], dyb + t * H);
     }
   };
-  auto process = [&](BwdIn<VEC, TC>& in, int tile) {
+  auto process = [&](const BwdIn<T, VEC, TC>& raw, int tile) {
     float hcar[VEC];
     ldc(hcar, carries + (b * nTc + tile) * H + cc);
+    struct {
+      float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC], g[TC][VEC];
+    } in;
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      unpack_raw(in.r[j], raw.r[j]);
+      unpack_raw(in.i[j], raw.i[j]);
+      unpack_raw(in.x[j], raw.x[j]);
+      unpack_raw(in.z[j], raw.z[j]);
+      unpack_raw(in.g[j], raw.g[j]);
+    }
 #pragma unroll
     for (int j = 0; j < TC; ++j)
 #pragma unroll
@@ -406,7 +419,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
     if (tile == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ein);
   };
 
-  BwdIn<VEC, TC> bufA, bufB;
+  BwdIn<T, VEC, TC> bufA, bufB;
   if constexpr (PF) {
     load(bufA, nT - 1);
     for (int tile = nT - 1; tile >= 0; tile -= 2) {
@@ -481,16 +494,16 @@ int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   return launch_status("rb_gate_scan_fwd");
 }
 
-template <typename T, int V>
+template <typename T, int V, int Q = kBwdQ, int TC = kBwdTC, bool PF = false>
 int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
                float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
                hipStream_t st) {
-  const int span = (kWave / kBwdQ) * V;
+  const int span = (kWave / Q) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
-  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, kBwdQ, kBwdTC, false>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
                      dh0_part, B, (int)L, (int)H, ncw, offs);
@@ -525,12 +538,21 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
                float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
                hipStream_t st) {
-  constexpr int VW = 4;  // bf16 at 8 channels per lane spills (256 VGPRs)
+  constexpr int VW = 4;
   const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)dy,
                     (const void*)drg, (const void*)dxc, (const void*)dz};
   const auto f32 = {(const void*)lam, (const void*)gb, (const void*)carries, (const void*)part,
                     (const void*)dh0_part};
+  // bf16 (configs[4], L = 2048): 4 chunks x 4 steps with the next tile
+  // prefetched in storage format — one wave walks 128 tiles, so it needs two
+  // tiles of loads in flight (tools/kbench.hip: 0.36 -> 0.59 of 8 TB/s)
+  if constexpr (sizeof(T) == 2) {
+    if (vec_ok<T, VW>(H, strides, act, f32))
+      return gate_bwd_v<T, VW, 4, 4, true>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy,
+                                           drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part, dh0_part,
+                                           B, L, H, offs, st);
+  }
   if (vec_ok<T, VW>(H, strides, act, f32)) {
     return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
                              dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);

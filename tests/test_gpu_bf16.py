@@ -7,7 +7,10 @@ against fp32 computations fed the SAME bf16-rounded inputs:
   the fp32 kernel's output on the rounded inputs, rounded to bf16 (RNE):
   asserted bit for bit; the fp32 partial sums (dW, dbias, dLambda, dh0) are
   asserted equal to the fp32 kernel's to 1e-5 relative (identical order, only
-  the vector width of a lane differs);
+  the vector width of a lane differs).  Exception: the gate-scan backward,
+  whose bf16 variant walks 4 chunks x 4 steps per tile (the fp32 one 8 x 2),
+  so its adjoint scan re-associates: outputs within one bf16 ulp (>= 99 %
+  bit-identical), partial sums to 1e-4;
 * layer level — GatedRecurrentLayer on bf16 activations (bf16 MFMA GEMMs with
   fp32 accumulation) against the CPU oracle (oracle/recblr_oracle.py, fp32)
   on the same bf16-rounded input: within 3e-2 of max|ref|, the expected bf16
@@ -32,6 +35,18 @@ def _bits_equal(a_bf16, ref_fp32, what):
     diff = (a_bf16.view(torch.int16) != exp.view(torch.int16))
     assert not diff.any(), (f"{what}: {int(diff.sum())} of {diff.numel()} elements differ; "
                             f"max |d| {(a_bf16.float() - exp.float()).abs().max().item():.3e}")
+
+
+def _within_ulp(a_bf16, ref_fp32, what, min_exact=0.99):
+    """a_bf16 within one bf16 ulp of ref rounded to bf16, and bit-identical for
+    at least min_exact of the elements (fp32 re-association only moves values
+    across a rounding boundary now and then)."""
+    exp = ref_fp32.to(BF).float()
+    a = a_bf16.float()
+    tol = 2.0 ** -7 * exp.abs() + 1e-6 * exp.abs().max()
+    assert ((a - exp).abs() <= tol).all(), f"{what}: max |d| {(a - exp).abs().max().item():.3e}"
+    exact = (a == exp).float().mean().item()
+    assert exact >= min_exact, f"{what}: only {exact:.4f} of the elements bit-identical"
 
 
 def _close(a, b, rtol=1e-5, what=""):
@@ -108,11 +123,13 @@ def test_gate_scan_bf16_equals_rounded_fp32_kernel(cuda, B, L, H, h0):
     dz16 = torch.empty_like(z, dtype=BF)
     r16 = kernels.gate_scan_bwd(rg.to(BF), xc.to(BF), z.to(BF), lam, c16, dy.to(BF), dz16,
                                 dh0_rows=h0 == "rows", gate_b=gb)
-    _bits_equal(dz16, dz32, "dz")
-    _bits_equal(r16[0], r32[0], "drg")
-    _bits_equal(r16[1], r32[1], "dxc")
+    # the bf16 backward walks 4 chunks x 4 steps per tile (the fp32 one 8 x 2),
+    # so its fp32 adjoints re-associate: equal after rounding up to one bf16 ulp
+    _within_ulp(dz16, dz32, "dz")
+    _within_ulp(r16[0], r32[0], "drg")
+    _within_ulp(r16[1], r32[1], "dxc")
     for k, n in ((2, "dLambda"), (3, "dgate_b"), (4, "dh0")):
-        _close(r16[k], r32[k], what=n)
+        _close(r16[k], r32[k], rtol=1e-4, what=n)
 
 
 @pytest.mark.parametrize("B,L,d", [(3, 50, 64), (2, 2048, 256)])

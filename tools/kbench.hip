@@ -92,7 +92,7 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
   }
 }
 
-template <typename T, int K, int VEC, int Q, int TC>
+template <typename T, int K, int VEC, int Q, int TC, bool PF = false>
 void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float* x, float* w,
               float* bias, float* xc, float* g1, float* dx, float* dwp, float* dbp, double N,
               int which = 3) {
@@ -115,7 +115,7 @@ void add_conv(std::vector<Case>& cs, const char* nm, int B, int L, int H, float*
     snprintf(f2, 64, "conv_bwd %s", nm);
     cs.push_back({f2, 3 * N * es, [=] {
       const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
-      hipLaunchKernelGGL((k_conv_silu_bwd<T, K, VEC, Q, TC>), dim3(blocks), dim3(256), 0, 0,
+      hipLaunchKernelGGL((k_conv_silu_bwd<T, K, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
                          A(x), 2 * H, w, bias, A(g1), (const T*)nullptr, A(dx), 2 * H, dwp, dbp,
                          (int64_t)B, L, H, ncw, nullptr);
     }, {}});
@@ -272,6 +272,14 @@ int main(int argc, char** argv) {
     add_gate<bf16_t, 8, 4, 4, false>(cs, "bf16 v8 q4 tc4", B, L, H, sep, N, 1);
     add_gate<bf16_t, 2, 4, 4, true>(cs, "bf16 v2 q4 tc4 pf", B, L, H, sep, N, 1);
     add_gate<bf16_t, 4, 8, 2, false>(cs, "bf16 v4 q8 tc2", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 4, 8, 2, true>(cs, "bf16 v4 q8 tc2 pf", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 8, 8, 2, true>(cs, "bf16 v8 q8 tc2 pf", B, L, H, sep, N, 2);
+    add_gate<bf16_t, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, sep, N, 2);
+    add_gate<float, 4, 8, 2, true>(cs, "f32 v4 q8 tc2 pf", B, L, H, sep, N, 2);
+    add_conv<bf16_t, 4, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N, 2);
+    add_conv<bf16_t, 4, 8, 4, 4, true>(cs, "bf16 v8 q4 tc4 pf", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N, 2);
+    add_conv<bf16_t, 4, 4, 8, 4, true>(cs, "bf16 v4 q8 tc4 pf", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N, 2);
+    add_conv<float, 4, 4, 4, 4, true>(cs, "f32 v4 q4 tc4 pf", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N, 2);
     add_gate<bf16_t, 8, 8, 2, false>(cs, "bf16 v8 q8 tc2", B, L, H, sep, N, 2);
     add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 2);
     add_gate<bf16_t, 8, 16, 1, false>(cs, "bf16 v8 q16 tc1", B, L, H, sep, N, 2);
@@ -290,6 +298,8 @@ int main(int argc, char** argv) {
   } else {
   add_gate<float, 2, 4, 4, true>(cs, "v2 q4 tc4 pf  sep", B, L, H, sep, N);
   add_gate<float, 4, 8, 2, false>(cs, "v4 q8 tc2     sep", B, L, H, sep, N);
+  add_gate<float, 4, 8, 2, true>(cs, "v4 q8 tc2 pf  sep", B, L, H, sep, N, 2);
+  add_conv<float, 4, 4, 4, 4, true>(cs, "v4 q4 tc4 pf", B, L, H, xz, w, bias, xc, g1, dxo, dwp, dbp, N, 2);
   add_gate<float, 2, 4, 4, true>(cs, "v2 q4 tc4 pf  comb", B, L, H, comb, N);
   add_gate<float, 4, 8, 2, false>(cs, "v4 q8 tc2     comb", B, L, H, comb, N);
   add_gate<float, 4, 4, 4, true>(cs, "v4 q4 tc4 pf  comb", B, L, H, comb, N);

@@ -5,7 +5,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=gpurun_out
-ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-full-tail --no-c5"
+ARGS="--steps 3 --warmup 1 --settle-seconds 0 --no-cpu-baseline --no-full-tail --no-c5"
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run \
   -- python3 bench.py $ARGS > $OUT/pmc_fetch.log 2>&1 || exit $?
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run \
