@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -34,6 +34,10 @@ SIGNATURES = {
     "rb_scan_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp]),
     "rb_scan_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp]),
     "rb_conv_silu_fwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64, _i64, _fp, _fp]),
+    "rb_conv_silu_fwd_rows": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64, _i64,
+                                             _fp, _fp]),
+    "rb_conv_silu_fwd_rows_bf16": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _i64, _i64, _i64,
+                                                  _i64, _fp, _fp]),
     "rb_conv_silu_bwd": (ctypes.c_int, [_fp, _i64, _fp, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
                                         _i64, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp,

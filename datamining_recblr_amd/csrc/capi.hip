@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 17; }
+int rb_version(void) { return 18; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -105,6 +105,17 @@ int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w, const float* 
   if (int r = check_dims("rb_conv_silu_fwd", B, L, H, max4(x_rs, xc_rs))) return r;
   return launch_conv_fwd(x, x_rs, w, bias, xc, xc_rs, B, L, H, K,
                          seq_offsets, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_conv_silu_fwd_rows(const float* x, int64_t x_rs, const float* w, const float* bias,
+                          float* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                          const int64_t* row_pos, void* stream) {
+  if (!x || !w || !bias || !xc || !row_pos) return fail("rb_conv_silu_fwd_rows: null pointer");
+  if (K < 1 || K > 8) return fail("rb_conv_silu_fwd_rows: kernel size K must be in [1, 8]");
+  if (x_rs < H || xc_rs < H) return fail("rb_conv_silu_fwd_rows: row stride < H");
+  if (int r = check_dims("rb_conv_silu_fwd_rows", ntok, 1, H, max4(x_rs, xc_rs))) return r;
+  return launch_conv_fwd_rows(x, x_rs, w, bias, xc, xc_rs, ntok, H, K, row_pos,
+                              reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
@@ -185,6 +196,18 @@ int rb_conv_silu_fwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const 
   if (int r = check_dims("rb_conv_silu_fwd_bf16", B, L, H, max4(x_rs, xc_rs))) return r;
   return launch_conv_fwd_bf16(BF(x), x_rs, w, bias, BFW(xc), xc_rs, B, L, H, K,
                               seq_offsets, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_conv_silu_fwd_rows_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
+                               rb_bf16* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                               const int64_t* row_pos, void* stream) {
+  if (!x || !w || !bias || !xc || !row_pos)
+    return fail("rb_conv_silu_fwd_rows_bf16: null pointer");
+  if (K < 1 || K > 8) return fail("rb_conv_silu_fwd_rows_bf16: kernel size K must be in [1, 8]");
+  if (x_rs < H || xc_rs < H) return fail("rb_conv_silu_fwd_rows_bf16: row stride < H");
+  if (int r = check_dims("rb_conv_silu_fwd_rows_bf16", ntok, 1, H, max4(x_rs, xc_rs))) return r;
+  return launch_conv_fwd_rows_bf16(BF(x), x_rs, w, bias, BFW(xc), xc_rs, ntok, H, K, row_pos,
+                                   reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,

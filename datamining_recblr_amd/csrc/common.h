@@ -288,6 +288,12 @@ int launch_scan_fwd_bf16(const bf16_t* gates, const bf16_t* tokens, bf16_t* stat
 int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t* grad,
                          bf16_t* d_gates, bf16_t* d_tokens, int64_t rows, int64_t T,
                          hipStream_t st);
+int launch_conv_fwd_rows(const float* x, int64_t x_rs, const float* w, const float* bias,
+                         float* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                         const int64_t* pos, hipStream_t st);
+int launch_conv_fwd_rows_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
+                              bf16_t* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                              const int64_t* pos, hipStream_t st);
 int launch_conv_fwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
                          bf16_t* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
                          const int64_t* offs, hipStream_t st);

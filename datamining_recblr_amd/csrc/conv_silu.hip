@@ -86,6 +86,62 @@ k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
   }
 }
 
+// Row-tiled forward for packed sequences: waves tile the packed rows
+// [0, ntok) themselves (16 rows x G*VEC channels each, channel block fastest),
+// ignoring sequence boundaries, so no wave is launched past a sequence's end.
+// row_pos[r] = position of packed row r inside its sequence: the tap at lag l
+// contributes to row r only if l <= row_pos[r] (zero history before a
+// sequence's first row, exactly the per-sequence kernel's masking).
+template <typename T, int K, int VEC, int Q, int TC>
+__global__ void __launch_bounds__(256)
+k_conv_silu_fwd_rows(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
+                     const float* __restrict__ bias, T* __restrict__ xc, int xc_rs,
+                     int64_t ntok, int H, int ncw, const int64_t* __restrict__ row_pos) {
+  constexpr int G = kWave / Q;
+  constexpr int NX = TC + K - 1;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int q = lane / G;
+  const int g = lane - q * G;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int cw = (int)(wid % ncw);
+  const int64_t tile = wid / ncw;
+  if (tile * (Q * TC) >= ntok) return;   // wave-uniform
+  const int c0 = cw * (G * VEC) + g * VEC;
+  const bool cv = c0 < H;
+  const int cc = cv ? c0 : 0;
+  float wk[K][VEC], bi[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k][v] = w[(cc + v) * K + k];
+  }
+  ldc(bi, bias + cc);
+  const int64_t r0 = tile * (Q * TC) + q * TC;
+  float xs[NX][VEC];   // x[r0-K+1 .. r0+TC-1]
+#pragma unroll
+  for (int m = 0; m < NX; ++m) {
+    int64_t r = r0 - (K - 1) + m;
+    r = r < 0 ? 0 : (r >= ntok ? ntok - 1 : r);
+    RB_CONV_LDX(xs[m], x + r * x_rs + cc);
+  }
+  int64_t pj[TC];
+#pragma unroll
+  for (int j = 0; j < TC; ++j) pj[j] = row_pos[min(r0 + j, ntok - 1)];
+#pragma unroll
+  for (int j = 0; j < TC; ++j) {
+    float out[VEC];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      float acc = bi[v];
+#pragma unroll
+      for (int k = 0; k < K; ++k)   // lag K-1-k: rows before the sequence start are zero
+        acc = acc + (K - 1 - k <= pj[j] ? wk[k][v] * xs[j + k][v] : 0.0f);
+      out[v] = fsilu(acc);
+    }
+    if (cv && r0 + j < ntok) stv(xc + (r0 + j) * xc_rs + cc, out);
+  }
+}
+
 // Backward.  A wave owns (b, channels) for the whole sequence so its dW/dbias
 // partial sums are complete per batch row (written to dw_part/db_part, summed
 // over b by the caller: deterministic, no atomics).  Tiles are walked from the
@@ -289,6 +345,28 @@ int conv_fwd_t(const T* x, int64_t x_rs, const float* w, const float* bias, T* x
   return launch_status("rb_conv_silu_fwd");
 }
 
+template <typename T, int K, int TC, int VW = 4>
+int conv_fwd_rows_t(const T* x, int64_t x_rs, const float* w, const float* bias, T* xc,
+                    int64_t xc_rs, int64_t ntok, int64_t H, bool vec, const int64_t* pos,
+                    hipStream_t st) {
+  const int V = vec ? VW : 1;
+  const int span = (kWave / kConvQ) * V;
+  const int ncw = (int)((H + span - 1) / span);
+  const int64_t ntile = (ntok + kConvQ * TC - 1) / (kConvQ * TC);
+  const int64_t blocks = (ntile * ncw + 3) / 4;
+  if (blocks > 0x7fffffffLL) return fail("rb_conv_silu_fwd_rows: grid too large");
+  if (blocks == 0) return 0;
+  if (vec)
+    hipLaunchKernelGGL((k_conv_silu_fwd_rows<T, K, VW, kConvQ, TC>), dim3((unsigned)blocks),
+                       dim3(256), 0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, ntok, (int)H, ncw,
+                       pos);
+  else
+    hipLaunchKernelGGL((k_conv_silu_fwd_rows<T, K, 1, kConvQ, TC>), dim3((unsigned)blocks),
+                       dim3(256), 0, st, x, (int)x_rs, w, bias, xc, (int)xc_rs, ntok, (int)H, ncw,
+                       pos);
+  return launch_status("rb_conv_silu_fwd_rows");
+}
+
 // backward chunks per tile: 4 x 4 steps (8 x 4 is 3% faster on dense L = 200
 // rows in tools/kbench.hip but 2% slower on the bench's packed sequences; bf16
 // at configs[4]: 0.59 of 8 TB/s with 4 chunks, 0.38 with 8)
@@ -345,6 +423,28 @@ int conv_fwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, T* x
 }
 
 template <typename T>
+int conv_fwd_rows_k(const T* x, int64_t x_rs, const float* w, const float* bias, T* xc,
+                    int64_t xc_rs, int64_t ntok, int64_t H, int64_t K, const int64_t* pos,
+                    hipStream_t st) {
+  const bool vec = H % 4 == 0 && x_rs % 4 == 0 && xc_rs % 4 == 0 && al4<T>(x) && al4<T>(xc) &&
+                   aligned16(bias);
+  if (sizeof(T) == 2 && K == 4 && vec && H % 8 == 0 && x_rs % 8 == 0 && xc_rs % 8 == 0 &&
+      aligned16(x) && aligned16(xc) && aligned16(bias) && aligned16(w))
+    return conv_fwd_rows_t<T, 4, 8, 8>(x, x_rs, w, bias, xc, xc_rs, ntok, H, true, pos, st);
+  switch (K) {
+    case 1: return conv_fwd_rows_t<T, 1, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 2: return conv_fwd_rows_t<T, 2, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 3: return conv_fwd_rows_t<T, 3, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 4: return conv_fwd_rows_t<T, 4, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 5: return conv_fwd_rows_t<T, 5, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 6: return conv_fwd_rows_t<T, 6, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 7: return conv_fwd_rows_t<T, 7, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 8: return conv_fwd_rows_t<T, 8, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    default: return fail("rb_conv_silu_fwd_rows: kernel size K must be in [1, 8]");
+  }
+}
+
+template <typename T>
 int conv_bwd_k(const T* x, int64_t x_rs, const float* w, const float* bias, const T* g1,
                const T* g2, T* dx, int64_t dx_rs, float* dw_part, float* db_part, int64_t B,
                int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st) {
@@ -376,6 +476,18 @@ int launch_conv_fwd_bf16(const bf16_t* x, int64_t x_rs, const float* w, const fl
                          bf16_t* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
                          const int64_t* offs, hipStream_t st) {
   return conv_fwd_k<bf16_t>(x, x_rs, w, bias, xc, xc_rs, B, L, H, K, offs, st);
+}
+
+int launch_conv_fwd_rows(const float* x, int64_t x_rs, const float* w, const float* bias,
+                         float* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                         const int64_t* pos, hipStream_t st) {
+  return conv_fwd_rows_k<float>(x, x_rs, w, bias, xc, xc_rs, ntok, H, K, pos, st);
+}
+
+int launch_conv_fwd_rows_bf16(const bf16_t* x, int64_t x_rs, const float* w, const float* bias,
+                              bf16_t* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                              const int64_t* pos, hipStream_t st) {
+  return conv_fwd_rows_k<bf16_t>(x, x_rs, w, bias, xc, xc_rs, ntok, H, K, pos, st);
 }
 
 int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,

@@ -235,7 +235,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 T* __restrict__ drg, int drg_rs, T* __restrict__ dxc, int dxc_rs,
                 T* __restrict__ dz, int dz_rs, float* __restrict__ part,
                 float* __restrict__ dh0_part, int64_t B, int Lmax, int H, int ncw,
-                const int64_t* __restrict__ offs) {
+                const int64_t* __restrict__ offs, int pair) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -243,29 +243,37 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   const int q = lane & (Q - 1);   // time chunk on the low lane bits (scans: DPP)
   const int g = lane / Q;
   const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t b = wid / ncw;
-  if (b >= B) return;
-  const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
+  // pair: the wave walks sequence bw and then sequence B-1-bw (packed batches
+  // are sorted longest first, so every wave gets about the same number of
+  // tiles and pays its per-wave prologue/epilogue once for two sequences)
+  const int64_t bw = wid / ncw;
+  if (bw >= (pair ? (B + 1) / 2 : B)) return;
+  const int c0 = (int)(wid - bw * ncw) * (G * VEC) + g * VEC;
   const bool cv = c0 < H;
   const int cc = cv ? c0 : 0;
   // dense rows (b, t) at b * Lmax + t, or packed variable-length sequences:
   // sequence b at rows offs[b] .. offs[b+1] (wave-uniform)
-  int64_t row0;
-  int L;
-  if (offs != nullptr) {
-    row0 = offs[b];
-    L = (int)(offs[b + 1] - row0);
-  } else {
-    row0 = b * Lmax;
-    L = Lmax;
-  }
-  const T* rgb = rg + row0 * rg_rs + cc;
-  const T* xcb = xc + row0 * xc_rs + cc;
-  const T* zb = z + row0 * z_rs + cc;
-  const T* dyb = dy + row0 * H + cc;
-  T* drgb = drg + row0 * drg_rs + cc;
-  T* dxcb = dxc + row0 * dxc_rs + cc;
-  T* dzb = dz + row0 * dz_rs + cc;
+  int64_t b = bw, row0 = 0;
+  int L = 0;
+  const T *rgb = nullptr, *xcb = nullptr, *zb = nullptr, *dyb = nullptr;
+  T *drgb = nullptr, *dxcb = nullptr, *dzb = nullptr;
+  auto bind = [&](int64_t bs) {
+    b = bs;
+    if (offs != nullptr) {
+      row0 = offs[b];
+      L = (int)(offs[b + 1] - row0);
+    } else {
+      row0 = b * Lmax;
+      L = Lmax;
+    }
+    rgb = rg + row0 * rg_rs + cc;
+    xcb = xc + row0 * xc_rs + cc;
+    zb = z + row0 * z_rs + cc;
+    dyb = dy + row0 * H + cc;
+    drgb = drg + row0 * drg_rs + cc;
+    dxcb = dxc + row0 * dxc_rs + cc;
+    dzb = dz + row0 * dz_rs + cc;
+  };
 
   float lamv[VEC], nsp[VEC], br[VEC], bi[VEC];
   ldc(lamv, lam + cc);
@@ -280,8 +288,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   }
   float ecarry[VEC], acc_v[VEC], acc_r[VEC], acc_i[VEC];
 #pragma unroll
-  for (int v = 0; v < VEC; ++v) ecarry[v] = acc_v[v] = acc_r[v] = acc_i[v] = 0.0f;
-  const int nT = (L + TILE - 1) / TILE;          // tiles of this row
+  for (int v = 0; v < VEC; ++v) acc_v[v] = acc_r[v] = acc_i[v] = 0.0f;
   const int nTc = (Lmax + TILE - 1) / TILE;      // carries row stride
 
   auto load = [&](BwdIn<T, VEC, TC>& in, int tile) {
@@ -420,23 +427,30 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   };
 
   BwdIn<T, VEC, TC> bufA, bufB;
-  if constexpr (PF) {
-    load(bufA, nT - 1);
-    for (int tile = nT - 1; tile >= 0; tile -= 2) {
-      if (tile - 1 >= 0) load(bufB, tile - 1);
-      process(bufA, tile);
-      if (tile - 1 >= 0) {
-        if (tile - 2 >= 0) load(bufA, tile - 2);
-        process(bufB, tile - 1);
+  const int nseq = (pair && B - 1 - bw != bw) ? 2 : 1;
+  for (int sq_i = 0; sq_i < nseq; ++sq_i) {
+    bind(sq_i == 0 ? bw : B - 1 - bw);
+    const int nT = (L + TILE - 1) / TILE;          // tiles of this row
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) ecarry[v] = 0.0f;
+    if constexpr (PF) {
+      if (nT > 0) load(bufA, nT - 1);
+      for (int tile = nT - 1; tile >= 0; tile -= 2) {
+        if (tile - 1 >= 0) load(bufB, tile - 1);
+        process(bufA, tile);
+        if (tile - 1 >= 0) {
+          if (tile - 2 >= 0) load(bufA, tile - 2);
+          process(bufB, tile - 1);
+        }
+      }
+    } else {
+      for (int tile = nT - 1; tile >= 0; --tile) {
+        load(bufA, tile);
+        process(bufA, tile);
       }
     }
-  } else {
-    for (int tile = nT - 1; tile >= 0; --tile) {
-      load(bufA, tile);
-      process(bufA, tile);
-    }
+    if (nT == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ecarry);   // empty row: zeros
   }
-  if (nT == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ecarry);   // empty row: zeros
   // per-channel partial sums: butterfly over the Q lanes sharing the channels
 #pragma unroll
   for (int v = 0; v < VEC; ++v) {
@@ -450,9 +464,18 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
     acc_v[v] = -acc_v[v] * dsoftplus_f(lamv[v]);
   }
   if (q == 0 && cv) {
-    stv(part + b * H + c0, acc_v);
-    stv(part + (B + b) * H + c0, acc_r);
-    stv(part + (2 * B + b) * H + c0, acc_i);
+    stv(part + bw * H + c0, acc_v);
+    stv(part + (B + bw) * H + c0, acc_r);
+    stv(part + (2 * B + bw) * H + c0, acc_i);
+    if (nseq == 2) {   // the partner's rows of the per-row partial sums: zeros
+      const int64_t bp = B - 1 - bw;
+      float zero[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) zero[v] = 0.0f;
+      stv(part + bp * H + c0, zero);
+      stv(part + (B + bp) * H + c0, zero);
+      stv(part + (2 * B + bp) * H + c0, zero);
+    }
   }
 }
 
@@ -464,6 +487,10 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
 // math runs at the same rate).
 constexpr int kFwdQ = 4, kFwdTC = RB_TILE / kFwdQ;
 constexpr int kBwdQ = 8, kBwdTC = RB_TILE / kBwdQ;
+#ifndef RB_GATE_BWD_PAIR
+#define RB_GATE_BWD_PAIR 1
+#endif
+constexpr bool kBwdPair = RB_GATE_BWD_PAIR != 0;
 
 // alignment/stride check for VEC-wide access: activation pointers (T) need
 // sizeof(T)*V-byte alignment, the fp32 per-channel vectors 4*V
@@ -502,11 +529,14 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                hipStream_t st) {
   const int span = (kWave / Q) * V;
   const int ncw = (int)((H + span - 1) / span);
-  const int64_t blocks = (B * ncw + 3) / 4;
+  // packed (variable-length, longest-first) batches: one wave per sequence pair
+  const int pair = offs != nullptr && kBwdPair;
+  const int64_t Bw = pair ? (B + 1) / 2 : B;
+  const int64_t blocks = (Bw * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
-                     dh0_part, B, (int)L, (int)H, ncw, offs);
+                     dh0_part, B, (int)L, (int)H, ncw, offs, pair);
   return launch_status("rb_gate_scan_bwd");
 }
 

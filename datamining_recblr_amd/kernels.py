@@ -181,12 +181,19 @@ class Packed:
     """Packed variable-length sequences: sequence b occupies rows
     offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
     right-padded batch without the padding; include/recblr_hip.h)."""
-    __slots__ = ("offsets", "B", "L", "ntok")
+    __slots__ = ("offsets", "B", "L", "ntok", "pos")
 
-    def __init__(self, offsets: torch.Tensor, L: int, ntok: int):
+    def __init__(self, offsets: torch.Tensor, L: int, ntok: int,
+                 pos: torch.Tensor | None = None):
         if offsets.dtype != torch.int64 or offsets.dim() != 1 or not offsets.is_contiguous():
             raise ValueError("offsets must be a contiguous int64 [B + 1] tensor")
+        if pos is not None and (pos.dtype != torch.int64 or pos.shape != (int(ntok),)
+                                or not pos.is_contiguous()):
+            raise ValueError("pos must be a contiguous int64 [ntok] tensor")
         self.offsets, self.B, self.L, self.ntok = offsets, offsets.numel() - 1, int(L), int(ntok)
+        # optional: position of every packed row inside its sequence; lets the
+        # conv forward tile the packed rows directly (rb_conv_silu_fwd_rows)
+        self.pos = pos
 
 
 def _layout(t: torch.Tensor, name: str, C: int, seq: "Packed | None"):
@@ -253,6 +260,14 @@ def conv_silu_fwd(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor,
     K = w.shape[1]
     xc = torch.empty(x.shape[:-1] + (H,), device=x.device, dtype=dt)
     n = x.numel() // max(H, 1) * H
+    if seq is not None and seq.pos is not None:
+        if seq.pos.device != x.device:
+            raise ValueError("pos must live on the activations' device")
+        # packed rows tiled directly: no waves past a sequence's end
+        _launch("rb_conv_silu_fwd" + _sfx(dt), 2 * n * x.element_size(), x.data_ptr(), x_rs,
+                w.data_ptr(), bias.contiguous().data_ptr(), xc.data_ptr(), H, seq.ntok, H, K,
+                seq.pos.data_ptr(), _stream(x), _fn="rb_conv_silu_fwd_rows" + _sfx(dt))
+        return xc
     _launch("rb_conv_silu_fwd" + _sfx(dt), 2 * n * x.element_size(), x.data_ptr(), x_rs,
             w.data_ptr(), bias.contiguous().data_ptr(), xc.data_ptr(), H, B, L, H, K, offs,
             _stream(x))

@@ -36,6 +36,9 @@ from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
+# RECBLR_CONV_ROWS=0: packed conv forward per sequence instead of per row tile
+_CONV_ROWS = os.environ.get("RECBLR_CONV_ROWS", "1") != "0"
+
 __all__ = ["RecBLR", "RecurrentLayer", "GatedRecurrentLayer", "FeedForward",
            "softplus_inverse", "lambda_init_range"]
 
@@ -266,11 +269,13 @@ class RecBLR(SequentialRecommender):
         # token -> packed sequence -> batch row; flat [B*L] position of each token
         seq_of = torch.repeat_interleave(torch.arange(B, device=dev), lens.index_select(0, order),
                                          output_size=ntok)
-        flat = (order.index_select(0, seq_of) * L
-                + (torch.arange(ntok, device=dev) - offsets.index_select(0, seq_of)))
+        pos = torch.arange(ntok, device=dev) - offsets.index_select(0, seq_of)
+        flat = order.index_select(0, seq_of) * L + pos
         inv = torch.empty_like(order)
         inv.scatter_(0, order, torch.arange(B, device=dev))
-        seq = Packed(offsets, L, ntok)
+        # pos (each token's position in its sequence) lets the conv forward
+        # tile the packed rows directly (kernels.conv_silu_fwd)
+        seq = Packed(offsets, L, ntok, pos if _CONV_ROWS else None)
         if pad is not None:
             pad = pad.index_select(0, order)
         h = embed_dropout_layer_norm(item_seq.reshape(-1).index_select(0, flat),

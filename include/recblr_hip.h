@@ -96,6 +96,17 @@ int rb_conv_silu_fwd(const float* x, int64_t x_rs, const float* w,
                      const float* bias, float* xc, int64_t xc_rs,
                      int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* seq_offsets, void* stream);
 
+/* rb_conv_silu_fwd on packed sequences, tiled over the packed rows
+ * [0, ntok) instead of per sequence (no work past a sequence's end):
+ * row_pos is a device int64 array [ntok], row_pos[r] = position of row r
+ * inside its sequence (r - seq_offsets[b] for the sequence b holding r); the
+ * tap at lag l reaches row r only when l <= row_pos[r] (zero history).  Same
+ * values as rb_conv_silu_fwd with the matching seq_offsets.  Replaces
+ * RecBLR.py:182-193 like rb_conv_silu_fwd. */
+int rb_conv_silu_fwd_rows(const float* x, int64_t x_rs, const float* w, const float* bias,
+                          float* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                          const int64_t* row_pos, void* stream);
+
 /* Backward of rb_conv_silu_fwd.  dxc = g1 + g2 (g2 may be NULL), both
  * [B, L, H] contiguous.  Writes dx (row stride dx_rs) and per-batch partial
  * sums dw_part[b, k, c] (B*K*H floats) and db_part[b, c] (B*H floats); the
@@ -312,6 +323,9 @@ int rb_scan_bwd_bf16(const rb_bf16* gates, const rb_bf16* states, const rb_bf16*
 int rb_conv_silu_fwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
                           rb_bf16* xc, int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K,
                           const int64_t* seq_offsets, void* stream);
+int rb_conv_silu_fwd_rows_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
+                               rb_bf16* xc, int64_t xc_rs, int64_t ntok, int64_t H, int64_t K,
+                               const int64_t* row_pos, void* stream);
 int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const float* bias,
                           const rb_bf16* g1, const rb_bf16* g2, rb_bf16* dx, int64_t dx_rs,
                           float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,

@@ -314,3 +314,40 @@ def test_silu_dropout_with_folded_bias(cuda):
     (F.silu(ar) * keep).backward(du)
     close(da, ar.grad, what="da")
     close(db, ar.grad.double().sum(0), what="db")
+
+
+@pytest.mark.parametrize("H,K,dt", [(64, 4, torch.float32), (20, 3, torch.float32),
+                                    (256, 4, torch.float32), (64, 8, torch.float32),
+                                    (128, 4, torch.bfloat16), (64, 1, torch.float32)])
+def test_conv_rows_equals_per_sequence(cuda, H, K, dt):
+    """rb_conv_silu_fwd_rows (packed rows tiled directly, row positions mask
+    the history) == rb_conv_silu_fwd on the same packed sequences (per-sequence
+    tiles) bit for bit, lengths 1..40 incl. single-row sequences, on a
+    row-strided view (the in-projection's x half)."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(H * 10 + K)
+    lens = torch.randint(1, 41, (37,), generator=g)
+    lens[3] = 1
+    lens[5] = 40
+    offs = torch.zeros(lens.numel() + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=offs[1:])
+    ntok = int(offs[-1])
+    xz = torch.randn(ntok, 2 * H, generator=g).to(dt).to(cuda)
+    w = (torch.randn(H, 1, K, generator=g) * 0.4).to(cuda)
+    b = (torch.randn(H, generator=g) * 0.1).to(cuda)
+    offs_d = offs.to(cuda)
+    pos = (torch.arange(ntok) - offs[:-1].repeat_interleave(lens)).to(cuda)
+    x = xz[:, :H]
+    ref = kernels.conv_silu_fwd(x, w, b, kernels.Packed(offs_d, 40, ntok))
+    out = kernels.conv_silu_fwd(x, w, b, kernels.Packed(offs_d, 40, ntok, pos))
+    assert out.dtype == dt
+    assert torch.equal(out, ref)
+    # and against the definition: each sequence alone, zero history
+    xf = x.float().cpu()
+    for s in (0, 3, 5):
+        a, e = int(offs[s]), int(offs[s + 1])
+        xs = torch.nn.functional.pad(xf[a:e].t()[None], (K - 1, 0))
+        y = torch.nn.functional.silu(torch.nn.functional.conv1d(xs, w.cpu(), b.cpu(), groups=H))
+        tol = 1e-5 if dt == torch.float32 else 1e-2
+        assert (out[a:e].float().cpu() - y[0].t()).abs().max().item() < tol

@@ -87,7 +87,7 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
       hipLaunchKernelGGL((k_gate_scan_bwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
                          A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr, g.car,
                          A(g.dy), A(g.drg), g.drg_rs, A(g.dxc), g.dxc_rs, A(g.dz), g.dz_rs, g.part,
-                         g.dh0, (int64_t)B, L, H, ncw, nullptr);
+                         g.dh0, (int64_t)B, L, H, ncw, nullptr, 0);
     }, {}});
   }
 }
