@@ -22,7 +22,7 @@ ok $rc || exit $rc
 
 if [ -z "$NO_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
-      -- python3 bench.py --steps 5 --warmup 2 --settle-seconds 0 --no-cpu-baseline --no-full-tail --no-c5 > $OUT/prof.log 2>&1
+      -- python3 bench.py --steps 5 --warmup 2 --settle-seconds 4 --no-cpu-baseline --no-full-tail --no-c5 > $OUT/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 $OUT/prof.log
 fi
 exit $rc
