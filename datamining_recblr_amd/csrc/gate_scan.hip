@@ -20,9 +20,9 @@
 namespace rb {
 namespace {
 
-template <int VEC, int TC>
+template <typename T, int VEC, int TC>
 struct FwdIn {
-  float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC];
+  RawVec<T, VEC> r[TC], i[TC], x[TC], z[TC];
 };
 
 // backward operands as loaded: raw storage words (bf16 stays packed until the
@@ -91,18 +91,28 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   const int nT = (L + TILE - 1) / TILE;          // tiles of this row
   const int nTc = (Lmax + TILE - 1) / TILE;      // carries row stride
 
-  auto load = [&](FwdIn<VEC, TC>& in, int tile) {
+  auto load = [&](FwdIn<T, VEC, TC>& in, int tile) {
     const int t0 = tile * TILE + q * TC;
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
       const int t = min(t0 + j, L - 1);
-      ldv(in.r[j], rgb + t * rg_rs);
-      ldv(in.i[j], rgb + t * rg_rs + H);
-      ldv(in.x[j], xcb + t * xc_rs);
-      ldv(in.z[j], zb + t * z_rs);
+      ld_raw(in.r[j], rgb + t * rg_rs);
+      ld_raw(in.i[j], rgb + t * rg_rs + H);
+      ld_raw(in.x[j], xcb + t * xc_rs);
+      ld_raw(in.z[j], zb + t * z_rs);
     }
   };
-  auto process = [&](FwdIn<VEC, TC>& in, int tile) {
+  auto process = [&](const FwdIn<T, VEC, TC>& raw, int tile) {
+    struct {
+      float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC];
+    } in;
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      unpack_raw(in.r[j], raw.r[j]);
+      unpack_raw(in.i[j], raw.i[j]);
+      unpack_raw(in.x[j], raw.x[j]);
+      unpack_raw(in.z[j], raw.z[j]);
+    }
     if (carries != nullptr && q == 0 && cv) stv(carries + (b * nTc + tile) * H + c0, carry);
     const int t0 = tile * TILE + q * TC;
     // in.r <- alpha, in.x <- b' = beta * xc
@@ -158,7 +168,7 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
     }
   };
 
-  FwdIn<VEC, TC> bufA, bufB;
+  FwdIn<T, VEC, TC> bufA, bufB;
   if constexpr (PF) {
     load(bufA, 0);
     for (int tile = 0; tile < nT; tile += 2) {

@@ -268,6 +268,8 @@ int main(int argc, char** argv) {
   } else if (bf16_only) {
     add_gate<bf16_t, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, sep, N, 1);
     add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 8, 8, 2, true>(cs, "bf16 v8 q8 tc2 pf", B, L, H, sep, N, 1);
+    add_gate<bf16_t, 4, 8, 2, true>(cs, "bf16 v4 q8 tc2 pf", B, L, H, sep, N, 1);
     add_gate<bf16_t, 8, 8, 2, false>(cs, "bf16 v8 q8 tc2", B, L, H, sep, N, 1);
     add_gate<bf16_t, 8, 4, 4, false>(cs, "bf16 v8 q4 tc4", B, L, H, sep, N, 1);
     add_gate<bf16_t, 2, 4, 4, true>(cs, "bf16 v2 q4 tc4 pf", B, L, H, sep, N, 1);
