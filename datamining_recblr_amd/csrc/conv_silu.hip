@@ -17,6 +17,12 @@
 #define RB_CONV_LDX ldc
 #endif
 
+// steps per lane of the row-tiled packed forward at K = 4 (tile = 4 x TC rows;
+// each tile re-fetches K-1 halo rows its predecessor loaded)
+#ifndef RB_CONV_ROWS_TC
+#define RB_CONV_ROWS_TC 4
+#endif
+
 namespace rb {
 namespace {
 
@@ -435,7 +441,7 @@ int conv_fwd_rows_k(const T* x, int64_t x_rs, const float* w, const float* bias,
     case 1: return conv_fwd_rows_t<T, 1, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 2: return conv_fwd_rows_t<T, 2, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 3: return conv_fwd_rows_t<T, 3, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
-    case 4: return conv_fwd_rows_t<T, 4, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 4: return conv_fwd_rows_t<T, 4, RB_CONV_ROWS_TC>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 5: return conv_fwd_rows_t<T, 5, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 6: return conv_fwd_rows_t<T, 6, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 7: return conv_fwd_rows_t<T, 7, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
