@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 18; }
+int rb_version(void) { return 19; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -482,6 +482,20 @@ int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int 
   if (!aligned16(Wf)) return fail("rb_gemm_split_weight: Wf must be 16-byte aligned");
   return launch_split_weight(W, ldw, (int)C, (int)R, transpose, Wf,
                              reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {
+  if (!jobs || n < 1 || n > RB_MAX_SPLIT_JOBS)
+    return fail("rb_gemm_split_weights: need 1..RB_MAX_SPLIT_JOBS jobs");
+  for (int64_t j = 0; j < n; ++j) {
+    const rb_split_job& b = jobs[j];
+    if (!b.W || !b.Wf) return fail("rb_gemm_split_weights: null pointer");
+    if (b.C <= 0 || b.R <= 0 || b.C % 32 || b.R % 16 || b.C > (1 << 20) || b.R > (1 << 20))
+      return fail("rb_gemm_split_weights: C must be a multiple of 32 and R of 16");
+    if (b.ldw < (b.transpose ? b.C : b.R)) return fail("rb_gemm_split_weights: bad row stride");
+    if (!aligned16(b.Wf)) return fail("rb_gemm_split_weights: Wf must be 16-byte aligned");
+  }
+  return launch_split_weights(jobs, (int)n, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,

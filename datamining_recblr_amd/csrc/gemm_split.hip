@@ -93,6 +93,52 @@ __global__ void __launch_bounds__(256) k_split_weight(const float* __restrict__ 
   dst[128] = o2;
 }
 
+// Several weights in one launch (rb_gemm_split_weights): job j owns the
+// 256-thread blocks [bstart[j], bstart[j+1]), each block one job (uniform).
+struct SplitJobs {
+  const float* W[RB_MAX_SPLIT_JOBS];
+  bf16x8* Wf[RB_MAX_SPLIT_JOBS];
+  int64_t ldw[RB_MAX_SPLIT_JOBS];
+  int C[RB_MAX_SPLIT_JOBS], R[RB_MAX_SPLIT_JOBS], tr[RB_MAX_SPLIT_JOBS];
+  int bstart[RB_MAX_SPLIT_JOBS + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) k_split_weights(const SplitJobs jobs) {
+  int j = 0;
+  while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.bstart[j + 1]) ++j;
+  const int C = jobs.C[j], R = jobs.R[j], transpose = jobs.tr[j];
+  const int64_t ldw = jobs.ldw[j];
+  const float* __restrict__ W = jobs.W[j];
+  const int64_t idx = (int64_t)(blockIdx.x - jobs.bstart[j]) * 256 + threadIdx.x;
+  const int KB = R / 16;
+  const int64_t total = (int64_t)(C / 32) * KB * 64;
+  if (idx >= total) return;
+  const int lane = (int)(idx & 63);
+  const int64_t frag = idx >> 6;
+  const int kb = (int)(frag % KB);
+  const int cb = (int)(frag / KB);
+  const int c = cb * 32 + (lane & 31);
+  const int r0 = kb * 16 + 8 * (lane >> 5);
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    v[k] = transpose ? W[(int64_t)(r0 + k) * ldw + c] : W[(int64_t)c * ldw + r0 + k];
+  bf16x8 o0, o1, o2;
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+    bf16x2 p0, p1, p2;
+    split2(v[k], v[k + 1], p0, p1, p2);
+    o0[k] = p0[0]; o0[k + 1] = p0[1];
+    o1[k] = p1[0]; o1[k + 1] = p1[1];
+    o2[k] = p2[0]; o2[k + 1] = p2[1];
+  }
+  bf16x8* dst = jobs.Wf[j] + (frag * 3) * 64 + lane;
+  dst[0] = o0;
+  dst[64] = o1;
+  dst[128] = o2;
+}
+
 __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -452,6 +498,25 @@ int launch_split_weight(const float* W, int64_t ldw, int C, int R, int transpose
   k_split_weight<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(W, ldw, C, R, transpose,
                                                                   (bf16x8*)Wf);
   return launch_status("rb_gemm_split_weight");
+}
+
+int launch_split_weights(const rb_split_job* jobs, int n, hipStream_t st) {
+  SplitJobs sj{};
+  sj.n = n;
+  int blocks = 0;
+  for (int j = 0; j < n; ++j) {
+    sj.W[j] = jobs[j].W;
+    sj.Wf[j] = (bf16x8*)jobs[j].Wf;
+    sj.ldw[j] = jobs[j].ldw;
+    sj.C[j] = (int)jobs[j].C;
+    sj.R[j] = (int)jobs[j].R;
+    sj.tr[j] = (int)jobs[j].transpose;
+    sj.bstart[j] = blocks;
+    blocks += (int)(((jobs[j].C / 32) * (jobs[j].R / 16) * 64 + 255) / 256);
+  }
+  sj.bstart[n] = blocks;
+  k_split_weights<<<(unsigned)blocks, 256, 0, st>>>(sj);
+  return launch_status("rb_gemm_split_weights");
 }
 
 int launch_gemm_nt(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,

@@ -8,6 +8,7 @@ No function here has a CPU path: tensors must live on a ROCm GPU.
 from __future__ import annotations
 
 import contextlib
+import ctypes
 
 import torch
 
@@ -762,6 +763,35 @@ def gemm_split_weight(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
     _lib.call("rb_gemm_split_weight", w.data_ptr(), w.stride(0), C, R, int(transpose),
               wf.data_ptr(), _stream(w))
     return wf
+
+
+class _SplitJob(ctypes.Structure):
+    """rb_split_job (include/recblr_hip.h)."""
+    _fields_ = [("W", ctypes.c_void_p), ("ldw", ctypes.c_int64), ("C", ctypes.c_int64),
+                ("R", ctypes.c_int64), ("transpose", ctypes.c_int64), ("Wf", ctypes.c_void_p)]
+
+
+MAX_SPLIT_JOBS = 32   # RB_MAX_SPLIT_JOBS
+
+
+def gemm_split_weights(jobs) -> None:
+    """Refresh several split images in one launch (rb_gemm_split_weights):
+    jobs = [(w, transpose, wf)], wf from gemm_split_weight's layout."""
+    jobs = list(jobs)
+    for k in range(0, len(jobs), MAX_SPLIT_JOBS):
+        chunk = jobs[k:k + MAX_SPLIT_JOBS]
+        arr = (_SplitJob * len(chunk))()
+        for d, (w, transpose, wf) in zip(arr, chunk):
+            _check(w, "weight")
+            if w.dim() != 2 or w.stride(1) != 1:
+                raise ValueError("weight must be a 2-D row-major tensor")
+            R, C = (w.shape[0], w.shape[1]) if transpose else (w.shape[1], w.shape[0])
+            if wf.numel() * 2 != C * R * 6 or wf.device != w.device:
+                raise ValueError("split image buffer does not match the weight")
+            d.W, d.ldw, d.C, d.R = w.data_ptr(), w.stride(0), C, R
+            d.transpose, d.Wf = int(transpose), wf.data_ptr()
+        _lib.call("rb_gemm_split_weights", ctypes.addressof(arr), len(chunk),
+                  _stream(chunk[0][0]))
 
 
 def gemm_nt(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None = None,

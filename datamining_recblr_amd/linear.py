@@ -23,6 +23,7 @@ nn.Linear's (RecBLR.py:162,165,167,213,214).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -32,6 +33,68 @@ __all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled"
 
 SPLIT_MIN_ROWS = 4096
 _split_on = os.environ.get("RECBLR_SPLIT_GEMM", "1") != "0"
+_cache_on = os.environ.get("RECBLR_SPLIT_CACHE", "1") != "0"
+
+# Split images of the weights, kept across calls: (id(w), transpose) ->
+# [weakref(w), data_ptr, (version, optimizer steps), wf].  An entry is current
+# while the weight's storage, its version counter (every in-place update:
+# optimizer steps, load_state_dict, nn.init) and the count of optimizer steps
+# taken anywhere (torch.optim step hook: also covers optimizers that write
+# through .data) are unchanged; the first stale lookup of a training step
+# refreshes every stale entry of that device in one launch
+# (rb_gemm_split_weights) instead of one launch per GEMM call.  Code that
+# rewrites weights through .data outside torch.optim calls
+# invalidate_split_cache() (or sets RECBLR_SPLIT_CACHE=0).
+_split_cache: dict = {}
+_opt_steps = [0]
+
+
+def _count_step(*_args, **_kw):
+    _opt_steps[0] += 1
+
+
+try:
+    from torch.optim.optimizer import register_optimizer_step_post_hook
+except ImportError:   # older torch: version counters only
+    register_optimizer_step_post_hook = None
+if register_optimizer_step_post_hook is not None:
+    register_optimizer_step_post_hook(_count_step)
+
+
+def invalidate_split_cache() -> None:
+    _split_cache.clear()
+
+
+def _stamp(w: torch.Tensor):
+    return (w._version, _opt_steps[0])
+
+
+def _weight_split(w: torch.Tensor, transpose: bool) -> torch.Tensor:
+    if not _cache_on:
+        return kernels.gemm_split_weight(w, transpose=transpose)
+    key = (id(w), transpose)
+    e = _split_cache.get(key)
+    if e is not None and e[0]() is w and e[1] == w.data_ptr() and e[2] == _stamp(w):
+        return e[3]
+    if e is None or e[0]() is not w or e[1] != w.data_ptr():
+        # new (or re-allocated) weight: its own split, then cached
+        wf = kernels.gemm_split_weight(w, transpose=transpose)
+        _split_cache[key] = [weakref.ref(w), w.data_ptr(), _stamp(w), wf]
+        return wf
+    # stale after an in-place update: refresh all stale entries at once
+    jobs, fresh = [], []
+    for k, ent in list(_split_cache.items()):
+        ww = ent[0]()
+        if ww is None or ww.data_ptr() != ent[1]:
+            del _split_cache[k]
+            continue
+        if _stamp(ww) != ent[2] and ww.device == w.device:
+            jobs.append((ww, k[1], ent[3]))
+            fresh.append(ent)
+    kernels.gemm_split_weights(jobs)
+    for ent in fresh:
+        ent[2] = _stamp(ent[0]())
+    return e[3]
 
 
 def split_gemm_enabled() -> bool:
@@ -53,7 +116,7 @@ def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) ->
         return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
     N, K = w.shape
     if _split_ok(a, N, K):
-        return kernels.gemm_nt(a, kernels.gemm_split_weight(w), N, bias=bias)
+        return kernels.gemm_nt(a, _weight_split(w, False), N, bias=bias)
     return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
 
 
@@ -65,7 +128,7 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) ->
         return out.addmm_(dy, wb) if out is not None else dy @ wb
     N, K = w.shape
     if _split_ok(dy, K, N) and (out is None or (out.stride(1) == 1 and out.shape == (dy.shape[0], K))):
-        return kernels.gemm_nt(dy, kernels.gemm_split_weight(w, transpose=True), K, out=out,
+        return kernels.gemm_nt(dy, _weight_split(w, True), K, out=out,
                                accumulate=out is not None)
     if out is not None:
         return out.addmm_(dy, w)

@@ -356,6 +356,21 @@ int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R);
 int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
                          void* Wf, void* stream);
 
+/* rb_gemm_split_weight for up to RB_MAX_SPLIT_JOBS weights in one launch
+ * (jobs: a HOST array of n descriptors, each with rb_gemm_split_weight's
+ * arguments and constraints).  The host side refreshes every split image a
+ * training step made stale (the optimizer changed the weights) at once. */
+#define RB_MAX_SPLIT_JOBS 32
+typedef struct {
+  const float* W;
+  int64_t ldw;
+  int64_t C;
+  int64_t R;
+  int64_t transpose;
+  void* Wf;
+} rb_split_job;
+int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
+
 /* out[m, c] = sum_r A[m, r] Bm[c, r] (+ bias[c] if bias) (+ out[m, c] if
  * accumulate), m < M, c < C: F.linear's forward (A = x, Bm = W) and input
  * gradient (A = dy, Bm = W^T, accumulate adds a residual gradient in place).

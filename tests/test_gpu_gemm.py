@@ -99,3 +99,54 @@ def test_split_path_in_the_encoder_matches_torch_path(cuda, monkeypatch):
     for n, gr in res[False][1].items():
         err = (res[True][1][n] - gr).abs().max().item()
         assert err <= 1e-5 + 1e-4 * gr.abs().max().item(), (n, err)
+
+
+def test_batched_weight_splits_equal_single(cuda):
+    """rb_gemm_split_weights (several weights, both orientations, one launch)
+    writes exactly the images rb_gemm_split_weight writes one at a time."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(3)
+    ws = [torch.randn(n, k, generator=g).to(cuda) for n, k in ((512, 128), (256, 512), (128, 256))]
+    jobs, refs = [], []
+    for w in ws:
+        for tr in (False, True):
+            ref = kernels.gemm_split_weight(w, transpose=tr)
+            jobs.append((w, tr, torch.empty_like(ref)))
+            refs.append(ref)
+    kernels.gemm_split_weights(jobs)
+    for (_, _, wf), ref in zip(jobs, refs):
+        assert torch.equal(wf.view(torch.int16), ref.view(torch.int16))
+
+
+def test_split_cache_tracks_optimizer_steps(cuda):
+    """Cached split images (refreshed in one launch after each optimizer step)
+    give bit-identical training to splitting at every GEMM call."""
+    from datamining_recblr_amd import linear
+    from datamining_recblr_amd.distributed import synthetic_interaction
+    from datamining_recblr_amd.model import RecBLR
+    from datamining_recblr_amd.recbole_compat import SyntheticDataset
+
+    cfg = dict(hidden_size=64, loss_type="CE", num_layers=2, dropout_prob=0.0, expand=2,
+               d_conv=4, bd_lru_only=False, disable_conv1d=False, disable_ffn=False,
+               MAX_ITEM_LIST_LENGTH=50)
+    batches = [synthetic_interaction(256, 50, 300, cuda, seed=s) for s in range(3)]
+    runs = []
+    for cache in (True, False):
+        linear._cache_on = cache
+        linear.invalidate_split_cache()
+        torch.manual_seed(0)
+        model = RecBLR(cfg, SyntheticDataset(300)).to(cuda).train()
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2, fused=True)
+        losses = []
+        for b in batches + batches:
+            opt.zero_grad(set_to_none=True)
+            loss = model.calculate_loss(b)
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        runs.append((losses, [p.detach().clone() for p in model.parameters()]))
+    linear._cache_on = True
+    assert runs[0][0] == runs[1][0]
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)

@@ -197,3 +197,19 @@ def test_rank_metrics_match_sklearn_and_recbole():
     # invalid rows (-1) are dropped
     m2 = rank_metrics(torch.cat([gt, torch.tensor([-1])]), None, topk=(10,))
     assert abs(m2["hit@10"] - m["hit@10"]) < 1e-12
+
+
+def test_split_cache_counts_optimizer_steps():
+    """The split-weight cache (linear._weight_split) is invalidated by every
+    torch.optim step through the global step hook, whatever the optimizer
+    does to the version counters."""
+    import torch
+
+    from datamining_recblr_amd import linear
+
+    w = torch.nn.Parameter(torch.randn(4, 4))
+    opt = torch.optim.SGD([w], lr=0.1)
+    n0 = linear._opt_steps[0]
+    w.grad = torch.ones(4, 4)
+    opt.step()
+    assert linear._opt_steps[0] == n0 + 1
