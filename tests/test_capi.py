@@ -47,3 +47,22 @@ def test_argument_errors_are_reported_without_touching_the_gpu():
     assert b"K must be" in lib.rb_last_error_string()
     rc = lib.rb_gate_scan_fwd(1, 3, 1, 4, 1, 4, 1, 0, 0, 0, 1, 4, 1, 1, 1, 4, None, None)
     assert rc == _lib.RB_EINVAL   # rg row stride < 2H
+
+
+def test_row_conv_and_batched_split_argument_errors():
+    """ABI 18/19 entry points validate before any HIP call."""
+    lib = _lib.load()
+    rc = lib.rb_conv_silu_fwd_rows(1, 4, 1, 1, 1, 4, 8, 4, 4, None, None)
+    assert rc == _lib.RB_EINVAL and b"null" in lib.rb_last_error_string()
+    rc = lib.rb_conv_silu_fwd_rows(1, 4, 1, 1, 1, 4, 8, 4, 9, 1, None)
+    assert rc == _lib.RB_EINVAL and b"K must be" in lib.rb_last_error_string()
+    from datamining_recblr_amd import kernels
+
+    jobs = (kernels._SplitJob * 1)()
+    jobs[0].W, jobs[0].ldw, jobs[0].C, jobs[0].R, jobs[0].transpose, jobs[0].Wf = 16, 40, 32, 40, 0, 16
+    rc = lib.rb_gemm_split_weights(ctypes.addressof(jobs), 1, None)
+    assert rc == _lib.RB_EINVAL and b"multiple of" in lib.rb_last_error_string()   # R % 16
+    rc = lib.rb_gemm_split_weights(ctypes.addressof(jobs), 0, None)
+    assert rc == _lib.RB_EINVAL
+    rc = lib.rb_gemm_split_weights(ctypes.addressof(jobs), 33, None)
+    assert rc == _lib.RB_EINVAL
