@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -42,6 +42,11 @@ SIGNATURES = {
                                         _i64, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp,
                                         _i64, _fp, _i64, _i64, _i64, _fp, _fp]),
+    "rb_gate_scan_fwd_last": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp,
+                                             _i64, _fp, _fp, _i64, _i64, _i64, _fp, _fp]),
+    "rb_gate_scan_bwd_last": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp,
+                                             _fp, _fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp,
+                                             _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
                                         _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
                                         _fp, _fp]),

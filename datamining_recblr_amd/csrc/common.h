@@ -191,6 +191,12 @@ __device__ __forceinline__ void unpack_raw(float (&o)[V], const RawVec<float, V>
 #pragma unroll
   for (int v = 0; v < V; ++v) o[v] = r.w[v];
 }
+template <typename T, int V>
+__device__ __forceinline__ void zero_raw(RawVec<T, V>& o) {
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(o.w) / sizeof(o.w[0])); ++k) o.w[k] = 0;
+}
+
 template <bool NT = kNT, int V>
 __device__ __forceinline__ void ld_raw(RawVec<bf16_t, V>& o, const bf16_t* p) {
   if constexpr (V == 8) {
@@ -278,12 +284,14 @@ int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* b
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
-                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st);
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
+                    float* y_last = nullptr);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
-                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st);
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
+                    const float* dy_last = nullptr);
 int launch_scan_fwd_bf16(const bf16_t* gates, const bf16_t* tokens, bf16_t* states,
                          int64_t rows, int64_t T, hipStream_t st);
 int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t* grad,

@@ -42,7 +42,7 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 const float* __restrict__ gbias, const float* __restrict__ h0, int h0_bs,
                 T* __restrict__ y, int y_rs,
                 float* __restrict__ carries, int64_t B, int Lmax, int H, int ncw,
-                const int64_t* __restrict__ offs) {
+                const int64_t* __restrict__ offs, T* __restrict__ y_last) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -164,7 +164,11 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
         cin[v] = cin[v] * in.r[j][v] + in.x[j][v];
         out[v] = fsilu(in.z[j][v]) * cin[v];
       }
-      if (cv && t0 + j < L) stv(yb + (t0 + j) * y_rs, out);
+      if (y_last != nullptr) {   // only each sequence's last position is kept: [B, H]
+        if (cv && t0 + j == L - 1) stv(y_last + b * H + c0, out);
+      } else if (cv && t0 + j < L) {
+        stv(yb + (t0 + j) * y_rs, out);
+      }
     }
   };
 
@@ -245,7 +249,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 T* __restrict__ drg, int drg_rs, T* __restrict__ dxc, int dxc_rs,
                 T* __restrict__ dz, int dz_rs, float* __restrict__ part,
                 float* __restrict__ dh0_part, int64_t B, int Lmax, int H, int ncw,
-                const int64_t* __restrict__ offs, int pair) {
+                const int64_t* __restrict__ offs, int pair, const T* __restrict__ dy_last) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -310,7 +314,13 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
       ld_raw(in.i[j], rgb + t * rg_rs + H);
       ld_raw(in.x[j], xcb + t * xc_rs);
       ld_raw(in.z[j], zb + t * z_rs);
-      ld_raw(in.g[j], dyb + t * H);
+      if (dy_last == nullptr) {
+        ld_raw(in.g[j], dyb + t * H);
+      } else if (t == L - 1) {   // dy is zero except at each sequence's last position
+        ld_raw(in.g[j], dy_last + b * H + cc);
+      } else {
+        zero_raw(in.g[j]);
+      }
     }
   };
   auto process = [&](const BwdIn<T, VEC, TC>& raw, int tile) {
@@ -521,13 +531,13 @@ template <typename T, int V, bool PF = true>
 int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-               const int64_t* offs, hipStream_t st) {
+               const int64_t* offs, hipStream_t st, T* y_last) {
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_fwd<T, V, kFwdQ, kFwdTC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
-                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw, offs);
+                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw, offs, y_last);
   return launch_status("rb_gate_scan_fwd");
 }
 
@@ -536,7 +546,7 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
                float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
-               hipStream_t st) {
+               hipStream_t st, const T* dy_last) {
   const int span = (kWave / Q) * V;
   const int ncw = (int)((H + span - 1) / span);
   // packed (variable-length, longest-first) batches: one wave per sequence pair
@@ -546,7 +556,7 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
-                     dh0_part, B, (int)L, (int)H, ncw, offs, pair);
+                     dh0_part, B, (int)L, (int)H, ncw, offs, pair, dy_last);
   return launch_status("rb_gate_scan_bwd");
 }
 
@@ -556,20 +566,21 @@ template <typename T>
 int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-               const int64_t* offs, hipStream_t st) {
+               const int64_t* offs, hipStream_t st, T* y_last) {
   constexpr int VW = sizeof(T) == 2 ? 4 : 2;
   const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
-  const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y};
+  const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y,
+                    (const void*)y_last};
   const auto f32 = {(const void*)lam, (const void*)gb, (const void*)h0, (const void*)carries};
   // bf16: no register prefetch (measured 3% faster at config 5, tools/kbench.hip)
   if (vec_ok<T, VW>(H, strides, act, f32))
     return gate_fwd_v<T, VW, sizeof(T) == 4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs,
-                                             y, y_rs, carries, B, L, H, offs, st);
+                                             y, y_rs, carries, B, L, H, offs, st, y_last);
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_fwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                            B, L, H, offs, st);
+                            B, L, H, offs, st, y_last);
   return gate_fwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B,
-                          L, H, offs, st);
+                          L, H, offs, st, y_last);
 }
 
 template <typename T>
@@ -577,11 +588,11 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
                float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
-               hipStream_t st) {
+               hipStream_t st, const T* dy_last) {
   constexpr int VW = 4;
   const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)dy,
-                    (const void*)drg, (const void*)dxc, (const void*)dz};
+                    (const void*)drg, (const void*)dxc, (const void*)dz, (const void*)dy_last};
   const auto f32 = {(const void*)lam, (const void*)gb, (const void*)carries, (const void*)part,
                     (const void*)dh0_part};
   // bf16 (configs[4], L = 2048): 4 chunks x 4 steps with the next tile
@@ -591,17 +602,17 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
     if (vec_ok<T, VW>(H, strides, act, f32))
       return gate_bwd_v<T, VW, 4, 4, true>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy,
                                            drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part, dh0_part,
-                                           B, L, H, offs, st);
+                                           B, L, H, offs, st, dy_last);
   }
   if (vec_ok<T, VW>(H, strides, act, f32)) {
     return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
+                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
   }
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_bwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
   return gate_bwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
+                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
 }
 
 }  // namespace
@@ -609,9 +620,10 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
 int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
-                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
+                    float* y_last) {
   return gate_fwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                           B, L, H, offs, st);
+                           B, L, H, offs, st, y_last);
 }
 
 int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
@@ -619,16 +631,17 @@ int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int6
                          const float* h0, int64_t h0_bs, bf16_t* y, int64_t y_rs, float* carries,
                          int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
   return gate_fwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                            B, L, H, offs, st);
+                            B, L, H, offs, st, nullptr);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
-                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
+                    int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
+                    const float* dy_last) {
   return gate_bwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
+                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
 }
 
 int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
@@ -638,7 +651,7 @@ int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int6
                          float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
                          hipStream_t st) {
   return gate_bwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st);
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, nullptr);
 }
 
 }  // namespace rb

@@ -182,7 +182,7 @@ class Packed:
     """Packed variable-length sequences: sequence b occupies rows
     offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
     right-padded batch without the padding; include/recblr_hip.h)."""
-    __slots__ = ("offsets", "B", "L", "ntok", "pos")
+    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv")
 
     def __init__(self, offsets: torch.Tensor, L: int, ntok: int,
                  pos: torch.Tensor | None = None):
@@ -195,6 +195,11 @@ class Packed:
         # optional: position of every packed row inside its sequence; lets the
         # conv forward tile the packed rows directly (rb_conv_silu_fwd_rows)
         self.pos = pos
+        # optional (RecBLR._forward_packed): each batch row's last packed row
+        # and its packed-sequence index; lets the last layer keep only the
+        # positions gather_indexes reads (rb_gate_scan_*_last)
+        self.last = None
+        self.inv = None
 
 
 def _layout(t: torch.Tensor, name: str, C: int, seq: "Packed | None"):
@@ -304,14 +309,15 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx, seq: Packed | None = None):
 
 
 def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=None,
-                  seq: Packed | None = None):
+                  seq: Packed | None = None, last_only: bool = False):
     """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
 
     rg: [B, L, 2H]; xc, z: [B, L, H] views (or packed [ntok, 2H] / [ntok, H]
     with `seq`); lam: [H]; h0: [H] (shared by every row), [B, H] (one initial
     state per row) or None; gate_b: [2H] bias added to rg inside the kernel
     (or None).  Returns (y in xc's layout, carries [B, nT, H] or None when not
-    wanted)."""
+    wanted).  last_only (fp32): y is only needed at each sequence's last
+    position — returns y_last [B, H] instead (rb_gate_scan_fwd_last)."""
     dt = _act_dtype(xc, "xc")
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z")):
         _check(t, n, dt)
@@ -331,13 +337,23 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
             raise ValueError(f"h0 must be [{H}] or [{B}, {H}]")
         h0 = h0.contiguous()
         h0_bs = H if h0.dim() == 2 else 0
+    carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
+               if want_carries else None)
+    n = xc.numel()
+    if last_only:
+        if dt != torch.float32:
+            raise ValueError("last_only is fp32")
+        y_last = torch.empty((B, H), device=xc.device, dtype=dt)
+        _launch("rb_gate_scan_fwd", 4 * n * 4 + B * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(),
+                xc_rs, z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H),
+                0 if h0 is None else h0.data_ptr(), h0_bs, y_last.data_ptr(),
+                0 if carries is None else carries.data_ptr(), B, L, H, offs, _stream(xc),
+                _fn="rb_gate_scan_fwd_last")
+        return y_last, carries
     if y is None:
         y = torch.empty(xc.shape[:-1] + (H,), device=xc.device, dtype=dt)
     _check(y, "y", dt)
     y_rs = _layout(y, "y", H, seq)[2]
-    carries = (torch.empty((B, num_tiles(L), H), device=xc.device, dtype=torch.float32)
-               if want_carries else None)
-    n = xc.numel()
     _launch("rb_gate_scan_fwd" + _sfx(dt), 5 * n * xc.element_size(), rg.data_ptr(), rg_rs,
             xc.data_ptr(), xc_rs, z.data_ptr(), z_rs,
             lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), 0 if h0 is None else h0.data_ptr(),
@@ -356,17 +372,22 @@ def _gb_ptr(gate_b, H):
 
 
 def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=False,
-                  gate_b=None, seq: Packed | None = None):
+                  gate_b=None, seq: Packed | None = None, last_only: bool = False):
     """Backward of gate_scan_fwd.  Writes dz (a row-strided view) and returns
     (drg, dxc, dlam [H], dgate_bias [2H], dh0), dh0 [H] (summed over rows) or
-    [B, H] when dh0_rows (a per-row h0).  Layouts as in gate_scan_fwd."""
+    [B, H] when dh0_rows (a per-row h0).  Layouts as in gate_scan_fwd.
+    last_only: dy is [B, H], the gradient at each sequence's last position
+    (zero elsewhere; rb_gate_scan_bwd_last)."""
     H = xc.shape[-1]
     dt = _act_dtype(xc, "xc")
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (dy, "dy"), (dz, "dz")):
         _check(t, n, dt)
     _check(carries, "carries")
     B, L, xc_rs, offs = _layout(xc, "xc", H, seq)
-    if not dy.is_contiguous() or dy.shape != xc.shape:
+    if last_only:
+        if dt != torch.float32 or not dy.is_contiguous() or dy.shape != (B, H):
+            raise ValueError(f"last_only: dy must be a contiguous fp32 [{B}, {H}]")
+    elif not dy.is_contiguous() or dy.shape != xc.shape:
         raise ValueError("dy must be contiguous, shaped like xc")
     if carries.shape != (B, num_tiles(L), H) or not carries.is_contiguous():
         raise ValueError("carries shape mismatch")
@@ -384,12 +405,14 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
     part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
     dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
     n = xc.numel()
-    _launch("rb_gate_scan_bwd" + _sfx(dt), 9 * n * xc.element_size(), rg.data_ptr(), rg_rs,
+    nbytes = (8 * n + B * H if last_only else 9 * n) * xc.element_size()
+    _launch("rb_gate_scan_bwd" + _sfx(dt), nbytes, rg.data_ptr(), rg_rs,
             xc.data_ptr(), xc_rs,
             z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), carries.data_ptr(),
             dy.data_ptr(),
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
-            part.data_ptr(), dh0_part.data_ptr(), B, L, H, offs, _stream(xc))
+            part.data_ptr(), dh0_part.data_ptr(), B, L, H, offs, _stream(xc),
+            _fn="rb_gate_scan_bwd_last" if last_only else None)
     sums = colsum(part)
     return (drg, dxc, sums[0], sums[1:].reshape(-1),
             dh0_part if dh0_rows else colsum(dh0_part))

@@ -38,6 +38,8 @@ from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
 # RECBLR_CONV_ROWS=0: packed conv forward per sequence instead of per row tile
 _CONV_ROWS = os.environ.get("RECBLR_CONV_ROWS", "1") != "0"
+# RECBLR_LAST_ONLY=0: the last layer's scan writes y at every position
+_LAST_ONLY = os.environ.get("RECBLR_LAST_ONLY", "1") != "0"
 
 __all__ = ["RecBLR", "RecurrentLayer", "GatedRecurrentLayer", "FeedForward",
            "softplus_inverse", "lambda_init_range"]
@@ -91,10 +93,16 @@ class GatedRecurrentLayer(nn.Module):
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
                 "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
         xz = linear(x, self.input, slot)
+        # the last layer under gather_indexes on packed sequences needs y only
+        # at each sequence's last row: the scan kernels keep just those
+        last_only = (_LAST_ONLY and rows is not None and seq is not None
+                     and rows is seq.last and xz.dtype == torch.float32)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad,
-                   seq=seq)
-        if rows is not None:
+                   seq=seq, last_only=last_only)
+        if last_only:
+            y = y.index_select(0, seq.inv)   # packed-sequence order -> batch order
+        elif rows is not None:
             y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
         return linear(y, self.output)
 
@@ -282,6 +290,7 @@ class RecBLR(SequentialRecommender):
                                      self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
         last = offsets.index_select(0, inv + 1) - 1   # each batch row's last token
+        seq.last, seq.inv = last, inv
         n = len(self.recurrent_layers)
         for i, layer in enumerate(self.recurrent_layers):
             if i == n - 1 and self.gather_last_layer:

@@ -82,7 +82,8 @@ class BDLRUCore(torch.autograd.Function):
     BD-LRU(conv_silu(x)), in xz's layout."""
 
     @staticmethod
-    def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq=None):
+    def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq=None,
+                last_only=False):
         H2 = xz.shape[-1]
         H = H2 // 2
         x, z = xz[..., :H], xz[..., H:]
@@ -97,8 +98,9 @@ class BDLRUCore(torch.autograd.Function):
             *xz.shape[:-1], H2)
         train = any(ctx.needs_input_grad)
         y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b,
-                                           seq=seq)
+                                           seq=seq, last_only=last_only)
         ctx.use_conv = use_conv
+        ctx.last_only = last_only
         ctx.has_h0 = h0 is not None
         ctx.h0_rows = h0 is not None and h0.dim() == 2
         ctx.seq = seq
@@ -120,7 +122,7 @@ class BDLRUCore(torch.autograd.Function):
         dxz = torch.empty_like(xz)
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
             rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows, gate_b=gate_b,
-            seq=seq)
+            seq=seq, last_only=ctx.last_only)
         drg2 = drg.view(rows, H2)
         gflops = 2 * rows * H * H2
         dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H))
@@ -134,7 +136,7 @@ class BDLRUCore(torch.autograd.Function):
         else:
             dxz[..., :H].copy_(dxc)
         return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
-                dh0 if ctx.has_h0 else None, None, None)
+                dh0 if ctx.has_h0 else None, None, None, None)
 
 
 def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
@@ -146,7 +148,8 @@ def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
     return p2 - n
 
 
-def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq=None):
+def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq=None,
+           last_only=False):
     """Everything between the in- and out-projections of RecBLR.py:170-207.
 
     pad=None: the reference's pad prefix pow2(L) - L for the batch's L.
@@ -155,10 +158,11 @@ def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq
     with pad[b] = pow2(n_b) - n_b reproduces a batch-1 forward on the
     unpadded sequence, run_with_unseen.py:222-225).
     seq: kernels.Packed — xz holds only each sequence's first len_b positions
-    ([ntok, 2H]); the batch's L (for the pad prefix) is seq.L."""
+    ([ntok, 2H]); the batch's L (for the pad prefix) is seq.L.
+    last_only: return only each sequence's last position, [B, H] (fp32)."""
     if pad is None:
         P = pow2_pad_len(seq.L if seq is not None else xz.shape[1])
         h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
     else:
         h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, pad) if use_conv else None
-    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq)
+    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq, last_only)

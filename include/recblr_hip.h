@@ -146,6 +146,24 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
                      float* dz, int64_t dz_rs, float* part, float* dh0_part,
                      int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream);
 
+/* rb_gate_scan_fwd / _bwd when only each sequence's LAST position of y is
+ * used downstream (RecBLR.forward's gather_indexes(seq_output, len - 1),
+ * RecBLR.py:84, on the last layer): the forward writes y_last [B, H]
+ * contiguous (row b = y at position L-1, or at seq_offsets[b+1]-1 packed)
+ * instead of y; the backward takes dy_last [B, H] with dy = 0 at every other
+ * position (no [B, L, H] dy is materialised or read).  fp32. */
+int rb_gate_scan_fwd_last(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                          const float* z, int64_t z_rs, const float* lam, const float* gate_b,
+                          const float* h0, int64_t h0_bs, float* y_last, float* carries,
+                          int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets,
+                          void* stream);
+int rb_gate_scan_bwd_last(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                          const float* z, int64_t z_rs, const float* lam, const float* gate_b,
+                          const float* carries, const float* dy_last, float* drg,
+                          int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz, int64_t dz_rs,
+                          float* part, float* dh0_part, int64_t B, int64_t L, int64_t H,
+                          const int64_t* seq_offsets, void* stream);
+
 /* The state the power-of-two left padding leaves in the recurrence
  * (RecBLR.py:176-179: F.pad of x by P zero steps before conv + scan), without
  * materialising the padding.  Pad steps see the per-channel constants

@@ -77,7 +77,7 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
     cs.push_back({f, 5 * N * es, [=] {
       hipLaunchKernelGGL((k_gate_scan_fwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
                          A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr,
-                         nullptr, 0, A(g.y), H, g.car, (int64_t)B, L, H, ncw, nullptr);
+                         nullptr, 0, A(g.y), H, g.car, (int64_t)B, L, H, ncw, nullptr, (T*)nullptr);
     }, {}});
   }
   if (which & 2) {
@@ -87,7 +87,7 @@ void add_gate(std::vector<Case>& cs, const char* nm, int B, int L, int H, GateBu
       hipLaunchKernelGGL((k_gate_scan_bwd<T, VEC, Q, TC, PF>), dim3(blocks), dim3(256), 0, 0,
                          A(g.rg), g.rg_rs, A(g.xc), g.xc_rs, A(g.z), g.z_rs, g.lam, nullptr, g.car,
                          A(g.dy), A(g.drg), g.drg_rs, A(g.dxc), g.dxc_rs, A(g.dz), g.dz_rs, g.part,
-                         g.dh0, (int64_t)B, L, H, ncw, nullptr, 0);
+                         g.dh0, (int64_t)B, L, H, ncw, nullptr, 0, (const T*)nullptr);
     }, {}});
   }
 }
@@ -249,7 +249,7 @@ int main(int argc, char** argv) {
                           H, dz + H, 2 * H, part, dh0, B, L, H, offs, 0);
         else
           gate_bwd_v<float, 4>(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, car, dy, drg, 2 * H,
-                               dxc, H, dz + H, 2 * H, part, dh0, B, L, H, offs, 0);
+                               dxc, H, dz + H, 2 * H, part, dh0, B, L, H, offs, 0, nullptr);
       }, {}};
     };
     cs.push_back(bwd("bwd dense regs", nullptr, false, 9 * N * 4));
