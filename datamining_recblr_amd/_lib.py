@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 20
+ABI_VERSION = 21
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -91,6 +91,7 @@ SIGNATURES = {
     "rb_gemm_split_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
     "rb_gemm_split_weight": (ctypes.c_int, [_fp, _i64, _i64, _i64, ctypes.c_int, _fp, _fp]),
     "rb_gemm_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
+    "rb_pack_plan": (ctypes.c_int, [_fp, _i64, _fp, _fp, _i64, _i64, _fp, _fp, _fp, _fp, _fp]),
     "rb_gemm_nt": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
                                   _fp]),
 }

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 20; }
+int rb_version(void) { return 21; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -517,6 +517,17 @@ int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int 
   if (!aligned16(Wf)) return fail("rb_gemm_split_weight: Wf must be 16-byte aligned");
   return launch_split_weight(W, ldw, (int)C, (int)R, transpose, Wf,
                              reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_offsets,
+                 const int64_t* order, int64_t B, int64_t L, int64_t* ids, int64_t* row_pos,
+                 int64_t* inv, int64_t* last, void* stream) {
+  if (!item_seq || !seq_offsets || !order || !ids || !row_pos || !inv || !last)
+    return fail("rb_pack_plan: null pointer");
+  if (B < 1 || L < 1 || seq_rs < L) return fail("rb_pack_plan: bad shape or row stride");
+  if ((B + 3) / 4 > 0x7fffffffLL) return fail("rb_pack_plan: grid too large");
+  return launch_pack_plan(item_seq, seq_rs, seq_offsets, order, B, ids, row_pos, inv, last,
+                          reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {

@@ -275,6 +275,9 @@ DropSpec make_drop(const uint8_t* mask, uint64_t seed, float p);
 // G; no LDS and no barriers.
 
 // host launch helpers (defined in the .hip files)
+int launch_pack_plan(const int64_t* seq, int64_t seq_rs, const int64_t* offs,
+                     const int64_t* order, int64_t B, int64_t* ids, int64_t* pos, int64_t* inv,
+                     int64_t* last, hipStream_t st);
 int launch_split_weights(const rb_split_job* jobs, int n, hipStream_t st);
 int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st);

@@ -788,6 +788,28 @@ def gemm_split_weight(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
     return wf
 
 
+def pack_plan(item_seq: torch.Tensor, offsets: torch.Tensor, order: torch.Tensor, ntok: int):
+    """rb_pack_plan: (ids [ntok], row_pos [ntok], inv [B], last [B]) of the
+    packed layout (sequence s = batch row order[s] at rows offsets[s] ..
+    offsets[s+1]); item_seq [B, L] int64 on the device."""
+    for t, n in ((item_seq, "item_seq"), (offsets, "offsets"), (order, "order")):
+        _check(t, n, torch.int64)
+    if item_seq.dim() != 2 or item_seq.stride(1) != 1:
+        item_seq = item_seq.contiguous()
+    B, L = item_seq.shape
+    if offsets.shape != (B + 1,) or order.shape != (B,):
+        raise ValueError("offsets must be [B + 1] and order [B]")
+    dev = item_seq.device
+    ids = torch.empty(ntok, device=dev, dtype=torch.int64)
+    pos = torch.empty(ntok, device=dev, dtype=torch.int64)
+    inv = torch.empty(B, device=dev, dtype=torch.int64)
+    last = torch.empty(B, device=dev, dtype=torch.int64)
+    _lib.call("rb_pack_plan", item_seq.data_ptr(), item_seq.stride(0), offsets.data_ptr(),
+              order.data_ptr(), B, L, ids.data_ptr(), pos.data_ptr(), inv.data_ptr(),
+              last.data_ptr(), _stream(item_seq))
+    return ids, pos, inv, last
+
+
 class _SplitJob(ctypes.Structure):
     """rb_split_job (include/recblr_hip.h)."""
     _fields_ = [("W", ctypes.c_void_p), ("ldw", ctypes.c_int64), ("C", ctypes.c_int64),

@@ -30,7 +30,7 @@ from torch import nn
 from ._lib import RecBLRNativeError
 from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
                      feed_forward)
-from .kernels import Packed
+from .kernels import Packed, pack_plan
 from .linear import linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
@@ -256,7 +256,6 @@ class RecBLR(SequentialRecommender):
         per-sequence offsets).  The pow2 pad prefix still uses the batch's L."""
         B, L = item_seq.shape
         dev = item_seq.device
-        lens = item_seq_len.to(torch.int64).clamp(1, L)
         # sequences are packed longest first: the recurrence kernels give one
         # wave per sequence, so the short ones fill in behind the long ones
         host = getattr(item_seq_len, HOST_LENGTHS, None)
@@ -270,27 +269,21 @@ class RecBLR(SequentialRecommender):
             both = torch.cat([offs_h, order_h]).pin_memory().to(dev, non_blocking=True)
             offsets, order = both[:B + 1], both[B + 1:]
         else:
+            lens = item_seq_len.to(torch.int64).clamp(1, L)
             order = torch.argsort(lens, descending=True, stable=True)
             offsets = torch.zeros(B + 1, dtype=torch.int64, device=dev)
             torch.cumsum(lens.index_select(0, order), 0, out=offsets[1:])
             ntok = int(offsets[-1])   # one device sync
-        # token -> packed sequence -> batch row; flat [B*L] position of each token
-        seq_of = torch.repeat_interleave(torch.arange(B, device=dev), lens.index_select(0, order),
-                                         output_size=ntok)
-        pos = torch.arange(ntok, device=dev) - offsets.index_select(0, seq_of)
-        flat = order.index_select(0, seq_of) * L + pos
-        inv = torch.empty_like(order)
-        inv.scatter_(0, order, torch.arange(B, device=dev))
-        # pos (each token's position in its sequence) lets the conv forward
-        # tile the packed rows directly (kernels.conv_silu_fwd)
+        # one launch (rb_pack_plan): the packed item ids, each token's position
+        # in its sequence (lets the conv forward tile the packed rows), each
+        # batch row's packed index and last token
+        ids, pos, inv, last = pack_plan(item_seq.to(torch.int64), offsets, order, ntok)
         seq = Packed(offsets, L, ntok, pos if _CONV_ROWS else None)
+        seq.last, seq.inv = last, inv
         if pad is not None:
             pad = pad.index_select(0, order)
-        h = embed_dropout_layer_norm(item_seq.reshape(-1).index_select(0, flat),
-                                     self.item_embedding, self.dropout, self.layer_norm,
+        h = embed_dropout_layer_norm(ids, self.item_embedding, self.dropout, self.layer_norm,
                                      self.training)
-        last = offsets.index_select(0, inv + 1) - 1   # each batch row's last token
-        seq.last, seq.inv = last, inv
         n = len(self.recurrent_layers)
         for i, layer in enumerate(self.recurrent_layers):
             if i == n - 1 and self.gather_last_layer:

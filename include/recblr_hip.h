@@ -374,6 +374,17 @@ int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R);
 int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
                          void* Wf, void* stream);
 
+/* Packed-sequence plan (RecBLR.forward on RecBole's right-padded batch,
+ * RecBLR.py:75, run on each sequence's first len_b positions only): item_seq
+ * [B, L] int64 (row stride seq_rs), seq_offsets [B+1] and order [B] (packed
+ * sequence s is batch row order[s], rows seq_offsets[s] .. seq_offsets[s+1])
+ * -> ids[r] = item_seq[order[s], t] and row_pos[r] = t for r =
+ * seq_offsets[s] + t (ntok = seq_offsets[B] entries each), inv[order[s]] = s,
+ * last[order[s]] = seq_offsets[s+1] - 1.  All device int64. */
+int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_offsets,
+                 const int64_t* order, int64_t B, int64_t L, int64_t* ids, int64_t* row_pos,
+                 int64_t* inv, int64_t* last, void* stream);
+
 /* rb_gemm_split_weight for up to RB_MAX_SPLIT_JOBS weights in one launch
  * (jobs: a HOST array of n descriptors, each with rb_gemm_split_weight's
  * arguments and constraints).  The host side refreshes every split image a

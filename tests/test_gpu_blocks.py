@@ -414,3 +414,26 @@ def test_last_only_model_equals_full_positions(cuda):
     assert torch.equal(res[0][0], res[1][0])
     for n in res[0][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+def test_pack_plan_matches_torch(cuda):
+    """rb_pack_plan == the torch index/scatter formulation of the packed layout."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(8)
+    B, L = 37, 70
+    item_seq = torch.randint(1, 500, (B, L), generator=g)
+    lens = torch.randint(1, L + 1, (B,), generator=g)
+    lens[2], lens[5] = 1, L
+    order = torch.argsort(lens, descending=True, stable=True)
+    offs = torch.zeros(B + 1, dtype=torch.int64)
+    torch.cumsum(lens[order], 0, out=offs[1:])
+    ntok = int(offs[-1])
+    ids, pos, inv, last = kernels.pack_plan(item_seq.to(cuda), offs.to(cuda), order.to(cuda), ntok)
+    seq_of = torch.repeat_interleave(torch.arange(B), lens[order])
+    pos_r = torch.arange(ntok) - offs[seq_of]
+    ids_r = item_seq.reshape(-1)[order[seq_of] * L + pos_r]
+    inv_r = torch.empty_like(order)
+    inv_r[order] = torch.arange(B)
+    assert torch.equal(ids.cpu(), ids_r) and torch.equal(pos.cpu(), pos_r)
+    assert torch.equal(inv.cpu(), inv_r) and torch.equal(last.cpu(), offs[inv_r + 1] - 1)
