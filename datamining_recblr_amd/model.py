@@ -38,6 +38,37 @@ from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
 # RECBLR_CONV_ROWS=0: packed conv forward per sequence instead of per row tile
 _CONV_ROWS = os.environ.get("RECBLR_CONV_ROWS", "1") != "0"
+class _PinnedRing:
+    """A few reusable page-locked staging buffers for the per-batch host ->
+    device copy of the packed layout (offsets, order): no pinned allocation
+    per step; slot i is reused only after the copy from it has completed
+    (its event; only waits if the device runs >= k batches behind)."""
+
+    def __init__(self, k: int = 4):
+        self.k, self.i = k, 0
+        self.bufs = [None] * k
+        self.events = [None] * k
+
+    def stage(self, host: torch.Tensor, device) -> torch.Tensor:
+        i = self.i
+        self.i = (i + 1) % self.k
+        n = host.numel()
+        buf = self.bufs[i]
+        if buf is None or buf.numel() < n or buf.dtype != host.dtype:
+            buf = self.bufs[i] = torch.empty(max(n, 4096), dtype=host.dtype, pin_memory=True)
+            self.events[i] = None
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        buf[:n].copy_(host)
+        out = buf[:n].to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[i] = ev
+        return out
+
+
+_host_ring = _PinnedRing()
+
 # RECBLR_LAST_ONLY=0: the last layer's scan writes y at every position
 _LAST_ONLY = os.environ.get("RECBLR_LAST_ONLY", "1") != "0"
 
@@ -266,7 +297,7 @@ class RecBLR(SequentialRecommender):
             offs_h = torch.zeros(B + 1, dtype=torch.int64)
             torch.cumsum(lens_h[order_h], 0, out=offs_h[1:])
             ntok = int(offs_h[-1])
-            both = torch.cat([offs_h, order_h]).pin_memory().to(dev, non_blocking=True)
+            both = _host_ring.stage(torch.cat([offs_h, order_h]), dev)
             offsets, order = both[:B + 1], both[B + 1:]
         else:
             lens = item_seq_len.to(torch.int64).clamp(1, L)
