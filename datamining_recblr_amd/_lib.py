@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 21
+ABI_VERSION = 22
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -52,7 +52,7 @@ SIGNATURES = {
                                         _fp, _fp]),
     "rb_pad_prefix_fwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp]),
     "rb_pad_prefix_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
-                                         _fp, _fp, _fp, _fp]),
+                                         _fp, _fp, _fp, ctypes.c_int, _fp]),
     "rb_add_ln_fwd": (ctypes.c_int, [_fp, _fp, _i64, _fp, _u64, _f32, _fp, _fp, _fp, _f32, _fp,
                                      _fp, _fp, _fp, _i64, _i64, _fp]),
     "rb_row_num_parts": (ctypes.c_int64, [_i64, _i64]),

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 21; }
+int rb_version(void) { return 22; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -486,14 +486,15 @@ int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gat
 int rb_pad_prefix_bwd(const float* conv_b, const float* gate_w, const float* gate_b,
                       const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                       int64_t H, const float* dh0, float* dconv_b, float* dgate_w,
-                      float* dgate_b, float* dlam, float* workspace, void* stream) {
+                      float* dgate_b, float* dlam, float* workspace, int accumulate,
+                      void* stream) {
   if (!conv_b || !gate_w || !gate_b || !lam || !dh0 || !dconv_b || !dgate_w || !dgate_b || !dlam ||
       !workspace)
     return fail("rb_pad_prefix_bwd: null pointer");
   if (H <= 0 || H > 4096 || n_rows <= 0 || pad_len < 0)
     return fail("rb_pad_prefix_bwd: need 0 < H <= 4096, n_rows > 0, pad_len >= 0");
   return launch_pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad, pad_len, n_rows, H, dh0,
-                               dconv_b, dgate_w, dgate_b, dlam, workspace,
+                               dconv_b, dgate_w, dgate_b, dlam, workspace, accumulate,
                                reinterpret_cast<hipStream_t>(stream));
 }
 

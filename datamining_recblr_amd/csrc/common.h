@@ -372,7 +372,7 @@ int launch_pad_prefix_fwd(const float* conv_b, const float* gw, const float* gb,
 int launch_pad_prefix_bwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                           int64_t H, const float* dh0, float* dconv_b, float* dgw, float* dgb,
-                          float* dlam, float* ws, hipStream_t st);
+                          float* dlam, float* ws, int accumulate, hipStream_t st);
 int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
                   float* out, hipStream_t st);
 int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,

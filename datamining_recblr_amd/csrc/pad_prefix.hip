@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256) void k_pad_prefix_bwd1(
     const float* __restrict__ conv_b, const float* __restrict__ rg, const float* __restrict__ lam,
     const int64_t* __restrict__ pad, int64_t pad_len, int64_t n_rows, int H,
     const float* __restrict__ dh0, float* __restrict__ drg, float* __restrict__ dxb,
-    float* __restrict__ dgb, float* __restrict__ dlam) {
+    float* __restrict__ dgb, float* __restrict__ dlam, int acc) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= H) return;
   const float xc = silu_f(conv_b[c]);
@@ -114,24 +114,26 @@ __global__ __launch_bounds__(256) void k_pad_prefix_bwd1(
   const float dsg_i = dbeta * k.q;
   const float dalpha = dq * (-k.alpha / k.q);
   const float ds = gs + dalpha * (-k.alpha);
-  dlam[c] = ds * k.sg_r * dsoftplus_f(lam[c]);     // s = softplus(lam) sg_r
+  const float dl = ds * k.sg_r * dsoftplus_f(lam[c]);   // s = softplus(lam) sg_r
+  dlam[c] = acc ? dlam[c] + dl : dl;
   const float dr = ds * k.sp * k.sg_r * (1.0f - k.sg_r);
   const float di = dsg_i * k.sg_i * (1.0f - k.sg_i);
   drg[c] = dr;
   drg[H + c] = di;
-  dgb[c] = dr;
-  dgb[H + c] = di;
+  dgb[c] = acc ? dgb[c] + dr : dr;
+  dgb[H + c] = acc ? dgb[H + c] + di : di;
 }
 
 // dW_g = drg (x) xc_p, grid-stride over the [2H, H] rows (coalesced)
 __global__ __launch_bounds__(256) void k_pad_prefix_bwd2(const float* __restrict__ conv_b, int H,
                                                          const float* __restrict__ drg,
-                                                         float* __restrict__ dgw) {
+                                                         float* __restrict__ dgw, int acc) {
   const int64_t n = 2 * (int64_t)H * H;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n;
        e += (int64_t)gridDim.x * 256) {
     const int64_t o = e / H, c = e - o * H;
-    dgw[e] = drg[o] * silu_f(conv_b[c]);
+    const float v = drg[o] * silu_f(conv_b[c]);
+    dgw[e] = acc ? dgw[e] + v : v;
   }
 }
 
@@ -141,7 +143,7 @@ __global__ __launch_bounds__(1024) void k_pad_prefix_bwd3(const float* __restric
                                                           const float* __restrict__ gw, int H,
                                                           const float* __restrict__ drg,
                                                           const float* __restrict__ dxb,
-                                                          float* __restrict__ dconv_b) {
+                                                          float* __restrict__ dconv_b, int accum) {
   __shared__ float red[16][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
@@ -154,7 +156,8 @@ __global__ __launch_bounds__(1024) void k_pad_prefix_bwd3(const float* __restric
     float t = red[0][tx];
 #pragma unroll
     for (int g = 1; g < 16; ++g) t += red[g][tx];
-    dconv_b[c] = (t + dxb[c]) * dsilu_f(conv_b[c]);
+    const float v = (t + dxb[c]) * dsilu_f(conv_b[c]);
+    dconv_b[c] = accum ? dconv_b[c] + v : v;
   }
 }
 
@@ -175,18 +178,20 @@ int launch_pad_prefix_fwd(const float* conv_b, const float* gw, const float* gb,
 int launch_pad_prefix_bwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                           int64_t H, const float* dh0, float* dconv_b, float* dgw, float* dgb,
-                          float* dlam, float* ws, hipStream_t st) {
+                          float* dlam, float* ws, int accumulate, hipStream_t st) {
   float* rg = ws;
   float* drg = ws + 2 * H;
   float* dxb = ws + 4 * H;
   hipLaunchKernelGGL(k_pad_gates, dim3((unsigned)((2 * H + 3) / 4)), dim3(256), 0, st, conv_b, gw,
                      gb, (int)H, rg);
   hipLaunchKernelGGL(k_pad_prefix_bwd1, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, st,
-                     conv_b, rg, lam, pad, pad_len, n_rows, (int)H, dh0, drg, dxb, dgb, dlam);
+                     conv_b, rg, lam, pad, pad_len, n_rows, (int)H, dh0, drg, dxb, dgb, dlam,
+                     accumulate);
   const unsigned nb = (unsigned)std::min<int64_t>(1024, (2 * H * H + 255) / 256);
-  hipLaunchKernelGGL(k_pad_prefix_bwd2, dim3(nb), dim3(256), 0, st, conv_b, (int)H, drg, dgw);
+  hipLaunchKernelGGL(k_pad_prefix_bwd2, dim3(nb), dim3(256), 0, st, conv_b, (int)H, drg, dgw,
+                     accumulate);
   hipLaunchKernelGGL(k_pad_prefix_bwd3, dim3((unsigned)((H + 63) / 64)), dim3(1024), 0, st, conv_b,
-                     gw, (int)H, drg, dxb, dconv_b);
+                     gw, (int)H, drg, dxb, dconv_b, accumulate);
   return launch_status("rb_pad_prefix_bwd");
 }
 

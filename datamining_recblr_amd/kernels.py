@@ -753,22 +753,32 @@ def pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad_len):
     return h0 if pad is not None else h0[0]
 
 
-def pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad_len, dh0):
-    """(dconv_b, dgate_w, dgate_b, dlam) for dh0 shaped like pad_prefix_fwd's h0."""
+def pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad_len, dh0, into=None):
+    """(dconv_b, dgate_w, dgate_b, dlam) for dh0 shaped like pad_prefix_fwd's h0.
+    into = (dconv_b, dgate_w, dgate_b, dlam): add this contribution to those
+    contiguous fp32 tensors in place (rb_pad_prefix_bwd accumulate) and
+    return them."""
     _check(dh0, "dh0")
     H = lam.shape[0]
     pad, plen, rows = _pad_args(pad_len, H, lam.device)
     dh0 = dh0.reshape(rows, H).contiguous()
-    dcb = torch.empty_like(conv_b)
-    dgw = torch.empty_like(gate_w)
-    dgb = torch.empty_like(gate_b)
-    dlam = torch.empty_like(lam)
+    if into is not None:
+        for t, ref in zip(into, (conv_b, gate_w, gate_b, lam)):
+            _check(t, "gradient")
+            if t.shape != ref.shape or not t.is_contiguous():
+                raise ValueError("into: contiguous tensors shaped like the parameters")
+        dcb, dgw, dgb, dlam = into
+    else:
+        dcb = torch.empty_like(conv_b)
+        dgw = torch.empty_like(gate_w)
+        dgb = torch.empty_like(gate_b)
+        dlam = torch.empty_like(lam)
     ws = torch.empty((5 * H,), device=lam.device, dtype=torch.float32)
     _lib.call("rb_pad_prefix_bwd", conv_b.contiguous().data_ptr(), gate_w.contiguous().data_ptr(),
               gate_b.contiguous().data_ptr(), lam.contiguous().data_ptr(),
               pad.data_ptr() if pad is not None else None, plen, rows, H, dh0.data_ptr(),
               dcb.data_ptr(), dgw.data_ptr(), dgb.data_ptr(), dlam.data_ptr(), ws.data_ptr(),
-              _stream(lam))
+              int(into is not None), _stream(lam))
     return dcb, dgw, dgb, dlam
 
 

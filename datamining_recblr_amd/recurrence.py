@@ -24,6 +24,8 @@ and the mirror-image backward (K2^T, two GEMMs, K1^T).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -32,6 +34,9 @@ from .linear import _timed, mm_nn, mm_nt, wgrad
 
 __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDLRUCore",
            "bd_lru"]
+
+
+_FOLD_PAD = os.environ.get("RECBLR_FOLD_PAD", "1") != "0"
 
 
 def pow2_pad_len(seq_len: int) -> int:
@@ -83,7 +88,14 @@ class BDLRUCore(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq=None,
-                last_only=False):
+                last_only=False, pad_len=None):
+        """h0: an initial state given as an input (its gradient returned), or
+        pad_len (int P > 0 or int64 [B] per-row lengths) with h0 None: the
+        pad-prefix state computed here, its gradient added in place into the
+        parameters' gradients (no separate autograd node and add launches)."""
+        if pad_len is not None:
+            h0 = kernels.pad_prefix_fwd(conv_b, gate_w, gate_b, lam, pad_len)
+        ctx.pad_len = pad_len
         H2 = xz.shape[-1]
         H = H2 // 2
         x, z = xz[..., :H], xz[..., H:]
@@ -101,7 +113,7 @@ class BDLRUCore(torch.autograd.Function):
                                            seq=seq, last_only=last_only)
         ctx.use_conv = use_conv
         ctx.last_only = last_only
-        ctx.has_h0 = h0 is not None
+        ctx.has_h0 = h0 is not None and pad_len is None
         ctx.h0_rows = h0 is not None and h0.dim() == 2
         ctx.seq = seq
         ctx.save_for_backward(xz, xc if use_conv else None, rg, carries, conv_w, conv_b,
@@ -135,8 +147,11 @@ class BDLRUCore(torch.autograd.Function):
             dconv_w = dw.view_as(conv_w)
         else:
             dxz[..., :H].copy_(dxc)
+        if ctx.pad_len is not None:   # + the pad-prefix state's share, in place
+            kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len, dh0.float(),
+                                   into=(dconv_b, dgate_w, dgate_b, dlam))
         return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
-                dh0 if ctx.has_h0 else None, None, None, None)
+                dh0 if ctx.has_h0 else None, None, None, None, None)
 
 
 def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
@@ -162,7 +177,12 @@ def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq
     last_only: return only each sequence's last position, [B, H] (fp32)."""
     if pad is None:
         P = pow2_pad_len(seq.L if seq is not None else xz.shape[1])
-        h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, P) if (P and use_conv) else None
+        pad_len = P if (P and use_conv) else None
     else:
-        h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, pad) if use_conv else None
-    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq, last_only)
+        pad_len = pad if use_conv else None
+    if not _FOLD_PAD and pad_len is not None:   # A/B: separate autograd node
+        h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, pad_len)
+        return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq,
+                               last_only)
+    return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, None, use_conv, seq,
+                           last_only, pad_len)

@@ -179,12 +179,15 @@ int rb_pad_prefix_fwd(const float* conv_b, const float* gate_w, const float* gat
                       int64_t H, float* h0, float* workspace, void* stream);
 
 /* Backward of rb_pad_prefix_fwd for dh0 [n_rows, H] (rows summed in order):
- * writes dconv_b [H], dgate_w [2H, H], dgate_b [2H], dlam [H] (overwritten,
- * the caller adds them to the other gradient contributions). */
+ * dconv_b [H], dgate_w [2H, H], dgate_b [2H], dlam [H] are overwritten
+ * (accumulate = 0) or have this contribution added to what they hold
+ * (accumulate = 1: the other gradient contributions of the same parameters,
+ * so no separate add launches). */
 int rb_pad_prefix_bwd(const float* conv_b, const float* gate_w, const float* gate_b,
                       const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                       int64_t H, const float* dh0, float* dconv_b, float* dgate_w,
-                      float* dgate_b, float* dlam, float* workspace, void* stream);
+                      float* dgate_b, float* dlam, float* workspace, int accumulate,
+                      void* stream);
 
 /* ---- blocks around the BD-LRU (RecurrentLayer / FeedForward / embedding) ---- */
 

@@ -437,3 +437,36 @@ def test_pack_plan_matches_torch(cuda):
     inv_r[order] = torch.arange(B)
     assert torch.equal(ids.cpu(), ids_r) and torch.equal(pos.cpu(), pos_r)
     assert torch.equal(inv.cpu(), inv_r) and torch.equal(last.cpu(), offs[inv_r + 1] - 1)
+
+
+@pytest.mark.parametrize("pads", [56, [0, 3, 14, 56]])
+def test_folded_pad_prefix_equals_separate_node(cuda, pads):
+    """bd_lru folds the pad-prefix state into BDLRUCore (its backward adds
+    into the parameter gradients in place, rb_pad_prefix_bwd accumulate=1):
+    bit-identical outputs and gradients to PadPrefix + BDLRUCore with an
+    explicit h0, where autograd sums the two contributions."""
+    from datamining_recblr_amd.recurrence import BDLRUCore, PadPrefix, bd_lru
+
+    B, L, H, K = 4, 72, 128, 4
+    g = torch.Generator(device="cpu").manual_seed(7)
+    xz = torch.randn(B, L, 2 * H, generator=g).to(cuda)
+    params = [(0.3 * torch.randn(H, 1, K, generator=g)).to(cuda),
+              (0.5 * torch.randn(H, generator=g)).to(cuda),
+              (0.1 * torch.randn(2 * H, H, generator=g)).to(cuda),
+              (0.1 * torch.randn(2 * H, generator=g)).to(cuda),
+              torch.linspace(-2.0, 1.0, H).to(cuda)]
+    pad = torch.tensor(pads, device=cuda) if isinstance(pads, list) else None
+    dy = torch.randn(B, L, H, generator=g).to(cuda)
+    outs = []
+    for fold in (True, False):
+        x = xz.clone().requires_grad_()
+        p = [t.clone().requires_grad_() for t in params]
+        if fold:
+            y = bd_lru(x, *p, use_conv=True, pad=pad)
+        else:
+            h0 = PadPrefix.apply(*p[1:], pad if pad is not None else pads)
+            y = BDLRUCore.apply(x, *p, h0, True, None, False)
+        (y * dy).sum().backward()
+        outs.append([y.detach(), x.grad] + [t.grad for t in p])
+    for a, b, n in zip(*outs, ("y", "dxz", "dconv_w", "dconv_b", "dgate_w", "dgate_b", "dlam")):
+        assert torch.equal(a, b), n
