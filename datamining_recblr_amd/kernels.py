@@ -402,8 +402,9 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
     _check(drg, "drg", dt)
     _check(dxc, "dxc", dt)
     dxc_rs = _layout(dxc, "dxc", H, seq)[2]
-    part = torch.empty((3, B, H), device=xc.device, dtype=torch.float32)
-    dh0_part = torch.empty((B, H), device=xc.device, dtype=torch.float32)
+    # dlam, dgate_b (2) and dh0 per-row partials in one buffer: one colsum
+    part = torch.empty((4, B, H), device=xc.device, dtype=torch.float32)
+    dh0_part = part[3]
     n = xc.numel()
     nbytes = (8 * n + B * H if last_only else 9 * n) * xc.element_size()
     _launch("rb_gate_scan_bwd" + _sfx(dt), nbytes, rg.data_ptr(), rg_rs,
@@ -413,9 +414,11 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
             part.data_ptr(), dh0_part.data_ptr(), B, L, H, offs, _stream(xc),
             _fn="rb_gate_scan_bwd_last" if last_only else None)
+    if dh0_rows:
+        sums = colsum(part[:3])
+        return drg, dxc, sums[0], sums[1:].reshape(-1), dh0_part
     sums = colsum(part)
-    return (drg, dxc, sums[0], sums[1:].reshape(-1),
-            dh0_part if dh0_rows else colsum(dh0_part))
+    return drg, dxc, sums[0], sums[1:3].reshape(-1), sums[3]
 
 
 # ---------------------------------------------------------------- row blocks
