@@ -47,13 +47,42 @@ def make_cfg(args):
                 disable_conv1d=False, disable_ffn=False, MAX_ITEM_LIST_LENGTH=args.seq_len)
 
 
+def _cpu_threads():
+    """(threads to use, physical cores visible, logical CPUs visible): the
+    physical cores of this process's CPU affinity set (lscpu -p), capped by
+    OMP_NUM_THREADS when set (the GPU box allots each one-GPU job a share of
+    the host and sets it)."""
+    import subprocess
+
+    cpus = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    phys = None
+    try:
+        txt = subprocess.run(["lscpu", "-p=CPU,CORE,SOCKET"], capture_output=True, text=True,
+                             timeout=10).stdout
+        core_of = {}
+        for line in txt.splitlines():
+            if line and not line.startswith("#"):
+                c, core, sock = line.split(",")[:3]
+                core_of[int(c)] = (sock, core)
+        phys = len({core_of[c] for c in cpus if c in core_of}) or None
+    except (OSError, ValueError, subprocess.SubprocessError):
+        pass
+    n = phys or len(cpus) or (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, phys, len(cpus) or os.cpu_count()
+
+
 def cpu_baseline(args, state_dict):
     """The CPU oracle (serial-scan restatement of the reference) on a bounded
-    sample of the same workload: one fwd+bwd+Adam step over `cpu_sample`
-    sequences, median of 3 after 1 warm-up."""
+    sample of the same workload: one fwd+bwd+Adam train step (dropout as the
+    GPU step) over `cpu_sample` sequences, median of 3 after 1 warm-up; and
+    the scan-only leg (SURVEY.md §8(d) CPU baseline (i)): the serial forward
+    scan at [B, C, T] = [2048, 256, 256], median of 3."""
     from oracle import recblr_oracle as orc
 
-    threads = min(16, os.cpu_count() or 1)
+    threads, phys, logical = _cpu_threads()
     torch.set_num_threads(threads)
     cfg = make_cfg(args)
     params = {k: v.detach().cpu().clone().requires_grad_(v.dtype.is_floating_point)
@@ -66,17 +95,34 @@ def cpu_baseline(args, state_dict):
         t0 = time.perf_counter()
         opt.zero_grad(set_to_none=True)
         loss = orc.calculate_loss(params, cfg, inter["item_id_list"], inter["item_length"],
-                                  inter["item_id"])
+                                  inter["item_id"], p_drop=args.dropout)
         loss.backward()
         opt.step()
         times.append(time.perf_counter() - t0)
     med = sorted(times[1:])[1]
+    B, C, T = 2048, 2 * args.hidden, 256
+    g = torch.Generator().manual_seed(0)
+    gates = torch.rand(B, C, T, generator=g) * 0.1 + 0.9
+    tokens = torch.randn(B, C, T, generator=g)
+    st = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        orc.serial_scan(gates, tokens)
+        st.append(time.perf_counter() - t0)
+    smed = sorted(st)[1]
+    where = (f"{threads} threads ({phys} physical cores / {logical} logical CPUs in this "
+             f"process's affinity set; OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})")
     return {"value": round(args.cpu_sample / med, 3), "unit": "sequences/sec", "cores": threads,
             "kind": "port",
-            "sample": (f"oracle (serial-scan CPU restatement) CE fwd+bwd+Adam step on "
-                       f"{args.cpu_sample} of the {args.batch} sequences, L={args.seq_len}, "
-                       f"d={args.hidden}, n_items={args.n_items}, dropout off; median of 3 "
-                       f"after 1 warm-up; {med:.2f} s/step on {threads} threads")}
+            "sample": (f"oracle (serial-scan CPU restatement of RecBLR.py + parallel_scan.py) "
+                       f"CE fwd+bwd+Adam train step on {args.cpu_sample} of the {args.batch} "
+                       f"sequences, L={args.seq_len}, d={args.hidden}, n_items={args.n_items}, "
+                       f"dropout {args.dropout} as the GPU step; median of 3 after 1 warm-up; "
+                       f"{med:.2f} s/step on {where}"),
+            "scan_fwd_only": {"shape_BCT": [B, C, T], "s": round(smed, 3),
+                              "sequences_per_sec": round(B / smed, 1),
+                              "note": "serial_scan (parallel_scan.py:44-60 order, no FMA), "
+                                      "median of 3"}}
 
 
 def pmc_traffic(args, kernel_prefix):
@@ -99,18 +145,29 @@ def pmc_traffic(args, kernel_prefix):
 def pmc_mfma(args):
     """MFMA busy fraction of the projection GEMMs (>= 20 GFLOP per launch) from
     the newest committed PMC summary (profiles/*_pmc_mfma.json,
-    tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs))."""
+    tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs)),
+    per family: the split-bf16 kernel (k_gemm_nt: bf16 MFMA instructions, 6
+    per fp32 product) and the hipBLASLt fp32 kernels.  Busy is the fraction
+    of the MFMA pipe's cycles, whatever the dtype."""
     if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_mfma.json")))
     if not files:
         return None
     data = json.load(open(files[-1]))
-    utils = [k["mfma_util"] for k in data.get("kernels", {}).values()
-             if k.get("mfma_util") and k["mfma_flops_f32_per_dispatch"] >= 2e10]
-    if not utils:
+    fam = {"split_bf16": [], "hipblaslt_f32": []}
+    for k in data.get("kernels", {}).values():
+        if not k.get("mfma_util"):
+            continue
+        if k.get("mfma_flops_bf16_per_dispatch", 0) >= 2e10:
+            fam["split_bf16"].append(k["mfma_util"])
+        elif k.get("mfma_flops_f32_per_dispatch", 0) >= 2e10:
+            fam["hipblaslt_f32"].append(k["mfma_util"])
+    out = {f: {"min": min(u), "max": max(u)} for f, u in fam.items() if u}
+    if not out:
         return None
-    return {"min": min(utils), "max": max(utils), "source": os.path.relpath(files[-1], ROOT)}
+    out["source"] = os.path.relpath(files[-1], ROOT)
+    return out
 
 
 def scan_microbench(args, dev, reps=20):
@@ -193,6 +250,49 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
                                     "kernels": kern}}
 
 
+def ddp_overhead(args, model, batches, dev, rounds=3):
+    """What DistributedDataParallel (bucketed gradient all-reduce over RCCL)
+    costs one GPU: the same train step on a copy of the model, plain and
+    wrapped in DDP inside a one-rank nccl (RCCL) group, alternated `rounds`
+    times on this lease, best of each.  At world size 1 the all-reduce moves
+    nothing between GPUs, so this is the per-step DDP tax (reducer hooks,
+    bucket copies, the RCCL launch) the N-GPU scaling pays on top of xGMI."""
+    import copy
+
+    from datamining_recblr_amd.distributed import LossModule, single_rank_group
+
+    twin = copy.deepcopy(model)
+    opt = torch.optim.Adam(twin.parameters(), lr=1e-3, fused=True)
+    plain = LossModule(twin)
+    env1 = single_rank_group("nccl")
+    try:
+        ddp = wrap_ddp(twin, env1)
+
+        def run(mod, n):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(n):
+                opt.zero_grad(set_to_none=True)
+                mod(batches[i % len(batches)]).backward()
+                opt.step()
+            torch.cuda.synchronize()
+            return 1000.0 * (time.perf_counter() - t0) / n
+
+        run(plain, 3)
+        run(ddp, 3)
+        p_ms, d_ms = [], []
+        for _ in range(rounds):
+            p_ms.append(run(plain, args.steps))
+            d_ms.append(run(ddp, args.steps))
+    finally:
+        dist.destroy_process_group()
+    p, d = min(p_ms), min(d_ms)
+    return {"plain_ms_per_step": round(p, 3), "ddp_ms_per_step": round(d, 3),
+            "overhead_frac": round(d / p - 1.0, 4), "backend": "nccl (RCCL), world size 1",
+            "note": "same lease, same step on a copy of the model, alternated plain/DDP "
+                    f"{rounds}x{args.steps} steps, best of each"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,12 +308,14 @@ def main():
     ap.add_argument("--layers", type=int, default=2)
     ap.add_argument("--n-items", type=int, default=10544)
     ap.add_argument("--dropout", type=float, default=0.2)
-    ap.add_argument("--cpu-sample", type=int, default=32)
+    ap.add_argument("--cpu-sample", type=int, default=128)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--c5-batch", type=int, default=1024,
                     help="sequences per GPU of the long-sequence bf16 run (configs[4])")
     ap.add_argument("--no-c5", action="store_true", help="skip the configs[4] run")
+    ap.add_argument("--no-ddp-ab", action="store_true",
+                    help="skip the single-GPU DDP overhead A/B (N=1 only)")
     ap.add_argument("--no-full-tail", action="store_true",
                     help="skip the comparison run that evaluates the last layer's "
                          "position-wise tail at every position")
@@ -323,6 +425,17 @@ def main():
         return {"value": round(env.world_size * args.batch * args.steps / el, 1),
                 "ms_per_step": round(1000.0 * el / args.steps, 3)}
 
+    fixed = None
+    if not args.no_full_tail:
+        full_len = [synthetic_interaction(args.batch, args.seq_len, args.n_items, dev,
+                                          seed=1000 * env.rank + 50 + i, fixed_len=True)
+                    for i in range(4)]
+        saved, batches[:] = list(batches), full_len
+        fixed = timed_variant(True, True)
+        batches[:] = saved
+        fixed["note"] = (f"every sequence of full length {args.seq_len} (packed == dense "
+                         "rows), the same step otherwise: a length-independent companion to "
+                         "the headline, whose lengths are ~U{1..L}")
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)
@@ -397,6 +510,9 @@ def main():
             "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
             "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    ddp_ab = None
+    if env.world_size == 1 and not args.no_ddp_ab:
+        ddp_ab = ddp_overhead(args, model, batches, dev)
     scan = scan_microbench(args, dev) if env.rank == 0 else None
     c5 = None if args.no_c5 else long_seq_c5(args, env, dev)   # every rank (weak scaling)
     cpu = None
@@ -425,6 +541,8 @@ def main():
             "gemm": gemm,
             "optimizer": optimizer,
             "kernels": kernels_report,
+            "fixed_length": fixed,
+            "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,
             "scan_fwd_only": scan,

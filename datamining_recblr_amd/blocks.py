@@ -28,9 +28,27 @@ __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout
            "feed_forward"]
 
 
+_GOLDEN = 0x9E3779B97F4A7C15   # odd 64-bit constant (2^64 / golden ratio)
+
+
+def _rank() -> int:
+    dist = torch.distributed
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
 def draw_seed() -> int:
-    """63-bit dropout seed from torch's default generator (host side, no sync)."""
-    return int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    """63-bit dropout seed from torch's default generator (host side, no sync).
+
+    The process-group rank is folded into the key: every rank seeds its
+    generator alike (RecBole seeds all processes with the same config seed),
+    so without it all data-parallel ranks would draw identical dropout masks
+    for their different batch shards.  Rank 0 (and a single process) keeps
+    the generator's value unchanged."""
+    s = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    r = _rank()
+    if r:
+        s = (s + r * _GOLDEN) % (2 ** 62)
+    return s
 
 
 def _drop(dropout: torch.nn.Dropout, training: bool):

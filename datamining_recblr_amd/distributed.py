@@ -16,7 +16,7 @@ import torch.distributed as dist
 from torch import nn
 
 __all__ = ["DistEnv", "init_from_env", "LossModule", "wrap_ddp", "synthetic_interaction",
-           "max_over_ranks", "shard_range", "barrier"]
+           "max_over_ranks", "shard_range", "barrier", "single_rank_group"]
 
 
 class DistEnv:
@@ -75,11 +75,14 @@ def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float = 32.0) -> nn.
 
 
 def synthetic_interaction(batch: int, seq_len: int, n_items: int, device, seed: int,
-                          with_neg: bool = False) -> dict:
-    """RecBole-shaped batch: ids ~ U{1..n_items-1}, lengths ~ U{1..seq_len},
-    sequences right-padded with item 0 past their length."""
+                          with_neg: bool = False, fixed_len: bool = False) -> dict:
+    """RecBole-shaped batch: ids ~ U{1..n_items-1}, lengths ~ U{1..seq_len}
+    (every length = seq_len with fixed_len), sequences right-padded with item
+    0 past their length."""
     g = torch.Generator(device="cpu").manual_seed(seed)
     lengths = torch.randint(1, seq_len + 1, (batch,), generator=g)
+    if fixed_len:
+        lengths = torch.full_like(lengths, seq_len)
     seq = torch.randint(1, n_items, (batch, seq_len), generator=g)
     seq = seq * (torch.arange(seq_len)[None, :] < lengths[:, None])
     inter = {"item_id_list": seq, "item_length": lengths,
@@ -90,6 +93,22 @@ def synthetic_interaction(batch: int, seq_len: int, n_items: int, device, seed: 
     from .model import attach_host_lengths
     attach_host_lengths(out["item_length"], lengths)
     return out
+
+
+def single_rank_group(backend: str = "nccl"):
+    """Join a one-process group (world size 1) on a free local port, for
+    bench.py's DDP-overhead A/B on a single GPU; returns a DistEnv whose
+    `distributed` is True.  The caller destroys the group."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    store = dist.TCPStore("127.0.0.1", port, 1, True)
+    dist.init_process_group(backend=backend, store=store, rank=0, world_size=1)
+    return DistEnv(0, torch.cuda.current_device() if torch.cuda.is_available() else 0, 1,
+                   forced=True)
 
 
 def shard_range(global_batch: int, rank: int, world: int):

@@ -121,18 +121,26 @@ def _layer_norm(p, prefix, x):
     return F.layer_norm(x, (x.shape[-1],), p[prefix + "weight"], p[prefix + "bias"], eps=1e-12)
 
 
-def ffn_forward(p, prefix: str, x: torch.Tensor) -> torch.Tensor:
-    """FeedForward.forward (RecBLR.py:218-227), dropout = identity (eval)."""
-    h = F.silu(x @ p[prefix + "w_1.weight"].t() + p[prefix + "w_1.bias"])
-    h = h @ p[prefix + "w_2.weight"].t() + p[prefix + "w_2.bias"]
+def _drop(x, p_drop):
+    """nn.Dropout in train mode (p_drop > 0) or eval (identity)."""
+    return F.dropout(x, p_drop, training=True) if p_drop > 0 else x
+
+
+def ffn_forward(p, prefix: str, x: torch.Tensor, p_drop: float = 0.0) -> torch.Tensor:
+    """FeedForward.forward (RecBLR.py:218-227); dropout after the SiLU (:221)
+    and after w_2 (:224) when p_drop > 0 (train mode), identity otherwise."""
+    h = _drop(F.silu(x @ p[prefix + "w_1.weight"].t() + p[prefix + "w_1.bias"]), p_drop)
+    h = _drop(h @ p[prefix + "w_2.weight"].t() + p[prefix + "w_2.bias"], p_drop)
     return _layer_norm(p, prefix + "layer_norm.", h + x)
 
 
-def recurrent_layer_forward(p, prefix: str, x, disable_conv1d=False, disable_ffn=False):
-    """RecurrentLayer.forward (RecBLR.py:140-145), dropout = identity (eval)."""
-    h = grl_forward(p, prefix + "behavior_modeling.", x, disable_conv1d)
+def recurrent_layer_forward(p, prefix: str, x, disable_conv1d=False, disable_ffn=False,
+                            p_drop: float = 0.0):
+    """RecurrentLayer.forward (RecBLR.py:140-145); dropout on the GRL output
+    (:142) when p_drop > 0."""
+    h = _drop(grl_forward(p, prefix + "behavior_modeling.", x, disable_conv1d), p_drop)
     h = _layer_norm(p, prefix + "layer_norm.", h + x)
-    return h if disable_ffn else ffn_forward(p, prefix + "ffn.", h)
+    return h if disable_ffn else ffn_forward(p, prefix + "ffn.", h, p_drop)
 
 
 def _flags(cfg):
@@ -142,20 +150,23 @@ def _flags(cfg):
     return dc, df
 
 
-def model_forward(p, cfg, item_seq, item_seq_len):
-    """RecBLR.forward (RecBLR.py:75-84) in eval mode -> seq_output [B, d]."""
+def model_forward(p, cfg, item_seq, item_seq_len, p_drop: float = 0.0):
+    """RecBLR.forward (RecBLR.py:75-84) -> seq_output [B, d]; eval mode, or
+    train-mode dropout at the reference's four sites when p_drop > 0 (used
+    only by bench.py's CPU baseline, whose timed step matches the GPU's)."""
     dc, df = _flags(cfg)
-    emb = F.embedding(item_seq, p["item_embedding.weight"], padding_idx=0)
+    emb = _drop(F.embedding(item_seq, p["item_embedding.weight"], padding_idx=0), p_drop)
     h = _layer_norm(p, "layer_norm.", emb)
     for li in range(cfg["num_layers"]):
-        h = recurrent_layer_forward(p, f"recurrent_layers.{li}.", h, dc, df)
+        h = recurrent_layer_forward(p, f"recurrent_layers.{li}.", h, dc, df, p_drop)
     idx = (item_seq_len - 1).view(-1, 1, 1).expand(-1, -1, h.shape[-1])
     return h.gather(1, idx).squeeze(1)
 
 
-def calculate_loss(p, cfg, item_seq, item_seq_len, pos_items, neg_items=None):
+def calculate_loss(p, cfg, item_seq, item_seq_len, pos_items, neg_items=None,
+                   p_drop: float = 0.0):
     """RecBLR.calculate_loss (RecBLR.py:86-103): CE over all items, or BPR."""
-    seq = model_forward(p, cfg, item_seq, item_seq_len)
+    seq = model_forward(p, cfg, item_seq, item_seq_len, p_drop)
     table = p["item_embedding.weight"]
     if cfg["loss_type"] == "BPR":
         pos = (seq * table[pos_items]).sum(-1)

@@ -28,3 +28,21 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.fail("GPU test selected but torch.cuda.is_available() is False")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def split_gemm_calls(monkeypatch):
+    """Records every launch of the split-bf16 GEMM (kernels.gemm_nt, the
+    rb_gemm_nt C-ABI entry) as (M, R, C): tests use it to assert that the
+    path they claim to check actually ran the kernel."""
+    from datamining_recblr_amd import kernels
+
+    calls = []
+    orig = kernels.gemm_nt
+
+    def counted(a, wf, C, *args, **kw):
+        calls.append((a.shape[0], a.shape[1], C))
+        return orig(a, wf, C, *args, **kw)
+
+    monkeypatch.setattr(kernels, "gemm_nt", counted)
+    return calls

@@ -75,3 +75,41 @@ def test_ddp_gloo_world2_matches_full_batch():
         assert tmax == float(world)
         for n, p in ref.named_parameters():
             torch.testing.assert_close(torch.from_numpy(grads[n]), p.grad, atol=1e-6, rtol=1e-5)
+
+
+def _seed_worker(rank, world, port, queue):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from datamining_recblr_amd.blocks import draw_seed
+    from datamining_recblr_amd.distributed import init_from_env
+
+    init_from_env(backend="gloo")
+    torch.manual_seed(2020)          # every rank seeds alike (RecBole's config seed)
+    queue.put((rank, [draw_seed() for _ in range(3)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dropout_keys_differ_across_ranks():
+    """The Philox dropout key folds in the rank: equal generator seeds on two
+    ranks still give different masks for their different batch shards; rank 0
+    keeps the single-process stream."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_seed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from datamining_recblr_amd.blocks import draw_seed
+
+    torch.manual_seed(2020)
+    single = [draw_seed() for _ in range(3)]
+    assert got[0] == single
+    assert all(a != b for a, b in zip(got[0], got[1]))
+    assert all(0 <= s < 2 ** 62 for s in got[1])

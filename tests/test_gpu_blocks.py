@@ -150,14 +150,16 @@ def test_silu_dropout(cuda, mode):
 
 
 @pytest.mark.parametrize("p", [0.0, 0.2])
-def test_fused_feed_forward(cuda, p):
+def test_fused_feed_forward(cuda, p, split_gemm_calls):
     """_FeedForward (two GEMMs, SiLU+dropout, dropout+residual+LN, folded bias
-    grads, residual grad through addmm) == the reference FeedForward math."""
+    grads, residual grad through addmm) == the reference FeedForward math.
+    M = 5000 rows: above SPLIT_MIN_ROWS, so all four fwd/dX GEMMs run the
+    split-bf16 kernel (asserted)."""
     from datamining_recblr_amd import kernels
     from datamining_recblr_amd.blocks import _FeedForward
 
     g = torch.Generator(device="cpu").manual_seed(21)
-    M, d = 3000, 128
+    M, d = 5000, 128
     x = torch.randn(M, d, generator=g).to(cuda).requires_grad_()
     w1 = (0.05 * torch.randn(4 * d, d, generator=g)).to(cuda).requires_grad_()
     b1 = (0.1 * torch.randn(4 * d, generator=g)).to(cuda).requires_grad_()
@@ -169,6 +171,8 @@ def test_fused_feed_forward(cuda, p):
     s1, s2 = 31, 32
     y = _FeedForward.apply(x, w1, b1, w2, b2, gamma, beta, s1, s2, p, 1e-12)
     y.backward(dy)
+    assert sorted(split_gemm_calls) == sorted([(M, d, 4 * d), (M, 4 * d, d), (M, d, 4 * d),
+                                               (M, 4 * d, d)]), split_gemm_calls
     leaves = [t.detach().clone().requires_grad_() for t in (x, w1, b1, w2, b2, gamma, beta)]
     xr, w1r, b1r, w2r, b2r, gr, br = leaves
     h = F.silu(F.linear(xr, w1r, b1r))

@@ -69,9 +69,12 @@ def test_row_strided_operand_and_output(cuda):
     assert outbig[:, 256:].abs().max().item() == 0.0
 
 
-def test_split_path_in_the_encoder_matches_torch_path(cuda, monkeypatch):
-    """The whole training step with RECBLR_SPLIT_GEMM=1 against the default
-    (hipBLASLt) path: same loss and gradients within fp32 re-association."""
+def test_split_path_in_the_encoder_matches_torch_path(cuda, monkeypatch, split_gemm_calls):
+    """The whole training step with the split-bf16 GEMM against the torch
+    (hipBLASLt) path: same loss and gradients within fp32 re-association.
+    B = 256, L = 50 (ntok ~ 6.5k, above SPLIT_MIN_ROWS) and the threshold at 0
+    in the split arm, so every projection of that arm runs rb_gemm_nt (asserted)
+    and none of the torch arm does."""
     from datamining_recblr_amd import linear
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
@@ -81,7 +84,7 @@ def test_split_path_in_the_encoder_matches_torch_path(cuda, monkeypatch):
                MAX_ITEM_LIST_LENGTH=50)
     torch.manual_seed(0)
     model = RecBLR(cfg, SyntheticDataset(500)).to(cuda)
-    B, L = 128, 50
+    B, L = 256, 50
     g = torch.Generator().manual_seed(1)
     lengths = torch.randint(1, L + 1, (B,), generator=g)
     seq = torch.randint(1, 500, (B, L), generator=g) * (torch.arange(L)[None] < lengths[:, None])
@@ -90,9 +93,17 @@ def test_split_path_in_the_encoder_matches_torch_path(cuda, monkeypatch):
     res = {}
     for on in (False, True):
         monkeypatch.setattr(linear, "_split_on", on)
+        monkeypatch.setattr(linear, "SPLIT_MIN_ROWS", 0 if on else 4096)
+        n0 = len(split_gemm_calls)
         model.zero_grad()
         loss = model.calculate_loss(inter)
         loss.backward()
+        launched = len(split_gemm_calls) - n0
+        if on:
+            assert launched >= 16, split_gemm_calls
+            assert any(c[0] >= 4096 for c in split_gemm_calls)
+        else:
+            assert launched == 0, split_gemm_calls
         res[on] = (loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()
                                  if p.grad is not None})
     assert abs(res[True][0] - res[False][0]) < 1e-5
