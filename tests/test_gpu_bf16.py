@@ -13,8 +13,11 @@ against fp32 computations fed the SAME bf16-rounded inputs:
   bit-identical), partial sums to 1e-4;
 * layer level — GatedRecurrentLayer on bf16 activations (bf16 MFMA GEMMs with
   fp32 accumulation) against the CPU oracle (oracle/recblr_oracle.py, fp32)
-  on the same bf16-rounded input: within 3e-2 of max|ref|, the expected bf16
-  storage error (2^-8 relative per rounding, a few roundings deep)."""
+  on the same bf16-rounded input: within 1.2e-2 of max|ref| — twice the
+  worst error measured over 5 seeds x 2 shapes on MI355X (6.2e-3 on y,
+  <= 5.8e-3 on dx and every parameter gradient; profiles/r02_bf16_err.json,
+  tools/bf16_err.py): bf16 storage error, 2^-9 relative per rounding, a few
+  roundings deep."""
 import pytest
 import torch
 
@@ -155,8 +158,9 @@ def test_grl_bf16_vs_oracle(cuda, B, L, d):
     def rel(a, b):
         return ((a.float().cpu() - b).abs().max() / b.abs().max()).item()
 
-    assert rel(y.detach(), ys.detach()) < 3e-2
-    assert rel(x.grad, xs.grad) < 3e-2
+    tol = 1.2e-2   # 2x the measured worst case (profiles/r02_bf16_err.json)
+    assert rel(y.detach(), ys.detach()) < tol
+    assert rel(x.grad, xs.grad) < tol
     for n, p in layer.named_parameters():
         assert p.grad.dtype == torch.float32
-        assert rel(p.grad, params[n].grad) < 5e-2, n
+        assert rel(p.grad, params[n].grad) < tol, n

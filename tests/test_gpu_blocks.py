@@ -382,7 +382,11 @@ def test_gate_scan_last_only_equals_full(cuda):
     y, car = kernels.gate_scan_fwd(rg, xc, z, lam, h0, gate_b=gb, seq=seq)
     yl, carl = kernels.gate_scan_fwd(rg, xc, z, lam, h0, gate_b=gb, seq=seq, last_only=True)
     assert torch.equal(yl, y.index_select(0, last))
-    assert torch.equal(carl, car)
+    # carries [B, nT, H]: a packed sequence writes only its own ceil(len / 16)
+    # tiles; the rest of the buffer is never written (torch.empty) nor read
+    for s in range(B):
+        nt = (int(lens[s]) + kernels.RB_TILE - 1) // kernels.RB_TILE
+        assert torch.equal(carl[s, :nt], car[s, :nt]), s
     dyl = torch.randn(B, H, generator=g).to(cuda)
     dy = torch.zeros(ntok, H, device=cuda)
     dy.index_copy_(0, last, dyl)

@@ -35,5 +35,8 @@ if [ -z "$NO_PROF" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bench \
       -- python3 bench.py --no-cpu-baseline --no-full-tail --no-c5 --no-ddp-ab > $OUT/prof.log 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -c 300 $OUT/prof.log
+  # keep the summaries, drop the (large) per-dispatch trace
+  cp $OUT/prof/bench_kernel_stats.csv $OUT/prof_kernel_stats.csv 2>/dev/null
+  rm -rf $OUT/prof
 fi
 exit $rc
