@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 22
+ABI_VERSION = 23
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -58,6 +58,8 @@ SIGNATURES = {
     "rb_row_num_parts": (ctypes.c_int64, [_i64, _i64]),
     "rb_add_ln_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _u64, _f32, _fp, _fp, _fp, _fp,
                                      _fp, _i64, _i64, _i64, _fp]),
+    "rb_add_ln_bwd2": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _fp, _u64, _f32, _fp, _fp, _fp, _fp,
+                                     _fp, _i64, _i64, _i64, _fp]),
     "rb_silu_dropout_fwd": (ctypes.c_int, [_fp, _fp, _fp, _u64, _f32, _fp, _i64, _i64, _fp]),
     "rb_silu_dropout_bwd": (ctypes.c_int, [_fp, _fp, _fp, _u64, _f32, _fp, _fp, _fp, _i64, _i64,
                                            _i64, _fp]),
@@ -94,6 +96,10 @@ SIGNATURES = {
     "rb_pack_plan": (ctypes.c_int, [_fp, _i64, _fp, _fp, _i64, _i64, _fp, _fp, _fp, _fp, _fp]),
     "rb_gemm_nt": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
                                   _fp]),
+    "rb_gemm_h_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
+    "rb_gemm_h_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
+    "rb_gemm_nt_h": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
+                                    _fp, _fp]),
 }
 
 

@@ -13,7 +13,10 @@ torch's own GPU ops.
 The FeedForward block is one autograd function: w_1 GEMM -> SiLU+dropout ->
 w_2 GEMM -> dropout+residual+LayerNorm.  Its backward takes both bias
 gradients from column partials of the row kernels (no separate reduction
-passes) and adds the residual gradient inside the dX GEMM (beta = 1).
+passes).  Residual gradients are never summed in a pass of their own: a
+tensor read by a projection and by a residual branch gets the residual's
+gradient added by its producer's LayerNorm backward while it loads the
+projection's input gradient (ResidualGrad, rb_add_ln_bwd2's dy2).
 """
 from __future__ import annotations
 
@@ -63,30 +66,54 @@ def _require_gpu(t):
 
 
 class ResidualGrad:
-    """Carries the residual branch's gradient of RecurrentLayer (RecBLR.py:142,
-    LN(dropout(GRL(x)) + x)) from the LayerNorm backward to the backward of
-    the GRL's input projection, whose dX GEMM adds it with beta = 1
-    (linear.LinearFn) instead of autograd summing two [B, L, d] gradients in
-    a separate pass.  The LayerNorm backward always runs first (the
-    projection's gradient depends on it).  ``rows``: when the LayerNorm ran
-    on a gathered subset of the positions (the last layer, see
-    RecBLR.forward), the flat [B*L] rows its residual came from."""
-    __slots__ = ("ds", "rows")
+    """A second gradient of one tensor, handed from the consumer that computes
+    it to the producer of the tensor, whose LayerNorm backward adds it while
+    loading its output gradient (rb_add_ln_bwd2's dy2) — instead of autograd
+    summing two [rows, d] gradients in a separate pass.
+
+    Uses: the residual branch of RecurrentLayer (RecBLR.py:142,
+    LN(dropout(GRL(x)) + x)): its LayerNorm backward sets ``ds``, the GRL's
+    input projection leaves it (``taken``: x's producer, the previous layer's
+    FeedForward or the embedding LayerNorm, registered to add it) and x's
+    producer adds it; the FeedForward's own residual (RecBLR.py:227) handed to
+    the LayerNorm that produced its input.  The consumer's backward always
+    runs before the producer's.  ``rows``: when the residual LayerNorm ran on
+    a gathered subset of the positions (the last layer, see RecBLR.forward),
+    the flat rows its residual came from (then the input projection adds it
+    with index_add, and no producer takes it)."""
+    __slots__ = ("ds", "rows", "taken")
 
     def __init__(self, rows=None):
         self.ds = None
         self.rows = rows
+        self.taken = False
+
+
+def _take(addend):
+    """Register a producer for `addend` (it will add addend.ds itself)."""
+    if addend is not None and addend.rows is None:
+        addend.taken = True
+        return addend
+    return None
+
+
+def _pop(addend):
+    if addend is None:
+        return None
+    ds, addend.ds = addend.ds, None
+    return ds
 
 
 class _AddDropoutLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, a, r, gamma, beta, mask, seed, p, eps, slot=None):
+    def forward(ctx, a, r, gamma, beta, mask, seed, p, eps, slot=None, addend=None):
         d = a.shape[-1]
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a.reshape(-1, d).contiguous(),
                                               r.reshape(-1, d).contiguous(), gamma, beta, eps,
                                               mask=mask, seed=seed, p=p, save=save)
         ctx.seed, ctx.p, ctx.slot = seed, p, slot
+        ctx.addend = _take(addend)
         ctx.save_for_backward(s, mean, rstd, gamma, mask)
         return y.view(a.shape)
 
@@ -96,13 +123,14 @@ class _AddDropoutLN(torch.autograd.Function):
         need_a, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
         ds, da, dg, db, _ = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask=mask,
                                                seed=ctx.seed, p=ctx.p, want_ds=need_r,
-                                               want_da=need_a or not need_r)
+                                               want_da=need_a or not need_r,
+                                               dy2=_pop(ctx.addend))
         shape = dy.shape
         if need_r and ctx.slot is not None:   # handed to the GRL input projection
             ctx.slot.ds = ds
             ds, need_r = None, False
         return (da.view(shape) if need_a else None, ds.view(shape) if need_r else None,
-                dg, db, None, None, None, None, None)
+                dg, db, None, None, None, None, None, None)
 
 
 _side_streams = {}
@@ -117,7 +145,7 @@ def _side_stream(device) -> torch.cuda.Stream:
 
 class _EmbedDropoutLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, table, idx, gamma, beta, mask, seed, p, eps, padding_idx):
+    def forward(ctx, table, idx, gamma, beta, mask, seed, p, eps, padding_idx, addend=None):
         save = any(ctx.needs_input_grad)
         flat = idx.reshape(-1).contiguous()
         plan = event = None
@@ -136,6 +164,7 @@ class _EmbedDropoutLN(torch.autograd.Function):
         ctx.seed, ctx.p = seed, p
         ctx.padding_idx, ctx.num_rows = padding_idx, table.shape[0]
         ctx.plan, ctx.event = plan, event
+        ctx.addend = _take(addend)
         ctx.save_for_backward(s, mean, rstd, gamma, mask, flat)
         return y.view(*idx.shape, table.shape[1])
 
@@ -144,7 +173,7 @@ class _EmbedDropoutLN(torch.autograd.Function):
         s, mean, rstd, gamma, mask, flat = ctx.saved_tensors
         _, da, dg, db, _ = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, mask=mask,
                                               seed=ctx.seed, p=ctx.p, want_ds=False,
-                                              want_da=True)
+                                              want_da=True, dy2=_pop(ctx.addend))
         dtable = None
         if ctx.needs_input_grad[0]:
             if ctx.event is not None:
@@ -154,7 +183,7 @@ class _EmbedDropoutLN(torch.autograd.Function):
             if ctx.plan is not None:   # allocated on the side stream, last used here
                 ctx.plan.record_stream(torch.cuda.current_stream(da.device))
             ctx.plan = ctx.event = None
-        return dtable, None, dg, db, None, None, None, None, None
+        return dtable, None, dg, db, None, None, None, None, None, None
 
 
 class _SiluDropout(torch.autograd.Function):
@@ -176,7 +205,8 @@ class _FeedForward(torch.autograd.Function):
     """LN(dropout(W2 dropout(silu(W1 x + b1)) + b2) + x), RecBLR.py:218-227."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, seed1, seed2, p, eps):
+    def forward(ctx, x, w1, b1, w2, b2, gamma, beta, seed1, seed2, p, eps, in_addend=None,
+                out_addend=None):
         d = x.shape[-1]
         x2 = x.reshape(-1, d)
         M, inner = x2.shape[0], w1.shape[0]
@@ -190,6 +220,9 @@ class _FeedForward(torch.autograd.Function):
         y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
                                               p=p, save=save)
         ctx.seed1, ctx.seed2, ctx.p = seed1, seed2, p
+        # in_addend: x's producer takes the residual's gradient (see ResidualGrad)
+        ctx.in_addend = in_addend if in_addend is not None and in_addend.taken else None
+        ctx.out_addend = _take(out_addend)
         ctx.save_for_backward(x2, a1, u, s, mean, rstd, w1, b1, w2, gamma)
         return y.view(x.shape)
 
@@ -200,36 +233,45 @@ class _FeedForward(torch.autograd.Function):
         f = 2 * M * d * w1.shape[0]
         ds, da2, dgamma, dbeta, db2 = kernels.add_ln_bwd(
             dy, s, gamma, mean, rstd, seed=ctx.seed2, p=ctx.p, want_ds=True, want_da=True,
-            want_dbias=True)
+            want_dbias=True, dy2=_pop(ctx.out_addend))
         du = _timed("gemm", f, mm_nn, da2, w2)
         dw2 = _timed("gemm", f, wgrad, da2, u)
         da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True,
                                             bias=b1)
-        dx = _timed("gemm", f, mm_nn, da1, w1, ds)   # residual grad + W1^T path, in place
+        dx = _timed("gemm", f, mm_nn, da1, w1)
+        if ctx.in_addend is not None:   # x's producer adds the residual's gradient
+            ctx.in_addend.ds = ds
+        else:
+            dx.add_(ds)
         dw1 = _timed("gemm", f, wgrad, da1, x2)
-        return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None)
+        return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None,
+                None, None)
 
 
 def add_dropout_layer_norm(a, residual, dropout: torch.nn.Dropout, ln: torch.nn.LayerNorm,
-                           training: bool, slot: ResidualGrad | None = None):
+                           training: bool, slot: ResidualGrad | None = None,
+                           addend: ResidualGrad | None = None):
     """ln(dropout(a) + residual) — RecBLR.py:142.  With `slot`, the residual's
-    gradient is handed over instead of returned (see ResidualGrad)."""
+    gradient is handed over instead of returned; `addend`: a second gradient
+    of the output that its consumer hands back (see ResidualGrad)."""
     _require_gpu(a)
     if a.shape[-1] not in kernels.ROW_SIZES:
         return ln(dropout(a) + residual)
     p, seed = _drop(dropout, training)
-    return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, None, seed, p, ln.eps, slot)
+    return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, None, seed, p, ln.eps, slot,
+                               addend)
 
 
 def embed_dropout_layer_norm(idx, emb: torch.nn.Embedding, dropout: torch.nn.Dropout,
-                             ln: torch.nn.LayerNorm, training: bool):
-    """ln(dropout(emb(idx))) — RecBLR.py:76-78."""
+                             ln: torch.nn.LayerNorm, training: bool,
+                             addend: ResidualGrad | None = None):
+    """ln(dropout(emb(idx))) — RecBLR.py:76-78 (`addend`: see ResidualGrad)."""
     _require_gpu(emb.weight)
     if emb.weight.shape[1] not in kernels.ROW_SIZES:
         return ln(dropout(emb(idx)))
     p, seed = _drop(dropout, training)
     return _EmbedDropoutLN.apply(emb.weight, idx, ln.weight, ln.bias, None, seed, p, ln.eps,
-                                 emb.padding_idx)
+                                 emb.padding_idx, addend)
 
 
 def silu_dropout(a, dropout: torch.nn.Dropout, training: bool):
@@ -241,8 +283,11 @@ def silu_dropout(a, dropout: torch.nn.Dropout, training: bool):
     return _SiluDropout.apply(a, None, seed, p)
 
 
-def feed_forward(x, ffn, training: bool):
-    """The whole FeedForward block (RecBLR.py:218-227) as one fused function."""
+def feed_forward(x, ffn, training: bool, in_addend: ResidualGrad | None = None,
+                 out_addend: ResidualGrad | None = None):
+    """The whole FeedForward block (RecBLR.py:218-227) as one fused function.
+    in_addend: the slot through which x's producer takes the block's residual
+    gradient; out_addend: a second gradient of the output (see ResidualGrad)."""
     _require_gpu(x)
     d, inner = x.shape[-1], ffn.w_1.weight.shape[0]
     if d not in kernels.ROW_SIZES or inner not in kernels.ROW_SIZES:
@@ -253,4 +298,4 @@ def feed_forward(x, ffn, training: bool):
     seed2 = draw_seed() if p > 0.0 else 0
     return _FeedForward.apply(x, ffn.w_1.weight, ffn.w_1.bias, ffn.w_2.weight, ffn.w_2.bias,
                               ffn.layer_norm.weight, ffn.layer_norm.bias, seed1, seed2, p,
-                              ffn.layer_norm.eps)
+                              ffn.layer_norm.eps, in_addend, out_addend)

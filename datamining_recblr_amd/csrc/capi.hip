@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 22; }
+int rb_version(void) { return 23; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -314,19 +314,27 @@ int64_t rb_row_num_parts(int64_t rows, int64_t width) {
   return ln_num_parts(rows, width);
 }
 
-int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
-                  const float* rstd, const uint8_t* mask, uint64_t seed, float p, float* ds,
-                  float* da, float* dgamma_part, float* dbeta_part, float* dbias_part,
-                  int64_t n_parts, int64_t rows, int64_t d, void* stream) {
+int rb_add_ln_bwd2(const float* dy, const float* dy2, const float* s, const float* gamma,
+                   const float* mean, const float* rstd, const uint8_t* mask, uint64_t seed,
+                   float p, float* ds, float* da, float* dgamma_part, float* dbeta_part,
+                   float* dbias_part, int64_t n_parts, int64_t rows, int64_t d, void* stream) {
   if (!dy || !s || !gamma || !mean || !rstd || !dgamma_part || !dbeta_part)
     return fail("rb_add_ln_bwd: null pointer");
   if (!ds && !da && !dbias_part) return fail("rb_add_ln_bwd: nothing to write");
   if (rows <= 0 || d <= 0) return fail("rb_add_ln_bwd: rows and d must be positive");
   if (!(p >= 0.0f && p < 1.0f)) return fail("rb_add_ln_bwd: dropout p must be in [0, 1)");
   if (n_parts != ln_num_parts(rows, d)) return fail("rb_add_ln_bwd: n_parts != rb_row_num_parts");
-  return launch_add_ln_bwd(dy, s, gamma, mean, rstd, make_drop(mask, seed, p), ds, da,
+  return launch_add_ln_bwd(dy, dy2, s, gamma, mean, rstd, make_drop(mask, seed, p), ds, da,
                            dgamma_part, dbeta_part, dbias_part, n_parts, rows, d,
                            reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
+                  const float* rstd, const uint8_t* mask, uint64_t seed, float p, float* ds,
+                  float* da, float* dgamma_part, float* dbeta_part, float* dbias_part,
+                  int64_t n_parts, int64_t rows, int64_t d, void* stream) {
+  return rb_add_ln_bwd2(dy, nullptr, s, gamma, mean, rstd, mask, seed, p, ds, da, dgamma_part,
+                        dbeta_part, dbias_part, n_parts, rows, d, stream);
 }
 
 int rb_silu_dropout_fwd(const float* a, const float* bias, const uint8_t* mask, uint64_t seed,
@@ -556,6 +564,38 @@ int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf
   if ((M + 127) / 128 * (C / 128) > 0x7fffffffLL) return fail("rb_gemm_nt: grid too large");
   return launch_gemm_nt(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate,
                         reinterpret_cast<hipStream_t>(stream));
+}
+
+int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R) { return C * R * 4 + ((C * 4 + 15) / 16) * 16; }
+
+int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {
+  if (!jobs || n < 1 || n > RB_MAX_SPLIT_JOBS)
+    return fail("rb_gemm_h_split_weights: need 1..RB_MAX_SPLIT_JOBS jobs");
+  for (int64_t j = 0; j < n; ++j) {
+    const rb_split_job& b = jobs[j];
+    if (!b.W || !b.Wf) return fail("rb_gemm_h_split_weights: null pointer");
+    if (b.C <= 0 || b.R <= 0 || b.C % 32 || b.R % 16 || b.C > (1 << 20) || b.R > (1 << 20))
+      return fail("rb_gemm_h_split_weights: C must be a multiple of 32 and R of 16");
+    if (b.ldw < (b.transpose ? b.C : b.R)) return fail("rb_gemm_h_split_weights: bad row stride");
+    if (!aligned16(b.Wf)) return fail("rb_gemm_h_split_weights: Wf must be 16-byte aligned");
+  }
+  return launch_split_weights_h(jobs, (int)n, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                 const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
+                 void* stream) {
+  if (!A || !Wf || !out) return fail("rb_gemm_nt_h: null pointer");
+  if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt_h: empty shape");
+  if (accumulate) return fail("rb_gemm_nt_h: accumulate is not supported (add the residual in its consumer)");
+  if (R % 32 || C % 128 || R > (1 << 16) || C > 1024)
+    return fail("rb_gemm_nt_h: R must be a multiple of 32 and C of 128 (C <= 1024)");
+  if (lda < R || lda % 4 || ldo < C || ldo % 2) return fail("rb_gemm_nt_h: bad row strides");
+  if (!aligned16(A) || !aligned16(Wf) || (reinterpret_cast<uintptr_t>(out) & 7))
+    return fail("rb_gemm_nt_h: A and Wf must be 16-byte aligned, out 8-byte aligned");
+  if ((M + 255) / 256 * (C / 128) > 0x7fffffffLL) return fail("rb_gemm_nt_h: grid too large");
+  return launch_gemm_nt_h(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate, rmax,
+                          reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

@@ -326,10 +326,10 @@ int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const Dr
                       const float* r, const float* gamma, const float* beta, float eps, float* y,
                       float* s_out, float* mean, float* rstd, int64_t rows, int64_t d,
                       hipStream_t st);
-int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
-                      const float* rstd, const DropSpec& drop, float* ds, float* da, float* dgp,
-                      float* dbp, float* dbiasp, int64_t nparts, int64_t rows, int64_t d,
-                      hipStream_t st);
+int launch_add_ln_bwd(const float* dy, const float* dy2, const float* s, const float* gamma,
+                      const float* mean, const float* rstd, const DropSpec& drop, float* ds,
+                      float* da, float* dgp, float* dbp, float* dbiasp, int64_t nparts,
+                      int64_t rows, int64_t d, hipStream_t st);
 int64_t ln_num_parts(int64_t rows, int64_t d);
 int launch_silu_dropout_fwd(const float* a, const float* bias, const DropSpec& drop, float* u,
                             int64_t rows, int64_t cols, hipStream_t st);
@@ -341,6 +341,10 @@ int launch_split_weight(const float* W, int64_t ldw, int C, int R, int transpose
                         hipStream_t st);
 int launch_gemm_nt(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                    const float* bias, float* out, int64_t ldo, int accumulate, hipStream_t st);
+int launch_split_weights_h(const rb_split_job* jobs, int n, hipStream_t st);
+int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                     const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
+                     hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
 int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, void* workspace,
                           int64_t ws_bytes, hipStream_t st);

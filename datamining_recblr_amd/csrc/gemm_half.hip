@@ -1,0 +1,626 @@
+// gemm_half.hip — fp32 projection GEMMs on the f16 MFMA pipe, 3 products.
+//
+// The encoder's projections (RecBLR.py:162,165,167,213,214 — nn.Linear in
+// fp32) are tall and skinny (ntok ~ 200k-410k rows, K, N in {128, 256, 512}):
+// at the HBM roofline they are bound by their row streams (the fp32 output
+// write or the fp32 input read), not by arithmetic, as soon as the
+// arithmetic runs at >= 1/3 of the bf16 pipe.  The six-product bf16 split
+// (gemm_split.hip) needs 6x the bf16 flops and is MFMA-bound at the tile
+// level; here each operand is split into TWO fp16 parts and three products
+// are accumulated:
+//     x = 2^-s (x0 + x1),  x0 = f16(x 2^s),  x1 = f16(x 2^s - x0)
+//     a.b ~= 2^-(sa+sb) (a0 b0 + a0 b1 + a1 b0)
+// fp16 carries 11 significant bits, so x0 + x1 holds 22 (|x - x0 - x1| <=
+// 2^-22 |x| for values near the scale, RNE), every product is exact in the
+// fp32 accumulator and the dropped a1 b1 is <= 2^-22 relative: the result is
+// within a few fp32 units of an fp32 GEMM (tests/test_gpu_gemm.py measures it
+// against fp64 beside hipBLASLt's fp32 kernels).  fp16's exponent range is
+// handled with power-of-two scales, which are exact:
+//   * weights (Bm [C, R]): one scale per output column c (a row of Bm), fixed
+//     when the image is built: the column max lands in [2^13, 2^14);
+//   * activations / gradients (A [M, R]): one scale per ROW (a row scale
+//     factors out of out[m, :]), chosen online: the first 16 k-values of a
+//     tile's row set its max to [2^3, 2^4), and 11 bits of headroom keep
+//     every later value < 2^15 (finite in fp16).  A later value beyond the
+//     headroom (rare: a row whose first 16 entries are all tiny or zero)
+//     re-scales that row — its accumulators are multiplied by the exact
+//     power-of-two ratio — so no input overflows and no row loses precision.
+//     Values far below their row max keep an absolute error <= 2^-29 of it
+//     (fp16 subnormal residuals), far below fp32 rounding of the dot product.
+// The output is un-scaled in the epilogue with v_ldexp (exact).
+//
+// k_gemm_nt_h: out[M, C] (+)= A[M, R] . Bm[C, R]^T (+ bias[C])
+//   One 512-thread workgroup per CU, persistent over 256 x 128 tiles, k-step
+//   32.  A (raw fp32, full 128-B row segments) and the pre-split weight
+//   fragments reach LDS by LDS-DMA (global_load_lds_dwordx4) into 3- and
+//   2-stage rings waited with counted vmcnt.  8 waves x 32 rows each: a wave
+//   DMAs, reads and splits only its own 32 rows (every A element is split
+//   once) and multiplies them by all 128 columns (4 blocks of
+//   v_mfma_f32_32x32x16_f16 x 3 products per k16).  The epilogue (un-scale,
+//   bias) is deferred by one tile and stored a block per k-step behind the
+//   next tile's MFMAs.  Per k-step the instruction stream is kept lean:
+//   DMA and store addresses are a wave-uniform base plus a constant 32-bit
+//   lane offset, tile coordinates advance incrementally (divisions once per
+//   tile), and the overflow check is one compare + ballot per k16.
+#include "common.h"
+
+namespace rb {
+namespace {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTA = 4;       // row scale target: first-k16 row max in [2^(kTA-1), 2^kTA)
+constexpr int kHead = 11;    // later values up to 2^(kTA + kHead) = 2^15 (fp16 max 65504)
+constexpr int kTW = 14;      // weight column scale target: column max in [2^13, 2^14)
+constexpr int kSent = -4096; // row exponent of a row that has been all zero so far
+
+// 2 fp32 (already scaled) -> hi, lo fp16 pairs (v_cvt_pk_f16_f32, RNE; the
+// residual is exact in fp32)
+__device__ __forceinline__ void split2h(f32x2 x, f16x2& h0, f16x2& h1) {
+  h0 = __builtin_convertvector(x, f16x2);
+  const f32x2 r = x - __builtin_convertvector(h0, f32x2);
+  h1 = __builtin_convertvector(r, f16x2);
+}
+
+__device__ __forceinline__ f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// max(|a|, |b|, |c|) in one instruction (no NaN canonicalisation: a NaN input
+// propagates to the output through the MFMA anyway)
+__device__ __forceinline__ float max3abs(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, |%1|, |%2|, |%3|" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+__device__ __forceinline__ float max8abs(f32x4 x, f32x4 y) {
+  float m = max3abs(x[0], x[1], x[2]);
+  m = max3abs(m, x[3], y[0]);
+  m = max3abs(m, y[1], y[2]);
+  float r;
+  asm("v_max_f32 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(y[3]));
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Weight image: Bm [C, R] (Bm = W, or W^T with transpose) ->
+//   planes: Wf[((cb * (R/16) + kb) * 2 + p) * 64 + lane] (16 B each) = plane p
+//     of Bm[cb*32 + (lane & 31)][kb*16 + 8*(lane >> 5) + 0..7] * 2^(kTW - e_c)
+//   exps:   int32 e_c at byte offset C*R*4 (frexp exponent of max_r |Bm[c, r]|)
+// One workgroup per (job, 32-column block).
+struct SplitJobsH {
+  const float* W[RB_MAX_SPLIT_JOBS];
+  f16x8* Wf[RB_MAX_SPLIT_JOBS];
+  int64_t ldw[RB_MAX_SPLIT_JOBS];
+  int C[RB_MAX_SPLIT_JOBS], R[RB_MAX_SPLIT_JOBS], tr[RB_MAX_SPLIT_JOBS];
+  int bstart[RB_MAX_SPLIT_JOBS + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) k_split_weights_h(const SplitJobsH jobs) {
+  __shared__ float smax[256];
+  __shared__ int sexp[32];
+  int j = 0;
+  while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.bstart[j + 1]) ++j;
+  const int C = jobs.C[j], R = jobs.R[j], tr = jobs.tr[j];
+  const int64_t ldw = jobs.ldw[j];
+  const float* __restrict__ W = jobs.W[j];
+  const int cb = blockIdx.x - jobs.bstart[j];
+  const int tid = threadIdx.x;
+  auto bm = [&](int c, int r) -> float {
+    return tr ? W[(int64_t)r * ldw + c] : W[(int64_t)c * ldw + r];
+  };
+  {
+    const int c = cb * 32 + (tid & 31);
+    float m = 0.0f;
+    for (int r = tid >> 5; r < R; r += 8) m = fmaxf(m, fabsf(bm(c, r)));
+    smax[tid] = m;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float m = smax[tid];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) m = fmaxf(m, smax[tid + 32 * q]);
+    const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
+    sexp[tid] = e;
+    int* ew = reinterpret_cast<int*>(reinterpret_cast<char*>(jobs.Wf[j]) + (int64_t)C * R * 4);
+    ew[cb * 32 + tid] = e;
+  }
+  __syncthreads();
+  const int KB = R / 16;
+  for (int it = tid; it < KB * 64; it += 256) {
+    const int kb = it >> 6, lane = it & 63;
+    const int c = cb * 32 + (lane & 31);
+    const int r0 = kb * 16 + 8 * (lane >> 5);
+    const int sh = kTW - sexp[lane & 31];
+    f16x8 o0, o1;
+#pragma unroll
+    for (int q = 0; q < 8; q += 2) {
+      const f32x2 x = {__builtin_amdgcn_ldexpf(bm(c, r0 + q), sh),
+                       __builtin_amdgcn_ldexpf(bm(c, r0 + q + 1), sh)};
+      f16x2 h0, h1;
+      split2h(x, h0, h1);
+      o0[q] = h0[0]; o0[q + 1] = h0[1];
+      o1[q] = h1[0]; o1[q + 1] = h1[1];
+    }
+    f16x8* dst = jobs.Wf[j] + ((int64_t)(cb * KB + kb) * 2) * 64 + lane;
+    dst[0] = o0;
+    dst[64] = o1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+#ifndef HN_NSA
+#define HN_NSA 3
+#endif
+constexpr int N_BM = 256, N_BN = 128, N_BK = 32;
+constexpr int N_NSA = HN_NSA, N_NSB = 2, N_WAVES = 8;
+constexpr int N_THREADS = 64 * N_WAVES;
+constexpr int N_LA = N_NSA - 1;                       // A steps in flight
+constexpr int N_NB = N_BN / 32;                       // column blocks per wave (4)
+constexpr int N_BFRAG = N_NB * 2 * 2;                 // B fragments per step (16)
+constexpr int N_BDMA = N_BFRAG / N_WAVES;             // B DMAs per wave per step (2)
+constexpr int N_A_STAGE = N_BM * N_BK * 4;            // 32 KB
+constexpr int N_B_STAGE = N_BFRAG * 1024;             // 16 KB
+constexpr int N_RING = N_NSA * N_A_STAGE + N_NSB * N_B_STAGE;  // 128 KB
+// + the column exponents and the bias of all C columns (C <= 1024)
+constexpr int N_MAXC = 1024;
+constexpr int N_MAXFLAG = 32;  // flagged tiles listed per wave (beyond: redo all)
+constexpr int N_LDS = N_RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <typename T>
+__device__ __forceinline__ T ds_read16(uint32_t addr) {
+  T r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+__device__ __forceinline__ int ds_read_i32(uint32_t addr) {
+  int r;
+  asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <bool BIAS>
+__global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restrict__ A, int64_t lda,
+                                                          int64_t M, int R,
+                                                          const f16x8* __restrict__ Wf,
+                                                          const int* __restrict__ ew, int C,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, int64_t ldo,
+                                                          float* __restrict__ rmax, int m_tiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nct = C / N_BN;
+  const int KT = R / N_BK;
+  const int KB16 = R / 16;
+  const int n_tiles = ((m_tiles + 7) >> 3) * 8 * nct;
+  const int G = gridDim.x;
+  const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
+  const int U = my_tiles * KT;  // k-steps of this workgroup
+  if (U == 0) return;
+
+  // column exponents and bias into LDS (before any DMA: ordinary loads)
+  int* s_ew = reinterpret_cast<int*>(smem + N_RING);
+  float* s_bias = reinterpret_cast<float*>(smem + N_RING + N_MAXC * 4);
+  for (int c = tid; c < C; c += N_THREADS) {
+    s_ew[c] = ew[c];
+    if (BIAS) s_bias[c] = bias[c];
+  }
+  __syncthreads();
+
+  // tile T = blockIdx.x + i*G: the column tiles of one row tile are
+  // neighbouring workgroups of one XCD (same blockIdx % 8), so their A
+  // re-reads hit that XCD's L2.  (Divisions: once per tile and stream.)
+  auto tile_of = [&](int i, int& mt, int& ct) {
+    const int T = blockIdx.x + i * G;
+    const int g = T >> 3;
+    ct = g % nct;
+    mt = (g / nct) * 8 + (T & 7);
+  };
+
+  // ---- A stream (own rows; issued N_LA steps ahead).  Stage image:
+  // row-major 128-B rows, 16-B chunk c of stage row r at chunk
+  // c ^ ((r >> 1) & 7) (conflict-free fragment reads); wave w owns stage
+  // rows 32w..32w+31 = 4 DMAs of 8 rows x 128 B.  Addresses: a uniform base
+  // (the wave's first row, the k-step) + a 32-bit per-lane offset.
+  int a_i = 0, a_kt = 0, a_slot = 0;
+  const char* a_base = nullptr;
+  int a_off[4];
+  auto a_tile = [&]() {
+    int mt, ct;
+    tile_of(a_i, mt, ct);
+    const int64_t r0 = (int64_t)mt * N_BM + wave * 32;
+    a_base = reinterpret_cast<const char*>(A + r0 * lda);
+    const int64_t lim = M - 1 - r0;  // rows past M repeat row M-1
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = q * 8 + (lane >> 3);
+      const int64_t r = rr < lim ? rr : lim;
+      const int srow = wave * 32 + rr;
+      const int lc = (lane & 7) ^ ((srow >> 1) & 7);
+      a_off[q] = (int)(r * lda * 4) + lc * 16;
+    }
+  };
+  auto issueA = [&]() {
+    char* st = smem + a_slot * N_A_STAGE + wave * 4096;
+    const char* b = a_base + a_kt * (N_BK * 4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024), 16,
+                                       0, 0);
+    a_slot = a_slot + 1 == N_NSA ? 0 : a_slot + 1;
+    if (++a_kt == KT) {
+      a_kt = 0;
+      if (++a_i < my_tiles) a_tile();
+    }
+  };
+  // ---- B stream (the k-step's 16 weight fragments, 1 KB each, shared by
+  // the 8 waves; issued one step ahead): fragment f = (n * 2 + s) * 2 + p,
+  // wave w DMAs fragments N_BDMA*w ...
+  int b_i = 0, b_kt = 0, b_slot = 0;
+  const f16x8* b_base = nullptr;
+  auto b_tile = [&]() {
+    int mt, ct;
+    tile_of(b_i, mt, ct);
+    b_base = Wf + (int64_t)ct * N_NB * KB16 * 2 * 64 + lane;
+  };
+  auto issueB = [&]() {
+    char* st = smem + N_NSA * N_A_STAGE + b_slot * N_B_STAGE;
+#pragma unroll
+    for (int q = 0; q < N_BDMA; ++q) {
+      const int f = wave * N_BDMA + q;
+      const int n = f >> 2, s = (f >> 1) & 1, p = f & 1;
+      const f16x8* src = b_base + ((n * KB16 + b_kt * 2 + s) * 2 + p) * 64;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + f * 1024), 16, 0, 0);
+    }
+    b_slot ^= 1;
+    if (++b_kt == KT) {
+      b_kt = 0;
+      if (++b_i < my_tiles) b_tile();
+    }
+  };
+
+  f32x16 acc[N_NB];
+#pragma unroll
+  for (int n = 0; n < N_NB; ++n)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[n][e] = 0.0f;
+
+  a_tile();
+  b_tile();
+  issueB();
+  for (int a = 0; a < N_LA && a < U; ++a) issueA();
+
+  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  const uint32_t s_ew_addr = smem_base + N_RING;
+  const uint32_t s_bias_addr = smem_base + N_RING + N_MAXC * 4;
+  // fragment read offsets inside an A stage: row 32*wave + (lane & 31),
+  // logical chunks 4s + 2h and 4s + 2h + 1
+  uint32_t a_rd[2][2];
+  {
+    const int row = wave * 32 + (lane & 31);
+    const int sw = (row >> 1) & 7;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        a_rd[s][c] = row * 128 + (((4 * s + 2 * (lane >> 5) + c) ^ sw) << 4);
+  }
+  const int ccol = lane & 31;
+  // C-layout row of accumulator register j: 8*(j>>2) + 4*(lane>>5) + (j&3)
+  auto crow = [&](int j) { return 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3); };
+
+  // per-row scale state of this lane's row (lanes l and l+32 hold the same row)
+  int er = kSent;
+  float scl = 1.0f, thr = 0.0f;
+  float tmax = 0.0f;         // max |A| over the lane's values of the current tile (rmax)
+  bool flag_tile = false;    // a row of this wave overflowed its headroom in this tile
+  int nflag = 0;             // flagged tiles (their iteration index i, in LDS)
+  int* s_flag = reinterpret_cast<int*>(smem + N_RING + N_MAXC * 8) + wave * N_MAXFLAG;
+
+  // deferred epilogue: pend[n] (un-scaled) stored one block per k-step during
+  // the next tile; 16 dword stores per block (lane: one column, 16 rows)
+  f32x16 pend[N_NB];
+  float pbias[N_NB];
+  int pend_q = N_NB;
+  bool pend_on = false, pend_full = true;
+  const char* pend_base = nullptr;  // the wave's first row of the pending tile
+  int64_t pend_r0 = 0;
+  const int st_lane = (int)((4 * (lane >> 5)) * ldo * 4) + ccol * 4;
+  auto store_block = [&](const f32x16& blk, int n) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int rj = 8 * (j >> 2) + (j & 3);
+      float* o = (float*)(pend_base + (int64_t)rj * ldo * 4 + n * 128 + st_lane);
+      const float v = BIAS ? blk[j] + pbias[n] : blk[j];
+      if (pend_full || pend_r0 + crow(j) < M) __builtin_nontemporal_store(v, o);
+    }
+  };
+  auto store_quarter = [&]() {
+    const int q = pend_q++;
+    if (q == 0) store_block(pend[0], 0);
+    else if (q == 1) store_block(pend[1], 1);
+    else if (q == 2) store_block(pend[2], 2);
+    else store_block(pend[3], 3);
+    return pend_full;
+  };
+  bool stored_prev = false;
+
+  int i = 0, kt = 0, c_slot_a = 0, c_slot_b = 0;
+  int cur_mt, cur_ct;
+  tile_of(0, cur_mt, cur_ct);
+  for (int u = 0; u < U; ++u) {
+    // operands of step u landed (own DMAs): the ops younger than B(u) are
+    // A(u-1+N_LA) (4, issued by step u-1 if it exists) and the 16 deferred
+    // stores step u-1 issued after it (at u = 0 the prologue's extra A
+    // batches make this wait conservative, never short)
+    {
+      const bool ya = u > 0 && u - 1 + N_LA < U;
+      if (ya) {
+        if (stored_prev) wait_vm<20>(); else wait_vm<4>();
+      } else if (u == 0 && U > 1) {
+        wait_vm<4 * (N_LA - 1)>();
+      } else {
+        if (stored_prev) wait_vm<16>(); else wait_vm<0>();
+      }
+    }
+    __builtin_amdgcn_s_barrier();
+
+    const uint32_t sa = smem_base + c_slot_a * N_A_STAGE;
+    const uint32_t sb = smem_base + N_NSA * N_A_STAGE + c_slot_b * N_B_STAGE + lane * 16;
+    auto substep = [&](int s) {
+      const f32x4 x0 = ds_read16<f32x4>(sa + a_rd[s][0]);
+      const f32x4 x1 = ds_read16<f32x4>(sa + a_rd[s][1]);
+      // B fragments two column blocks ahead of the MFMAs that use them
+      auto rb = [&](int n, int p) { return ds_read16<f16x8>(sb + ((n * 2 + s) * 2 + p) * 1024); };
+      f16x8 b00 = rb(0, 0), b01 = rb(0, 1), b10 = rb(1, 0), b11 = rb(1, 1);
+      f32x4 xa = x0, xb = x1;
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa), "+v"(xb));
+      const float mx = max8abs(xa, xb);
+      tmax = fmaxf(tmax, mx);
+      if (kt == 0 && s == 0) {
+        // tile start: the row scale from the first 16 k-values of the row
+        const float mm = fmaxf(mx, __shfl_xor(mx, 32));
+        const bool z = !(mm > 0.0f);
+        const int e = __builtin_amdgcn_frexp_expf(mm);
+        er = z ? kSent : e;
+        scl = z ? 1.0f : __builtin_amdgcn_ldexpf(1.0f, kTA - e);
+        thr = z ? 0.0f : __builtin_amdgcn_ldexpf(1.0f, e + kHead);
+      } else {
+        // rare: a value beyond its row's headroom (its fp16 image may
+        // overflow): the wave's rows of this tile are recomputed exactly
+        // after the main loop
+        flag_tile = flag_tile || __builtin_amdgcn_ballot_w64(mx > thr) != 0;
+      }
+      f16x8 a0, a1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x2 v = (q < 2 ? f32x2{xa[2 * q], xa[2 * q + 1]}
+                               : f32x2{xb[2 * q - 4], xb[2 * q - 3]}) * scl;
+        f16x2 h0, h1;
+        split2h(v, h0, h1);
+        a0[2 * q] = h0[0]; a0[2 * q + 1] = h0[1];
+        a1[2 * q] = h1[0]; a1[2 * q + 1] = h1[1];
+      }
+      // per column block: the small partial products first
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b00), "+v"(b01));
+      acc[0] = mfma_h(a1, b00, acc[0]);
+      acc[0] = mfma_h(a0, b01, acc[0]);
+      acc[0] = mfma_h(a0, b00, acc[0]);
+      b00 = rb(2, 0);
+      b01 = rb(2, 1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b10), "+v"(b11));
+      acc[1] = mfma_h(a1, b10, acc[1]);
+      acc[1] = mfma_h(a0, b11, acc[1]);
+      acc[1] = mfma_h(a0, b10, acc[1]);
+      b10 = rb(3, 0);
+      b11 = rb(3, 1);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b00), "+v"(b01));
+      acc[2] = mfma_h(a1, b00, acc[2]);
+      acc[2] = mfma_h(a0, b01, acc[2]);
+      acc[2] = mfma_h(a0, b00, acc[2]);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b10), "+v"(b11));
+      acc[3] = mfma_h(a1, b10, acc[3]);
+      acc[3] = mfma_h(a0, b11, acc[3]);
+      acc[3] = mfma_h(a0, b10, acc[3]);
+    };
+    substep(0);
+    if (u + 1 < U) issueB();
+#ifndef HN_NO_ADMA
+    if (u + N_LA < U) issueA();
+#endif
+    stored_prev = false;
+    if (pend_on && pend_q < N_NB) {
+      // a partial tile's guarded stores may issue fewer than 16: not counted
+      stored_prev = store_quarter();
+    }
+    substep(1);
+    c_slot_a = c_slot_a + 1 == N_NSA ? 0 : c_slot_a + 1;
+    c_slot_b ^= 1;
+
+    if (kt == KT - 1) {
+      // the tile's results (un-scaled) move to pend[] and are stored a block
+      // per step during the next tile's first steps (behind its MFMAs)
+      while (pend_on && pend_q < N_NB) store_quarter();
+      int ecol[N_NB];
+#pragma unroll
+      for (int n = 0; n < N_NB; ++n) ecol[n] = ds_read_i32(s_ew_addr + (cur_ct * N_BN + n * 32 + ccol) * 4);
+      if (BIAS) {
+#pragma unroll
+        for (int n = 0; n < N_NB; ++n)
+          pbias[n] = __builtin_bit_cast(float, ds_read_i32(s_bias_addr + (cur_ct * N_BN + n * 32 + ccol) * 4));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ecol[0]), "+v"(ecol[1]), "+v"(ecol[2]), "+v"(ecol[3]));
+      if (BIAS) asm volatile("" : "+v"(pbias[0]), "+v"(pbias[1]), "+v"(pbias[2]), "+v"(pbias[3]));
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int erj = __shfl(er, crow(j)) - kTA - kTW;
+#pragma unroll
+        for (int n = 0; n < N_NB; ++n) {
+          pend[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
+          acc[n][j] = 0.0f;
+        }
+      }
+      if (rmax && cur_ct == 0 && cur_mt < m_tiles) {
+        // max |A| of the wave's 32 rows (all R columns): the weight-gradient
+        // kernel's operand scale (rows past M repeat row M-1: harmless)
+        float w = tmax;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) w = fmaxf(w, __shfl_xor(w, o));
+        const int64_t grp = (int64_t)cur_mt * (N_BM / 32) + wave;
+        if (lane == 0 && grp * 32 < M) rmax[grp] = w;
+      }
+      tmax = 0.0f;
+      if (flag_tile) {
+        if (nflag < N_MAXFLAG) s_flag[nflag] = i;
+        ++nflag;
+        flag_tile = false;
+      }
+      pend_on = cur_mt < m_tiles;
+      pend_r0 = (int64_t)cur_mt * N_BM + wave * 32;
+      pend_full = pend_r0 + 32 <= M;
+      pend_base = reinterpret_cast<const char*>(out + pend_r0 * ldo + cur_ct * N_BN);
+      pend_q = 0;
+      kt = 0;
+      ++i;
+      if (i < my_tiles) tile_of(i, cur_mt, cur_ct);
+    } else {
+      ++kt;
+    }
+  }
+  while (pend_on && pend_q < N_NB) store_quarter();
+
+  // cold tail: the wave's rows of every flagged tile again, with each row's
+  // exact max known first (no overflow possible), operands straight from
+  // global memory, stored directly (after this wave's earlier stores)
+  if (nflag > 0) {
+    wait_vm<0>();
+    const int ntodo = nflag > N_MAXFLAG ? my_tiles : nflag;
+    for (int f = 0; f < ntodo; ++f) {
+      const int ii = nflag > N_MAXFLAG ? f : s_flag[f];
+      int mt, ct;
+      tile_of(ii, mt, ct);
+      if (mt >= m_tiles) continue;
+      int64_t row = (int64_t)mt * N_BM + wave * 32 + (lane & 31);
+      if (row >= M) row = M - 1;
+      const float* arow = A + row * lda + 8 * (lane >> 5);
+      float m = 0.0f;
+      for (int kb = 0; kb < KB16; ++kb) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(arow + kb * 16);
+        const f32x4 q = *reinterpret_cast<const f32x4*>(arow + kb * 16 + 4);
+        m = fmaxf(m, max8abs(p, q));
+      }
+      m = fmaxf(m, __shfl_xor(m, 32));
+      const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
+      const float sc = __builtin_amdgcn_ldexpf(1.0f, kTW - e);  // row max < 2^14
+      f32x16 c[N_NB];
+#pragma unroll
+      for (int n = 0; n < N_NB; ++n)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) c[n][j] = 0.0f;
+      for (int kb = 0; kb < KB16; ++kb) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(arow + kb * 16);
+        const f32x4 q = *reinterpret_cast<const f32x4*>(arow + kb * 16 + 4);
+        f16x8 a0, a1;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const f32x2 v = (t < 2 ? f32x2{p[2 * t], p[2 * t + 1]} : f32x2{q[2 * t - 4], q[2 * t - 3]}) * sc;
+          f16x2 h0, h1;
+          split2h(v, h0, h1);
+          a0[2 * t] = h0[0]; a0[2 * t + 1] = h0[1];
+          a1[2 * t] = h1[0]; a1[2 * t + 1] = h1[1];
+        }
+#pragma unroll
+        for (int n = 0; n < N_NB; ++n) {
+          const f16x8* bp = Wf + ((int64_t)((ct * N_NB + n) * KB16 + kb) * 2) * 64 + lane;
+          const f16x8 b0 = bp[0], b1 = bp[64];
+          c[n] = mfma_h(a1, b0, c[n]);
+          c[n] = mfma_h(a0, b1, c[n]);
+          c[n] = mfma_h(a0, b0, c[n]);
+        }
+      }
+      int erow[16];  // the exact exponent of each C-layout row
+#pragma unroll
+      for (int j = 0; j < 16; ++j) erow[j] = __shfl(e, crow(j)) - 2 * kTW;
+#pragma unroll
+      for (int n = 0; n < N_NB; ++n) {
+        const int col = ct * N_BN + n * 32 + ccol;
+        const int ecol = s_ew[col];
+        const float bv = BIAS ? s_bias[col] : 0.0f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+          const int64_t r = (int64_t)mt * N_BM + wave * 32 + crow(j);
+          if (r < M) out[r * ldo + col] = __builtin_amdgcn_ldexpf(c[n][j], erow[j] + ecol) + bv;
+        }
+      }
+    }
+  }
+}
+
+template <bool BIAS>
+void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
+              const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
+              hipStream_t st) {
+  static bool done = false;  // benign race: idempotent
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, N_LDS);
+    done = true;
+  }
+  k_gemm_nt_h<BIAS><<<grid, N_THREADS, N_LDS, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo,
+                                                        rmax, m_tiles);
+}
+
+}  // namespace
+
+int launch_split_weights_h(const rb_split_job* jobs, int n, hipStream_t st) {
+  SplitJobsH sj{};
+  sj.n = n;
+  int blocks = 0;
+  for (int j = 0; j < n; ++j) {
+    sj.W[j] = jobs[j].W;
+    sj.Wf[j] = (f16x8*)jobs[j].Wf;
+    sj.ldw[j] = jobs[j].ldw;
+    sj.C[j] = (int)jobs[j].C;
+    sj.R[j] = (int)jobs[j].R;
+    sj.tr[j] = (int)jobs[j].transpose;
+    sj.bstart[j] = blocks;
+    blocks += (int)(jobs[j].C / 32);
+  }
+  sj.bstart[n] = blocks;
+  k_split_weights_h<<<(unsigned)blocks, 256, 0, st>>>(sj);
+  return launch_status("rb_gemm_h_split_weights");
+}
+
+int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                     const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
+                     hipStream_t st) {
+  const int m_tiles = (int)((M + N_BM - 1) / N_BM);
+  const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / N_BN);
+  // persistent: one workgroup per CU (a multiple of 8: the XCD pairing above)
+  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8);
+  const f16x8* wf = (const f16x8*)Wf;
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
+  (void)accumulate;  // rejected by rb_gemm_nt_h
+  if (bias)
+    run_nt_h<true>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+  else
+    run_nt_h<false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+  return launch_status("rb_gemm_nt_h");
+}
+
+}  // namespace rb

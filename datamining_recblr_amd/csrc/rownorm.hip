@@ -114,7 +114,8 @@ k_add_ln_fwd(const float* __restrict__ a, const int64_t* __restrict__ idx, int64
 // dbias += da (the bias gradient of the GEMM that produced a).
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
-k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
+k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ dy2,
+             const float* __restrict__ s,
              const float* __restrict__ gamma, const float* __restrict__ mean,
              const float* __restrict__ rstd, DropSpec drop, float* __restrict__ ds_out,
              float* __restrict__ da_out, float* __restrict__ dgamma_part,
@@ -147,6 +148,12 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ s,
       const int c = (l + k * LPR) * 4;
       float dyv[4];
       ldc(dyv, dy + rr * D + c);
+      if (dy2) {  // a second gradient of the same output (autograd's sum)
+        float d2[4];
+        ldc(d2, dy2 + rr * D + c);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) dyv[v] += d2[v];
+      }
       ldc(xh[k], s + rr * D + c);
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
@@ -345,10 +352,11 @@ int add_ln_fwd_t(const float* a, const int64_t* idx, int64_t nidx, const DropSpe
 }
 
 template <int NV, int LPR>
-int add_ln_bwd_t(const float* dy, const float* s, const float* gamma, const float* mean,
-                 const float* rstd, const DropSpec& drop, float* ds, float* da, float* dgp,
-                 float* dbp, float* dbiasp, int64_t nparts, int64_t rows, hipStream_t st) {
-  hipLaunchKernelGGL((k_add_ln_bwd<NV, LPR>), dim3((unsigned)nparts), dim3(256), 0, st, dy, s,
+int add_ln_bwd_t(const float* dy, const float* dy2, const float* s, const float* gamma,
+                 const float* mean, const float* rstd, const DropSpec& drop, float* ds, float* da,
+                 float* dgp, float* dbp, float* dbiasp, int64_t nparts, int64_t rows,
+                 hipStream_t st) {
+  hipLaunchKernelGGL((k_add_ln_bwd<NV, LPR>), dim3((unsigned)nparts), dim3(256), 0, st, dy, dy2, s,
                      gamma, mean, rstd, drop, ds, da, dgp, dbp, dbiasp, rows);
   return launch_status("rb_add_ln_bwd");
 }
@@ -403,11 +411,11 @@ int launch_add_ln_fwd(const float* a, const int64_t* idx, int64_t nidx, const Dr
                   rstd, rows, st)
 }
 
-int launch_add_ln_bwd(const float* dy, const float* s, const float* gamma, const float* mean,
-                      const float* rstd, const DropSpec& drop, float* ds, float* da, float* dgp,
-                      float* dbp, float* dbiasp, int64_t nparts, int64_t rows, int64_t d,
-                      hipStream_t st) {
-  RB_ROW_DISPATCH(d, add_ln_bwd_t, dy, s, gamma, mean, rstd, drop, ds, da, dgp, dbp, dbiasp,
+int launch_add_ln_bwd(const float* dy, const float* dy2, const float* s, const float* gamma,
+                      const float* mean, const float* rstd, const DropSpec& drop, float* ds,
+                      float* da, float* dgp, float* dbp, float* dbiasp, int64_t nparts,
+                      int64_t rows, int64_t d, hipStream_t st) {
+  RB_ROW_DISPATCH(d, add_ln_bwd_t, dy, dy2, s, gamma, mean, rstd, drop, ds, da, dgp, dbp, dbiasp,
                   nparts, rows, st)
 }
 

@@ -495,14 +495,20 @@ def add_ln_fwd(a, r, gamma, beta, eps, mask=None, seed=0, p=0.0, idx=None, save=
 
 
 def add_ln_bwd(dy, s, gamma, mean, rstd, mask=None, seed=0, p=0.0, want_ds=True,
-               want_da=True, want_dbias=False):
-    """Returns (ds, da, dgamma, dbeta, dbias); unwanted outputs are None."""
+               want_da=True, want_dbias=False, dy2=None):
+    """Returns (ds, da, dgamma, dbeta, dbias); unwanted outputs are None.
+    dy2: a second gradient of the same output, added on load (dy + dy2)."""
     _check(dy, "dy")
     _check_p(p)
     rows, d = s.shape
     dy = dy.reshape(rows, d)
     if not dy.is_contiguous():
         dy = dy.contiguous()
+    if dy2 is not None:
+        _check(dy2, "dy2")
+        dy2 = dy2.reshape(rows, d)
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
     _check_mask(mask, (rows, d))
     nparts = row_num_parts(rows, d)
     dev = s.device
@@ -512,8 +518,8 @@ def add_ln_bwd(dy, s, gamma, mean, rstd, mask=None, seed=0, p=0.0, want_ds=True,
     ds = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_ds else None
     da = torch.empty((rows, d), device=dev, dtype=torch.float32) if want_da else None
     n = rows * d
-    nbytes = 4 * n * (2 + want_ds + want_da) + (n if mask is not None else 0)
-    _launch("rb_add_ln_bwd", nbytes, dy.data_ptr(), s.data_ptr(), gamma.data_ptr(),
+    nbytes = 4 * n * (2 + (dy2 is not None) + want_ds + want_da) + (n if mask is not None else 0)
+    _launch("rb_add_ln_bwd2", nbytes, dy.data_ptr(), _ptr(dy2), s.data_ptr(), gamma.data_ptr(),
             mean.data_ptr(), rstd.data_ptr(), _ptr(mask), int(seed), float(p), _ptr(ds),
             _ptr(da), dgp.data_ptr(), dbp.data_ptr(), _ptr(dbias_p), nparts, rows, d,
             _stream(dy))
@@ -871,4 +877,64 @@ def gemm_nt(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None
     _lib.call("rb_gemm_nt", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
               0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0),
               int(accumulate), _stream(a))
+    return out
+
+
+# ---- fp16 two-part split GEMMs (csrc/gemm_half.hip) --------------------------
+
+def gemm_h_weight(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """f16 weight image of Bm = w (transpose=False, w [C, R]) or Bm = w^T
+    (w [R, C]) for gemm_nt_h (rb_gemm_h_split_weights, one job)."""
+    _check(w, "weight")
+    if w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("weight must be a 2-D row-major tensor")
+    R, C = (w.shape[0], w.shape[1]) if transpose else (w.shape[1], w.shape[0])
+    nbytes = _lib.load().rb_gemm_h_weight_bytes(C, R)
+    wf = torch.empty(nbytes // 2, device=w.device, dtype=torch.float16)
+    gemm_h_split_weights([(w, transpose, wf)])
+    return wf
+
+
+def gemm_h_split_weights(jobs) -> None:
+    """(Re)build several f16 weight images in one launch
+    (rb_gemm_h_split_weights): jobs = [(w, transpose, wf)]."""
+    jobs = list(jobs)
+    lib = _lib.load()
+    for k in range(0, len(jobs), MAX_SPLIT_JOBS):
+        chunk = jobs[k:k + MAX_SPLIT_JOBS]
+        arr = (_SplitJob * len(chunk))()
+        for d, (w, transpose, wf) in zip(arr, chunk):
+            _check(w, "weight")
+            if w.dim() != 2 or w.stride(1) != 1:
+                raise ValueError("weight must be a 2-D row-major tensor")
+            R, C = (w.shape[0], w.shape[1]) if transpose else (w.shape[1], w.shape[0])
+            if wf.numel() * 2 != lib.rb_gemm_h_weight_bytes(C, R) or wf.device != w.device:
+                raise ValueError("f16 weight image buffer does not match the weight")
+            d.W, d.ldw, d.C, d.R = w.data_ptr(), w.stride(0), C, R
+            d.transpose, d.Wf = int(transpose), wf.data_ptr()
+        _lib.call("rb_gemm_h_split_weights", ctypes.addressof(arr), len(chunk),
+                  _stream(chunk[0][0]))
+
+
+def gemm_nt_h(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None = None,
+              out: torch.Tensor | None = None, rmax: torch.Tensor | None = None) -> torch.Tensor:
+    """out[M, C] = a[M, R] @ Bm^T (+ bias) on the f16 pipe with Bm's f16 image
+    wf (rb_gemm_nt_h); rmax [ceil(M/32)] receives max|a| per 32-row group."""
+    _check(a, "a")
+    if a.dim() != 2 or a.stride(1) != 1:
+        raise ValueError("a must be a 2-D tensor with unit inner stride")
+    M, R = a.shape
+    if out is None:
+        out = torch.empty((M, C), device=a.device, dtype=torch.float32)
+    elif out.shape != (M, C) or out.stride(1) != 1:
+        raise ValueError("out must be [M, C] with unit inner stride")
+    if bias is not None:
+        _check(bias, "bias")
+    if rmax is not None:
+        _check(rmax, "rmax")
+        if rmax.numel() < (M + 31) // 32:
+            raise ValueError("rmax needs ceil(M/32) entries")
+    _lib.call("rb_gemm_nt_h", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
+              0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0), 0,
+              0 if rmax is None else rmax.data_ptr(), _stream(a))
     return out

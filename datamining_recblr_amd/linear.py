@@ -10,15 +10,20 @@ MFMA peak 157).  Splitting the reduction into S row blocks as one batched GEMM
 order runs 2-4.5x faster (tools/gemm_probe.py) and is deterministic.
 
 The forward and input-gradient GEMMs of the packed [ntok, *] projections run
-on the split-bf16 MFMA kernel (csrc/gemm_split.hip, ``mm_nt`` / ``mm_nn``):
-fp32 operands split exactly into three bf16 parts, six partial products, fp32
-accumulation — fp32-level accuracy on the bf16 pipe.  Its speed does not
-depend on the row count, which changes every batch once the sequences are
-packed (RecBLR._forward_packed): there hipBLASLt's untuned heuristic picks
-run at 86-117 TFLOP/s, this kernel at 120-156.  Shapes it does
-not cover (and small M) stay on hipBLASLt/rocBLAS through torch;
-RECBLR_SPLIT_GEMM=0 routes everything through torch.  The math is exactly
-nn.Linear's (RecBLR.py:162,165,167,213,214).
+on split-operand MFMA kernels (``mm_nt`` / ``mm_nn``), selected by
+RECBLR_GEMM:
+  f16x3  (default, csrc/gemm_half.hip): every fp32 operand scaled by an exact
+         power of two and split into two fp16 parts, three products, fp32
+         accumulation — error vs fp64 at or below hipBLASLt's fp32 kernels;
+  bf16x6 (csrc/gemm_split.hip): three exact bf16 parts, six products;
+  torch  (or RECBLR_SPLIT_GEMM=0): hipBLASLt/rocBLAS fp32 through torch.
+Their speed does not depend on the row count, which changes every batch once
+the sequences are packed (RecBLR._forward_packed): there hipBLASLt's untuned
+heuristic picks run at 86-117 TFLOP/s.  Shapes they do not
+cover (and small M) stay on torch.  The math is exactly nn.Linear's
+(RecBLR.py:162,165,167,213,214).  The input-gradient GEMM never accumulates
+into a residual gradient: the consumer of that gradient adds it while loading
+(rb_add_ln_bwd2's dy2, rb_conv_silu_bwd's g2; see blocks.ResidualGrad).
 """
 from __future__ import annotations
 
@@ -32,7 +37,11 @@ from . import gemm_tuning, kernels
 __all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled"]
 
 SPLIT_MIN_ROWS = 4096
-_split_on = os.environ.get("RECBLR_SPLIT_GEMM", "1") != "0"
+_GEMM = os.environ.get("RECBLR_GEMM", "f16x3")
+if _GEMM not in ("f16x3", "bf16x6", "torch"):
+    raise ValueError(f"RECBLR_GEMM must be f16x3, bf16x6 or torch, got {_GEMM!r}")
+_split_on = os.environ.get("RECBLR_SPLIT_GEMM", "1") != "0" and _GEMM != "torch"
+_half = _GEMM == "f16x3"
 _cache_on = os.environ.get("RECBLR_SPLIT_CACHE", "1") != "0"
 
 # Split images of the weights, kept across calls: (id(w), transpose) ->
@@ -69,16 +78,22 @@ def _stamp(w: torch.Tensor):
     return (w._version, _opt_steps[0])
 
 
+def _make_image(w, transpose):
+    return (kernels.gemm_h_weight(w, transpose=transpose) if _half
+            else kernels.gemm_split_weight(w, transpose=transpose))
+
+
 def _weight_split(w: torch.Tensor, transpose: bool) -> torch.Tensor:
+    """The split weight image of the selected format (f16x3 or bf16x6)."""
     if not _cache_on:
-        return kernels.gemm_split_weight(w, transpose=transpose)
+        return _make_image(w, transpose)
     key = (id(w), transpose)
     e = _split_cache.get(key)
     if e is not None and e[0]() is w and e[1] == w.data_ptr() and e[2] == _stamp(w):
         return e[3]
     if e is None or e[0]() is not w or e[1] != w.data_ptr():
         # new (or re-allocated) weight: its own split, then cached
-        wf = kernels.gemm_split_weight(w, transpose=transpose)
+        wf = _make_image(w, transpose)
         _split_cache[key] = [weakref.ref(w), w.data_ptr(), _stamp(w), wf]
         return wf
     # stale after an in-place update: refresh all stale entries at once
@@ -91,7 +106,7 @@ def _weight_split(w: torch.Tensor, transpose: bool) -> torch.Tensor:
         if _stamp(ww) != ent[2] and ww.device == w.device:
             jobs.append((ww, k[1], ent[3]))
             fresh.append(ent)
-    kernels.gemm_split_weights(jobs)
+    (kernels.gemm_h_split_weights if _half else kernels.gemm_split_weights)(jobs)
     for ent in fresh:
         ent[2] = _stamp(ent[0]())
     return e[3]
@@ -104,7 +119,13 @@ def split_gemm_enabled() -> bool:
 def _split_ok(a: torch.Tensor, C: int, R: int) -> bool:
     return (_split_on and a.is_cuda and a.dim() == 2 and a.shape[0] >= SPLIT_MIN_ROWS
             and C % 128 == 0 and R % 32 == 0 and a.stride(1) == 1 and a.stride(0) % 4 == 0
-            and a.data_ptr() % 16 == 0 and a.dtype == torch.float32)
+            and a.data_ptr() % 16 == 0 and a.dtype == torch.float32
+            and (not _half or C <= 1024))
+
+
+def gemm_format() -> str:
+    """The split GEMM format in use: 'f16x3', 'bf16x6' or 'torch'."""
+    return _GEMM if _split_on else "torch"
 
 
 def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
@@ -116,6 +137,8 @@ def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) ->
         return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
     N, K = w.shape
     if _split_ok(a, N, K):
+        if _half:
+            return kernels.gemm_nt_h(a, _weight_split(w, False), N, bias=bias)
         return kernels.gemm_nt(a, _weight_split(w, False), N, bias=bias)
     return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
 
@@ -127,6 +150,9 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) ->
         wb = w.to(dy.dtype)
         return out.addmm_(dy, wb) if out is not None else dy @ wb
     N, K = w.shape
+    if _split_ok(dy, K, N) and _half:
+        r = kernels.gemm_nt_h(dy, _weight_split(w, True), K)
+        return r if out is None else out.add_(r)
     if _split_ok(dy, K, N) and (out is None or (out.stride(1) == 1 and out.shape == (dy.shape[0], K))):
         return kernels.gemm_nt(dy, _weight_split(w, True), K, out=out,
                                accumulate=out is not None)
@@ -208,15 +234,15 @@ class LinearFn(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             slot = ctx.slot
-            if slot is not None and slot.ds is not None and slot.rows is None:
-                # + a handed-over residual gradient, inside the GEMM (beta = 1)
-                dx = _timed("gemm", flops, mm_nn, dy2, weight, slot.ds.view(-1, weight.shape[1]))
-                slot.ds = None
-            else:
-                dx = _timed("gemm", flops, mm_nn, dy2, weight)
-                if slot is not None and slot.ds is not None:   # residual of gathered rows
+            dx = _timed("gemm", flops, mm_nn, dy2, weight)
+            if slot is not None and slot.ds is not None:
+                if slot.rows is not None:        # residual of gathered rows
                     dx.index_add_(0, slot.rows, slot.ds.view(-1, weight.shape[1]))
                     slot.ds = None
+                elif not slot.taken:             # nobody downstream adds it
+                    dx.add_(slot.ds.view(-1, weight.shape[1]))
+                    slot.ds = None
+                # else: x's producer adds slot.ds while loading (rb_add_ln_bwd2)
             dx = dx.view(*dy.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
             dw = _timed("gemm", flops, wgrad, dy2, x2)

@@ -152,8 +152,8 @@ class FeedForward(nn.Module):
         self.dropout = nn.Dropout(dropout)
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
 
-    def forward(self, input_tensor):
-        return feed_forward(input_tensor, self, self.training)
+    def forward(self, input_tensor, in_addend=None, out_addend=None):
+        return feed_forward(input_tensor, self, self.training, in_addend, out_addend)
 
 
 class RecurrentLayer(nn.Module):
@@ -171,19 +171,31 @@ class RecurrentLayer(nn.Module):
         self.layer_norm = nn.LayerNorm(d_model, eps=1e-12)
         self.ffn = FeedForward(d_model=d_model, inner_size=d_model * 4, dropout=dropout)
 
-    def forward(self, input_tensor, pad=None, rows=None, seq=None):
+    def forward(self, input_tensor, pad=None, rows=None, seq=None, slot=None, out_addend=None):
         """rows: evaluate the position-wise tail (out-projection, residual
         LayerNorm, FFN) only at these flat positions -> [len(rows), d].
-        seq: kernels.Packed (input_tensor is [ntok, d])."""
-        slot = (ResidualGrad(rows) if torch.is_grad_enabled() and input_tensor.requires_grad
-                else None)
+        seq: kernels.Packed (input_tensor is [ntok, d]).
+        slot: blocks.ResidualGrad for the residual branch's gradient (RecBLR
+        creates it so that input_tensor's producer can take it);
+        out_addend: the next layer's slot (a second gradient of the output)."""
+        grad = torch.is_grad_enabled() and input_tensor.requires_grad
+        if slot is None and grad:
+            slot = ResidualGrad(rows)
+        if not grad:
+            slot = out_addend = None
         residual = input_tensor
         if rows is not None:
             residual = input_tensor.reshape(-1, input_tensor.shape[-1]).index_select(0, rows)
-        h = add_dropout_layer_norm(self.behavior_modeling(input_tensor, pad, slot, rows, seq),
-                                   residual,
-                                   self.dropout, self.layer_norm, self.training, slot)
-        return h if self.disable_ffn else self.ffn(h)
+        y = self.behavior_modeling(input_tensor, pad, slot, rows, seq)
+        if self.disable_ffn:
+            return add_dropout_layer_norm(y, residual, self.dropout, self.layer_norm,
+                                          self.training, slot, out_addend)
+        # the FFN's own residual gradient goes back through h_slot to the
+        # LayerNorm that produced h
+        h_slot = ResidualGrad() if grad else None
+        h = add_dropout_layer_norm(y, residual, self.dropout, self.layer_norm, self.training,
+                                   slot, h_slot)
+        return self.ffn(h, h_slot, out_addend)
 
 
 # Attribute a data path may set on the item_seq_len device tensor: the same
@@ -261,19 +273,31 @@ class RecBLR(SequentialRecommender):
         pad = row_pad_lens(item_seq_len) if exact_lengths else None
         if self.pack_sequences:
             return self._forward_packed(item_seq, item_seq_len, pad)
-        h = embed_dropout_layer_norm(item_seq, self.item_embedding, self.dropout, self.layer_norm,
-                                     self.training)
         n = len(self.recurrent_layers)
+        rows = None
+        if self.gather_last_layer:
+            # Everything after the last layer's scan is position-wise and only
+            # the positions gather_indexes picks reach the output: evaluate
+            # that tail at those B positions (identical results).
+            B, L = item_seq.shape
+            rows = torch.arange(B, device=item_seq.device) * L + (item_seq_len - 1)
+        slots = self._residual_slots(rows)
+        h = embed_dropout_layer_norm(item_seq, self.item_embedding, self.dropout, self.layer_norm,
+                                     self.training, slots[0])
         for i, layer in enumerate(self.recurrent_layers):
-            if i == n - 1 and self.gather_last_layer:
-                # Everything after the last layer's scan is position-wise and only
-                # the positions gather_indexes picks reach the output: evaluate
-                # that tail at those B positions (identical results).
-                B, L = item_seq.shape
-                rows = torch.arange(B, device=item_seq.device) * L + (item_seq_len - 1)
-                return layer(h, pad, rows)
-            h = layer(h, pad)
+            if i == n - 1 and rows is not None:
+                return layer(h, pad, rows, slot=slots[i])
+            h = layer(h, pad, slot=slots[i], out_addend=slots[i + 1])
         return self.gather_indexes(h, item_seq_len - 1)
+
+    def _residual_slots(self, last_rows):
+        """One blocks.ResidualGrad per layer (+ None): layer i's residual
+        gradient, taken by its input's producer (slot i is handed to that
+        producer as its out_addend)."""
+        n = len(self.recurrent_layers)
+        if not torch.is_grad_enabled():
+            return [None] * (n + 1)
+        return [ResidualGrad(last_rows if i == n - 1 else None) for i in range(n)] + [None]
 
     def _forward_packed(self, item_seq, item_seq_len, pad):
         """forward() on the valid positions only.  RecBole right-pads every
@@ -313,13 +337,14 @@ class RecBLR(SequentialRecommender):
         seq.last, seq.inv = last, inv
         if pad is not None:
             pad = pad.index_select(0, order)
-        h = embed_dropout_layer_norm(ids, self.item_embedding, self.dropout, self.layer_norm,
-                                     self.training)
         n = len(self.recurrent_layers)
+        slots = self._residual_slots(last if self.gather_last_layer else None)
+        h = embed_dropout_layer_norm(ids, self.item_embedding, self.dropout, self.layer_norm,
+                                     self.training, slots[0])
         for i, layer in enumerate(self.recurrent_layers):
             if i == n - 1 and self.gather_last_layer:
-                return layer(h, pad, last, seq)
-            h = layer(h, pad, seq=seq)
+                return layer(h, pad, last, seq, slot=slots[i])
+            h = layer(h, pad, seq=seq, slot=slots[i], out_addend=slots[i + 1])
         return h.index_select(0, last)
 
     def _scores_all(self, seq_output):

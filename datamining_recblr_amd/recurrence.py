@@ -138,15 +138,16 @@ class BDLRUCore(torch.autograd.Function):
         drg2 = drg.view(rows, H2)
         gflops = 2 * rows * H * H2
         dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H))
-        # + dL/dxc through the gates GEMM, accumulated in place (beta = 1)
-        _timed("gemm", gflops, mm_nn, drg2, gate_w, dxc.view(rows, H))
+        # dL/dxc through the gates GEMM: the conv backward reads it as its second
+        # gradient term (g1 + g2 on load, no separate add pass)
+        dxc_g = _timed("gemm", gflops, mm_nn, drg2, gate_w).view_as(dxc)
         dconv_w = dconv_b = None
         if ctx.use_conv:
-            dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, None, dxz[..., :H],
+            dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, dxc_g, dxz[..., :H],
                                                 seq=seq)
             dconv_w = dw.view_as(conv_w)
         else:
-            dxz[..., :H].copy_(dxc)
+            torch.add(dxc, dxc_g, out=dxz[..., :H])
         if ctx.pad_len is not None:   # + the pad-prefix state's share, in place
             kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len, dh0.float(),
                                    into=(dconv_b, dgate_w, dgate_b, dlam))

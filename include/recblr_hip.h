@@ -223,6 +223,15 @@ int rb_add_ln_bwd(const float* dy, const float* s, const float* gamma,
                   uint64_t seed, float p, float* ds, float* da,
                   float* dgamma_part, float* dbeta_part, float* dbias_part,
                   int64_t n_parts, int64_t rows, int64_t d, void* stream);
+/* rb_add_ln_bwd with the output's gradient given as two terms, dy + dy2
+ * (dy2 may be NULL): autograd's sum of the gradients of a LayerNorm output
+ * read by two consumers (the next projection's input gradient and a
+ * residual branch), added while loading instead of in a separate pass. */
+int rb_add_ln_bwd2(const float* dy, const float* dy2, const float* s, const float* gamma,
+                   const float* mean, const float* rstd, const uint8_t* mask,
+                   uint64_t seed, float p, float* ds, float* da,
+                   float* dgamma_part, float* dbeta_part, float* dbias_part,
+                   int64_t n_parts, int64_t rows, int64_t d, void* stream);
 
 /* FeedForward's inner activation (RecBLR.py:220-221) on [rows, cols]:
  * u = dropout(silu(a + bias)) (bias [cols] may be NULL: the w_1 bias folded
@@ -410,6 +419,27 @@ int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
  * R % 32 == 0, C % 128 == 0. */
 int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
                const float* bias, float* out, int64_t ldo, int accumulate, void* stream);
+
+/* ---- the same GEMMs on the f16 pipe, two-part split (csrc/gemm_half.hip) ----
+ * Every fp32 operand is scaled by an exact power of two and split into two
+ * fp16 parts, x = 2^-s (x0 + x1) (22 significant bits); the three products
+ * a0b0 + a0b1 + a1b0 accumulate in fp32 (error vs fp64 within a few fp32
+ * units, tests/test_gpu_gemm.py).  Weights: one scale per output column;
+ * A rows: one scale per row, chosen online by the kernel.
+ *
+ * Bytes of the f16 weight image of Bm [C, R] (two planes + C exponents). */
+int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R);
+
+/* Build the f16 weight images of up to RB_MAX_SPLIT_JOBS weights (jobs as for
+ * rb_gemm_split_weights; each Wf rb_gemm_h_weight_bytes(C, R) bytes). */
+int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
+
+/* rb_gemm_nt's contract on the f16 image (R % 32 == 0, C % 128 == 0,
+ * C <= 1024; accumulate must be 0).  rmax (optional, [ceil(M/32)] floats): max |A| over each
+ * 32-row group, the operand scale of rb_gemm_tn_h on the same rows. */
+int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                 const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
+                 void* stream);
 
 #ifdef __cplusplus
 }

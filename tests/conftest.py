@@ -32,17 +32,19 @@ def cuda():
 
 @pytest.fixture
 def split_gemm_calls(monkeypatch):
-    """Records every launch of the split-bf16 GEMM (kernels.gemm_nt, the
-    rb_gemm_nt C-ABI entry) as (M, R, C): tests use it to assert that the
-    path they claim to check actually ran the kernel."""
+    """Records every launch of the split-operand GEMM of the selected format
+    (kernels.gemm_nt_h / rb_gemm_nt_h for f16x3, kernels.gemm_nt / rb_gemm_nt
+    for bf16x6) as (M, R, C): tests use it to assert that the path they claim
+    to check actually ran the kernel."""
     from datamining_recblr_amd import kernels
 
     calls = []
-    orig = kernels.gemm_nt
+    for name in ("gemm_nt", "gemm_nt_h"):
+        orig = getattr(kernels, name)
 
-    def counted(a, wf, C, *args, **kw):
-        calls.append((a.shape[0], a.shape[1], C))
-        return orig(a, wf, C, *args, **kw)
+        def counted(a, wf, C, *args, _orig=orig, **kw):
+            calls.append((a.shape[0], a.shape[1], C))
+            return _orig(a, wf, C, *args, **kw)
 
-    monkeypatch.setattr(kernels, "gemm_nt", counted)
+        monkeypatch.setattr(kernels, name, counted)
     return calls

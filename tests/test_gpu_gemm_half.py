@@ -1,0 +1,172 @@
+"""GPU tests of the f16 two-part split fp32 GEMM (csrc/gemm_half.hip,
+rb_gemm_nt_h) — the default projection GEMM (RECBLR_GEMM=f16x3) of F.linear's
+forward and input-gradient products (RecBLR.py:162,165,167,213,214).
+
+Every operand is scaled by an exact power of two and split into two fp16
+parts; the error against an fp64 product is held to the level of torch's own
+fp32 GEMM (hipBLASLt) on the same data, also on rows whose magnitudes span
+the whole fp32 range (the per-row scale, and the exact recompute of rows that
+outgrow their first scale)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel_err(y, ref):
+    return ((y.double() - ref).abs().max() / ref.abs().max()).item()
+
+
+@pytest.mark.parametrize("M,K,N", [(4096, 128, 512), (5000, 256, 512), (4097, 512, 128),
+                                   (8192, 256, 128), (300, 128, 256), (1, 32, 128),
+                                   (257, 512, 384), (70001, 256, 512), (33, 1024, 1024)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_forward_matches_fp64_at_fp32_accuracy(cuda, M, K, N, bias):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + K + N)
+    x = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda) if bias else None
+    y = kernels.gemm_nt_h(x, kernels.gemm_h_weight(w), N, bias=b)
+    ref = x.double() @ w.double().t()
+    if bias:
+        ref = ref + b.double()
+    yt = torch.addmm(b, x, w.t()) if bias else x @ w.t()
+    e_h, e_torch = _rel_err(y, ref), _rel_err(yt, ref)
+    # fp32-level: a few ulps of the output scale, on a par with hipBLASLt
+    assert e_h < 2e-6, e_h
+    assert e_h < 4 * max(e_torch, 1e-7), (e_h, e_torch)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 128), (4100, 256, 512), (1024, 128, 256)])
+def test_input_gradient_orientation(cuda, M, N, K):
+    """Bm = W^T (the dX GEMM): the transposed image equals the image of the
+    materialised transpose, bit for bit."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(7 * M + N)
+    dy = torch.randn(M, N, generator=g).to(cuda)
+    w = (torch.randn(N, K, generator=g) / N ** 0.5).to(cuda)
+    wt = kernels.gemm_h_weight(w, transpose=True)
+    assert torch.equal(wt.view(torch.int16),
+                       kernels.gemm_h_weight(w.t().contiguous()).view(torch.int16))
+    dx = kernels.gemm_nt_h(dy, wt, K)
+    assert _rel_err(dx, dy.double() @ w.double()) < 2e-6
+
+
+def test_rows_across_the_fp32_range(cuda):
+    """Per-row relative error at fp32 level on rows scaled by 2^-60 .. 2^60,
+    zero rows, rows whose first 16 (or 48) entries are zero or tiny and rows
+    growing by 2^64 along K (their fp16 images would overflow the first
+    scale: the kernel flags the tile and recomputes the wave's rows with the
+    exact row max), a 3e37 entry; weight columns scaled by 1e-25 and zero."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(11)
+    M, K, N = 4096 + 77, 256, 128
+    a = torch.randn(M, K, generator=g)
+    a *= torch.exp2(torch.randint(-60, 60, (M, 1), generator=g).float())
+    a[5] = 0
+    a[6, :48] = 0
+    a[7, :16] *= 1e-12
+    a[8] *= torch.exp2(torch.arange(K).float() / 4)
+    a[9, 100] = 3e37
+    a[10] = 0
+    a[10, 255] = 1e-30
+    a[11, :200] = 1e-20
+    a[300:340, :16] = 0          # a whole wave's rows flagged
+    a = a.to(cuda)
+    w = torch.randn(N, K, generator=g)
+    w[3] *= 1e-25
+    w[4, :10] = 0
+    w[5] = 0
+    w = w.to(cuda)
+    ref = a.double() @ w.double().t()
+    y = kernels.gemm_nt_h(a, kernels.gemm_h_weight(w), N)
+    yt = a @ w.t()
+    den = a.double().abs() @ w.double().abs().t()
+    ok = den > 1e-30              # products inside fp32's normal range
+    e_h = ((y.double() - ref).abs() / den)[ok].max().item()
+    e_t = ((yt.double() - ref).abs() / den)[ok].max().item()
+    assert torch.isfinite(y).all()
+    assert e_h < 4 * max(e_t, 6e-8), (e_h, e_t)
+    assert (y[5] == 0).all()
+
+
+def test_row_strided_operand_and_output(cuda):
+    """A as a column slice of a wider activation (the x half of xz), out as a
+    row-strided view — the layouts the encoder hands over."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(3)
+    big = torch.randn(4096, 512, generator=g).to(cuda)
+    x = big[:, 256:]
+    w = (torch.randn(256, 256, generator=g) / 16).to(cuda)
+    outbig = torch.zeros(4096, 384, device=cuda)
+    out = outbig[:, :256]
+    kernels.gemm_nt_h(x, kernels.gemm_h_weight(w), 256, out=out)
+    assert _rel_err(out, x.double() @ w.double().t()) < 2e-6
+    assert outbig[:, 256:].abs().max().item() == 0.0
+
+
+def test_row_group_max_side_output(cuda):
+    """rmax[g] = max |A| over rows 32g .. 32g+31 (all columns), for a partial
+    last group too — the weight-gradient kernel's operand scale."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(5)
+    for M in (4096, 5000, 70001):
+        a = (torch.randn(M, 256, generator=g) * torch.rand(M, 1, generator=g) * 100).to(cuda)
+        w = torch.randn(512, 256, generator=g).to(cuda)
+        rmax = torch.full(((M + 31) // 32,), -1.0, device=cuda)
+        kernels.gemm_nt_h(a, kernels.gemm_h_weight(w), 512, rmax=rmax)
+        ref = torch.nn.functional.pad(a.abs().amax(1), (0, (-M) % 32)).view(-1, 32).amax(1)
+        assert torch.equal(rmax, ref)
+
+
+def test_deterministic(cuda):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(20000, 256, generator=g).to(cuda)
+    wf = kernels.gemm_h_weight(torch.randn(512, 256, generator=g).to(cuda))
+    y0 = kernels.gemm_nt_h(x, wf, 512)
+    for _ in range(3):
+        assert torch.equal(kernels.gemm_nt_h(x, wf, 512), y0)
+
+
+def test_batched_weight_images_equal_single(cuda):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(3)
+    ws = [torch.randn(n, k, generator=g).to(cuda) for n, k in ((512, 128), (256, 512), (128, 256))]
+    jobs, refs = [], []
+    for w in ws:
+        for tr in (False, True):
+            ref = kernels.gemm_h_weight(w, transpose=tr)
+            jobs.append((w, tr, torch.empty_like(ref)))
+            refs.append(ref)
+    kernels.gemm_h_split_weights(jobs)
+    for (_, _, wf), ref in zip(jobs, refs):
+        assert torch.equal(wf.view(torch.int16), ref.view(torch.int16))
+
+
+def test_layer_norm_backward_second_gradient(cuda):
+    """rb_add_ln_bwd2: LN backward of dy + dy2 (added on load) equals the LN
+    backward of the materialised sum, bit for bit."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(2)
+    rows, d = 5000, 128
+    a = torch.randn(rows, d, generator=g).to(cuda)
+    r = torch.randn(rows, d, generator=g).to(cuda)
+    gamma = torch.randn(d, generator=g).to(cuda)
+    beta = torch.randn(d, generator=g).to(cuda)
+    y, s, mean, rstd = kernels.add_ln_fwd(a, r, gamma, beta, 1e-12, save=True)
+    dy = torch.randn(rows, d, generator=g).to(cuda)
+    dy2 = torch.randn(rows, d, generator=g).to(cuda)
+    one = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, dy2=dy2, want_dbias=True)
+    ref = kernels.add_ln_bwd(dy + dy2, s, gamma, mean, rstd, want_dbias=True)
+    for x, xr in zip(one, ref):
+        assert torch.equal(x, xr)

@@ -1,0 +1,89 @@
+// gemmbench_h.hip — timing of the f16 two-part split GEMM (csrc/gemm_half.hip)
+// on the encoder's projection shapes.  Ablation builds:
+//   -DHN_NO_STORE / -DHN_NO_ADMA / -DHN_NSA=n
+//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 -I include \
+//       tools/gemmbench_h.hip -o tools/bin/gemmbench_h
+#include <cstdio>
+
+#include "../datamining_recblr_amd/csrc/gemm_half.hip"
+
+namespace rb {
+int launch_status(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) fprintf(stderr, "%s: %s\n", what, hipGetErrorString(e));
+  return (int)e;
+}
+int num_cus() {
+  int n = 0;
+  (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
+  return n;
+}
+}  // namespace rb
+using namespace rb;
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__global__ void fill(float* p, int64_t n, uint32_t seed, float scale) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 13; h *= 0x5bd1e995u; h ^= h >> 15;
+    p[i] = scale * ((h & 0xffffff) / 16777216.0f - 0.5f);
+  }
+}
+
+int main(int argc, char** argv) {
+  const int64_t M = argc > 1 ? atoll(argv[1]) : 204632;
+  struct Shape { const char* name; int R, C; };
+  const Shape shapes[] = {{"in.fwd", 128, 512}, {"in.dX", 512, 128}, {"gates.fwd", 256, 512},
+                          {"gates.dX", 512, 256}, {"out.fwd", 256, 128}, {"out.dX", 128, 256},
+                          {"w2.fwd", 512, 128}, {"w2.dX", 128, 512}};
+  float *A, *W, *O;
+  void* Wf;
+  CK(hipMalloc(&A, M * 512 * 4));
+  CK(hipMalloc(&O, M * 512 * 4));
+  CK(hipMalloc(&W, 512 * 512 * 4));
+  CK(hipMalloc(&Wf, 512 * 512 * 4 + 4096));
+  fill<<<4096, 256>>>(A, M * 512, 1, 2.0f);
+  fill<<<256, 256>>>(W, 512 * 512, 2, 0.1f);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  double tot = 0, totb = 0;
+  for (const Shape& s : shapes) {
+    rb_split_job job{W, s.R, s.C, s.R, 0, Wf};
+    CK((hipError_t)launch_split_weights_h(&job, 1, 0));
+    std::vector<float> ts;
+    for (int rep = 0; rep < 12; ++rep) {
+      CK(hipEventRecord(e0, 0));
+      int rc = launch_gemm_nt_h(A, s.R, M, s.R, Wf, s.C, nullptr, O, s.C, 0, nullptr, 0);
+      if (rc) { fprintf(stderr, "launch failed %d\n", rc); return 1; }
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ts.push_back(ms * 1e3f);
+    }
+    std::sort(ts.begin(), ts.end());
+    const double us = ts[ts.size() / 2];
+    const double fl = 2.0 * M * s.R * s.C;
+    const double by = 4.0 * M * (s.R + s.C);
+    tot += us;
+    totb += by;
+    printf("%-10s R=%3d C=%3d  %7.1f us  %6.1f TF  %6.2f TB/s\n", s.name, s.R, s.C, us,
+           fl / us / 1e6, by / us / 1e6);
+  }
+  printf("total %.1f us  (%.2f TB/s)\n", tot, totb / tot / 1e6);
+  return 0;
+}
