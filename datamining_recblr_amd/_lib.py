@@ -100,6 +100,8 @@ SIGNATURES = {
     "rb_gemm_h_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
     "rb_gemm_nt_h": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
                                     _fp, _fp]),
+    "rb_gemm_tn_h": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _i64,
+                                    _fp]),
 }
 
 

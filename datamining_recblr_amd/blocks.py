@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from . import kernels
 from ._lib import RecBLRNativeError
-from .linear import _timed, linear, mm_nn, mm_nt, wgrad
+from .linear import _timed, linear, mm_nn, mm_nt, rmax_buffer, wgrad
 
 __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
            "feed_forward"]
@@ -213,9 +213,14 @@ class _FeedForward(torch.autograd.Function):
         f = 2 * M * d * inner
         # b1 is added inside the activation kernel (the bias epilogue of the
         # library GEMM costs more than the add on the fly)
-        a1 = _timed("gemm", f, mm_nt, x2, w1)
+        # row-group maxima of the GEMM inputs: the weight gradients' operand scales
+        want = ctx.needs_input_grad[1] or ctx.needs_input_grad[3]
+        r_x = rmax_buffer(x2, inner, d) if want else None
+        a1 = _timed("gemm", f, mm_nt, x2, w1, rmax=r_x)
         u = kernels.silu_dropout_fwd(a1, seed=seed1, p=p, bias=b1)
-        a2 = _timed("gemm", f, mm_nt, u, w2, b2)
+        r_u = rmax_buffer(u, d, inner) if want else None
+        a2 = _timed("gemm", f, mm_nt, u, w2, b2, rmax=r_u)
+        ctx.r_x, ctx.r_u = r_x, r_u
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
                                               p=p, save=save)
@@ -234,16 +239,18 @@ class _FeedForward(torch.autograd.Function):
         ds, da2, dgamma, dbeta, db2 = kernels.add_ln_bwd(
             dy, s, gamma, mean, rstd, seed=ctx.seed2, p=ctx.p, want_ds=True, want_da=True,
             want_dbias=True, dy2=_pop(ctx.out_addend))
-        du = _timed("gemm", f, mm_nn, da2, w2)
-        dw2 = _timed("gemm", f, wgrad, da2, u)
+        r_da2 = rmax_buffer(da2, w2.shape[1], d) if ctx.r_u is not None else None
+        du = _timed("gemm", f, mm_nn, da2, w2, rmax=r_da2)
+        dw2 = _timed("gemm", f, wgrad, da2, u, ymax=r_da2, xmax=ctx.r_u)
         da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True,
                                             bias=b1)
-        dx = _timed("gemm", f, mm_nn, da1, w1)
+        r_da1 = rmax_buffer(da1, d, w1.shape[0]) if ctx.r_x is not None else None
+        dx = _timed("gemm", f, mm_nn, da1, w1, rmax=r_da1)
         if ctx.in_addend is not None:   # x's producer adds the residual's gradient
             ctx.in_addend.ds = ds
         else:
             dx.add_(ds)
-        dw1 = _timed("gemm", f, wgrad, da1, x2)
+        dw1 = _timed("gemm", f, wgrad, da1, x2, ymax=r_da1, xmax=ctx.r_x)
         return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None,
                 None, None)
 

@@ -598,4 +598,20 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
                           reinterpret_cast<hipStream_t>(stream));
 }
 
+int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
+                 int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
+                 void* stream) {
+  if (!dY || !X || !ymax || !xmax || !parts) return fail("rb_gemm_tn_h: null pointer");
+  if (M <= 0 || N <= 0 || K <= 0) return fail("rb_gemm_tn_h: empty shape");
+  if (N % 128 || K % 128 || N > 8192 || K > 8192)
+    return fail("rb_gemm_tn_h: N and K must be multiples of 128 (<= 8192)");
+  if (splits < 8 || splits % 8 || splits > 65536)
+    return fail("rb_gemm_tn_h: splits must be a positive multiple of 8");
+  if (ldy < N || ldx < K || ldy % 4 || ldx % 4) return fail("rb_gemm_tn_h: bad row strides");
+  if (!aligned16(dY) || !aligned16(X)) return fail("rb_gemm_tn_h: dY and X must be 16-byte aligned");
+  if ((N / 128) * (K / 128) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_h: grid too large");
+  return launch_gemm_tn_h(dY, ldy, X, ldx, M, (int)N, (int)K, ymax, xmax, parts, (int)splits,
+                          reinterpret_cast<hipStream_t>(stream));
+}
+
 }  // extern "C"

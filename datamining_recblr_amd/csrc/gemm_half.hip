@@ -571,6 +571,194 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_gemm_tn_h (weight gradient, split over rows):
+//   part[s][n, k] = sum over rows m of chunk s of dY[m, n] X[m, k]
+// (RecBLR.py:162,165,167,213,214: F.linear's dW = dY^T X).  The reduction
+// axis m is each operand's row axis, so the MFMA fragments (8 consecutive m
+// of one column per lane) are gathered by a transpose in LDS: every m-step of
+// 32 rows, each thread loads 8 rows x 4 columns of raw fp32 (16-B loads, two
+// steps ahead, in registers), scales, splits into the two fp16 planes and
+// writes each column's 8 values as one 16-B chunk of a column-major image
+// (80-B column pitch, chunk XOR (col >> 4) & 3: conflict-free writes and
+// fragment reads).  Scales: one power of two per operand and row chunk, from
+// the max over the chunk's 32-row groups that the forward / input-gradient
+// GEMMs wrote (rmax): values within 2^17 of the chunk max keep 22 bits.
+// Workgroup: 256 threads (2 x 2 waves of 64 x 64), a 128 x 128 tile of dW;
+// the tiles of one row chunk run on one XCD (their row re-reads hit its L2).
+constexpr int T_BT = 128;
+constexpr int T_PITCH = 80;                   // bytes per column of an image plane
+constexpr int T_PLANE = T_BT * T_PITCH;       // 10 KB
+constexpr int T_STAGE = 4 * T_PLANE;          // dY planes 0, 1 and X planes 0, 1
+constexpr int T_LDS = 2 * T_STAGE;            // double buffered: 80 KB
+constexpr int kTT = 14;                       // chunk max lands in [2^13, 2^14)
+
+__device__ __forceinline__ uint32_t tn_off(int col, int chunk) {
+  return col * T_PITCH + ((chunk ^ ((col >> 4) & 3)) << 4);
+}
+
+__device__ __forceinline__ void ds_write16(uint32_t addr, f16x8 v) {
+  asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
+}
+
+__global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy,
+                                                    const float* __restrict__ X, int64_t ldx,
+                                                    int64_t M, int N, int K,
+                                                    const float* __restrict__ ymax,
+                                                    const float* __restrict__ xmax,
+                                                    float* __restrict__ parts, int S, int64_t mk,
+                                                    int nt_k) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wk = wave & 1;
+  // block -> (tile, split): the tiles of one split share an XCD
+  const int G = gridDim.x;
+  const int idx = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int nt = (N / T_BT) * nt_k;
+  const int tile = idx % nt, s = idx / nt;
+  const int n0 = (tile / nt_k) * T_BT, k0 = (tile % nt_k) * T_BT;
+  const int64_t r_begin = (int64_t)s * mk;
+  const int64_t r_end = r_begin + mk < M ? r_begin + mk : M;
+  const int64_t nrows = r_end > r_begin ? r_end - r_begin : 0;
+  const int T = (int)((nrows + 31) / 32);
+
+  // chunk scales from the 32-row group maxima
+  float my = 0.0f, mx = 0.0f;
+  for (int64_t g = r_begin / 32 + tid; g * 32 < r_end; g += 256) {
+    my = fmaxf(my, ymax[g]);
+    mx = fmaxf(mx, xmax[g]);
+  }
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    my = fmaxf(my, __shfl_xor(my, o));
+    mx = fmaxf(mx, __shfl_xor(mx, o));
+  }
+  if (lane == 0) { red[wave] = my; red[4 + wave] = mx; }
+  __syncthreads();
+  my = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+  const int ey = my > 0.0f ? __builtin_amdgcn_frexp_expf(my) : 0;
+  const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;
+  __syncthreads();
+
+  // conversion role: operand op (0 = dY, 1 = X), columns 4cc..4cc+3,
+  // rows 8rg..8rg+7 of each m-step
+  const int op = tid >> 7;
+  const int cc = tid & 31;
+  const int rg = (tid >> 5) & 3;
+  const float* src = op == 0 ? Y + n0 + 4 * cc : X + k0 + 4 * cc;
+  const int64_t ld = op == 0 ? ldy : ldx;
+  const float sc = __builtin_amdgcn_ldexpf(1.0f, kTT - (op == 0 ? ey : ex));
+  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+
+  f32x4 raw0[8], raw1[8];
+  auto load = [&](int t, f32x4 (&r)[8]) {
+    const int64_t row0 = r_begin + (int64_t)t * 32 + rg * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      int64_t row = row0 + q;
+      row = row < r_end ? row : r_end - 1;  // rows past the chunk: zeroed on convert
+      r[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + row * ld));
+    }
+  };
+  auto convert = [&](f32x4 (&r)[8], int t, int buf) {
+    const int64_t row0 = r_begin + (int64_t)t * 32 + rg * 8;
+    if (row0 + 8 > r_end) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (row0 + q >= r_end) r[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    const uint32_t img = smem_base + buf * T_STAGE + op * 2 * T_PLANE;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f16x8 h0, h1;
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        f16x2 p0, p1;
+        split2h(f32x2{r[q][c], r[q + 1][c]} * sc, p0, p1);
+        h0[q] = p0[0]; h0[q + 1] = p0[1];
+        h1[q] = p1[0]; h1[q + 1] = p1[1];
+      }
+      const uint32_t off = tn_off(4 * cc + c, rg);
+      ds_write16(img + off, h0);
+      ds_write16(img + T_PLANE + off, h1);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+
+  const int h = lane >> 5;
+  auto mma = [&](int buf) {
+    const uint32_t iy = smem_base + buf * T_STAGE;
+    const uint32_t ix = iy + 2 * T_PLANE;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f16x8 a[2][2], b[2][2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const uint32_t oa = tn_off(64 * wm + 32 * i + (lane & 31), 2 * st + h);
+        const uint32_t ob = tn_off(64 * wk + 32 * i + (lane & 31), 2 * st + h);
+        a[i][0] = ds_read16<f16x8>(iy + oa);
+        a[i][1] = ds_read16<f16x8>(iy + T_PLANE + oa);
+        b[i][0] = ds_read16<f16x8>(ix + ob);
+        b[i][1] = ds_read16<f16x8>(ix + T_PLANE + ob);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0][0]),
+                     "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma_h(a[i][1], b[j][0], acc[i][j]);
+          acc[i][j] = mfma_h(a[i][0], b[j][1], acc[i][j]);
+          acc[i][j] = mfma_h(a[i][0], b[j][0], acc[i][j]);
+        }
+    }
+  };
+
+  if (T > 0) load(0, raw0);
+  if (T > 1) load(1, raw1);
+  for (int t = 0; t < T; t += 2) {
+    convert(raw0, t, 0);
+    if (t + 2 < T) load(t + 2, raw0);
+    __syncthreads();
+    mma(0);
+    if (t + 1 < T) {
+      convert(raw1, t + 1, 1);
+      if (t + 3 < T) load(t + 3, raw1);
+      __syncthreads();
+      mma(1);
+    }
+  }
+
+  // un-scale and store the partial tile (every split writes its slot, empty
+  // chunks zeros)
+  const int sh = ey + ex - 2 * kTT;
+  float* out = parts + (int64_t)s * N * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = k0 + 64 * wk + 32 * j + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = n0 + 64 * wm + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+        out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
+      }
+    }
+}
+
 template <bool BIAS>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
               const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
@@ -621,6 +809,24 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
   else
     run_nt_h<false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
   return launch_status("rb_gemm_nt_h");
+}
+
+int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
+                     int K, const float* ymax, const float* xmax, float* parts, int S,
+                     hipStream_t st) {
+  static bool done = false;  // benign race: idempotent
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_tn_h, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              T_LDS);
+    done = true;
+  }
+  const int nt_k = K / T_BT;
+  const int nt = (N / T_BT) * nt_k;
+  // rows per split: a multiple of 32 (the rmax groups)
+  const int64_t mk = ((M + S - 1) / S + 31) / 32 * 32;
+  k_gemm_tn_h<<<(unsigned)(nt * S), 256, T_LDS, st>>>(Y, ldy, X, ldx, M, N, K, ymax, xmax, parts,
+                                                      S, mk, nt_k);
+  return launch_status("rb_gemm_tn_h");
 }
 
 }  // namespace rb

@@ -938,3 +938,24 @@ def gemm_nt_h(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | No
               0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0), 0,
               0 if rmax is None else rmax.data_ptr(), _stream(a))
     return out
+
+
+def gemm_tn_h(dy: torch.Tensor, x: torch.Tensor, ymax: torch.Tensor, xmax: torch.Tensor,
+              splits: int) -> torch.Tensor:
+    """Row-chunk partials of dW = dy^T x on the f16 pipe (rb_gemm_tn_h):
+    [splits, N, K]; ymax / xmax: the 32-row-group maxima of dy / x (the
+    rmax outputs of gemm_nt_h on the same operands)."""
+    for t, n in ((dy, "dy"), (x, "x"), (ymax, "ymax"), (xmax, "xmax")):
+        _check(t, n)
+    if dy.dim() != 2 or x.dim() != 2 or dy.stride(1) != 1 or x.stride(1) != 1:
+        raise ValueError("dy and x must be 2-D with unit inner stride")
+    M, N = dy.shape
+    K = x.shape[1]
+    if x.shape[0] != M:
+        raise ValueError("dy and x must have the same rows")
+    if ymax.numel() < (M + 31) // 32 or xmax.numel() < (M + 31) // 32:
+        raise ValueError("ymax / xmax need ceil(M/32) entries")
+    parts = torch.empty((splits, N, K), device=dy.device, dtype=torch.float32)
+    _lib.call("rb_gemm_tn_h", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K,
+              ymax.data_ptr(), xmax.data_ptr(), parts.data_ptr(), splits, _stream(dy))
+    return parts

@@ -42,6 +42,9 @@ if _GEMM not in ("f16x3", "bf16x6", "torch"):
     raise ValueError(f"RECBLR_GEMM must be f16x3, bf16x6 or torch, got {_GEMM!r}")
 _split_on = os.environ.get("RECBLR_SPLIT_GEMM", "1") != "0" and _GEMM != "torch"
 _half = _GEMM == "f16x3"
+# weight gradients on the f16 pipe (rb_gemm_tn_h) when both operands' row-group
+# maxima are known (RECBLR_TN=0: hipBLASLt split-K, below)
+_tn_on = os.environ.get("RECBLR_TN", "1") != "0"
 _cache_on = os.environ.get("RECBLR_SPLIT_CACHE", "1") != "0"
 
 # Split images of the weights, kept across calls: (id(w), transpose) ->
@@ -128,22 +131,33 @@ def gemm_format() -> str:
     return _GEMM if _split_on else "torch"
 
 
-def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None) -> torch.Tensor:
+def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
+    """A [ceil(M/32)] buffer for the row-group maxima of `a` that the f16 GEMM
+    writes (the weight-gradient kernel's operand scale) — None when a's GEMM
+    with C outputs and R inputs will not run on the f16 kernel."""
+    if _half and _tn_on and _split_ok(a, C, R):
+        return torch.empty((a.shape[0] + 31) // 32, device=a.device, dtype=torch.float32)
+    return None
+
+
+def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
+          rmax: torch.Tensor | None = None) -> torch.Tensor:
     """a [M, K] @ w[N, K]^T (+ bias): F.linear's forward GEMM.  bf16
     activations (config 5) use the weight rounded to bf16 (bf16 MFMA, fp32
-    accumulation, bf16 output)."""
+    accumulation, bf16 output).  rmax: from rmax_buffer(a, N, K)."""
     if a.dtype != w.dtype:
         wb = w.to(a.dtype)
         return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
     N, K = w.shape
     if _split_ok(a, N, K):
         if _half:
-            return kernels.gemm_nt_h(a, _weight_split(w, False), N, bias=bias)
+            return kernels.gemm_nt_h(a, _weight_split(w, False), N, bias=bias, rmax=rmax)
         return kernels.gemm_nt(a, _weight_split(w, False), N, bias=bias)
     return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
 
 
-def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
+          rmax: torch.Tensor | None = None) -> torch.Tensor:
     """dy [M, N] @ w [N, K] (the input gradient of F.linear); with `out`,
     accumulated into it in place (out += dy @ w)."""
     if dy.dtype != w.dtype:
@@ -151,7 +165,7 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None) ->
         return out.addmm_(dy, wb) if out is not None else dy @ wb
     N, K = w.shape
     if _split_ok(dy, K, N) and _half:
-        r = kernels.gemm_nt_h(dy, _weight_split(w, True), K)
+        r = kernels.gemm_nt_h(dy, _weight_split(w, True), K, rmax=rmax)
         return r if out is None else out.add_(r)
     if _split_ok(dy, K, N) and (out is None or (out.stride(1) == 1 and out.shape == (dy.shape[0], K))):
         return kernels.gemm_nt(dy, _weight_split(w, True), K, out=out,
@@ -165,18 +179,39 @@ SPLIT_K = 64
 MIN_ROWS_FOR_SPLIT = 16384
 
 
-def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K) -> torch.Tensor:
+_ncus = {}
+
+
+def _tn_splits(dev, nt: int) -> int:
+    n = _ncus.get(dev)
+    if n is None:
+        n = _ncus[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return max(8, (2 * n // nt) // 8 * 8)   # ~2 workgroups per CU, a multiple of 8
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
+          ymax: torch.Tensor | None = None, xmax: torch.Tensor | None = None) -> torch.Tensor:
     """dW = dy2^T @ x2 for dy2 [M, N], x2 [M, K] (row-strided views allowed).
-    bf16 activations (config 5): bf16 MFMA partials, summed in fp32; the
-    result is fp32 like the parameter."""
+    With both operands' row-group maxima (ymax, xmax: the rmax outputs of the
+    f16 GEMMs that read dy2 and x2), on the f16 pipe (rb_gemm_tn_h: fixed-order
+    row-chunk partials); else hipBLASLt's batched split-K.  bf16 activations
+    (config 5): bf16 MFMA partials, summed in fp32; the result is fp32 like
+    the parameter."""
     M = dy2.shape[0]
+    N, K = dy2.shape[1], x2.shape[1]
+    if (ymax is not None and xmax is not None and M >= MIN_ROWS_FOR_SPLIT and N % 128 == 0
+            and K % 128 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1
+            and dy2.stride(0) % 4 == 0 and x2.stride(0) % 4 == 0
+            and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0):
+        S = _tn_splits(dy2.device, (N // 128) * (K // 128))
+        parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
+        return kernels.colsum(parts.view(S, -1)).view(N, K)
     if M < MIN_ROWS_FOR_SPLIT or splits <= 1:
         return (dy2.t() @ x2).float()
     mk = M // splits
     main = mk * splits
     a = dy2[:main].unflatten(0, (splits, mk)).transpose(1, 2)
     b = x2[:main].unflatten(0, (splits, mk))
-    N, K = dy2.shape[1], x2.shape[1]
     # the M % splits leftover rows (packed batches have any M) go to one more
     # partial slot, summed by the same fixed-order colsum (no extra add pass)
     parts = torch.empty((splits + (main < M), N, K), device=dy2.device, dtype=dy2.dtype)
@@ -220,7 +255,9 @@ class LinearFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, slot=None):
         x2 = x.reshape(-1, x.shape[-1])
         flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
-        y = _timed("gemm", flops, mm_nt, x2, weight, bias)
+        rx = rmax_buffer(x2, weight.shape[0], weight.shape[1]) if ctx.needs_input_grad[1] else None
+        y = _timed("gemm", flops, mm_nt, x2, weight, bias, rmax=rx)
+        ctx.rx = rx
         ctx.save_for_backward(x2, weight)
         ctx.has_bias = bias is not None
         ctx.slot = slot
@@ -232,9 +269,11 @@ class LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         flops = 2 * x2.shape[0] * x2.shape[1] * weight.shape[0]
         dx = dw = db = None
+        ry = None
         if ctx.needs_input_grad[0]:
             slot = ctx.slot
-            dx = _timed("gemm", flops, mm_nn, dy2, weight)
+            ry = rmax_buffer(dy2, weight.shape[1], weight.shape[0]) if ctx.rx is not None else None
+            dx = _timed("gemm", flops, mm_nn, dy2, weight, rmax=ry)
             if slot is not None and slot.ds is not None:
                 if slot.rows is not None:        # residual of gathered rows
                     dx.index_add_(0, slot.rows, slot.ds.view(-1, weight.shape[1]))
@@ -245,7 +284,7 @@ class LinearFn(torch.autograd.Function):
                 # else: x's producer adds slot.ds while loading (rb_add_ln_bwd2)
             dx = dx.view(*dy.shape[:-1], weight.shape[1])
         if ctx.needs_input_grad[1]:
-            dw = _timed("gemm", flops, wgrad, dy2, x2)
+            dw = _timed("gemm", flops, wgrad, dy2, x2, ymax=ry, xmax=ctx.rx)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = (kernels.colsum(dy2.contiguous()) if dy2.dtype == torch.float32
                   else dy2.sum(0, dtype=torch.float32))

@@ -30,7 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from . import kernels
-from .linear import _timed, mm_nn, mm_nt, wgrad
+from .linear import _timed, mm_nn, mm_nt, rmax_buffer, wgrad
 
 __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDLRUCore",
            "bd_lru"]
@@ -106,8 +106,10 @@ class BDLRUCore(torch.autograd.Function):
         rows = xz.numel() // H2
         gflops = 2 * rows * H * H2
         # gates GEMM without its bias: the gate kernels add gate_b on the fly
-        rg = _timed("gemm", gflops, mm_nt, xc.reshape(rows, H), gate_w).view(
-            *xz.shape[:-1], H2)
+        xc2 = xc.reshape(rows, H)
+        r_xc = rmax_buffer(xc2, H2, H) if ctx.needs_input_grad[3] else None
+        rg = _timed("gemm", gflops, mm_nt, xc2, gate_w, rmax=r_xc).view(*xz.shape[:-1], H2)
+        ctx.r_xc = r_xc
         train = any(ctx.needs_input_grad)
         y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b,
                                            seq=seq, last_only=last_only)
@@ -137,10 +139,12 @@ class BDLRUCore(torch.autograd.Function):
             seq=seq, last_only=ctx.last_only)
         drg2 = drg.view(rows, H2)
         gflops = 2 * rows * H * H2
-        dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H))
         # dL/dxc through the gates GEMM: the conv backward reads it as its second
         # gradient term (g1 + g2 on load, no separate add pass)
-        dxc_g = _timed("gemm", gflops, mm_nn, drg2, gate_w).view_as(dxc)
+        r_drg = rmax_buffer(drg2, H, H2) if ctx.r_xc is not None else None
+        dxc_g = _timed("gemm", gflops, mm_nn, drg2, gate_w, rmax=r_drg).view_as(dxc)
+        dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H), ymax=r_drg,
+                         xmax=ctx.r_xc)
         dconv_w = dconv_b = None
         if ctx.use_conv:
             dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, dxc_g, dxz[..., :H],

@@ -441,6 +441,19 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
                  const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                  void* stream);
 
+/* Weight gradient of F.linear, dW = dY^T X, as `splits` fixed-order row-chunk
+ * partials on the f16 pipe (two-part split, three products):
+ * parts[s][n, k] = sum over the rows m of chunk s of dY[m, n] X[m, k]
+ * (rows split into `splits` chunks of a multiple of 32 rows; parts [splits,
+ * N, K] fp32, every slot written; sum them in order, e.g. rb_colsum).
+ * ymax / xmax [ceil(M/32)]: max |dY| / |X| over each 32-row group — the rmax
+ * side outputs of the rb_gemm_nt_h calls that read the same operands (the
+ * operand scales).  N % 128 == 0, K % 128 == 0, splits % 8 == 0, row strides
+ * multiples of 4, operands 16-B aligned. */
+int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
+                 int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
+                 void* stream);
+
 #ifdef __cplusplus
 }
 #endif

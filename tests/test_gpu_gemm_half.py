@@ -170,3 +170,55 @@ def test_layer_norm_backward_second_gradient(cuda):
     ref = kernels.add_ln_bwd(dy + dy2, s, gamma, mean, rstd, want_dbias=True)
     for x, xr in zip(one, ref):
         assert torch.equal(x, xr)
+
+
+def _row_group_max(a):
+    M = a.shape[0]
+    return torch.nn.functional.pad(a.abs().amax(1), (0, (-M) % 32)).view(-1, 32).amax(1)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(204632, 512, 256, 64), (70001, 512, 128, 128),
+                                     (4096 + 77, 128, 256, 256), (5000, 128, 512, 8),
+                                     (300, 256, 128, 64)])
+def test_weight_gradient_tn_matches_fp64(cuda, M, N, K, S):
+    """rb_gemm_tn_h: dW = dY^T X from fixed-order row-chunk partials (empty
+    chunks write zeros) at fp32-level error next to hipBLASLt's fp32 GEMM, with
+    the operand scales taken from the forward/input-gradient GEMMs' rmax."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + N + K)
+    dy = (torch.randn(M, N, generator=g) * torch.rand(M, 1, generator=g) * 1e-3).to(cuda)
+    x = (torch.randn(M, K, generator=g) * 3).to(cuda)
+    ymax = torch.empty((M + 31) // 32, device=cuda)
+    xmax = torch.empty((M + 31) // 32, device=cuda)
+    # the side outputs of the GEMMs that read the same operands
+    kernels.gemm_nt_h(dy, kernels.gemm_h_weight(torch.randn(128, N, device=cuda)), 128, rmax=ymax)
+    kernels.gemm_nt_h(x, kernels.gemm_h_weight(torch.randn(128, K, device=cuda)), 128, rmax=xmax)
+    assert torch.equal(ymax, _row_group_max(dy)) and torch.equal(xmax, _row_group_max(x))
+    parts = kernels.gemm_tn_h(dy, x, ymax, xmax, S)
+    assert parts.shape == (S, N, K)
+    dw = kernels.colsum(parts.view(S, -1)).view(N, K)
+    ref = dy.double().t() @ x.double()
+    e_h = _rel_err(dw, ref)
+    e_t = _rel_err(dy.t() @ x, ref)
+    assert e_h < 2e-6 and e_h < 4 * max(e_t, 1e-7), (e_h, e_t)
+    # deterministic
+    assert torch.equal(kernels.gemm_tn_h(dy, x, ymax, xmax, S), parts)
+
+
+def test_weight_gradient_rows_decaying_over_2_to_the_60(cuda):
+    """Rows whose magnitudes decay by 2^60 along the chunk (the BD-LRU's
+    alpha^t gradients): the per-chunk scale keeps the dominant rows exact and
+    the tiny rows' contributions below fp32 rounding of the sum."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(4)
+    M, N, K = 65536, 256, 128
+    decay = torch.exp2(-(torch.arange(M) % 1000).float() * 0.06)[:, None]
+    dy = (torch.randn(M, N, generator=g) * decay).to(cuda)
+    x = torch.randn(M, K, generator=g).to(cuda)
+    S = 64
+    dw = kernels.colsum(kernels.gemm_tn_h(dy, x, _row_group_max(dy), _row_group_max(x), S)
+                        .view(S, -1)).view(N, K)
+    ref = dy.double().t() @ x.double()
+    assert _rel_err(dw, ref) < 4 * max(_rel_err(dy.t() @ x, ref), 1e-7)
