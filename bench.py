@@ -38,6 +38,8 @@ from datamining_recblr_amd.recbole_compat import SyntheticDataset  # noqa: E402
 METRIC = "sequences/sec fwd+bwd at B=2048 L=200 d=128; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP32_MFMA_PEAK_TFS = 157.3     # MI355X dense fp32 MFMA spec (MI355X_MICROARCH.md)
+F16_MFMA_PEAK_TFS = 2516.6     # MI355X dense f16/bf16 MFMA (MI355X_MICROARCH.md)
+F16X3_PEAK_TFS = F16_MFMA_PEAK_TFS / 3   # fp32-equivalent: 3 f16 products per fp32 product
 DOMINANT = "rb_gate_scan_bwd"  # the HIP kernel moving the most bytes per step
 
 
@@ -143,24 +145,27 @@ def pmc_traffic(args, kernel_prefix):
 
 
 def pmc_mfma(args):
-    """MFMA busy fraction of the projection GEMMs (>= 20 GFLOP per launch) from
-    the newest committed PMC summary (profiles/*_pmc_mfma.json,
-    tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs)),
-    per family: the split-bf16 kernel (k_gemm_nt: bf16 MFMA instructions, 6
-    per fp32 product) and the hipBLASLt fp32 kernels.  Busy is the fraction
-    of the MFMA pipe's cycles, whatever the dtype."""
+    """MFMA busy fraction of the projection GEMMs from the newest committed PMC
+    summary (profiles/*_pmc_mfma.json, tools/pmc_mfma.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs)), per kernel family:
+    the f16 split kernels (k_gemm_nt_h / k_gemm_tn_h: 3 f16 MFMA products per
+    fp32 product), the bf16 six-product kernel (k_gemm_nt) and hipBLASLt's fp32
+    kernels (>= 20 GFLOP per launch).  Busy is the fraction of the MFMA pipe's
+    cycles, whatever the dtype."""
     if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
         return None
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_mfma.json")))
     if not files:
         return None
     data = json.load(open(files[-1]))
-    fam = {"split_bf16": [], "hipblaslt_f32": []}
-    for k in data.get("kernels", {}).values():
+    fam = {"f16x3": [], "bf16x6": [], "hipblaslt_f32": []}
+    for name, k in data.get("kernels", {}).items():
         if not k.get("mfma_util"):
             continue
-        if k.get("mfma_flops_bf16_per_dispatch", 0) >= 2e10:
-            fam["split_bf16"].append(k["mfma_util"])
+        if "k_gemm_nt_h" in name or "k_gemm_tn_h" in name:
+            fam["f16x3"].append(k["mfma_util"])
+        elif k.get("mfma_flops_bf16_per_dispatch", 0) >= 2e10:
+            fam["bf16x6"].append(k["mfma_util"])
         elif k.get("mfma_flops_f32_per_dispatch", 0) >= 2e10:
             fam["hipblaslt_f32"].append(k["mfma_util"])
     out = {f: {"min": min(u), "max": max(u)} for f, u in fam.items() if u}
@@ -168,6 +173,26 @@ def pmc_mfma(args):
         return None
     out["source"] = os.path.relpath(files[-1], ROOT)
     return out
+
+
+def gemm_bytes(by_shape):
+    """Algorithmic HBM bytes per step of the projection GEMMs from the
+    per-shape labels: fwd / dX (mm_nt, mm_nn) read A [M, K] and write
+    out [M, N]; a weight gradient (wgrad) reads dY [M, N] and X [M, K]
+    (weights, partials and row-group maxima are negligible)."""
+    import re
+    total = 0.0
+    for label, v in by_shape.items():
+        m = re.match(r"(mm_nt|mm_nn)\[(\d+)x(\d+)->(\d+)\]", label)
+        if m:
+            M, K, N = int(m.group(2)), int(m.group(3)), int(m.group(4))
+            total += v["per_step"] * 4.0 * M * (K + N)
+            continue
+        m = re.match(r"wgrad\[(\d+):(\d+)x(\d+)\]", label)
+        if m:
+            M, N, K = int(m.group(1)), int(m.group(2)), int(m.group(3))
+            total += v["per_step"] * 4.0 * M * (N + K)
+    return total
 
 
 def scan_microbench(args, dev, reps=20):
@@ -453,18 +478,35 @@ def main():
         g = summ.pop("gemm", None)
         if g is not None:
             tf = g["bytes"] / (g["ms"] * 1e-3) / 1e12
-            gemm = {"bound": "mfma", "dtype": "f32", "achieved": round(tf, 1),
-                    "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                    "frac": round(tf / FP32_MFMA_PEAK_TFS, 4),
-                    "ms_per_step": round(g["ms"] / args.steps, 3),
+            from datamining_recblr_amd.linear import gemm_format
+            fmt = gemm_format()
+            peak = F16X3_PEAK_TFS if fmt == "f16x3" else FP32_MFMA_PEAK_TFS
+            by_shape = timer.gemm_detail(args.steps)
+            gb = gemm_bytes(by_shape)
+            gms = g["ms"] / args.steps
+            gemm = {"bound": "hbm", "dtype": "f32 (" + fmt + " split operands)" if fmt != "torch"
+                    else "f32",
+                    "achieved": round(tf, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(tf / peak, 4),
+                    "hbm": {"algo_bytes_per_step": int(gb),
+                            "achieved_gbs": round(gb / (gms * 1e-3) / 1e9, 1),
+                            "frac": round(gb / (gms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                            "note": "fp32 A read + fp32 output write per GEMM (dY, X reads "
+                                    "for weight gradients): these tall-skinny GEMMs are "
+                                    "bound by their row streams at f16x3"},
+                    "ms_per_step": round(gms, 3),
                     "gemms_per_step": g["launches"] / args.steps,
                     "flops_per_step": int(g["bytes"] / args.steps),
-                    "library": ("split-bf16 MFMA kernel (csrc/gemm_split.hip) for the [B*L] "
-                                "forward/input-gradient GEMMs, " if split_gemm_enabled() else "")
-                               + "hipBLASLt/rocBLAS via torch (split-K batched weight gradients)",
+                    "library": {"f16x3": "f16 two-part split MFMA kernels (csrc/gemm_half.hip): "
+                                         "rb_gemm_nt_h forward/input-gradient, rb_gemm_tn_h "
+                                         "weight gradients; torch/hipBLASLt below 4096 rows",
+                                "bf16x6": "split-bf16 MFMA kernel (csrc/gemm_split.hip) for the "
+                                          "[B*L] forward/input-gradient GEMMs, hipBLASLt split-K "
+                                          "weight gradients",
+                                "torch": "hipBLASLt/rocBLAS via torch"}[fmt],
                     "tuned_table": tuned_gemms_active(),
                     "mfma_busy": pmc_mfma(args),
-                    "by_shape": timer.gemm_detail(args.steps),
+                    "by_shape": by_shape,
                     "breakdown_pass_ms_per_step": round(breakdown_ms, 3)}
         kernels_report = {}
         for name, d in summ.items():

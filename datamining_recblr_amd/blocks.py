@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from . import kernels
 from ._lib import RecBLRNativeError
-from .linear import _timed, linear, mm_nn, mm_nt, rmax_buffer, wgrad
+from .linear import _timed, fire_hooks, has_hooks, linear, mm_nn, mm_nt, rmax_buffer, wgrad
 
 __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
            "feed_forward"]
@@ -206,7 +206,7 @@ class _FeedForward(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, gamma, beta, seed1, seed2, p, eps, in_addend=None,
-                out_addend=None):
+                out_addend=None, observe=None):
         d = x.shape[-1]
         x2 = x.reshape(-1, d)
         M, inner = x2.shape[0], w1.shape[0]
@@ -221,6 +221,9 @@ class _FeedForward(torch.autograd.Function):
         r_u = rmax_buffer(u, d, inner) if want else None
         a2 = _timed("gemm", f, mm_nt, u, w2, b2, rmax=r_u)
         ctx.r_x, ctx.r_u = r_x, r_u
+        if observe is not None:   # module hooks of w_1 / w_2 (feed_forward)
+            observe(x2.view(x.shape), (a1 + b1).view(*x.shape[:-1], inner), u.view(*x.shape[:-1], inner),
+                    a2.view(x.shape))
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
                                               p=p, save=save)
@@ -252,7 +255,7 @@ class _FeedForward(torch.autograd.Function):
             dx.add_(ds)
         dw1 = _timed("gemm", f, wgrad, da1, x2, ymax=r_da1, xmax=ctx.r_x)
         return (dx.view(dy.shape), dw1, db1, dw2, db2, dgamma, dbeta, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 def add_dropout_layer_norm(a, residual, dropout: torch.nn.Dropout, ln: torch.nn.LayerNorm,
@@ -301,8 +304,13 @@ def feed_forward(x, ffn, training: bool, in_addend: ResidualGrad | None = None,
         h = silu_dropout(linear(x, ffn.w_1), ffn.dropout, training)
         return add_dropout_layer_norm(linear(h, ffn.w_2), x, ffn.dropout, ffn.layer_norm,
                                       training)
+    observe = None
+    if has_hooks(ffn.w_1) or has_hooks(ffn.w_2):
+        def observe(x_, a1, u, a2):
+            fire_hooks(ffn.w_1, (x_,), a1)
+            fire_hooks(ffn.w_2, (u,), a2)
     p, seed1 = _drop(ffn.dropout, training)
     seed2 = draw_seed() if p > 0.0 else 0
     return _FeedForward.apply(x, ffn.w_1.weight, ffn.w_1.bias, ffn.w_2.weight, ffn.w_2.bias,
                               ffn.layer_norm.weight, ffn.layer_norm.bias, seed1, seed2, p,
-                              ffn.layer_norm.eps, in_addend, out_addend)
+                              ffn.layer_norm.eps, in_addend, out_addend, observe)

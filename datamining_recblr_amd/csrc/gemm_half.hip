@@ -67,7 +67,12 @@ __device__ __forceinline__ void split2h(f32x2 x, f16x2& h0, f16x2& h1) {
 }
 
 __device__ __forceinline__ f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
+#ifdef HN_NO_MFMA
+  c[0] += (float)a[0] * (float)b[1];
+  return c;
+#else
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+#endif
 }
 
 // max(|a|, |b|, |c|) in one instruction (no NaN canonicalisation: a NaN input
@@ -378,7 +383,9 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         if (stored_prev) wait_vm<16>(); else wait_vm<0>();
       }
     }
+#ifndef HN_NO_BARRIER
     __builtin_amdgcn_s_barrier();
+#endif
 
     const uint32_t sa = smem_base + c_slot_a * N_A_STAGE;
     const uint32_t sb = smem_base + N_NSA * N_A_STAGE + c_slot_b * N_B_STAGE + lane * 16;
@@ -407,6 +414,10 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         flag_tile = flag_tile || __builtin_amdgcn_ballot_w64(mx > thr) != 0;
       }
       f16x8 a0, a1;
+#ifdef HN_NO_SPLIT
+      a0 = __builtin_bit_cast(f16x8, xa);
+      a1 = __builtin_bit_cast(f16x8, xb);
+#else
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f32x2 v = (q < 2 ? f32x2{xa[2 * q], xa[2 * q + 1]}
@@ -416,6 +427,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         a0[2 * q] = h0[0]; a0[2 * q + 1] = h0[1];
         a1[2 * q] = h1[0]; a1[2 * q + 1] = h1[1];
       }
+#endif
       // per column block: the small partial products first
       asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b00), "+v"(b01));
       acc[0] = mfma_h(a1, b00, acc[0]);
@@ -439,7 +451,9 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       acc[3] = mfma_h(a0, b10, acc[3]);
     };
     substep(0);
+#ifndef HN_NO_BDMA
     if (u + 1 < U) issueB();
+#endif
 #ifndef HN_NO_ADMA
     if (u + N_LA < U) issueA();
 #endif
@@ -758,6 +772,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
       }
     }
 }
+
 
 template <bool BIAS>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,

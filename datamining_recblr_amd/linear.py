@@ -34,7 +34,8 @@ import torch
 
 from . import gemm_tuning, kernels
 
-__all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled"]
+__all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled",
+           "HipLinearForward", "has_hooks", "fire_hooks"]
 
 SPLIT_MIN_ROWS = 4096
 _GEMM = os.environ.get("RECBLR_GEMM", "f16x3")
@@ -59,6 +60,14 @@ _cache_on = os.environ.get("RECBLR_SPLIT_CACHE", "1") != "0"
 # invalidate_split_cache() (or sets RECBLR_SPLIT_CACHE=0).
 _split_cache: dict = {}
 _opt_steps = [0]
+# RECBLR_SPLIT_CACHE_CHECK=1: every cached image is compared with a fresh
+# split of the weight at each use and a stale one raises (debug mode for code
+# that rewrites weights behind torch.optim's back, e.g. through .data)
+_cache_check = os.environ.get("RECBLR_SPLIT_CACHE_CHECK", "0") == "1"
+
+
+class StaleSplitCacheError(RuntimeError):
+    """A cached split weight image no longer matches its weight."""
 
 
 def _count_step(*_args, **_kw):
@@ -93,6 +102,10 @@ def _weight_split(w: torch.Tensor, transpose: bool) -> torch.Tensor:
     key = (id(w), transpose)
     e = _split_cache.get(key)
     if e is not None and e[0]() is w and e[1] == w.data_ptr() and e[2] == _stamp(w):
+        if _cache_check and not torch.equal(e[3], _make_image(w, transpose)):
+            raise StaleSplitCacheError(
+                "cached split image of a weight is stale: the weight was rewritten without "
+                "a torch.optim step or a version bump; call linear.invalidate_split_cache()")
         return e[3]
     if e is None or e[0]() is not w or e[1] != w.data_ptr():
         # new (or re-allocated) weight: its own split, then cached
@@ -289,6 +302,52 @@ class LinearFn(torch.autograd.Function):
             db = (kernels.colsum(dy2.contiguous()) if dy2.dtype == torch.float32
                   else dy2.sum(0, dtype=torch.float32))
         return dx, dw, db, None
+
+
+def has_hooks(module: torch.nn.Module) -> bool:
+    """Forward (pre-)hooks registered on `module` or globally."""
+    g = torch.nn.modules.module
+    return bool(module._forward_hooks or module._forward_pre_hooks
+                or g._global_forward_hooks or g._global_forward_pre_hooks)
+
+
+def fire_hooks(module: torch.nn.Module, args: tuple, output) -> None:
+    """Run the forward pre-hooks and hooks nn.Module.__call__ would run for
+    `module(*args) -> output`, for a module whose arithmetic happens inside a
+    fused kernel (the gates Linear inside the BD-LRU kernels, the FeedForward
+    Linears): observers — FLOP counters such as RecBole's get_flops
+    (run.py:76-77), profilers — see the call.  A hook that returns a value
+    (would replace the input or the output) cannot be honoured there and
+    raises."""
+    g = torch.nn.modules.module
+    for hook in (*g._global_forward_pre_hooks.values(), *module._forward_pre_hooks.values()):
+        if hook(module, args) is not None:
+            raise NotImplementedError(
+                "a forward pre-hook that modifies the input of a Linear fused into a RecBLR "
+                "HIP kernel is not supported")
+    for hook in (*g._global_forward_hooks.values(), *module._forward_hooks.values()):
+        if hook(module, args, output) is not None:
+            raise NotImplementedError(
+                "a forward hook that replaces the output of a Linear fused into a RecBLR "
+                "HIP kernel is not supported")
+
+
+class HipLinearForward:
+    """nn.Linear.forward on the HIP path, installed per instance
+    (``m.forward = HipLinearForward(m)``) so the module's own __call__ —
+    hooks included — runs it while its type stays nn.Linear (FLOP counters
+    dispatch on the exact type).  A residual-gradient slot for the next call
+    is passed through the ``_recblr_slot`` attribute (blocks.ResidualGrad).
+    A plain object (not a bound method) so the module still pickles."""
+
+    def __init__(self, module: torch.nn.Linear):
+        self.module = module
+
+    def __call__(self, x: torch.Tensor) -> torch.Tensor:
+        m = self.module
+        slot = m.__dict__.get("_recblr_slot")
+        m.__dict__["_recblr_slot"] = None
+        return linear(x, m, slot)
 
 
 def linear(x: torch.Tensor, module: torch.nn.Linear, slot=None) -> torch.Tensor:

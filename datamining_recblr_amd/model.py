@@ -31,7 +31,7 @@ from ._lib import RecBLRNativeError
 from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
                      feed_forward)
 from .kernels import Packed, pack_plan
-from .linear import linear
+from .linear import HipLinearForward, fire_hooks, has_hooks, linear
 from .recbole_compat import BPRLoss, SequentialRecommender
 from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
@@ -60,9 +60,12 @@ class _PinnedRing:
         if self.events[i] is not None:
             self.events[i].synchronize()
         buf[:n].copy_(host)
-        out = buf[:n].to(device, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
+        # the copy and its event on the TARGET device's current stream (the
+        # current device may be another one)
+        with torch.cuda.device(device):
+            out = buf[:n].to(device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(device))
         self.events[i] = ev
         return out
 
@@ -109,6 +112,10 @@ class GatedRecurrentLayer(nn.Module):
         self.gates = nn.Linear(hidden, 2 * hidden, bias=True)
         self.Lambda = nn.Parameter(torch.linspace(lo, hi, hidden))
         self.output = nn.Linear(hidden, d_model, bias=False)
+        # the projections run on the HIP path through their own nn.Linear
+        # __call__ (forward hooks fire, the module type stays nn.Linear)
+        for m in (self.input, self.output):
+            m.forward = HipLinearForward(m)
 
     def forward(self, x, pad=None, slot=None, rows=None, seq=None):
         """pad: None (the reference's pow2 pad prefix for x's length) or an
@@ -123,19 +130,26 @@ class GatedRecurrentLayer(nn.Module):
             raise RecBLRNativeError(
                 "GatedRecurrentLayer runs only on the MI355X HIP path (ROCm GPU tensors); "
                 "move the model to a GPU. The CPU restatement under oracle/ is test-only.")
-        xz = linear(x, self.input, slot)
+        self.input._recblr_slot = slot
+        xz = self.input(x)
         # the last layer under gather_indexes on packed sequences needs y only
         # at each sequence's last row: the scan kernels keep just those
         last_only = (_LAST_ONLY and rows is not None and seq is not None
                      and rows is seq.last and xz.dtype == torch.float32)
+        observe = None
+        if has_hooks(self.gates) or has_hooks(self.conv1d):
+            def observe(x_, xc, rg):   # hooks of the Linear / Conv1d fused into bd_lru
+                if not self.disable_conv1d:
+                    fire_hooks(self.conv1d, (x_.transpose(-1, -2),), xc.transpose(-1, -2))
+                fire_hooks(self.gates, (xc,), rg + self.gates.bias)
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad,
-                   seq=seq, last_only=last_only)
+                   seq=seq, last_only=last_only, observe=observe)
         if last_only:
             y = y.index_select(0, seq.inv)   # packed-sequence order -> batch order
         elif rows is not None:
             y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
-        return linear(y, self.output)
+        return self.output(y)
 
     @staticmethod
     def pad_len(seq_len: int) -> int:

@@ -88,7 +88,7 @@ class BDLRUCore(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq=None,
-                last_only=False, pad_len=None):
+                last_only=False, pad_len=None, observe=None):
         """h0: an initial state given as an input (its gradient returned), or
         pad_len (int P > 0 or int64 [B] per-row lengths) with h0 None: the
         pad-prefix state computed here, its gradient added in place into the
@@ -110,6 +110,8 @@ class BDLRUCore(torch.autograd.Function):
         r_xc = rmax_buffer(xc2, H2, H) if ctx.needs_input_grad[3] else None
         rg = _timed("gemm", gflops, mm_nt, xc2, gate_w, rmax=r_xc).view(*xz.shape[:-1], H2)
         ctx.r_xc = r_xc
+        if observe is not None:   # module hooks of the fused conv / gates (model.py)
+            observe(x, xc, rg)
         train = any(ctx.needs_input_grad)
         y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b,
                                            seq=seq, last_only=last_only)
@@ -156,7 +158,7 @@ class BDLRUCore(torch.autograd.Function):
             kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len, dh0.float(),
                                    into=(dconv_b, dgate_w, dgate_b, dlam))
         return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
-                dh0 if ctx.has_h0 else None, None, None, None, None)
+                dh0 if ctx.has_h0 else None, None, None, None, None, None)
 
 
 def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
@@ -169,7 +171,7 @@ def row_pad_lens(lengths: torch.Tensor) -> torch.Tensor:
 
 
 def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq=None,
-           last_only=False):
+           last_only=False, observe=None):
     """Everything between the in- and out-projections of RecBLR.py:170-207.
 
     pad=None: the reference's pad prefix pow2(L) - L for the batch's L.
@@ -179,7 +181,8 @@ def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq
     unpadded sequence, run_with_unseen.py:222-225).
     seq: kernels.Packed — xz holds only each sequence's first len_b positions
     ([ntok, 2H]); the batch's L (for the pad prefix) is seq.L.
-    last_only: return only each sequence's last position, [B, H] (fp32)."""
+    last_only: return only each sequence's last position, [B, H] (fp32).
+    observe: optional callable (x, xc, rg) run in the forward (module hooks)."""
     if pad is None:
         P = pow2_pad_len(seq.L if seq is not None else xz.shape[1])
         pad_len = P if (P and use_conv) else None
@@ -188,6 +191,6 @@ def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq
     if not _FOLD_PAD and pad_len is not None:   # A/B: separate autograd node
         h0 = PadPrefix.apply(conv_b, gate_w, gate_b, lam, pad_len)
         return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, h0, use_conv, seq,
-                               last_only)
+                               last_only, None, observe)
     return BDLRUCore.apply(xz, conv_w, conv_b, gate_w, gate_b, lam, None, use_conv, seq,
-                           last_only, pad_len)
+                           last_only, pad_len, observe)

@@ -1,0 +1,85 @@
+"""Module hooks on the HIP path (boundary fidelity): RecBole's
+FLOP counter (get_flops, run.py:76-77) and profilers observe the model through
+forward hooks on its nn.Linear / nn.Conv1d modules.  The in/out projections run
+through their own nn.Linear __call__; the Linears and the conv fused into the
+HIP kernels (gates, FeedForward w_1 / w_2, conv1d) fire their hooks with the
+actual tensors.  Hooks only observe: the loss and every gradient are
+bit-identical with and without them."""
+import pytest
+import torch
+from torch import nn
+
+pytestmark = pytest.mark.gpu
+
+
+def _model_and_batch(cuda):
+    from datamining_recblr_amd.distributed import synthetic_interaction
+    from datamining_recblr_amd.model import RecBLR
+    from datamining_recblr_amd.recbole_compat import SyntheticDataset
+
+    cfg = dict(hidden_size=64, loss_type="CE", num_layers=2, dropout_prob=0.0, expand=2,
+               d_conv=4, bd_lru_only=False, disable_conv1d=False, disable_ffn=False,
+               MAX_ITEM_LIST_LENGTH=50)
+    torch.manual_seed(0)
+    model = RecBLR(cfg, SyntheticDataset(300)).to(cuda)
+    return model, synthetic_interaction(256, 50, 300, cuda, seed=1)
+
+
+def _step(model, batch):
+    model.zero_grad(set_to_none=True)
+    loss = model.calculate_loss(batch)
+    loss.backward()
+    return loss.detach().clone(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                   if p.grad is not None}
+
+
+def test_every_projection_and_conv_fires_its_hooks(cuda):
+    model, batch = _model_and_batch(cuda)
+    ref = _step(model, batch)
+    seen = {}
+
+    def hook(mod, args, out):
+        seen.setdefault(mod, []).append((tuple(args[0].shape), tuple(out.shape)))
+        if isinstance(mod, nn.Linear):
+            x = args[0].reshape(-1, mod.in_features).double()
+            want = x @ mod.weight.double().t()
+            if mod.bias is not None:
+                want = want + mod.bias.double()
+            got = out.reshape(-1, mod.out_features).double()
+            assert (got - want).abs().max().item() <= 1e-5 * (1 + want.abs().max().item())
+
+    handles = [m.register_forward_hook(hook) for m in model.modules()
+               if isinstance(m, (nn.Linear, nn.Conv1d))]
+    try:
+        got = _step(model, batch)
+    finally:
+        for h in handles:
+            h.remove()
+    mods = [m for m in model.modules() if isinstance(m, (nn.Linear, nn.Conv1d))]
+    assert mods and all(m in seen for m in mods), [type(m).__name__ for m in mods if m not in seen]
+    for m, calls in seen.items():
+        for shp_in, shp_out in calls:
+            if isinstance(m, nn.Linear):
+                assert shp_in[-1] == m.in_features and shp_out[-1] == m.out_features
+            else:
+                assert shp_in[-2] == m.in_channels and shp_out[-2] == m.out_channels
+    # observers only: bit-identical training step
+    assert torch.equal(got[0], ref[0])
+    for n, g in ref[1].items():
+        assert torch.equal(got[1][n], g), n
+    # a thop-style count over the Linears (RecBole's get_flops hook kind)
+    flops = sum(shp_out_numel * m.in_features
+                for m, calls in seen.items() if isinstance(m, nn.Linear)
+                for shp_out_numel in [torch.Size(c[1]).numel() for c in calls])
+    assert flops > 0
+    assert type(model.recurrent_layers[0].behavior_modeling.input) is nn.Linear
+
+
+def test_modifying_hook_on_a_fused_linear_is_rejected(cuda):
+    model, batch = _model_and_batch(cuda)
+    h = model.recurrent_layers[0].ffn.w_1.register_forward_hook(lambda m, a, o: o * 2)
+    try:
+        with pytest.raises(NotImplementedError):
+            model.calculate_loss(batch)
+    finally:
+        h.remove()
