@@ -774,6 +774,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
 }
 
 
+
 template <bool BIAS>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
               const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
