@@ -181,19 +181,19 @@ constexpr int N_LDS = N_RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <typename T>
-__device__ __forceinline__ T ds_read16(uint32_t addr) {
+__device__ __forceinline__ T hds_read16(uint32_t addr) {
   T r;
   asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
   return r;
 }
-__device__ __forceinline__ int ds_read_i32(uint32_t addr) {
+__device__ __forceinline__ int hds_read_i32(uint32_t addr) {
   int r;
   asm volatile("ds_read_b32 %0, %1" : "=v"(r) : "v"(addr));
   return r;
 }
 
 template <int N>
-__device__ __forceinline__ void wait_vm() {
+__device__ __forceinline__ void hwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
@@ -376,11 +376,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     {
       const bool ya = u > 0 && u - 1 + N_LA < U;
       if (ya) {
-        if (stored_prev) wait_vm<20>(); else wait_vm<4>();
+        if (stored_prev) hwait_vm<20>(); else hwait_vm<4>();
       } else if (u == 0 && U > 1) {
-        wait_vm<4 * (N_LA - 1)>();
+        hwait_vm<4 * (N_LA - 1)>();
       } else {
-        if (stored_prev) wait_vm<16>(); else wait_vm<0>();
+        if (stored_prev) hwait_vm<16>(); else hwait_vm<0>();
       }
     }
 #ifndef HN_NO_BARRIER
@@ -390,10 +390,10 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     const uint32_t sa = smem_base + c_slot_a * N_A_STAGE;
     const uint32_t sb = smem_base + N_NSA * N_A_STAGE + c_slot_b * N_B_STAGE + lane * 16;
     auto substep = [&](int s) {
-      const f32x4 x0 = ds_read16<f32x4>(sa + a_rd[s][0]);
-      const f32x4 x1 = ds_read16<f32x4>(sa + a_rd[s][1]);
+      const f32x4 x0 = hds_read16<f32x4>(sa + a_rd[s][0]);
+      const f32x4 x1 = hds_read16<f32x4>(sa + a_rd[s][1]);
       // B fragments two column blocks ahead of the MFMAs that use them
-      auto rb = [&](int n, int p) { return ds_read16<f16x8>(sb + ((n * 2 + s) * 2 + p) * 1024); };
+      auto rb = [&](int n, int p) { return hds_read16<f16x8>(sb + ((n * 2 + s) * 2 + p) * 1024); };
       f16x8 b00 = rb(0, 0), b01 = rb(0, 1), b10 = rb(1, 0), b11 = rb(1, 1);
       f32x4 xa = x0, xb = x1;
       asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa), "+v"(xb));
@@ -472,11 +472,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       while (pend_on && pend_q < N_NB) store_quarter();
       int ecol[N_NB];
 #pragma unroll
-      for (int n = 0; n < N_NB; ++n) ecol[n] = ds_read_i32(s_ew_addr + (cur_ct * N_BN + n * 32 + ccol) * 4);
+      for (int n = 0; n < N_NB; ++n) ecol[n] = hds_read_i32(s_ew_addr + (cur_ct * N_BN + n * 32 + ccol) * 4);
       if (BIAS) {
 #pragma unroll
         for (int n = 0; n < N_NB; ++n)
-          pbias[n] = __builtin_bit_cast(float, ds_read_i32(s_bias_addr + (cur_ct * N_BN + n * 32 + ccol) * 4));
+          pbias[n] = __builtin_bit_cast(float, hds_read_i32(s_bias_addr + (cur_ct * N_BN + n * 32 + ccol) * 4));
       }
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ecol[0]), "+v"(ecol[1]), "+v"(ecol[2]), "+v"(ecol[3]));
       if (BIAS) asm volatile("" : "+v"(pbias[0]), "+v"(pbias[1]), "+v"(pbias[2]), "+v"(pbias[3]));
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   // exact max known first (no overflow possible), operands straight from
   // global memory, stored directly (after this wave's earlier stores)
   if (nflag > 0) {
-    wait_vm<0>();
+    hwait_vm<0>();
     const int ntodo = nflag > N_MAXFLAG ? my_tiles : nflag;
     for (int f = 0; f < ntodo; ++f) {
       const int ii = nflag > N_MAXFLAG ? f : s_flag[f];
@@ -612,7 +612,7 @@ __device__ __forceinline__ uint32_t tn_off(int col, int chunk) {
   return col * T_PITCH + ((chunk ^ ((col >> 4) & 3)) << 4);
 }
 
-__device__ __forceinline__ void ds_write16(uint32_t addr, f16x8 v) {
+__device__ __forceinline__ void hds_write16(uint32_t addr, f16x8 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 
@@ -698,8 +698,8 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
         h1[q] = p1[0]; h1[q + 1] = p1[1];
       }
       const uint32_t off = tn_off(4 * cc + c, rg);
-      ds_write16(img + off, h0);
-      ds_write16(img + T_PLANE + off, h1);
+      hds_write16(img + off, h0);
+      hds_write16(img + T_PLANE + off, h1);
     }
   };
 
@@ -722,10 +722,10 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
       for (int i = 0; i < 2; ++i) {
         const uint32_t oa = tn_off(64 * wm + 32 * i + (lane & 31), 2 * st + h);
         const uint32_t ob = tn_off(64 * wk + 32 * i + (lane & 31), 2 * st + h);
-        a[i][0] = ds_read16<f16x8>(iy + oa);
-        a[i][1] = ds_read16<f16x8>(iy + T_PLANE + oa);
-        b[i][0] = ds_read16<f16x8>(ix + ob);
-        b[i][1] = ds_read16<f16x8>(ix + T_PLANE + ob);
+        a[i][0] = hds_read16<f16x8>(iy + oa);
+        a[i][1] = hds_read16<f16x8>(iy + T_PLANE + oa);
+        b[i][0] = hds_read16<f16x8>(ix + ob);
+        b[i][1] = hds_read16<f16x8>(ix + T_PLANE + ob);
       }
       asm volatile("s_waitcnt lgkmcnt(0)"
                    : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0][0]),

@@ -15,6 +15,8 @@
 #include "../datamining_recblr_amd/csrc/pad_prefix.hip"
 #include "../datamining_recblr_amd/csrc/reduce.hip"
 #include "../datamining_recblr_amd/csrc/gemm_split.hip"
+#include "../datamining_recblr_amd/csrc/gemm_half.hip"
+#include "../datamining_recblr_amd/csrc/pack.hip"
 
 #include <algorithm>
 #include <cstdio>
