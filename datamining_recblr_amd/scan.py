@@ -8,12 +8,16 @@ backward returns ``(d_gates, d_tokens)`` with ``d_t = grad_t + gates_{t+1}
 d_{t+1}`` and ``d_gates_t = h_{t-1} d_t``.  Unlike the Triton version T does
 not need to be a power of two.  Both directions run the gfx950 wave-shuffle
 scan (``rb_scan_fwd`` / ``rb_scan_bwd``); there is no CPU path.
+``parallel_scan`` dispatches the registered operator ``recblr::scan_fwd``
+(ops.py: fake implementation + autograd, so ``torch.compile`` traces it
+without a graph break); ``Scan`` is the same computation as an
+``autograd.Function``.
 """
 from __future__ import annotations
 
 import torch
 
-from . import kernels
+from . import kernels, ops
 
 __all__ = ["Scan", "parallel_scan"]
 
@@ -41,4 +45,8 @@ class Scan(torch.autograd.Function):
 
 
 def parallel_scan(gates, tokens):
-    return Scan.apply(gates, tokens)
+    # the reference's preconditions (parallel_scan.py:86-89)
+    assert tokens.shape == gates.shape and gates.dim() == 3
+    assert gates.is_contiguous()
+    assert tokens.is_contiguous()
+    return ops.scan_fwd(gates, tokens)
