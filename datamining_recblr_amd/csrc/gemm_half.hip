@@ -38,7 +38,9 @@
 //   once) and multiplies them by all 128 columns (4 blocks of
 //   v_mfma_f32_32x32x16_f16 x 3 products per k16).  The epilogue (un-scale,
 //   bias) is deferred by one tile and stored a block per k-step behind the
-//   next tile's MFMAs.  Per k-step the instruction stream is kept lean:
+//   next tile's MFMAs, as dwordx4 row pieces after a 4 x 4 transpose inside
+//   each lane quad (4 stores per block instead of 16 dword column stores).
+//   The next steps' DMAs are issued right after each k-step's barrier.  Per k-step the instruction stream is kept lean:
 //   DMA and store addresses are a wave-uniform base plus a constant 32-bit
 //   lane offset, tile coordinates advance incrementally (divisions once per
 //   tile), and the overflow check is one compare + ballot per k16.
@@ -163,8 +165,15 @@ __global__ void __launch_bounds__(256) k_split_weights_h(const SplitJobsH jobs) 
 #ifndef HN_NSA
 #define HN_NSA 3
 #endif
-constexpr int N_BM = 256, N_BN = 128, N_BK = 32;
-constexpr int N_NSA = HN_NSA, N_NSB = 2, N_WAVES = 8;
+#ifndef HN_WAVES
+#define HN_WAVES 8
+#endif
+#ifndef HN_MAXC
+#define HN_MAXC 1024
+#endif
+constexpr int N_WAVES = HN_WAVES;
+constexpr int N_BM = 32 * N_WAVES, N_BN = 128, N_BK = 32;
+constexpr int N_NSA = HN_NSA, N_NSB = 2;
 constexpr int N_THREADS = 64 * N_WAVES;
 constexpr int N_LA = N_NSA - 1;                       // A steps in flight
 constexpr int N_NB = N_BN / 32;                       // column blocks per wave (4)
@@ -174,7 +183,7 @@ constexpr int N_A_STAGE = N_BM * N_BK * 4;            // 32 KB
 constexpr int N_B_STAGE = N_BFRAG * 1024;             // 16 KB
 constexpr int N_RING = N_NSA * N_A_STAGE + N_NSB * N_B_STAGE;  // 128 KB
 // + the column exponents and the bias of all C columns (C <= 1024)
-constexpr int N_MAXC = 1024;
+constexpr int N_MAXC = HN_MAXC;
 constexpr int N_MAXFLAG = 32;  // flagged tiles listed per wave (beyond: redo all)
 constexpr int N_LDS = N_RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
 
@@ -197,7 +206,54 @@ __device__ __forceinline__ void hwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool BIAS>
+// Diagnostic build only (-DHN_STAMPS, tools/gemmbench_h.hip): per-wave cycle
+// sums of the k-step's segments (wait, barrier, substep 0, DMA issue +
+// deferred stores, substep 1, tile bookkeeping), read their shares, not the
+// build's run time (the stamps' lgkmcnt(0) forbid overlaps).
+#ifdef HN_STAMPS
+constexpr int HN_NSEG = 6;
+__device__ unsigned long long hn_stamps[2048 * 8 * HN_NSEG];
+#define HN_STAMP(k)                                                                  \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long t_;                                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    if ((k) >= 0) st_acc[(k) < 0 ? 0 : (k)] += t_ - st_prev;                           \
+    st_prev = t_;                                                                    \
+  } while (0)
+#else
+#define HN_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
+// quad_perm DPP moves (lane k of each quad reads lane k ^ 1 / k ^ 2)
+__device__ __forceinline__ float dpp_xor1(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_xor2(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+}
+
+// 4 x 4 transpose inside each lane quad: on entry lane k of a quad holds
+// column k (v[r] = row r), on exit row k (v[c] = column c).  Two butterfly
+// stages (lane distance 2, then 1), each a select + DPP move + select.
+__device__ __forceinline__ void quad_transpose(float (&v)[4], int lane) {
+  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const float y = dpp_xor2(b1 ? v[r] : v[r + 2]);
+    if (b1) v[r] = y; else v[r + 2] = y;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r += 2) {
+    const float y = dpp_xor1(b0 ? v[r] : v[r + 1]);
+    if (b0) v[r] = y; else v[r + 1] = y;
+  }
+}
+
+template <bool BIAS, bool WIDE>
 __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restrict__ A, int64_t lda,
                                                           int64_t M, int R,
                                                           const f16x8* __restrict__ Wf,
@@ -345,14 +401,32 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   bool pend_on = false, pend_full = true;
   const char* pend_base = nullptr;  // the wave's first row of the pending tile
   int64_t pend_r0 = 0;
-  const int st_lane = (int)((4 * (lane >> 5)) * ldo * 4) + ccol * 4;
+  // narrow stores: lane = one column, 16 dword stores per block (2 rows of
+  // 128 B each); wide stores (WIDE: out 16-B aligned, ldo % 4 == 0): each
+  // group of 4 registers transposed inside the lane quads, so a lane holds 4
+  // columns of one row: 4 dwordx4 stores per block (8 rows of 128 B each)
+  const int st_lane = WIDE ? (int)(((4 * (lane >> 5) + (lane & 3)) * ldo + (lane & 28)) * 4)
+                           : (int)((4 * (lane >> 5)) * ldo * 4) + ccol * 4;
   auto store_block = [&](const f32x16& blk, int n) {
+    if constexpr (WIDE) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int rj = 8 * (j >> 2) + (j & 3);
-      float* o = (float*)(pend_base + (int64_t)rj * ldo * 4 + n * 128 + st_lane);
-      const float v = BIAS ? blk[j] + pbias[n] : blk[j];
-      if (pend_full || pend_r0 + crow(j) < M) __builtin_nontemporal_store(v, o);
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = BIAS ? blk[4 * g + r] + pbias[n] : blk[4 * g + r];
+        quad_transpose(v, lane);
+        f32x4* o = (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane);
+        if (pend_full || pend_r0 + 8 * g + 4 * (lane >> 5) + (lane & 3) < M)
+          __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, o);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int rj = 8 * (j >> 2) + (j & 3);
+        float* o = (float*)(pend_base + (int64_t)rj * ldo * 4 + n * 128 + st_lane);
+        const float v = BIAS ? blk[j] + pbias[n] : blk[j];
+        if (pend_full || pend_r0 + crow(j) < M) __builtin_nontemporal_store(v, o);
+      }
     }
   };
   auto store_quarter = [&]() {
@@ -368,6 +442,10 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   int i = 0, kt = 0, c_slot_a = 0, c_slot_b = 0;
   int cur_mt, cur_ct;
   tile_of(0, cur_mt, cur_ct);
+#ifdef HN_STAMPS
+  unsigned long long st_acc[HN_NSEG] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+#endif
+  HN_STAMP(-1);
   for (int u = 0; u < U; ++u) {
     // operands of step u landed (own DMAs): the ops younger than B(u) are
     // A(u-1+N_LA) (4, issued by step u-1 if it exists) and the 16 deferred
@@ -375,17 +453,44 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     // batches make this wait conservative, never short)
     {
       const bool ya = u > 0 && u - 1 + N_LA < U;
-      if (ya) {
-        if (stored_prev) hwait_vm<20>(); else hwait_vm<4>();
+      constexpr int NST = WIDE ? 4 : 16;  // stores of one block
+      if constexpr (N_LA == 1) {
+        // A(u) itself was issued in step u-1 (after B(u)): only the stores
+        // issued after it may stay in flight
+        if (stored_prev) hwait_vm<NST>(); else hwait_vm<0>();
+      } else if (ya) {
+        if (stored_prev) hwait_vm<4 + NST>(); else hwait_vm<4>();
       } else if (u == 0 && U > 1) {
         hwait_vm<4 * (N_LA - 1)>();
       } else {
-        if (stored_prev) hwait_vm<16>(); else hwait_vm<0>();
+        if (stored_prev) hwait_vm<NST>(); else hwait_vm<0>();
       }
     }
+    HN_STAMP(0);
 #ifndef HN_NO_BARRIER
     __builtin_amdgcn_s_barrier();
 #endif
+    HN_STAMP(1);
+    // DMA issue position: right after the barrier (default: their slots
+    // were last read in step u-1, which every wave has finished; 2-4% faster
+    // than after substep 0, HN_LATE_DMA), or for the waves 4-7 only
+    // (HN_LATE_DMA + HN_STAGGER_DMA: the two waves sharing a SIMD issue at
+    // different times; measured null).  The same issue order (B before A,
+    // stores after), so the counted waits above are unchanged.
+#if !defined(HN_LATE_DMA)
+    constexpr bool early_all = true;
+#else
+    constexpr bool early_all = false;
+#endif
+#if defined(HN_STAGGER_DMA)
+    const bool early = early_all || (wave & 4) != 0;
+#else
+    const bool early = early_all;
+#endif
+    if (early) {
+      if (u + 1 < U) issueB();
+      if (u + N_LA < U) issueA();
+    }
 
     const uint32_t sa = smem_base + c_slot_a * N_A_STAGE;
     const uint32_t sb = smem_base + N_NSA * N_A_STAGE + c_slot_b * N_B_STAGE + lane * 16;
@@ -451,18 +556,23 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       acc[3] = mfma_h(a0, b10, acc[3]);
     };
     substep(0);
+    HN_STAMP(2);
+    if (!early) {
 #ifndef HN_NO_BDMA
-    if (u + 1 < U) issueB();
+      if (u + 1 < U) issueB();
 #endif
 #ifndef HN_NO_ADMA
-    if (u + N_LA < U) issueA();
+      if (u + N_LA < U) issueA();
 #endif
+    }
     stored_prev = false;
     if (pend_on && pend_q < N_NB) {
       // a partial tile's guarded stores may issue fewer than 16: not counted
       stored_prev = store_quarter();
     }
+    HN_STAMP(3);
     substep(1);
+    HN_STAMP(4);
     c_slot_a = c_slot_a + 1 == N_NSA ? 0 : c_slot_a + 1;
     c_slot_b ^= 1;
 
@@ -515,7 +625,12 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     } else {
       ++kt;
     }
+    HN_STAMP(5);
   }
+#ifdef HN_STAMPS
+  if (lane == 0 && blockIdx.x < 2048)
+    for (int k = 0; k < HN_NSEG; ++k) hn_stamps[((int)blockIdx.x * 8 + wave) * HN_NSEG + k] = st_acc[k];
+#endif
   while (pend_on && pend_q < N_NB) store_quarter();
 
   // cold tail: the wave's rows of every flagged tile again, with each row's
@@ -775,18 +890,18 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
 
 
 
-template <bool BIAS>
+template <bool BIAS, bool WIDE>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
               const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
               hipStream_t st) {
   static bool done = false;  // benign race: idempotent
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS, WIDE>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, N_LDS);
     done = true;
   }
-  k_gemm_nt_h<BIAS><<<grid, N_THREADS, N_LDS, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo,
-                                                        rmax, m_tiles);
+  k_gemm_nt_h<BIAS, WIDE><<<grid, N_THREADS, N_LDS, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo,
+                                                              rmax, m_tiles);
 }
 
 }  // namespace
@@ -816,14 +931,22 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
   const int m_tiles = (int)((M + N_BM - 1) / N_BM);
   const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / N_BN);
   // persistent: one workgroup per CU (a multiple of 8: the XCD pairing above)
-  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8);
+  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8 * (8 / N_WAVES));
   const f16x8* wf = (const f16x8*)Wf;
   const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   (void)accumulate;  // rejected by rb_gemm_nt_h
-  if (bias)
-    run_nt_h<true>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
-  else
-    run_nt_h<false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+#ifdef HN_NARROW_STORE
+  const bool wide = false;
+#else
+  const bool wide = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && ldo % 4 == 0;
+#endif
+  if (bias) {
+    if (wide) run_nt_h<true, true>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    else run_nt_h<true, false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+  } else {
+    if (wide) run_nt_h<false, true>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    else run_nt_h<false, false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+  }
   return launch_status("rb_gemm_nt_h");
 }
 

@@ -1,6 +1,8 @@
 // gemmbench_h.hip — timing of the f16 two-part split GEMM (csrc/gemm_half.hip)
 // on the encoder's projection shapes.  Ablation builds:
-//   -DHN_NO_STORE / -DHN_NO_ADMA / -DHN_NSA=n
+//   -DHN_NO_ADMA / -DHN_NSA=n / -DHN_LATE_DMA / -DHN_NARROW_STORE / -DHN_WAVES=n;
+//   -DHN_STAMPS prints each
+//   k-step segment's share of the waves' cycles
 //   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 -I include \
 //       tools/gemmbench_h.hip -o tools/bin/gemmbench_h
 #include <cstdio>
@@ -22,6 +24,7 @@ int num_cus() {
 using namespace rb;
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -75,6 +78,28 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       ts.push_back(ms * 1e3f);
     }
+    {
+      // sampled check against fp64 on the host: rows at both ends and a stride
+      std::vector<float> hw((size_t)s.C * s.R), ha(s.R), ho(s.C);
+      CK(hipMemcpy(hw.data(), W, hw.size() * 4, hipMemcpyDeviceToHost));
+      double worst = 0;
+      for (int64_t r = 0; r < M; r += (r < 300 || r > M - 300) ? 1 : 997) {
+        CK(hipMemcpy(ha.data(), A + r * s.R, s.R * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(ho.data(), O + r * s.C, s.C * 4, hipMemcpyDeviceToHost));
+        for (int c = 0; c < s.C; ++c) {
+          double ref = 0, mag = 0;
+          for (int k = 0; k < s.R; ++k) {
+            ref += (double)ha[k] * hw[(size_t)c * s.R + k];
+            mag += fabs((double)ha[k] * hw[(size_t)c * s.R + k]);
+          }
+          worst = std::max(worst, fabs(ho[c] - ref) / (mag + 1e-30));
+        }
+      }
+      if (!(worst < 1e-6)) {
+        fprintf(stderr, "%s: WRONG RESULT (max err %.3e)\n", s.name, worst);
+        return 2;
+      }
+    }
     std::sort(ts.begin(), ts.end());
     const double us = ts[ts.size() / 2];
     const double fl = 2.0 * M * s.R * s.C;
@@ -83,6 +108,21 @@ int main(int argc, char** argv) {
     totb += by;
     printf("%-10s R=%3d C=%3d  %7.1f us  %6.1f TF  %6.2f TB/s\n", s.name, s.R, s.C, us,
            fl / us / 1e6, by / us / 1e6);
+#ifdef HN_STAMPS
+    {
+      // segment shares summed over every wave of the last run
+      std::vector<unsigned long long> st(2048 * 8 * HN_NSEG);
+      CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(hn_stamps), st.size() * 8));
+      double seg[HN_NSEG] = {0}, all = 0;
+      for (size_t w = 0; w < st.size() / HN_NSEG; ++w)
+        for (int k = 0; k < HN_NSEG; ++k) seg[k] += (double)st[w * HN_NSEG + k];
+      for (int k = 0; k < HN_NSEG; ++k) all += seg[k];
+      const char* nm[HN_NSEG] = {"wait", "barrier", "sub0", "dma+st", "sub1", "tile"};
+      printf("    stamps (share of wave time):");
+      for (int k = 0; k < HN_NSEG; ++k) printf(" %s %.3f", nm[k], seg[k] / all);
+      printf("  | mean per-wave cycles %.0f\n", all / (256.0 * 8));
+    }
+#endif
   }
   printf("total %.1f us  (%.2f TB/s)\n", tot, totb / tot / 1e6);
   return 0;
