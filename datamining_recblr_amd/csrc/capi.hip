@@ -121,7 +121,7 @@ int rb_conv_silu_fwd_rows(const float* x, int64_t x_rs, const float* w, const fl
 int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
                      const float* g1, const float* g2, float* dx, int64_t dx_rs, float* dw_part,
                      float* db_part, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* seq_offsets, void* stream) {
-  if (!x || !w || !bias || !g1 || !dx || !dw_part || !db_part)
+  if (!x || !w || !bias || !g1 || !dx || !dw_part)   // db_part NULL: folded layout
     return fail("rb_conv_silu_bwd: null pointer");
   if (K < 1 || K > 8) return fail("rb_conv_silu_bwd: kernel size K must be in [1, 8]");
   if (x_rs < H || dx_rs < H) return fail("rb_conv_silu_bwd: row stride < H");
@@ -249,7 +249,7 @@ int rb_conv_silu_bwd_bf16(const rb_bf16* x, int64_t x_rs, const float* w, const 
                           const rb_bf16* g1, const rb_bf16* g2, rb_bf16* dx, int64_t dx_rs,
                           float* dw_part, float* db_part, int64_t B, int64_t L, int64_t H,
                           int64_t K, const int64_t* seq_offsets, void* stream) {
-  if (!x || !w || !bias || !g1 || !dx || !dw_part || !db_part)
+  if (!x || !w || !bias || !g1 || !dx || !dw_part)   // db_part NULL: folded layout
     return fail("rb_conv_silu_bwd_bf16: null pointer");
   if (K < 1 || K > 8) return fail("rb_conv_silu_bwd_bf16: kernel size K must be in [1, 8]");
   if (x_rs < H || dx_rs < H) return fail("rb_conv_silu_bwd_bf16: row stride < H");

@@ -323,9 +323,21 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
     }
   }
   if (q == 0 && cv) {
+    if (db_part == nullptr) {
+      // folded: one row of (K + 1) * H partials per sequence, dW in the
+      // weight's own [c, k] order, then dbias — one column sum gives both,
+      // already in parameter layout
+      float* row = dw_part + b * (K + 1) * H;
 #pragma unroll
-    for (int k = 0; k < K; ++k) stv(dw_part + (b * K + k) * H + c0, accw[k]);
-    stv(db_part + b * H + c0, accb);
+      for (int v = 0; v < VEC; ++v)
+#pragma unroll
+        for (int k = 0; k < K; ++k) row[(c0 + v) * K + k] = accw[k][v];
+      stv(row + K * H + c0, accb);
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; ++k) stv(dw_part + (b * K + k) * H + c0, accw[k]);
+      stv(db_part + b * H + c0, accb);
+    }
   }
 }
 

@@ -187,6 +187,23 @@ constexpr int N_MAXC = HN_MAXC;
 constexpr int N_MAXFLAG = 32;  // flagged tiles listed per wave (beyond: redo all)
 constexpr int N_LDS = N_RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
 
+// NB column blocks of 32 per wave: NB = 4 (256 x 128 tiles, the tile's
+// results stored a block per k-step during the next tile) or NB = 8 (256 x
+// 256 tiles for C % 256 == 0: a quarter fewer bytes through each CU's load
+// path per output — every A row is re-read C/256 instead of C/128 times and
+// each weight fragment DMA serves twice the outputs — with the results
+// stored at the tile's end, 2 A stages)
+template <int NB>
+struct NtCfg {
+  static constexpr int BN = 32 * NB;
+  static constexpr int BFRAG = NB * 4;                  // B fragments per k-step
+  static constexpr int BDMA = BFRAG / N_WAVES;          // B DMAs per wave per k-step
+  static constexpr int B_STAGE = BFRAG * 1024;
+  static constexpr int NSA = NB == 4 ? HN_NSA : 2;
+  static constexpr int RING = NSA * N_A_STAGE + N_NSB * B_STAGE;
+  static constexpr int LDS = RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
+};
+
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 template <typename T>
@@ -253,7 +270,7 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int lane) {
   }
 }
 
-template <bool BIAS, bool WIDE>
+template <bool BIAS, bool WIDE, int NB>
 __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restrict__ A, int64_t lda,
                                                           int64_t M, int R,
                                                           const f16x8* __restrict__ Wf,
@@ -262,6 +279,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
                                                           float* __restrict__ out, int64_t ldo,
                                                           float* __restrict__ rmax, int m_tiles) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  using CF = NtCfg<NB>;
+  constexpr int N_BN = CF::BN, N_NB = NB, N_BDMA = CF::BDMA, N_NSA = CF::NSA, N_LA = N_NSA - 1;
+  constexpr int N_B_STAGE = CF::B_STAGE, N_RING = CF::RING;
+  constexpr bool DEFER = NB == 4;   // deferred epilogue (NB = 8: stored at the tile's end)
+  static_assert(!(NB == 8) || WIDE, "256-column tiles store through the wide epilogue");
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -395,7 +417,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
 
   // deferred epilogue: pend[n] (un-scaled) stored one block per k-step during
   // the next tile; 16 dword stores per block (lane: one column, 16 rows)
-  f32x16 pend[N_NB];
+  f32x16 pend[DEFER ? N_NB : 1];
   float pbias[N_NB];
   int pend_q = N_NB;
   bool pend_on = false, pend_full = true;
@@ -431,10 +453,12 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   };
   auto store_quarter = [&]() {
     const int q = pend_q++;
-    if (q == 0) store_block(pend[0], 0);
-    else if (q == 1) store_block(pend[1], 1);
-    else if (q == 2) store_block(pend[2], 2);
-    else store_block(pend[3], 3);
+    if constexpr (DEFER) {
+      if (q == 0) store_block(pend[0], 0);
+      else if (q == 1) store_block(pend[1], 1);
+      else if (q == 2) store_block(pend[2], 2);
+      else store_block(pend[3], 3);
+    }
     return pend_full;
   };
   bool stored_prev = false;
@@ -453,7 +477,9 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     // batches make this wait conservative, never short)
     {
       const bool ya = u > 0 && u - 1 + N_LA < U;
-      constexpr int NST = WIDE ? 4 : 16;  // stores of one block
+      // stores after the DMAs: one block per step (DEFER), or the whole
+      // tile at its end (NB = 8)
+      constexpr int NST = DEFER ? (WIDE ? 4 : 16) : 4 * NB;
       if constexpr (N_LA == 1) {
         // A(u) itself was issued in step u-1 (after B(u)): only the stores
         // issued after it may stay in flight
@@ -499,7 +525,8 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       const f32x4 x1 = hds_read16<f32x4>(sa + a_rd[s][1]);
       // B fragments two column blocks ahead of the MFMAs that use them
       auto rb = [&](int n, int p) { return hds_read16<f16x8>(sb + ((n * 2 + s) * 2 + p) * 1024); };
-      f16x8 b00 = rb(0, 0), b01 = rb(0, 1), b10 = rb(1, 0), b11 = rb(1, 1);
+      f16x8 bq[N_NB][2];
+      bq[0][0] = rb(0, 0); bq[0][1] = rb(0, 1); bq[1][0] = rb(1, 0); bq[1][1] = rb(1, 1);
       f32x4 xa = x0, xb = x1;
       asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(xa), "+v"(xb));
       const float mx = max8abs(xa, xb);
@@ -533,27 +560,22 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         a1[2 * q] = h1[0]; a1[2 * q + 1] = h1[1];
       }
 #endif
-      // per column block: the small partial products first
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b00), "+v"(b01));
-      acc[0] = mfma_h(a1, b00, acc[0]);
-      acc[0] = mfma_h(a0, b01, acc[0]);
-      acc[0] = mfma_h(a0, b00, acc[0]);
-      b00 = rb(2, 0);
-      b01 = rb(2, 1);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b10), "+v"(b11));
-      acc[1] = mfma_h(a1, b10, acc[1]);
-      acc[1] = mfma_h(a0, b11, acc[1]);
-      acc[1] = mfma_h(a0, b10, acc[1]);
-      b10 = rb(3, 0);
-      b11 = rb(3, 1);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b00), "+v"(b01));
-      acc[2] = mfma_h(a1, b00, acc[2]);
-      acc[2] = mfma_h(a0, b01, acc[2]);
-      acc[2] = mfma_h(a0, b00, acc[2]);
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b10), "+v"(b11));
-      acc[3] = mfma_h(a1, b10, acc[3]);
-      acc[3] = mfma_h(a0, b11, acc[3]);
-      acc[3] = mfma_h(a0, b10, acc[3]);
+      // per column block: the small partial products first; block n + 2's
+      // fragments are read behind block n's MFMAs
+#pragma unroll
+      for (int n = 0; n < N_NB; ++n) {
+        if (n + 1 < N_NB)
+          asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(bq[n][0]), "+v"(bq[n][1]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bq[n][0]), "+v"(bq[n][1]));
+        acc[n] = mfma_h(a1, bq[n][0], acc[n]);
+        acc[n] = mfma_h(a0, bq[n][1], acc[n]);
+        acc[n] = mfma_h(a0, bq[n][0], acc[n]);
+        if (n + 2 < N_NB) {
+          bq[n + 2][0] = rb(n + 2, 0);
+          bq[n + 2][1] = rb(n + 2, 1);
+        }
+      }
     };
     substep(0);
     HN_STAMP(2);
@@ -566,7 +588,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
 #endif
     }
     stored_prev = false;
-    if (pend_on && pend_q < N_NB) {
+    if (DEFER && pend_on && pend_q < N_NB) {
       // a partial tile's guarded stores may issue fewer than 16: not counted
       stored_prev = store_quarter();
     }
@@ -577,9 +599,12 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     c_slot_b ^= 1;
 
     if (kt == KT - 1) {
-      // the tile's results (un-scaled) move to pend[] and are stored a block
-      // per step during the next tile's first steps (behind its MFMAs)
-      while (pend_on && pend_q < N_NB) store_quarter();
+      // DEFER: the tile's results (un-scaled) move to pend[] and are stored a
+      // block per step during the next tile's first steps (behind its MFMAs);
+      // NB = 8: un-scaled and stored now
+      if constexpr (DEFER) {
+        while (pend_on && pend_q < N_NB) store_quarter();
+      }
       int ecol[N_NB];
 #pragma unroll
       for (int n = 0; n < N_NB; ++n) ecol[n] = hds_read_i32(s_ew_addr + (cur_ct * N_BN + n * 32 + ccol) * 4);
@@ -588,16 +613,43 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         for (int n = 0; n < N_NB; ++n)
           pbias[n] = __builtin_bit_cast(float, hds_read_i32(s_bias_addr + (cur_ct * N_BN + n * 32 + ccol) * 4));
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(ecol[0]), "+v"(ecol[1]), "+v"(ecol[2]), "+v"(ecol[3]));
-      if (BIAS) asm volatile("" : "+v"(pbias[0]), "+v"(pbias[1]), "+v"(pbias[2]), "+v"(pbias[3]));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int erj = __shfl(er, crow(j)) - kTA - kTW;
+      for (int n = 0; n < N_NB; ++n) {
+        asm volatile("" : "+v"(ecol[n]));
+        if (BIAS) asm volatile("" : "+v"(pbias[n]));
+      }
+      if constexpr (DEFER) {
 #pragma unroll
-        for (int n = 0; n < N_NB; ++n) {
-          pend[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
-          acc[n][j] = 0.0f;
+        for (int j = 0; j < 16; ++j) {
+          const int erj = __shfl(er, crow(j)) - kTA - kTW;
+#pragma unroll
+          for (int n = 0; n < N_NB; ++n) {
+            pend[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
+            acc[n][j] = 0.0f;
+          }
         }
+      } else {
+        const int64_t r0 = (int64_t)cur_mt * N_BM + wave * 32;
+        const bool full = r0 + 32 <= M;
+        if (cur_mt < m_tiles) {
+          pend_base = reinterpret_cast<const char*>(out + r0 * ldo + cur_ct * N_BN);
+          pend_r0 = r0;
+          pend_full = full;
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int erj = __shfl(er, crow(j)) - kTA - kTW;
+#pragma unroll
+            for (int n = 0; n < N_NB; ++n) acc[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
+          }
+#pragma unroll
+          for (int n = 0; n < N_NB; ++n) store_block(acc[n], n);
+          stored_prev = full;
+        }
+#pragma unroll
+        for (int n = 0; n < N_NB; ++n)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[n][j] = 0.0f;
       }
       if (rmax && cur_ct == 0 && cur_mt < m_tiles) {
         // max |A| of the wave's 32 rows (all R columns): the weight-gradient
@@ -614,11 +666,13 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         ++nflag;
         flag_tile = false;
       }
-      pend_on = cur_mt < m_tiles;
-      pend_r0 = (int64_t)cur_mt * N_BM + wave * 32;
-      pend_full = pend_r0 + 32 <= M;
-      pend_base = reinterpret_cast<const char*>(out + pend_r0 * ldo + cur_ct * N_BN);
-      pend_q = 0;
+      if constexpr (DEFER) {
+        pend_on = cur_mt < m_tiles;
+        pend_r0 = (int64_t)cur_mt * N_BM + wave * 32;
+        pend_full = pend_r0 + 32 <= M;
+        pend_base = reinterpret_cast<const char*>(out + pend_r0 * ldo + cur_ct * N_BN);
+        pend_q = 0;
+      }
       kt = 0;
       ++i;
       if (i < my_tiles) tile_of(i, cur_mt, cur_ct);
@@ -890,18 +944,19 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
 
 
 
-template <bool BIAS, bool WIDE>
+template <bool BIAS, bool WIDE, int NB>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
               const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
               hipStream_t st) {
+  constexpr int lds = NtCfg<NB>::LDS;
   static bool done = false;  // benign race: idempotent
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS, WIDE>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, N_LDS);
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS, WIDE, NB>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     done = true;
   }
-  k_gemm_nt_h<BIAS, WIDE><<<grid, N_THREADS, N_LDS, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo,
-                                                              rmax, m_tiles);
+  k_gemm_nt_h<BIAS, WIDE, NB><<<grid, N_THREADS, lds, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo,
+                                                                rmax, m_tiles);
 }
 
 }  // namespace
@@ -929,9 +984,6 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st) {
   const int m_tiles = (int)((M + N_BM - 1) / N_BM);
-  const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / N_BN);
-  // persistent: one workgroup per CU (a multiple of 8: the XCD pairing above)
-  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8 * (8 / N_WAVES));
   const f16x8* wf = (const f16x8*)Wf;
   const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   (void)accumulate;  // rejected by rb_gemm_nt_h
@@ -940,12 +992,22 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
 #else
   const bool wide = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && ldo % 4 == 0;
 #endif
+#ifdef HN_NB4_ONLY
+  const bool nb8 = false;
+#else
+  const bool nb8 = wide && C % 256 == 0;
+#endif
+  const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / (nb8 ? 256 : 128));
+  // persistent: one workgroup per CU (a multiple of 8: the XCD pairing above)
+  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8 * (8 / N_WAVES));
   if (bias) {
-    if (wide) run_nt_h<true, true>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
-    else run_nt_h<true, false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    if (nb8) run_nt_h<true, true, 8>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    else if (wide) run_nt_h<true, true, 4>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    else run_nt_h<true, false, 4>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
   } else {
-    if (wide) run_nt_h<false, true>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
-    else run_nt_h<false, false>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    if (nb8) run_nt_h<false, true, 8>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    else if (wide) run_nt_h<false, true, 4>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
+    else run_nt_h<false, false, 4>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
   }
   return launch_status("rb_gemm_nt_h");
 }

@@ -298,14 +298,16 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx, seq: Packed | None = None):
             raise ValueError("g2 must be contiguous, shaped like x")
     w = weight.reshape(H, -1).contiguous()
     K = w.shape[1]
-    dw_part = torch.empty((B, K, H), device=x.device, dtype=torch.float32)
-    db_part = torch.empty((B, H), device=x.device, dtype=torch.float32)
+    # folded partials (db_part NULL): row b = [dW[c, k] (H*K) | dbias[c] (H)],
+    # one fixed-order column sum, results already in parameter layout
+    part = torch.empty((B, (K + 1) * H), device=x.device, dtype=torch.float32)
     n = x.numel()
     _launch("rb_conv_silu_bwd" + _sfx(dt), (3 if g2 is None else 4) * n * x.element_size(),
             x.data_ptr(), x_rs, w.data_ptr(), bias.contiguous().data_ptr(),
             g1.data_ptr(), 0 if g2 is None else g2.data_ptr(), dx.data_ptr(), dx_rs,
-            dw_part.data_ptr(), db_part.data_ptr(), B, L, H, K, offs, _stream(x))
-    return colsum(dw_part.view(B, -1)).view(-1, H).t().contiguous(), colsum(db_part)
+            part.data_ptr(), 0, B, L, H, K, offs, _stream(x))
+    sums = colsum(part)
+    return sums[:H * K].view(H, K), sums[H * K:]
 
 
 def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=None,

@@ -110,7 +110,10 @@ int rb_conv_silu_fwd_rows(const float* x, int64_t x_rs, const float* w, const fl
 /* Backward of rb_conv_silu_fwd.  dxc = g1 + g2 (g2 may be NULL), both
  * [B, L, H] contiguous.  Writes dx (row stride dx_rs) and per-batch partial
  * sums dw_part[b, k, c] (B*K*H floats) and db_part[b, c] (B*H floats); the
- * caller sums the partials over b (deterministic, no atomics). */
+ * caller sums the partials over b (deterministic, no atomics).  db_part NULL
+ * selects the folded layout: dw_part holds B rows of (K+1)*H floats, dW[c, k]
+ * at c*K + k then dbias[c] at K*H + c, so one column sum over the rows gives
+ * both gradients in parameter layout. */
 int rb_conv_silu_bwd(const float* x, int64_t x_rs, const float* w,
                      const float* bias, const float* g1, const float* g2,
                      float* dx, int64_t dx_rs, float* dw_part, float* db_part,

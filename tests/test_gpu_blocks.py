@@ -478,3 +478,45 @@ def test_folded_pad_prefix_equals_separate_node(cuda, pads):
         outs.append([y.detach(), x.grad] + [t.grad for t in p])
     for a, b, n in zip(*outs, ("y", "dxz", "dconv_w", "dconv_b", "dgate_w", "dgate_b", "dlam")):
         assert torch.equal(a, b), n
+
+
+@pytest.mark.parametrize("K,dt", [(4, torch.float32), (3, torch.float32), (4, torch.bfloat16)])
+def test_conv_bwd_folded_partials_equal_separate(cuda, K, dt):
+    """rb_conv_silu_bwd with db_part NULL (folded per-sequence partials:
+    [dW in [c, k] order | dbias] per row, one column sum) writes bit for bit
+    the values of the separate dw_part[b, k, c] / db_part[b, c] layout, and
+    the same dx."""
+    from datamining_recblr_amd import _lib
+    from datamining_recblr_amd.kernels import _stream
+
+    g = torch.Generator().manual_seed(K)
+    B, L, H = 9, 37, 64
+    sfx = "_bf16" if dt == torch.bfloat16 else ""
+    xz = torch.randn(B, L, 2 * H, generator=g).to(dt).to(cuda)
+    x = xz[..., :H]
+    w = (torch.randn(H, K, generator=g) * 0.4).to(cuda)
+    b = (torch.randn(H, generator=g) * 0.1).to(cuda)
+    g1 = torch.randn(B, L, H, generator=g).to(dt).to(cuda)
+    g2 = torch.randn(B, L, H, generator=g).to(dt).to(cuda)
+    outs = []
+    for folded in (False, True):
+        dx = torch.empty(B, L, 2 * H, dtype=dt, device=cuda)[..., :H]
+        if folded:
+            part = torch.full((B, (K + 1) * H), float("nan"), device=cuda)
+            ptrs = (part.data_ptr(), 0)
+        else:
+            dwp = torch.full((B, K, H), float("nan"), device=cuda)
+            dbp = torch.full((B, H), float("nan"), device=cuda)
+            ptrs = (dwp.data_ptr(), dbp.data_ptr())
+        _lib.call("rb_conv_silu_bwd" + sfx, x.data_ptr(), 2 * H, w.data_ptr(), b.data_ptr(),
+                  g1.data_ptr(), g2.data_ptr(), dx.data_ptr(), 2 * H, *ptrs, B, L, H, K, None,
+                  _stream(x))
+        torch.cuda.synchronize()
+        if folded:
+            outs.append((dx.clone(), part[:, :H * K].view(B, H, K), part[:, H * K:]))
+        else:
+            outs.append((dx.clone(), dwp.permute(0, 2, 1), dbp))
+    (dx0, dw0, db0), (dx1, dw1, db1) = outs
+    assert torch.equal(dx0, dx1)
+    assert torch.equal(dw0, dw1)
+    assert torch.equal(db0, db1)

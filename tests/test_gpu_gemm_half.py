@@ -55,16 +55,19 @@ def test_input_gradient_orientation(cuda, M, N, K):
     assert _rel_err(dx, dy.double() @ w.double()) < 2e-6
 
 
-def test_rows_across_the_fp32_range(cuda):
+@pytest.mark.parametrize("N", [128, 512])
+def test_rows_across_the_fp32_range(cuda, N):
     """Per-row relative error at fp32 level on rows scaled by 2^-60 .. 2^60,
     zero rows, rows whose first 16 (or 48) entries are zero or tiny and rows
     growing by 2^64 along K (their fp16 images would overflow the first
     scale: the kernel flags the tile and recomputes the wave's rows with the
-    exact row max), a 3e37 entry; weight columns scaled by 1e-25 and zero."""
+    exact row max), a 3e37 entry; weight columns scaled by 1e-25 and zero.
+    N = 128: 256 x 128 tiles with the deferred epilogue; N = 512: 256 x 256
+    tiles stored at the tile's end."""
     from datamining_recblr_amd import kernels
 
     g = torch.Generator().manual_seed(11)
-    M, K, N = 4096 + 77, 256, 128
+    M, K = 4096 + 77, 256
     a = torch.randn(M, K, generator=g)
     a *= torch.exp2(torch.randint(-60, 60, (M, 1), generator=g).float())
     a[5] = 0

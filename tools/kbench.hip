@@ -180,6 +180,53 @@ pattern4to1(const float* rg, int rg_rs, const float* xc, int xc_rs, const float*
   }
 }
 
+// the gate backward's access pattern (5 reads, 4 writes per step and
+// channel, same strides and wave/lane layout, reverse tile order), trivial math
+template <int Q, int TC, typename T = float, int VEC = 4>
+__global__ void __launch_bounds__(256)
+pattern5to4(const T* rg, int rg_rs, const T* xc, int xc_rs, const T* z, int z_rs,
+            const T* dy, T* drg, int drg_rs, T* dxc, int dxc_rs, T* dz, int dz_rs,
+            int64_t B, int L, int H, int ncw) {
+  constexpr int G = 64 / Q, TILE = Q * TC;
+  const int lane = threadIdx.x & 63, q = lane & (Q - 1), g = lane / Q;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t b = wid / ncw;
+  if (b >= B) return;
+  const int c0 = (int)(wid - b * ncw) * (G * VEC) + g * VEC;
+  const int64_t row0 = b * L;
+  const int nT = (L + TILE - 1) / TILE;
+  for (int tile = nT - 1; tile >= 0; --tile) {
+    const int t0 = tile * TILE + q * TC;
+    float r[TC][VEC], i[TC][VEC], x[TC][VEC], zz[TC][VEC], d[TC][VEC];
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int64_t t = row0 + min(t0 + j, L - 1);
+      ldv(r[j], rg + t * rg_rs + c0);
+      ldv(i[j], rg + t * rg_rs + H + c0);
+      ldv(x[j], xc + t * xc_rs + c0);
+      ldv(zz[j], z + t * z_rs + c0);
+      ldv(d[j], dy + t * H + c0);
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      if (t0 + j >= L) continue;
+      const int64_t t = row0 + t0 + j;
+      float o1[VEC], o2[VEC], o3[VEC], o4[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        o1[v] = r[j][v] * d[j][v];
+        o2[v] = i[j][v] * d[j][v];
+        o3[v] = x[j][v] * d[j][v];
+        o4[v] = zz[j][v] * d[j][v];
+      }
+      stv(dz + t * dz_rs + c0, o4);
+      stv(drg + t * drg_rs + c0, o1);
+      stv(drg + t * drg_rs + H + c0, o2);
+      stv(dxc + t * dxc_rs + c0, o3);
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 2048;
   const int L = argc > 2 ? atoi(argv[2]) : 200;
@@ -254,6 +301,24 @@ int main(int argc, char** argv) {
                                dxc, H, dz + H, 2 * H, part, dh0, B, L, H, offs, 0, nullptr);
       }, {}};
     };
+    cs.push_back({"pattern5to4 q8 tc2 dense", 9 * N * 4, [=] {
+      const int ncw = H / 32;
+      hipLaunchKernelGGL((pattern5to4<8, 2>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0,
+                         rg, 2 * H, xc, H, xz + H, 2 * H, dy, drg, 2 * H, dxc, H, dz + H, 2 * H,
+                         (int64_t)B, L, H, ncw);
+    }, {}});
+    cs.push_back({"pattern5to4 q4 tc4 dense", 9 * N * 4, [=] {
+      const int ncw = H / 64;
+      hipLaunchKernelGGL((pattern5to4<4, 4>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0,
+                         rg, 2 * H, xc, H, xz + H, 2 * H, dy, drg, 2 * H, dxc, H, dz + H, 2 * H,
+                         (int64_t)B, L, H, ncw);
+    }, {}});
+    cs.push_back({"pattern5to4 q2 tc8 dense", 9 * N * 4, [=] {
+      const int ncw = H / 128;
+      hipLaunchKernelGGL((pattern5to4<2, 8>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0,
+                         rg, 2 * H, xc, H, xz + H, 2 * H, dy, drg, 2 * H, dxc, H, dz + H, 2 * H,
+                         (int64_t)B, L, H, ncw);
+    }, {}});
     cs.push_back(bwd("bwd dense regs", nullptr, false, 9 * N * 4));
     cs.push_back(bwd("bwd dense dma", nullptr, true, 9 * N * 4));
     cs.push_back(bwd("bwd packed regs", offs_sorted, false, 9 * NP * 4));
@@ -268,6 +333,27 @@ int main(int argc, char** argv) {
                       H, nullptr, 0);
     }, {}});
   } else if (bf16_only) {
+    {
+      auto bp = [](float* p) { return reinterpret_cast<bf16_t*>(p); };
+      cs.push_back({"pattern5to4 bf16 v4 q4 tc4", 9 * N * 2, [=] {
+        const int ncw = H / 64;
+        hipLaunchKernelGGL((pattern5to4<4, 4, bf16_t, 4>), dim3(((int64_t)B * ncw + 3) / 4),
+                           dim3(256), 0, 0, bp(rg), 2 * H, bp(xc), H, bp(xz + H), 2 * H, bp(dy),
+                           bp(drg), 2 * H, bp(dxc), H, bp(dz + H), 2 * H, (int64_t)B, L, H, ncw);
+      }, {}});
+      cs.push_back({"pattern5to4 bf16 v8 q8 tc2", 9 * N * 2, [=] {
+        const int ncw = H / 64;
+        hipLaunchKernelGGL((pattern5to4<8, 2, bf16_t, 8>), dim3(((int64_t)B * ncw + 3) / 4),
+                           dim3(256), 0, 0, bp(rg), 2 * H, bp(xc), H, bp(xz + H), 2 * H, bp(dy),
+                           bp(drg), 2 * H, bp(dxc), H, bp(dz + H), 2 * H, (int64_t)B, L, H, ncw);
+      }, {}});
+      cs.push_back({"pattern5to4 f32 v4 q8 tc2", 9 * N * 4, [=] {
+        const int ncw = H / 32;
+        hipLaunchKernelGGL((pattern5to4<8, 2>), dim3(((int64_t)B * ncw + 3) / 4), dim3(256), 0, 0,
+                           rg, 2 * H, xc, H, xz + H, 2 * H, dy, drg, 2 * H, dxc, H, dz + H, 2 * H,
+                           (int64_t)B, L, H, ncw);
+      }, {}});
+    }
     add_gate<bf16_t, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, sep, N, 1);
     add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 1);
     add_gate<bf16_t, 8, 8, 2, true>(cs, "bf16 v8 q8 tc2 pf", B, L, H, sep, N, 1);
