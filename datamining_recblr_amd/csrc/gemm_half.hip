@@ -46,6 +46,8 @@
 //   tile), and the overflow check is one compare + ballot per k16.
 #include "common.h"
 
+#include <type_traits>
+
 namespace rb {
 namespace {
 
@@ -772,10 +774,23 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
 // the tiles of one row chunk run on one XCD (their row re-reads hit its L2).
 constexpr int T_BT = 128;
 constexpr int T_PITCH = 80;                   // bytes per column of an image plane
-constexpr int T_PLANE = T_BT * T_PITCH;       // 10 KB
-constexpr int T_STAGE = 4 * T_PLANE;          // dY planes 0, 1 and X planes 0, 1
-constexpr int T_LDS = 2 * T_STAGE;            // double buffered: 80 KB
 constexpr int kTT = 14;                       // chunk max lands in [2^13, 2^14)
+
+// Tile of dW: (128 NBN) x (128 NBK), NBN * NBK <= 2, 4 NBN NBK waves of
+// 64 x 64.  A 256-wide side (N % 256 == 0, else K % 256 == 0) halves the
+// re-reads of the other operand's rows: each row of dY is read K / (128 NBK)
+// times and each row of X N / (128 NBN) times, and these kernels are bound by
+// those row streams through each CU's load path (a quarter fewer bytes for
+// every projection shape).
+template <int NBN, int NBK>
+struct TnCfg {
+  static constexpr int THREADS = 256 * NBN * NBK;
+  static constexpr int YC = T_BT * NBN, XC = T_BT * NBK;       // dY / X columns of the tile
+  static constexpr int YPLANE = YC * T_PITCH, XPLANE = XC * T_PITCH;
+  static constexpr int STAGE = 2 * YPLANE + 2 * XPLANE;        // dY planes 0, 1, X planes 0, 1
+  static constexpr int LDS = 2 * STAGE;                        // double buffered
+  static constexpr int LOADERS = (YC + XC) / 4 * 4;            // 4 columns x 8 rows per thread
+};
 
 __device__ __forceinline__ uint32_t tn_off(int col, int chunk) {
   return col * T_PITCH + ((chunk ^ ((col >> 4) & 3)) << 4);
@@ -785,24 +800,24 @@ __device__ __forceinline__ void hds_write16(uint32_t addr, f16x8 v) {
   asm volatile("ds_write_b128 %0, %1" ::"v"(addr), "v"(v) : "memory");
 }
 
-__global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy,
-                                                    const float* __restrict__ X, int64_t ldx,
-                                                    int64_t M, int N, int K,
-                                                    const float* __restrict__ ymax,
-                                                    const float* __restrict__ xmax,
-                                                    float* __restrict__ parts, int S, int64_t mk,
-                                                    int nt_k) {
+template <int NBN, int NBK>
+__global__ void __launch_bounds__(256 * NBN * NBK, 2 / (NBN * NBK))
+k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X, int64_t ldx,
+            int64_t M, int N, int K, const float* __restrict__ ymax,
+            const float* __restrict__ xmax, float* __restrict__ parts, int S, int64_t mk,
+            int nt_k) {
+  using CF = TnCfg<NBN, NBK>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wk = wave & 1;
+  const int wm = wave / (2 * NBK), wk = wave % (2 * NBK);
   // block -> (tile, split): the tiles of one split share an XCD
   const int G = gridDim.x;
   const int idx = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  const int nt = (N / T_BT) * nt_k;
+  const int nt = (N / CF::YC) * nt_k;
   const int tile = idx % nt, s = idx / nt;
-  const int n0 = (tile / nt_k) * T_BT, k0 = (tile % nt_k) * T_BT;
+  const int n0 = (tile / nt_k) * CF::YC, k0 = (tile % nt_k) * CF::XC;
   const int64_t r_begin = (int64_t)s * mk;
   const int64_t r_end = r_begin + mk < M ? r_begin + mk : M;
   const int64_t nrows = r_end > r_begin ? r_end - r_begin : 0;
@@ -810,7 +825,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
 
   // chunk scales from the 32-row group maxima
   float my = 0.0f, mx = 0.0f;
-  for (int64_t g = r_begin / 32 + tid; g * 32 < r_end; g += 256) {
+  for (int64_t g = r_begin / 32 + tid; g * 32 < r_end; g += CF::THREADS) {
     my = fmaxf(my, ymax[g]);
     mx = fmaxf(mx, xmax[g]);
   }
@@ -820,19 +835,29 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
     my = fmaxf(my, __shfl_xor(my, o));
     mx = fmaxf(mx, __shfl_xor(mx, o));
   }
-  if (lane == 0) { red[wave] = my; red[4 + wave] = mx; }
+  constexpr int NW = CF::THREADS / 64;
+  if (lane == 0) { red[wave] = my; red[NW + wave] = mx; }
   __syncthreads();
-  my = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  mx = fmaxf(fmaxf(red[4], red[5]), fmaxf(red[6], red[7]));
+  my = 0.0f;
+  mx = 0.0f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    my = fmaxf(my, red[w]);
+    mx = fmaxf(mx, red[NW + w]);
+  }
   const int ey = my > 0.0f ? __builtin_amdgcn_frexp_expf(my) : 0;
   const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;
   __syncthreads();
 
-  // conversion role: operand op (0 = dY, 1 = X), columns 4cc..4cc+3,
-  // rows 8rg..8rg+7 of each m-step
-  const int op = tid >> 7;
-  const int cc = tid & 31;
-  const int rg = (tid >> 5) & 3;
+  // conversion role: threads [0, YC) load dY, [YC, YC + XC) load X (YC / 4
+  // column groups x 4 row groups, resp. XC / 4 x 4); columns 4cc..4cc+3,
+  // rows 8rg..8rg+7 of each m-step; the remaining threads only multiply
+  const bool loader = tid < CF::LOADERS;
+  const int op = tid < CF::YC ? 0 : 1;
+  const int lt = op == 0 ? tid : tid - CF::YC;
+  const int ncg = (op == 0 ? CF::YC : CF::XC) / 4;   // column groups of the operand
+  const int cc = loader ? lt % ncg : 0;
+  const int rg = loader ? lt / ncg : 0;
   const float* src = op == 0 ? Y + n0 + 4 * cc : X + k0 + 4 * cc;
   const int64_t ld = op == 0 ? ldy : ldx;
   const float sc = __builtin_amdgcn_ldexpf(1.0f, kTT - (op == 0 ? ey : ex));
@@ -840,22 +865,30 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
 
   f32x4 raw0[8], raw1[8];
   auto load = [&](int t, f32x4 (&r)[8]) {
+    if (!loader) return;
     const int64_t row0 = r_begin + (int64_t)t * 32 + rg * 8;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       int64_t row = row0 + q;
       row = row < r_end ? row : r_end - 1;  // rows past the chunk: zeroed on convert
+#ifdef HN_TN_NONTEMPORAL
       r[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + row * ld));
+#else
+      // plain loads: the other tiles of this split re-read these rows (L2)
+      r[q] = *reinterpret_cast<const f32x4*>(src + row * ld);
+#endif
     }
   };
   auto convert = [&](f32x4 (&r)[8], int t, int buf) {
+    if (!loader) return;
     const int64_t row0 = r_begin + (int64_t)t * 32 + rg * 8;
     if (row0 + 8 > r_end) {
 #pragma unroll
       for (int q = 0; q < 8; ++q)
         if (row0 + q >= r_end) r[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
-    const uint32_t img = smem_base + buf * T_STAGE + op * 2 * T_PLANE;
+    const uint32_t img = smem_base + buf * CF::STAGE + (op == 0 ? 0 : 2 * CF::YPLANE);
+    const uint32_t plane = op == 0 ? CF::YPLANE : CF::XPLANE;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       f16x8 h0, h1;
@@ -868,7 +901,7 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
       }
       const uint32_t off = tn_off(4 * cc + c, rg);
       hds_write16(img + off, h0);
-      hds_write16(img + T_PLANE + off, h1);
+      hds_write16(img + plane + off, h1);
     }
   };
 
@@ -882,8 +915,8 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
 
   const int h = lane >> 5;
   auto mma = [&](int buf) {
-    const uint32_t iy = smem_base + buf * T_STAGE;
-    const uint32_t ix = iy + 2 * T_PLANE;
+    const uint32_t iy = smem_base + buf * CF::STAGE;
+    const uint32_t ix = iy + 2 * CF::YPLANE;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
       f16x8 a[2][2], b[2][2];
@@ -892,9 +925,9 @@ __global__ void __launch_bounds__(256, 2) k_gemm_tn_h(const float* __restrict__ 
         const uint32_t oa = tn_off(64 * wm + 32 * i + (lane & 31), 2 * st + h);
         const uint32_t ob = tn_off(64 * wk + 32 * i + (lane & 31), 2 * st + h);
         a[i][0] = hds_read16<f16x8>(iy + oa);
-        a[i][1] = hds_read16<f16x8>(iy + T_PLANE + oa);
+        a[i][1] = hds_read16<f16x8>(iy + CF::YPLANE + oa);
         b[i][0] = hds_read16<f16x8>(ix + ob);
-        b[i][1] = hds_read16<f16x8>(ix + T_PLANE + ob);
+        b[i][1] = hds_read16<f16x8>(ix + CF::XPLANE + ob);
       }
       asm volatile("s_waitcnt lgkmcnt(0)"
                    : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0][0]),
@@ -1012,21 +1045,42 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
   return launch_status("rb_gemm_nt_h");
 }
 
+// dW tile: 256 x 128 when N % 256 == 0 (2), else 128 x 256 when K % 256 == 0
+// (1), else 128 x 128 (0).  The big tiles are 512-thread workgroups, one per
+// CU, so the same split count S (~2 x CUs / (N/128 x K/128)) fills the chip.
+inline int tn_tile_shape(int N, int K) {
+#ifdef HN_TN_SMALL
+  (void)N; (void)K;
+  return 0;
+#else
+  return N % 256 == 0 ? 2 : (K % 256 == 0 ? 1 : 0);
+#endif
+}
+
 int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
                      int K, const float* ymax, const float* xmax, float* parts, int S,
                      hipStream_t st) {
-  static bool done = false;  // benign race: idempotent
-  if (!done) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_tn_h, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              T_LDS);
-    done = true;
-  }
-  const int nt_k = K / T_BT;
-  const int nt = (N / T_BT) * nt_k;
   // rows per split: a multiple of 32 (the rmax groups)
   const int64_t mk = ((M + S - 1) / S + 31) / 32 * 32;
-  k_gemm_tn_h<<<(unsigned)(nt * S), 256, T_LDS, st>>>(Y, ldy, X, ldx, M, N, K, ymax, xmax, parts,
-                                                      S, mk, nt_k);
+  auto run = [&](auto nbn_c, auto nbk_c) {
+    constexpr int NBN = decltype(nbn_c)::value, NBK = decltype(nbk_c)::value;
+    using CF = TnCfg<NBN, NBK>;
+    static bool done = false;  // benign race: idempotent
+    if (!done) {
+      (void)hipFuncSetAttribute((const void*)k_gemm_tn_h<NBN, NBK>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS);
+      done = true;
+    }
+    const int nt_k = K / CF::XC;
+    const int nt = (N / CF::YC) * nt_k;
+    k_gemm_tn_h<NBN, NBK><<<(unsigned)(nt * S), CF::THREADS, CF::LDS, st>>>(
+        Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
+  };
+  switch (tn_tile_shape(N, K)) {
+    case 2: run(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}); break;
+    case 1: run(std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}); break;
+    default: run(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}); break;
+  }
   return launch_status("rb_gemm_tn_h");
 }
 

@@ -125,5 +125,67 @@ int main(int argc, char** argv) {
 #endif
   }
   printf("total %.1f us  (%.2f TB/s)\n", tot, totb / tot / 1e6);
+
+  // weight gradients (rb_gemm_tn_h): dW[N, K] = dY^T X over M rows, row-chunk
+  // partials [S, N, K] (S as linear._tn_splits picks for 256 CUs); the
+  // operands' 32-row-group maxima: the fill's bound (|x| <= 1)
+  struct TShape { const char* name; int N, K; };
+  const TShape tsh[] = {{"gates.dW", 512, 256}, {"in.dW", 512, 128}, {"w2.dW", 128, 512},
+                        {"out.dW", 128, 256}};
+  float *X, *rm, *parts;
+  CK(hipMalloc(&X, M * 512 * 4));
+  CK(hipMalloc(&rm, ((M + 31) / 32) * 4));
+  CK(hipMalloc(&parts, (size_t)256 * 512 * 256 * 4));
+  fill<<<4096, 256>>>(X, M * 512, 3, 2.0f);
+  {
+    std::vector<float> ones((M + 31) / 32, 1.0f);
+    CK(hipMemcpy(rm, ones.data(), ones.size() * 4, hipMemcpyHostToDevice));
+  }
+  double ttot = 0;
+  for (const TShape& t : tsh) {
+    const int nt = (t.N / 128) * (t.K / 128);
+    const int S = std::max(8, (2 * num_cus() / nt) / 8 * 8);
+    std::vector<float> ts;
+    for (int rep = 0; rep < 12; ++rep) {
+      CK(hipEventRecord(e0, 0));
+      int rc = launch_gemm_tn_h(A, t.N, X, t.K, M, t.N, t.K, rm, rm, parts, S, 0);
+      if (rc) { fprintf(stderr, "tn launch failed %d\n", rc); return 1; }
+      CK(hipEventRecord(e1, 0));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      ts.push_back(ms * 1e3f);
+    }
+    {
+      // a few dW entries against fp64 (all M rows)
+      std::vector<float> hp((size_t)S * t.N * t.K);
+      CK(hipMemcpy(hp.data(), parts, hp.size() * 4, hipMemcpyDeviceToHost));
+      std::vector<float> ca(M), cb(M);
+      double worst = 0;
+      for (int e = 0; e < 6; ++e) {
+        const int n = (e * 97) % t.N, k = (e * 61 + 5) % t.K;
+        CK(hipMemcpy2D(ca.data(), 4, A + n, (size_t)t.N * 4, 4, M, hipMemcpyDeviceToHost));
+        CK(hipMemcpy2D(cb.data(), 4, X + k, (size_t)t.K * 4, 4, M, hipMemcpyDeviceToHost));
+        double ref = 0, mag = 0, got = 0;
+        for (int64_t m = 0; m < M; ++m) {
+          ref += (double)ca[m] * cb[m];
+          mag += fabs((double)ca[m] * cb[m]);
+        }
+        for (int sp = 0; sp < S; ++sp) got += hp[((size_t)sp * t.N + n) * t.K + k];
+        worst = std::max(worst, fabs(got - ref) / mag);
+      }
+      if (!(worst < 1e-6)) {
+        fprintf(stderr, "%s: WRONG RESULT (max err %.3e)\n", t.name, worst);
+        return 2;
+      }
+    }
+    std::sort(ts.begin(), ts.end());
+    const double us = ts[ts.size() / 2];
+    const double by = 4.0 * M * (t.N + t.K);
+    ttot += us;
+    printf("%-10s N=%3d K=%3d S=%3d %7.1f us  %6.1f TF  %6.2f TB/s\n", t.name, t.N, t.K, S, us,
+           2.0 * M * t.N * t.K / us / 1e6, by / us / 1e6);
+  }
+  printf("tn total %.1f us\n", ttot);
   return 0;
 }

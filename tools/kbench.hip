@@ -234,6 +234,7 @@ int main(int argc, char** argv) {
   const int rounds = argc > 4 ? atoi(argv[4]) : 15;
   const bool bf16_only = argc > 5 && atoi(argv[5]) == 1;   // the config-5 bf16 sweep only
   const bool packed_only = argc > 5 && atoi(argv[5]) == 2; // gate bwd: dense vs packed lengths
+  const bool predecessor = argc > 5 && atoi(argv[5]) == 3;  // gate bwd after different kernels
   const double N = (double)B * L * H;
   const int64_t n = (int64_t)B * L * H;
   const int nT = (L + RB_TILE - 1) / RB_TILE;
@@ -260,6 +261,53 @@ int main(int argc, char** argv) {
   float* so = dalloc(n, 21);
   float* sd = dalloc(n, 22);
   CK(hipDeviceSynchronize());
+
+  if (predecessor) {
+    // the dense gate backward timed alone, with HIP events around it only,
+    // right after (no sync) a preceding launch: nothing (GPU idle), a float4
+    // copy, the f16x3 gates GEMM (MFMA-heavy), or another gate backward
+    float* A = dalloc((int64_t)B * L * H, 50);
+    float* O = dalloc((int64_t)B * L * 2 * H, 51);
+    float* W = dalloc((int64_t)2 * H * H, 52, -0.05f, 0.05f);
+    void* Wf;
+    CK(hipMalloc(&Wf, (size_t)2 * H * H * 4 + 8192));
+    rb_split_job job{W, H, 2 * H, H, 0, Wf};
+    CK((hipError_t)launch_split_weights_h(&job, 1, 0));
+    auto gate = [=] {
+      gate_bwd_v<float, 4>(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, car, dy, drg, 2 * H, dxc,
+                           H, dz + H, 2 * H, part, dh0, B, L, H, nullptr, 0, nullptr);
+    };
+    struct Pre { const char* name; std::function<void()> run; };
+    std::vector<Pre> pres = {
+        {"idle", [] {}},
+        {"copy4 x3", [=] { for (int k = 0; k < 3; ++k) hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)xc, (float4*)dxc, n / 4); }},
+        {"gemm_nt_h x3", [=] { for (int k = 0; k < 3; ++k) launch_gemm_nt_h(A, H, (int64_t)B * L, H, Wf, 2 * H, nullptr, O, 2 * H, 0, nullptr, 0); }},
+        {"gate_bwd x3", [=] { for (int k = 0; k < 3; ++k) gate(); }},
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<std::vector<float>> ms(pres.size());
+    for (int r = 0; r < rounds; ++r)
+      for (size_t i = 0; i < pres.size(); ++i) {
+        CK(hipDeviceSynchronize());
+        pres[i].run();
+        CK(hipEventRecord(e0, 0));
+        gate();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms[i].push_back(t);
+      }
+    printf("B=%d L=%d H=%d dense gate backward after a predecessor (median of %d)\n", B, L, H, rounds);
+    for (size_t i = 0; i < pres.size(); ++i) {
+      std::sort(ms[i].begin(), ms[i].end());
+      const double med = ms[i][ms[i].size() / 2];
+      printf("after %-14s %8.1f us  %.3f of 8 TB/s\n", pres[i].name, med * 1e3, 9 * N * 4 / (med * 1e-3) / 8e12);
+    }
+    return 0;
+  }
 
   std::vector<Case> cs;
   GateBufs sep{rg, xc, xz + H, y, car, dy, drg, dxc, dz + H, part, dh0, lam,
