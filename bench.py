@@ -275,6 +275,74 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
                                     "kernels": kern}}
 
 
+def gate_bwd_pattern(args, batch, dev, rounds=15):
+    """The dominant kernel beside a trivial-math kernel with its exact memory
+    access pattern (rb_probe_gate_bwd_pattern: the same 5 reads + 4 writes
+    per step and channel, strides, wave/lane layout, sequence pairing and
+    reverse tile order), alternated on this lease over the bench's packed
+    layout (the batch's lengths, longest first, as the model packs them):
+    the pattern's rate is the ceiling the memory system grants this
+    read/write mix, here and now.  Median per-launch of each."""
+    from datamining_recblr_amd import _lib
+    from datamining_recblr_amd.kernels import _stream
+    H = 2 * args.hidden
+    lens = batch["item_length"].to("cpu").sort(descending=True).values
+    B = lens.numel()
+    offs_h = torch.zeros(B + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=offs_h[1:])
+    ntok = int(offs_h[-1])
+    offs = offs_h.to(dev)
+    g = torch.Generator(device=dev).manual_seed(5)
+    rg = torch.randn(ntok, 2 * H, device=dev, generator=g)
+    xz = torch.randn(ntok, 2 * H, device=dev, generator=g)
+    xc = torch.randn(ntok, H, device=dev, generator=g)
+    dy = torch.randn(ntok, H, device=dev, generator=g)
+    lam = torch.full((H,), -3.0, device=dev)
+    carries = torch.zeros(B, kernels.num_tiles(args.seq_len), H, device=dev)
+    drg = torch.empty(ntok, 2 * H, device=dev)
+    dxc = torch.empty(ntok, H, device=dev)
+    dxz = torch.empty(ntok, 2 * H, device=dev)
+    part = torch.empty(4, B, H, device=dev)
+    z, dz = xz[:, H:], dxz[:, H:]
+    st = _stream(xc)
+
+    def real():
+        _lib.call("rb_gate_scan_bwd", rg.data_ptr(), 2 * H, xc.data_ptr(), H, z.data_ptr(), 2 * H,
+                  lam.data_ptr(), 0, carries.data_ptr(), dy.data_ptr(), drg.data_ptr(), 2 * H,
+                  dxc.data_ptr(), H, dz.data_ptr(), 2 * H, part.data_ptr(), part[3].data_ptr(),
+                  B, args.seq_len, H, offs.data_ptr(), st)
+
+    def pattern():
+        _lib.call("rb_probe_gate_bwd_pattern", rg.data_ptr(), 2 * H, xc.data_ptr(), H,
+                  z.data_ptr(), 2 * H, dy.data_ptr(), drg.data_ptr(), 2 * H, dxc.data_ptr(), H,
+                  dz.data_ptr(), 2 * H, B, args.seq_len, H, offs.data_ptr(), st)
+
+    ts = {"kernel": [], "pattern": []}
+    for fn in (real, pattern):
+        fn()
+    torch.cuda.synchronize()
+    for _ in range(rounds):
+        for name, fn in (("kernel", real), ("pattern", pattern)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts[name].append(e0.elapsed_time(e1) * 1e3)
+    nbytes = 9 * ntok * H * 4
+    out = {}
+    for name, v in ts.items():
+        us = sorted(v)[len(v) // 2]
+        out[name + "_frac"] = round(nbytes / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)
+        out[name + "_us"] = round(us, 2)
+    out["kernel_over_pattern"] = round(out["kernel_frac"] / out["pattern_frac"], 4)
+    out["note"] = ("rb_gate_scan_bwd vs rb_probe_gate_bwd_pattern (its access pattern, trivial "
+                   "math) alternated on this lease over a packed batch of the bench's lengths, "
+                   "9 streams x ntok x H x 4 B; the pattern's rate on these boxes moves between "
+                   "~0.63 and ~0.75 of 8 TB/s (profiles/r02_kbench_gate_bwd_pattern.log)")
+    return out
+
+
 def ddp_overhead(args, model, batches, dev, rounds=3):
     """What DistributedDataParallel (bucketed gradient all-reduce over RCCL)
     costs one GPU: the same train step on a copy of the model, plain and
@@ -552,6 +620,8 @@ def main():
             "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
             "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    if roofline is not None and env.rank == 0 and args.hidden * 2 % 4 == 0:
+        roofline["pattern"] = gate_bwd_pattern(args, batches[0], dev)
     ddp_ab = None
     if env.world_size == 1 and not args.no_ddp_ab:
         ddp_ab = ddp_overhead(args, model, batches, dev)

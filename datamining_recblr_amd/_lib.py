@@ -50,6 +50,9 @@ SIGNATURES = {
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
                                         _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
                                         _fp, _fp]),
+    "rb_probe_gate_bwd_pattern": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64,
+                                                 _fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp,
+                                                 _fp]),
     "rb_pad_prefix_fwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp]),
     "rb_pad_prefix_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
                                          _fp, _fp, _fp, ctypes.c_int, _fp]),

@@ -457,6 +457,19 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
                  int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
                  void* stream);
 
+/* Measurement aid (bench.py, not the model's path; no reference counterpart):
+ * the memory access pattern of rb_gate_scan_bwd (fp32) — the same reads of
+ * r, i, xc, z, dy and writes of dr, di, dxc, dz with the same row strides,
+ * wave/lane layout, sequence pairing and reverse tile order — with one
+ * product per output instead of the BD-LRU backward arithmetic.  Its rate is
+ * the ceiling the memory system grants that pattern; outputs are
+ * meaningless. */
+int rb_probe_gate_bwd_pattern(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
+                              const float* z, int64_t z_rs, const float* dy, float* drg,
+                              int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz,
+                              int64_t dz_rs, int64_t B, int64_t L, int64_t H,
+                              const int64_t* seq_offsets, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

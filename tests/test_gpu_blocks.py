@@ -520,3 +520,37 @@ def test_conv_bwd_folded_partials_equal_separate(cuda, K, dt):
     assert torch.equal(dx0, dx1)
     assert torch.equal(dw0, dw1)
     assert torch.equal(db0, db1)
+
+
+def test_gate_bwd_pattern_probe_covers_every_element(cuda):
+    """rb_probe_gate_bwd_pattern (bench.py's pattern ceiling) touches exactly
+    the gate backward's elements: on a packed batch (lengths 1..37, paired
+    longest-first waves) every output row of every sequence is written with
+    its trivial product, and nothing past ntok."""
+    from datamining_recblr_amd import _lib
+    from datamining_recblr_amd.kernels import _stream
+
+    g = torch.Generator().manual_seed(3)
+    H = 64
+    lens = torch.randint(1, 38, (23,), generator=g).sort(descending=True).values
+    offs = torch.zeros(lens.numel() + 1, dtype=torch.int64)
+    torch.cumsum(lens, 0, out=offs[1:])
+    ntok = int(offs[-1])
+    rg = torch.randn(ntok, 2 * H, generator=g).to(cuda)
+    xz = torch.randn(ntok, 2 * H, generator=g).to(cuda)
+    xc = torch.randn(ntok, H, generator=g).to(cuda)
+    dy = torch.randn(ntok, H, generator=g).to(cuda)
+    drg = torch.full((ntok + 5, 2 * H), float("nan"), device=cuda)
+    dxc = torch.full((ntok + 5, H), float("nan"), device=cuda)
+    dxz = torch.full((ntok + 5, 2 * H), float("nan"), device=cuda)
+    z, dz = xz[:, H:], dxz[:, H:]
+    _lib.call("rb_probe_gate_bwd_pattern", rg.data_ptr(), 2 * H, xc.data_ptr(), H, z.data_ptr(),
+              2 * H, dy.data_ptr(), drg.data_ptr(), 2 * H, dxc.data_ptr(), H, dz.data_ptr(), 2 * H,
+              lens.numel(), 37, H, offs.to(cuda).data_ptr(), _stream(xc))
+    torch.cuda.synchronize()
+    assert torch.equal(drg[:ntok, :H], rg[:, :H] * dy)
+    assert torch.equal(drg[:ntok, H:], rg[:, H:] * dy)
+    assert torch.equal(dxc[:ntok], xc * dy)
+    assert torch.equal(dz[:ntok], z * dy)
+    assert torch.isnan(drg[ntok:]).all() and torch.isnan(dxc[ntok:]).all()
+    assert torch.isnan(dxz[:, :H]).all() and torch.isnan(dxz[ntok:]).all()
