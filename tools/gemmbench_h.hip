@@ -1,6 +1,7 @@
 // gemmbench_h.hip — timing of the f16 two-part split GEMM (csrc/gemm_half.hip)
 // on the encoder's projection shapes.  Ablation builds:
-//   -DHN_NO_ADMA / -DHN_NSA=n / -DHN_LATE_DMA / -DHN_NARROW_STORE / -DHN_WAVES=n;
+//   -DHN_NO_SPLIT / -DHN_NO_MFMA / -DHN_NO_BARRIER (wrong results: run with
+//   GB_NOCHECK=1) / -DHN_NO_ADMA / -DHN_NSA=n / -DHN_LATE_DMA / -DHN_NARROW_STORE / -DHN_WAVES=n;
 //   -DHN_STAMPS prints each
 //   k-step segment's share of the waves' cycles
 //   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 -I include \
@@ -97,7 +98,7 @@ int main(int argc, char** argv) {
       }
       if (!(worst < 1e-6)) {
         fprintf(stderr, "%s: WRONG RESULT (max err %.3e)\n", s.name, worst);
-        return 2;
+        if (!getenv("GB_NOCHECK")) return 2;   // ablation builds: time anyway
       }
     }
     std::sort(ts.begin(), ts.end());
@@ -176,7 +177,7 @@ int main(int argc, char** argv) {
       }
       if (!(worst < 1e-6)) {
         fprintf(stderr, "%s: WRONG RESULT (max err %.3e)\n", t.name, worst);
-        return 2;
+        if (!getenv("GB_NOCHECK")) return 2;
       }
     }
     std::sort(ts.begin(), ts.end());
