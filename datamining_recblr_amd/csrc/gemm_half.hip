@@ -574,6 +574,15 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         acc[n] = mfma_h(a0, bq[n][1], acc[n]);
         acc[n] = mfma_h(a0, bq[n][0], acc[n]);
         if (n + 2 < N_NB) {
+#ifdef HN_HALF_B
+          // ablation (wrong results): the upper half of the column blocks
+          // reuse the lower half's fragments (half the B LDS reads)
+          if (n + 2 >= N_NB / 2 && N_NB >= 4) {
+            bq[n + 2][0] = bq[n + 2 - N_NB / 2][0];
+            bq[n + 2][1] = bq[n + 2 - N_NB / 2][1];
+            continue;
+          }
+#endif
           bq[n + 2][0] = rb(n + 2, 0);
           bq[n + 2][1] = rb(n + 2, 1);
         }

@@ -1,6 +1,6 @@
 // gemmbench_h.hip — timing of the f16 two-part split GEMM (csrc/gemm_half.hip)
 // on the encoder's projection shapes.  Ablation builds:
-//   -DHN_NO_SPLIT / -DHN_NO_MFMA / -DHN_NO_BARRIER (wrong results: run with
+//   -DHN_NO_SPLIT / -DHN_NO_MFMA / -DHN_NO_BARRIER / -DHN_HALF_B (wrong results: run with
 //   GB_NOCHECK=1) / -DHN_NO_ADMA / -DHN_NSA=n / -DHN_LATE_DMA / -DHN_NARROW_STORE / -DHN_WAVES=n;
 //   -DHN_STAMPS prints each
 //   k-step segment's share of the waves' cycles
