@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 23; }
+int rb_version(void) { return 24; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -492,6 +492,46 @@ int rb_item_ce_probs(const float* seq, const float* items, const int64_t* target
   if (ld < V) return fail("rb_item_ce_probs: ld < V");
   return launch_item_ce_probs(seq, items, target, lse, dloss, B, V, d, item_offset, V, probs, ld,
                               reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_split_h(const float* x, int64_t n, int64_t d, void* image, int* exps, void* stream) {
+  if (!x || !image || !exps) return fail("rb_item_split_h: null pointer");
+  if (n <= 0) return fail("rb_item_split_h: n must be positive");
+  if (d != 16 && d != 32 && d != 64 && d != 128 && d != 256)
+    return fail("rb_item_split_h: d must be 16, 32, 64, 128 or 256");
+  if (!aligned16(x) || !aligned16(image)) return fail("rb_item_split_h: operands must be 16-B aligned");
+  if (n >= (int64_t(1) << 31)) return fail("rb_item_split_h: n too large");
+  return launch_item_split_h(x, n, d, image, exps, reinterpret_cast<hipStream_t>(stream));
+}
+
+namespace {
+int check_items_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                  const int* item_exp, int64_t B, int64_t V, int64_t d) {
+  if (!seq_exp || !item_exp) return fail("item scores (f16): null exponent pointer");
+  return check_items("item scores (f16)", reinterpret_cast<const float*>(seq_img),
+                     reinterpret_cast<const float*>(item_img), B, V, d);
+}
+}  // namespace
+
+int rb_item_ce_fwd_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                     const int* item_exp, const int64_t* target, int64_t B, int64_t V, int64_t d,
+                     float* lse, float* loss, void* workspace, int64_t workspace_bytes,
+                     void* stream) {
+  if (int rc = check_items_h(seq_img, seq_exp, item_img, item_exp, B, V, d)) return rc;
+  if (!target || !lse || !loss || !workspace) return fail("rb_item_ce_fwd_h: null pointer");
+  return launch_item_ce_fwd_h(seq_img, seq_exp, item_img, item_exp, target, B, V, d, lse, loss,
+                              workspace, workspace_bytes, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_ce_probs_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                       const int* item_exp, const int64_t* target, const float* lse,
+                       const float* dloss, int64_t B, int64_t V, int64_t d, int64_t item_offset,
+                       float* probs, int64_t ld, void* stream) {
+  if (int rc = check_items_h(seq_img, seq_exp, item_img, item_exp, B, V, d)) return rc;
+  if (!target || !lse || !dloss || !probs) return fail("rb_item_ce_probs_h: null pointer");
+  if (ld < V) return fail("rb_item_ce_probs_h: ld < V");
+  return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
+                                item_offset, probs, ld, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,

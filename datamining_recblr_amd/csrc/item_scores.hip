@@ -97,6 +97,14 @@ __device__ __forceinline__ void rowdata_dma(float* lbuf, int64_t* tbuf, const fl
   __builtin_amdgcn_global_load_lds(tp, (lds_ptr_t)tbuf, 4, 0, 0);
 }
 
+// per-row int32 exponents of rows [r0, r0 + 32) -> LDS (wave 0; lanes 32-63
+// repeat them into the buffer's upper half)
+__device__ __forceinline__ void rowexp_dma(float* ebuf, const float* ex, int64_t r0, int64_t n) {
+  const int lane = threadIdx.x & 63;
+  if ((threadIdx.x >> 6) != 0) return;
+  __builtin_amdgcn_global_load_lds(ex + min(r0 + (lane & 31), n - 1), (lds_ptr_t)ebuf, 4, 0, 0);
+}
+
 template <int D>
 __device__ __forceinline__ float lds_at(const float* tile, int row, int col) {
   using S = Stream<D>;
@@ -264,9 +272,10 @@ __device__ __forceinline__ bool place(int64_t RB, int64_t S, Place& p) {
 // Shared frame of the row-stationary kernels: the workgroup's 4 waves own
 // 128 fixed rows (32 per wave) and walk tiles [split*per, ...) of `strm`
 // [n_strm, D].  body(tile_index, lds_tile, lds_lse, lds_tgt) runs once per
-// streamed tile with the tile resident in LDS; with kRowData the tile's
-// per-row lse / target values ride along.
-template <int D, bool kRowData, class Body>
+// streamed tile with the tile resident in LDS; with kRowData 1 the tile's
+// per-row lse / target values ride along, with 2 the per-row int32 scale
+// exponents of a split image (passed as lse_g, landing in lds_lse).
+template <int D, int kRowData, class Body>
 __device__ __forceinline__ void stream_tiles(const float* strm, int64_t n_strm, int64_t per,
                                              int64_t split, const float* lse_g,
                                              const int64_t* tgt_g, Body&& body) {
@@ -285,7 +294,8 @@ __device__ __forceinline__ void stream_tiles(const float* strm, int64_t n_strm, 
   if (t0 >= t1) return;
   auto issue = [&](int64_t t, float* b, float* lb, int64_t* tb) {
     tile_dma<D>(b, strm, t * kTile, n_strm);
-    if constexpr (kRowData) rowdata_dma(lb, tb, lse_g, tgt_g, t * kTile, n_strm);
+    if constexpr (kRowData == 1) rowdata_dma(lb, tb, lse_g, tgt_g, t * kTile, n_strm);
+    if constexpr (kRowData == 2) rowexp_dma(lb, lse_g, t * kTile, n_strm);
   };
 #ifdef RB_ITEM_PROF
   uint64_t c0 = clock64(), cb = 0, cw = 0, cx;
@@ -379,7 +389,7 @@ __global__ __launch_bounds__(256) void k_ce_fwd(const float* __restrict__ E,
   }
 }
 
-// lse[b] over the S splits (one wave per row, fixed-order butterfly), the
+// lse[b] over the S splits (a lane per row, four waves over the splits), the
 // per-row loss lse - score(target) (NaN for an out-of-range target, which
 // k_ce_fwd never matches), and - in the workgroup that finishes last - the
 // batch mean in a fixed order.  `ticket` is zeroed by k_ce_fwd.
@@ -391,21 +401,27 @@ __global__ __launch_bounds__(256) void k_ce_rows(const float* __restrict__ m_par
                                                  float* __restrict__ loss_rows,
                                                  unsigned* __restrict__ ticket,
                                                  float* __restrict__ loss) {
+  // 64 rows per workgroup, one per lane; wave w merges splits w, w + 4, ...
+  // in order (coalesced: a wave reads 64 consecutive rows of a split), then
+  // the four waves' states merge in wave order
   __shared__ float red[256];
+  __shared__ float sm[4][64], ss[4][64];
   __shared__ bool last;
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (b < B) {
-    float m = -INFINITY, s = 0.0f;
-    for (int64_t i = lane; i < S; i += 64) lse_merge(m, s, m_part[i * B + b], s_part[i * B + b]);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t b = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t bc = b < B ? b : B - 1;
+  float m = -INFINITY, s = 0.0f;
+  for (int64_t i = w; i < S; i += 4) lse_merge(m, s, m_part[i * B + bc], s_part[i * B + bc]);
+  sm[w][lane] = m;
+  ss[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && b < B) {
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) lse_merge(m, s, __shfl_xor(m, off), __shfl_xor(s, off));
-    if (lane == 0) {
-      const float l = m + logf(s);
-      const int64_t t = tgt[b];
-      lse[b] = l;
-      loss_rows[b] = (t < 0 || t >= V) ? NAN : l - ts[b];
-    }
+    for (int k = 1; k < 4; ++k) lse_merge(m, s, sm[k][lane], ss[k][lane]);
+    const float l = m + logf(s);
+    const int64_t t = tgt[b];
+    lse[b] = l;
+    loss_rows[b] = (t < 0 || t >= V) ? NAN : l - ts[b];
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -662,6 +678,234 @@ __global__ __launch_bounds__(256) void k_item_scores(const float* __restrict__ E
   });
 }
 
+// ---- the f16 pipe: two-part split operands -------------------------------------
+// The CE forward and the logits' gradient (the training step's two scoring
+// kernels) run on v_mfma_f32_32x32x16_f16, 16x the fp32 MFMA rate, with
+// fp32-level accuracy (the GEMMs' scheme, csrc/gemm_half.hip): each row x of
+// seq and of the item table is scaled by an exact power of two and split,
+//   x = 2^(e - kTS) (x0 + x1), x0 = f16(x 2^(kTS - e)), x1 = f16(x 2^(kTS - e) - x0),
+// e the frexp exponent of max|x| (the row max lands in [2^13, 2^14)): 22
+// significant bits.  A score is x0.y0 + x0.y1 + x1.y0 accumulated in fp32
+// (each product exact; the dropped x1.y1 <= 2^-22 relative), un-scaled by
+// v_ldexp (exact).  Image row = [x0 (D halfs) | x1 (D halfs)] = the fp32
+// row's D*4 bytes, so the tile DMA and its swizzle are unchanged; the
+// exponents are one int32 per row beside it.  Both kernels run the three
+// products in the same order with the item parts first, so the forward's
+// log-sum-exp and the gradient kernel see bit-identical logits.
+// The rank / score kernels (evaluation) stay on the fp32 pipe: their target
+// score replays the exact fma chain (k_target_dot).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kTS = 14;
+
+// one wave per row: max|x| over the row, then the two planes (4 values per
+// lane and pass)
+__global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ X, int64_t N, int D,
+                                                      _Float16* __restrict__ img,
+                                                      int* __restrict__ ex) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= N) return;
+  const float4* x = reinterpret_cast<const float4*>(X + r * D);
+  const int nq = D / 4;
+  float m = 0.0f;
+  for (int q = lane; q < nq; q += 64) {
+    const float4 v = x[q];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
+  _Float16* h0 = img + r * 2 * D;
+  _Float16* h1 = h0 + D;
+  for (int q = lane; q < nq; q += 64) {
+    const float4 v = x[q];
+    const float t[4] = {v.x, v.y, v.z, v.w};
+    _Float16 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float sv = __builtin_amdgcn_ldexpf(t[i], kTS - e);   // exact (power of two)
+      a[i] = (_Float16)sv;
+      b[i] = (_Float16)(sv - (float)a[i]);
+    }
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<f16x4*>(h0 + 4 * q) = f16x4{a[0], a[1], a[2], a[3]};
+    *reinterpret_cast<f16x4*>(h1 + 4 * q) = f16x4{b[0], b[1], b[2], b[3]};
+  }
+  if (lane == 0) ex[r] = e;
+}
+
+// this lane's register operand: row `row` of an image, k-blocks 16s + 8h ..
+// 16s + 8h + 7 of both planes (the MFMA fragment of step s)
+template <int D>
+__device__ __forceinline__ void ld_frag_h(f16x8 (&p0)[D / 16], f16x8 (&p1)[D / 16],
+                                          const _Float16* img, int64_t row, int h) {
+  const _Float16* r = img + row * 2 * D + 8 * h;
+#pragma unroll
+  for (int s = 0; s < D / 16; ++s) {
+    p0[s] = *reinterpret_cast<const f16x8*>(r + 16 * s);
+    p1[s] = *reinterpret_cast<const f16x8*>(r + D + 16 * s);
+  }
+}
+
+// X = items . seq over the full depth, item row j's fragments from the
+// swizzled LDS image tile, the other operand's from registers (kTileIsA:
+// the tile supplies A — rows of X are items — else B).  Per k16 step the
+// three products item1.seq0, item0.seq1, item0.seq0, in that order in both
+// orientations.  The tile reads run one step ahead of the MFMAs.
+template <int D, bool kTileIsA>
+__device__ __forceinline__ f32x16 lds_dot_h(const float* tile, int j, int h, const f16x8 (&r0)[D / 16],
+                                            const f16x8 (&r1)[D / 16]) {
+  constexpr int KS = D / 16;
+  const float* row = tile + j * D;
+  int sw = j % Stream<D>::NS;
+  asm volatile("" : "+v"(sw));
+  auto rd = [&](int slot) {
+    return __builtin_bit_cast(f16x8, *reinterpret_cast<const float4*>(row + ((slot ^ sw) << 2)));
+  };
+  f16x8 w0[KS], w1[KS];
+  w0[0] = rd(h);
+  w1[0] = rd(D / 8 + h);
+  f32x16 acc = {};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (s + 1 < KS) {
+      w0[s + 1] = rd(2 * (s + 1) + h);
+      w1[s + 1] = rd(D / 8 + 2 * (s + 1) + h);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (kTileIsA) {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1[s], r0[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0[s], r1[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0[s], r0[s], acc, 0, 0, 0);
+    } else {
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(r0[s], w1[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(r1[s], w0[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(r0[s], w0[s], acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return acc;
+}
+
+// k_ce_fwd on the f16 pipe: the same tiles, partials and target capture;
+// the item exponents of each tile ride along in LDS (rows crow(r, h): four
+// 16-B reads)
+template <int D>
+__global__ __launch_bounds__(256) void k_ce_fwd_h(const _Float16* __restrict__ Ei,
+                                                  const int* __restrict__ Ee,
+                                                  const _Float16* __restrict__ Wi,
+                                                  const int* __restrict__ We,
+                                                  const int64_t* __restrict__ tgt, int64_t B,
+                                                  int64_t V, int64_t per, int64_t RB, int64_t NS,
+                                                  float* __restrict__ m_part,
+                                                  float* __restrict__ s_part,
+                                                  float* __restrict__ ts,
+                                                  unsigned* __restrict__ ticket) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
+  Place pl;
+  if (!place(RB, NS, pl)) return;
+  const int64_t b = (pl.rb * kWaves + wave) * kTile + j;
+  const int64_t bc = min(b, B - 1);
+  f16x8 e0[D / 16], e1[D / 16];
+  ld_frag_h<D>(e0, e1, Ei, bc, h);
+  const int eb = Ee[bc] - 2 * kTS;
+  const int64_t tb = tgt[bc];
+  float m = -INFINITY, s = 0.0f, tsv = 0.0f;
+  bool has_ts = false;
+  stream_tiles<D, 2>(reinterpret_cast<const float*>(Wi), V, per, pl.split,
+                     reinterpret_cast<const float*>(We), nullptr,
+                     [&](int64_t t, const float* tile, const float* ebuf, const int64_t*) {
+    const int64_t v0 = t * kTile;
+    f32x16 x = lds_dot_h<D, true>(tile, j, h, e0, e1);
+    const int4* ev = reinterpret_cast<const int4*>(ebuf);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int4 q = ev[2 * g + h];   // items 8g + 4h .. 8g + 4h + 3 = rows crow(4g .. 4g + 3, h)
+      x[4 * g] = __builtin_amdgcn_ldexpf(x[4 * g], q.x + eb);
+      x[4 * g + 1] = __builtin_amdgcn_ldexpf(x[4 * g + 1], q.y + eb);
+      x[4 * g + 2] = __builtin_amdgcn_ldexpf(x[4 * g + 2], q.z + eb);
+      x[4 * g + 3] = __builtin_amdgcn_ldexpf(x[4 * g + 3], q.w + eb);
+    }
+    const int hi = rel32(V, v0), tt = rel32(tb, v0);
+    if (hi >= kTile) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) lse_push(m, s, x[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (crow(r, h) < hi) lse_push(m, s, x[r]);
+    }
+    if (tt >= 0 && tt < kTile) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (crow(r, h) == tt) {
+          tsv = x[r];
+          has_ts = true;
+        }
+    }
+  });
+  if (has_ts && b < B) ts[b] = tsv;
+  lse_merge(m, s, __shfl_xor(m, 32), __shfl_xor(s, 32));
+  if (h == 0 && b < B) {
+    m_part[pl.split * B + b] = m;
+    s_part[pl.split * B + b] = s;
+  }
+}
+
+// k_item_scores<D, true> on the f16 pipe (the logits' gradient P): seq rows
+// in registers (A), item tiles streamed (B) with their exponents
+template <int D>
+__global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__ Ei,
+                                                    const int* __restrict__ Ee,
+                                                    const _Float16* __restrict__ Wi,
+                                                    const int* __restrict__ We, int64_t B,
+                                                    int64_t V, int64_t per, int64_t RB, int64_t NS,
+                                                    float* __restrict__ out, int64_t ld,
+                                                    const float* __restrict__ lse,
+                                                    const int64_t* __restrict__ tgt,
+                                                    const float* __restrict__ dloss, float inv_n,
+                                                    int64_t v_off) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
+  Place pl;
+  if (!place(RB, NS, pl)) return;
+  const int64_t b0 = (pl.rb * kWaves + wave) * kTile;
+  f16x8 e0[D / 16], e1[D / 16];
+  ld_frag_h<D>(e0, e1, Ei, min(b0 + j, B - 1), h);
+  // per output row (registers r): lse, the target's column in this slice
+  // (-1 outside it; V < 2^31) and the row's exponent — 48 registers, int32
+  // where possible so two waves fit per SIMD
+  float lr[16];
+  int tr[16], er[16];
+  const float g = dloss[0] * inv_n;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t row = min(b0 + crow(r, h), B - 1);
+    lr[r] = lse[row];
+    const int64_t tv = tgt[row] - v_off;
+    tr[r] = (tv >= 0 && tv < V) ? (int)tv : -1;
+    er[r] = Ee[row] - 2 * kTS;
+  }
+  const bool full = b0 + kTile <= B;
+  stream_tiles<D, 2>(reinterpret_cast<const float*>(Wi), V, per, pl.split,
+                     reinterpret_cast<const float*>(We), nullptr,
+                     [&](int64_t t, const float* tile, const float* ebuf, const int64_t*) {
+    const int v = (int)(t * kTile) + j;
+    const f32x16 x = lds_dot_h<D, false>(tile, j, h, e0, e1);
+    const int ev = reinterpret_cast<const int*>(ebuf)[j];
+    if (v < V) {
+      float* o = out + (b0 + 4 * h) * ld + v;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = crow(r, 0);   // row - b0 - 4h
+        const float xs = __builtin_amdgcn_ldexpf(x[r], ev + er[r]);
+        const float val = (fexp(xs - lr[r]) - (v == tr[r] ? 1.0f : 0.0f)) * g;
+        if (full || b0 + 4 * h + rr < B) o[rr * ld] = val;
+      }
+    }
+  });
+}
+
 // ---- host side ---------------------------------------------------------------------
 size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -779,6 +1023,24 @@ void probs_t(const float* E, const float* W, int64_t B, int64_t V, const Grid2& 
                      g.blocks, g.splits, out, ld, lse, tgt, dloss, inv_n, v_off);
 }
 
+template <int D>
+void ce_fwd_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, const int64_t* tgt,
+                int64_t B, int64_t V, const Grid2& g, float* m, float* s, float* ts,
+                unsigned* ticket, hipStream_t st) {
+  hipLaunchKernelGGL(k_ce_fwd_h<D>, dim3(g.wgs()), dim3(256), 0, st, (const _Float16*)Ei, Ee,
+                     (const _Float16*)Wi, We, tgt, B, V, g.per, g.blocks, g.splits, m, s, ts,
+                     ticket);
+}
+
+template <int D>
+void probs_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, int64_t B, int64_t V,
+               const Grid2& g, float* out, int64_t ld, const float* lse, const int64_t* tgt,
+               const float* dloss, float inv_n, int64_t v_off, hipStream_t st) {
+  hipLaunchKernelGGL(k_ce_probs_h<D>, dim3(g.wgs()), dim3(256), 0, st, (const _Float16*)Ei, Ee,
+                     (const _Float16*)Wi, We, B, V, g.per, g.blocks, g.splits, out, ld, lse, tgt,
+                     dloss, inv_n, v_off);
+}
+
 void sum_parts(const float* parts, int64_t P, int64_t n, float* out, hipStream_t st) {
   const int64_t threads = (n + 3) / 4;
   hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, parts,
@@ -808,7 +1070,7 @@ int launch_item_ce_fwd(const float* E, const float* W, const int64_t* tgt, int64
   const Grid2 g = plan(B, ntiles(V));
   unsigned* ticket = reinterpret_cast<unsigned*>(w + L.ticket);
   RB_ITEM_DISPATCH(D, ce_fwd_t, E, W, tgt, B, V, g, m, s, ts, ticket, st);
-  hipLaunchKernelGGL(k_ce_rows, dim3((unsigned)((B + kWaves - 1) / kWaves)), dim3(256), 0, st, m,
+  hipLaunchKernelGGL(k_ce_rows, dim3((unsigned)((B + 63) / 64)), dim3(256), 0, st, m,
                      s, g.splits, ts, tgt, B, V, lse, rows, ticket, loss);
   return launch_status("rb_item_ce_fwd");
 }
@@ -860,6 +1122,42 @@ int launch_item_ce_probs(const float* E, const float* W, const int64_t* tgt, con
   (void)n_total;
   RB_ITEM_DISPATCH(D, probs_t, E, W, B, V, g, out, ld, lse, tgt, dloss, inv_n, v_off, st);
   return launch_status("rb_item_ce_probs");
+}
+
+int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_split_rows_h, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, X, N, (int)D,
+                     (_Float16*)img, ex);
+  return launch_status("rb_item_split_h");
+}
+
+int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
+                         const int64_t* tgt, int64_t B, int64_t V, int64_t D, float* lse,
+                         float* loss, void* ws, int64_t ws_bytes, hipStream_t st) {
+  const CeWs L = ce_layout(B, V, D);
+  if (ws_bytes < (int64_t)L.total) return fail("rb_item_ce_fwd_h: workspace too small");
+  char* w = static_cast<char*>(ws);
+  float* ts = reinterpret_cast<float*>(w + L.ts);
+  float* m = reinterpret_cast<float*>(w + L.m);
+  float* s = reinterpret_cast<float*>(w + L.s);
+  float* rows = reinterpret_cast<float*>(w + L.rows);
+  const Grid2 g = plan(B, ntiles(V));
+  unsigned* ticket = reinterpret_cast<unsigned*>(w + L.ticket);
+  RB_ITEM_DISPATCH(D, ce_fwd_h_t, Ei, Ee, Wi, We, tgt, B, V, g, m, s, ts, ticket, st);
+  hipLaunchKernelGGL(k_ce_rows, dim3((unsigned)((B + 63) / 64)), dim3(256), 0, st, m,
+                     s, g.splits, ts, tgt, B, V, lse, rows, ticket, loss);
+  return launch_status("rb_item_ce_fwd_h");
+}
+
+int launch_item_ce_probs_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
+                           const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
+                           int64_t V, int64_t D, int64_t v_off, float* out, int64_t ld,
+                           hipStream_t st) {
+  const Grid2 g = plan(B, ntiles(V));
+  const float inv_n = 1.0f / (float)B;
+  RB_ITEM_DISPATCH(D, probs_h_t, Ei, Ee, Wi, We, B, V, g, out, ld, lse, tgt, dloss, inv_n, v_off,
+                   st);
+  return launch_status("rb_item_ce_probs_h");
 }
 
 int launch_item_scores(const float* E, const float* W, int64_t B, int64_t V, int64_t D,

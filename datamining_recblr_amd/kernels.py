@@ -19,6 +19,7 @@ __all__ = [
     "scan_fwd", "scan_bwd", "conv_silu_fwd", "conv_silu_bwd", "gate_scan_fwd",
     "gate_scan_bwd", "num_tiles", "RecBLRNativeError", "kernel_timing", "KernelTimer",
     "item_ce_fwd", "item_ce_bwd", "item_ce_probs", "item_rank", "item_scores",
+    "SplitRows", "item_split_h", "item_ce_fwd_h", "item_ce_probs_h",
     "embedding_bwd", "embedding_plan",
 ]
 
@@ -631,7 +632,7 @@ def embedding_plan(idx, num_rows, d, stream=None):
 # Launches timed in FLOPs rather than bytes (bench.py reports them against the
 # MFMA roofline).
 FLOP_KERNELS = frozenset({"rb_item_ce_fwd", "rb_item_ce_bwd", "rb_item_ce_probs", "rb_item_rank",
-                          "rb_item_scores"})
+                          "rb_item_scores", "rb_item_ce_fwd_h", "rb_item_ce_probs_h"})
 ITEM_DIMS = (16, 32, 64, 128, 256)
 
 
@@ -707,6 +708,87 @@ def item_ce_probs(seq, items, target, lse, dloss, item_offset=0, out=None):
     _launch("rb_item_ce_probs", 2 * B * V * d, seq.data_ptr(), items.data_ptr(),
             target.data_ptr(), lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(),
             B, V, d, int(item_offset), out.data_ptr(), out.stride(0), _stream(seq))
+    return out
+
+
+class SplitRows:
+    """A [n, d] fp32 matrix as the f16 pipe's two-part split image (rb_item_split_h):
+    img [n, 2d] fp16 (per row d halfs x0 | d halfs x1), exps [n] int32.  Row
+    slices are views (rows(v0, v1)) for the sliced CE backward."""
+
+    __slots__ = ("img", "exps")
+
+    def __init__(self, img, exps):
+        self.img, self.exps = img, exps
+
+    @property
+    def shape(self):
+        return (self.img.shape[0], self.img.shape[1] // 2)
+
+    def rows(self, v0, v1):
+        return SplitRows(self.img[v0:v1], self.exps[v0:v1])
+
+
+def item_split_h(x) -> SplitRows:
+    """x [n, d] fp32 -> SplitRows (x = 2^(e-14) (x0 + x1) per row, 22 bits)."""
+    _check(x, "split operand")
+    if x.dim() != 2 or x.shape[1] not in ITEM_DIMS:
+        raise ValueError(f"[n, d] with d in {ITEM_DIMS} required, got {tuple(x.shape)}")
+    x = x.contiguous()
+    n, d = x.shape
+    img = torch.empty((n, 2 * d), device=x.device, dtype=torch.float16)
+    exps = torch.empty((n,), device=x.device, dtype=torch.int32)
+    _launch("rb_item_split_h", 8 * n * d + 4 * n, x.data_ptr(), n, d, img.data_ptr(),
+            exps.data_ptr(), _stream(x))
+    return SplitRows(img, exps)
+
+
+def _split_operands(seq, items, target):
+    for sr, what in ((seq, "seq"), (items, "items")):
+        if not isinstance(sr, SplitRows):
+            raise TypeError(f"{what} must be a SplitRows (item_split_h)")
+        if not (sr.img.is_contiguous() and sr.exps.is_contiguous()):
+            raise ValueError(f"{what} split image must be contiguous")
+    B, d = seq.shape
+    if items.shape[1] != d or d not in ITEM_DIMS:
+        raise ValueError("seq and items split images must share d in " + str(ITEM_DIMS))
+    if target.dtype != torch.int64 or target.shape != (B,):
+        raise ValueError("target must be int64 [B]")
+    return B, items.shape[0], d, target.contiguous()
+
+
+def item_ce_fwd_h(seq: SplitRows, items: SplitRows, target):
+    """item_ce_fwd on split images (the f16 MFMA pipe): (loss, lse)."""
+    B, V, d, target = _split_operands(seq, items, target)
+    dev = seq.img.device
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_item_ce_workspace(B, V, d))
+    ws = torch.empty((ws_bytes,), device=dev, dtype=torch.uint8)
+    lse = torch.empty((B,), device=dev, dtype=torch.float32)
+    loss = torch.empty((), device=dev, dtype=torch.float32)
+    _launch("rb_item_ce_fwd_h", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
+            items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(), B, V, d,
+            lse.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws_bytes, _stream(seq.img))
+    return loss, lse
+
+
+def item_ce_probs_h(seq: SplitRows, items: SplitRows, target, lse, dloss, item_offset=0,
+                    out=None):
+    """item_ce_probs on split images; items = the table image's rows
+    [item_offset, item_offset + V) (SplitRows.rows)."""
+    B, V, d, target = _split_operands(seq, items, target)
+    _check(lse, "lse")
+    _check(dloss, "dloss")
+    dev = seq.img.device
+    if out is None:
+        out = torch.empty((B, V), device=dev, dtype=torch.float32)
+    _check(out, "probs")
+    if out.shape != (B, V) or out.stride(1) != 1:
+        raise ValueError("probs must be [B, V] with unit column stride")
+    _launch("rb_item_ce_probs_h", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
+            items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
+            lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
+            int(item_offset), out.data_ptr(), out.stride(0), _stream(seq.img))
     return out
 
 

@@ -4,8 +4,10 @@ RecBLR.calculate_loss with loss_type "CE" (RecBLR.py:100-102) multiplies the
 [B, d] sequence representations by the [V, d] item table and applies
 nn.CrossEntropyLoss; full_sort_predict (RecBLR.py:114-122) returns the same
 [B, V] score matrix, which RecBole's evaluator (and run_with_unseen.py:229-265)
-reduces to the rank of each row's target item.  Here both run on the fp32
-MFMA kernels of csrc/item_scores.hip without materialising [B, V]:
+reduces to the rank of each row's target item.  Here both run on the MFMA
+kernels of csrc/item_scores.hip without materialising [B, V] — the training
+CE on the f16 pipe with two-part split operands (fp32-level accuracy,
+RECBLR_CE_PIPE), ranking and scores on the fp32 pipe:
 
   * item_cross_entropy: forward computes the per-row log-sum-exp tile by
     tile; backward recomputes the logits and forms dseq = P W and
@@ -38,9 +40,12 @@ def supported(seq: torch.Tensor, table: torch.Tensor) -> bool:
 # logits inside the MFMA kernels and needs no [B, V] buffer at all.
 CE_BACKWARD = os.environ.get("RECBLR_CE_BACKWARD", "slices")
 PROBS_SLICE_BYTES = 1 << 30
+# Logits pipe of the CE forward and of the sliced backward's P: "f16" (two-part
+# split operands on the f16 MFMA, fp32-level accuracy; default) or "f32".
+CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
 
 
-def _bwd_slices(seq, table, target, lse, dloss, want_seq, want_items):
+def _bwd_slices(seq, table, target, lse, dloss, want_seq, want_items, split=None):
     from .linear import _timed
 
     B, d = seq.shape
@@ -51,7 +56,12 @@ def _bwd_slices(seq, table, target, lse, dloss, want_seq, want_items):
         dtable = torch.empty_like(table)
     for v0 in range(0, V, vc):
         rows = table[v0:v0 + vc]
-        p = kernels.item_ce_probs(seq, rows, target, lse, dloss, item_offset=v0)
+        if split is not None:   # the forward's split images: bit-identical logits
+            s_seq, s_tab = split
+            p = kernels.item_ce_probs_h(s_seq, s_tab.rows(v0, v0 + vc), target, lse, dloss,
+                                        item_offset=v0)
+        else:
+            p = kernels.item_ce_probs(seq, rows, target, lse, dloss, item_offset=v0)
         fl = 2 * B * rows.shape[0] * d
         if want_seq:   # slices accumulate in a fixed order
             dseq = (_timed("gemm", fl, torch.mm, p, rows) if dseq is None
@@ -65,7 +75,13 @@ class _ItemCE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, seq, table, target):
         seq, table = seq.contiguous(), table.contiguous()
-        loss, lse = kernels.item_ce_fwd(seq, table, target)
+        if CE_PIPE == "f16":
+            s_seq, s_tab = kernels.item_split_h(seq), kernels.item_split_h(table)
+            loss, lse = kernels.item_ce_fwd_h(s_seq, s_tab, target)
+            ctx.split = (s_seq, s_tab)
+        else:
+            loss, lse = kernels.item_ce_fwd(seq, table, target)
+            ctx.split = None
         ctx.save_for_backward(seq, table, target, lse)
         return loss
 
@@ -78,7 +94,8 @@ class _ItemCE(torch.autograd.Function):
                                                want_seq=want_seq, want_items=want_items)
         else:
             dseq, dtable = _bwd_slices(seq, table, target, lse, dloss.float(), want_seq,
-                                       want_items)
+                                       want_items, split=ctx.split)
+        ctx.split = None
         return dseq, dtable, None
 
 

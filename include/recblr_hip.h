@@ -319,6 +319,29 @@ int rb_item_ce_probs(const float* seq, const float* items, const int64_t* target
                      const float* lse, const float* dloss, int64_t B, int64_t V, int64_t d,
                      int64_t item_offset, float* probs, int64_t ld, void* stream);
 
+/* ---- the same CE on the f16 MFMA pipe (the training step's default) ----
+ * fp32-level accuracy from two-part split operands: each row x of seq and of
+ * the item table is scaled by 2^(14 - e) (e = frexp exponent of max|x|) and
+ * split into x0 = f16(x'), x1 = f16(x' - x0); a score is x0.y0 + x0.y1 + x1.y0
+ * in fp32 on v_mfma_f32_32x32x16_f16, un-scaled exactly.
+ * rb_item_split_h: x [n, d] fp32 (16-B aligned) -> image [n, 2d] fp16
+ * (row: d halfs x0 | d halfs x1, 16-B aligned) and exps [n] int32. */
+int rb_item_split_h(const float* x, int64_t n, int64_t d, void* image, int* exps, void* stream);
+
+/* rb_item_ce_fwd on split images (workspace: rb_item_ce_workspace). */
+int rb_item_ce_fwd_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                     const int* item_exp, const int64_t* target, int64_t B, int64_t V, int64_t d,
+                     float* lse, float* loss, void* workspace, int64_t workspace_bytes,
+                     void* stream);
+
+/* rb_item_ce_probs on split images: item_img / item_exp point at image rows
+ * [item_offset, item_offset + V); lse from rb_item_ce_fwd_h on the same
+ * images (bit-identical logits in both kernels). */
+int rb_item_ce_probs_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                       const int* item_exp, const int64_t* target, const float* lse,
+                       const float* dloss, int64_t B, int64_t V, int64_t d, int64_t item_offset,
+                       float* probs, int64_t ld, void* stream);
+
 /* Workspace bytes of rb_item_rank. */
 int64_t rb_item_rank_workspace(int64_t B, int64_t V, int64_t d);
 

@@ -79,10 +79,13 @@ def test_item_rank_ties_and_invalid_targets(cuda):
     assert (gt0[:8] >= gt[:8]).all() and (gt0[:8] - gt[:8] <= 1).all()
 
 
+@pytest.mark.parametrize("pipe", ["f16", "f32"])
 @pytest.mark.parametrize("B,V,d", SHAPES)
-def test_item_ce_matches_torch(cuda, B, V, d):
+def test_item_ce_matches_torch(cuda, monkeypatch, B, V, d, pipe):
+    from datamining_recblr_amd import scoring
     from datamining_recblr_amd.scoring import item_cross_entropy
 
+    monkeypatch.setattr(scoring, "CE_PIPE", pipe)
     seq, W, tgt = _data(B, V, d, cuda, seed=3, scale=0.5)
     s1 = seq.clone().requires_grad_()
     w1 = W.clone().requires_grad_()
@@ -207,3 +210,122 @@ def test_item_ce_probs_slice_offsets(cuda):
     part = kernels.item_ce_probs(seq, W[300:600], tgt, lse, dl, item_offset=300, out=out[:, 100:400])
     assert torch.equal(part, full[:, 300:600])
     assert (out[:, :100] == 7).all() and (out[:, 400:] == 7).all()
+
+
+# ---- the f16 pipe (two-part split operands, csrc/item_scores.hip) -----------------
+# Scores there are x0.y0 + x0.y1 + x1.y0 of 11+11-bit parts of power-of-two
+# scaled rows, accumulated in fp32: error <= ~(d * 2^-24 + 2^-21) * sum|a b|,
+# the fp32 kernels' bound up to the dropped x1.y1 term — the same test
+# tolerances as the fp32 pipe.
+
+
+def _split_ref(x):
+    """(x0, x1, e) of rb_item_split_h, restated with numpy on the host (exact
+    power-of-two scaling in float64, RNE fp16 casts with subnormals)."""
+    import numpy as np
+
+    xn = x.cpu().numpy().astype(np.float64)
+    m = np.abs(xn).max(1)
+    e = np.where(m > 0, np.frexp(m)[1], 0).astype(np.int32)
+    sv = (xn * np.exp2(14.0 - e)[:, None]).astype(np.float32)   # exact shift
+    x0 = sv.astype(np.float16)
+    x1 = (sv - x0.astype(np.float32)).astype(np.float16)
+    dev = x.device
+    return (torch.from_numpy(x0).to(dev), torch.from_numpy(x1).to(dev),
+            torch.from_numpy(e).to(dev))
+
+
+@pytest.mark.parametrize("n,d", [(1, 16), (37, 32), (300, 64), (1000, 128), (5, 256)])
+def test_item_split_h_planes(cuda, n, d):
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator(device="cpu").manual_seed(n + d)
+    x = torch.randn(n, d, generator=g) * torch.exp2(torch.randint(-60, 60, (n, 1), generator=g).float())
+    x[0, : d // 2] = 0.0
+    if n > 2:
+        x[2] = 0.0                      # an all-zero row
+    x = x.to(cuda)
+    sp = kernels.item_split_h(x)
+    x0, x1, e = _split_ref(x)
+    assert torch.equal(sp.exps, e)
+    assert torch.equal(sp.img[:, :d], x0) and torch.equal(sp.img[:, d:], x1)
+    back = torch.ldexp(sp.img[:, :d].double() + sp.img[:, d:].double(),
+                       (sp.exps - 14)[:, None].double())
+    rel = ((back - x.double()).abs().amax(1) / x.double().abs().amax(1).clamp_min(1e-300))
+    assert (rel <= 2.0 ** -21).all()
+
+
+@pytest.mark.parametrize("B,V,d", [(1, 1, 16), (33, 64, 64), (300, 10544, 128), (37, 515, 256),
+                                   (2048, 10544, 128)])
+def test_item_ce_f16_kernels_vs_fp64(cuda, B, V, d):
+    """lse, loss and P on split images against fp64 (logits up to ~40 at d = 128)."""
+    from datamining_recblr_amd import kernels
+
+    seq_s, W_s, tgt = _data(B, V, d, cuda, seed=11, scale=1.0)
+    logits = seq_s.double() @ W_s.double().t()
+    ss, sw = kernels.item_split_h(seq_s), kernels.item_split_h(W_s)
+    loss, lse = kernels.item_ce_fwd_h(ss, sw, tgt)
+    ref_lse = torch.logsumexp(logits, 1)
+    assert torch.allclose(lse.double(), ref_lse, rtol=2e-6, atol=2e-5)
+    ref = F.cross_entropy(logits, tgt)
+    assert abs(loss.item() - ref.item()) <= 2e-5 * max(1.0, abs(ref.item()))
+    dl = torch.full((), 1.5, device=cuda)
+    p = kernels.item_ce_probs_h(ss, sw, tgt, lse, dl)
+    pref = (torch.softmax(logits, 1) - F.one_hot(tgt, V).double()) * 1.5 / B
+    assert (p.double() - pref).abs().max() <= 2e-5 * 1.5 / B
+    # deterministic
+    loss2, lse2 = kernels.item_ce_fwd_h(ss, sw, tgt)
+    assert torch.equal(loss, loss2) and torch.equal(lse, lse2)
+
+
+def test_item_ce_f16_row_scales(cuda):
+    """seq rows 2^k and item rows 2^-k (every exponent path), logits moderate:
+    per-row scales make each row's relative accuracy independent of k."""
+    from datamining_recblr_amd import kernels
+
+    B, V, d = 64, 300, 64
+    seq, W, tgt = _data(B, V, d, cuda, seed=12, scale=0.5)
+    k = torch.randint(-60, 60, (1,)).item()
+    seq_s = torch.ldexp(seq, torch.full((B, 1), float(k), device=cuda))
+    W_s = torch.ldexp(W, torch.full((V, 1), float(-k), device=cuda))
+    seq_s[5] = 0.0                                  # a zero row: logits 0
+    logits = seq_s.double() @ W_s.double().t()
+    loss, lse = kernels.item_ce_fwd_h(kernels.item_split_h(seq_s), kernels.item_split_h(W_s), tgt)
+    assert torch.allclose(lse.double(), torch.logsumexp(logits, 1), rtol=2e-6, atol=2e-5)
+    assert abs(loss.item() - F.cross_entropy(logits, tgt).item()) <= 2e-5
+
+
+def test_item_ce_f16_probs_slices_and_invalid_target(cuda):
+    from datamining_recblr_amd import kernels
+
+    seq, W, tgt = _data(50, 700, 64, cuda, seed=13)
+    ss, sw = kernels.item_split_h(seq), kernels.item_split_h(W)
+    _, lse = kernels.item_ce_fwd_h(ss, sw, tgt)
+    dl = torch.full((), 2.0, device=cuda)
+    full = kernels.item_ce_probs_h(ss, sw, tgt, lse, dl)
+    out = torch.full((50, 1000), 7.0, device=cuda)
+    part = kernels.item_ce_probs_h(ss, sw.rows(300, 600), tgt, lse, dl, item_offset=300,
+                                   out=out[:, 100:400])
+    assert torch.equal(part, full[:, 300:600])
+    assert (out[:, :100] == 7).all() and (out[:, 400:] == 7).all()
+    tgt[3] = 700
+    loss, _ = kernels.item_ce_fwd_h(ss, sw, tgt)
+    assert torch.isnan(loss)
+
+
+def test_item_ce_f16_engaged_in_training_loss(cuda):
+    """The model's CE (calculate_loss) runs the f16 kernels by default."""
+    from datamining_recblr_amd import kernels
+    from datamining_recblr_amd.distributed import synthetic_interaction
+    from datamining_recblr_amd.model import RecBLR
+    from datamining_recblr_amd.recbole_compat import SyntheticDataset
+
+    cfg = {"hidden_size": 64, "loss_type": "CE", "num_layers": 1, "dropout_prob": 0.0,
+           "expand": 2, "d_conv": 4, "bd_lru_only": False, "disable_conv1d": False,
+           "disable_ffn": False, "MAX_ITEM_LIST_LENGTH": 20}
+    model = RecBLR(cfg, SyntheticDataset(500)).to(cuda)
+    inter = synthetic_interaction(16, 20, 500, cuda, seed=3)
+    with kernels.kernel_timing() as t:
+        model.calculate_loss(inter).backward()
+    names = {r[0] for r in t.records}
+    assert {"rb_item_split_h", "rb_item_ce_fwd_h", "rb_item_ce_probs_h"} <= names, names
