@@ -41,9 +41,17 @@ __device__ __forceinline__ float dsilu_f(float x) {
 // 1 - alpha^2 with alpha -> 0.999, depends on alpha's absolute error (~ulp(1))
 // exactly as it does with expf.
 constexpr float kLog2e = 1.4426950408889634f;
+#ifdef RB_ABL_CHEAP_MATH
+// timing ablation only (tools/kbench.hip; wrong results): the transcendentals
+// as one full-rate op each
+__device__ __forceinline__ float fexp(float x) { return x * kLog2e; }
+__device__ __forceinline__ float frcp(float x) { return 1.5f - x; }
+__device__ __forceinline__ float fsqrt(float x) { return 0.5f * x; }
+#else
 __device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+#endif
 __device__ __forceinline__ float fsigm(float x) { return frcp(1.0f + fexp(-x)); }
 __device__ __forceinline__ float fsilu(float x) { return x * fsigm(x); }
 __device__ __forceinline__ float fdsilu(float x) {

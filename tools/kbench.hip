@@ -17,6 +17,7 @@
 #include "../datamining_recblr_amd/csrc/gemm_split.hip"
 #include "../datamining_recblr_amd/csrc/gemm_half.hip"
 #include "../datamining_recblr_amd/csrc/pack.hip"
+#include "../datamining_recblr_amd/csrc/probe.hip"
 
 #include <algorithm>
 #include <cstdio>
