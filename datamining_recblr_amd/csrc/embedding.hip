@@ -10,7 +10,8 @@
 //   2. seg[v] = lower_bound(sorted keys, v) for v in [0, V];
 //   3. every key's run is cut into chunks of kChunk rows (long runs of very
 //      popular items are spread over many waves); chunk offsets by a scan;
-//   4. one wave per chunk sums its rows in position order; single-chunk keys
+//   4. one wave per chunk sums its rows in a fixed order (its key and rows
+//      from a chunk descriptor planned with the sort); single-chunk keys
 //      write dW directly, the rest write a partial;
 //   5. one wave per multi-chunk key adds its partials in chunk order.
 // Every sum has a fixed order, so the result is bitwise reproducible, and no
@@ -115,6 +116,74 @@ k_emb_chunk_sum(const int* __restrict__ vals, const int* __restrict__ seg,
   }
 }
 
+// desc[c] = {key, first row, end row, single-chunk key} of chunk c, planned
+// on the side stream with the sort: the apply kernel needs one 16-B load to
+// place its chunk (instead of a 14-step dependent binary search over choff)
+__global__ void k_emb_chunk_desc(const int* __restrict__ seg, const int* __restrict__ nch,
+                                 const int* __restrict__ choff, int V, int4* __restrict__ desc) {
+  for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < V; v += gridDim.x * blockDim.x) {
+    const int n = nch[v], o = choff[v], s0 = seg[v], s1 = seg[v + 1];
+    for (int i = 0; i < n; ++i)
+      desc[o + i] = make_int4(v, s0 + i * kChunk, min(s1, s0 + (i + 1) * kChunk), n == 1);
+  }
+}
+
+// The apply kernel for 16-B aligned rows (d % 4 == 0): one wave per chunk of
+// <= 64 rows.  Three dependent steps only: the chunk descriptor, the chunk's
+// row ids (one per lane, one load), then every row of the chunk at once — the
+// two half-waves take alternate rows (512 B of a row per instruction, 16 B
+// per lane), 16 rows per half-wave in flight.  Each half sums its rows in
+// position order and the halves are added (even rows + odd rows): a fixed
+// order, bitwise reproducible.
+template <int NV4>
+__global__ void __launch_bounds__(256)
+k_emb_chunk_sum4(const int* __restrict__ vals, const int* __restrict__ choff,
+                 const int4* __restrict__ desc, const float* __restrict__ grad, int d, int V,
+                 int padding_idx, float* __restrict__ dw, float* __restrict__ partial) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int hw = lane >> 5, l32 = lane & 31;
+  const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int total = choff[V];
+  const int4 dc = desc[c < total ? c : 0];
+  if (c >= total || dc.x == padding_idx) return;   // the padding row: zeroed by k_emb_finish
+  const int beg = dc.y, n = dc.z - dc.y;
+  const int pv = lane < n ? vals[beg + lane] : 0;
+  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float4 acc[NV4];
+#pragma unroll
+  for (int k = 0; k < NV4; ++k) acc[k] = zero;
+  for (int r0 = 0; r0 < n; r0 += 32) {
+    float4 x[16][NV4];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int r = r0 + 2 * u + hw;
+      const int p = __shfl(pv, r & 63);
+#pragma unroll
+      for (int k = 0; k < NV4; ++k) {
+        const int col = 4 * (l32 + 32 * k);
+        x[u][k] = (r < n && col < d) ? *reinterpret_cast<const float4*>(grad + (int64_t)p * d + col)
+                                     : zero;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+#pragma unroll
+      for (int k = 0; k < NV4; ++k) {
+        acc[k].x += x[u][k].x; acc[k].y += x[u][k].y;
+        acc[k].z += x[u][k].z; acc[k].w += x[u][k].w;
+      }
+  }
+  float* out = dc.w ? dw + (int64_t)dc.x * d : partial + c * d;
+#pragma unroll
+  for (int k = 0; k < NV4; ++k) {
+    float4 t = acc[k];
+    t.x += __shfl_xor(t.x, 32); t.y += __shfl_xor(t.y, 32);
+    t.z += __shfl_xor(t.z, 32); t.w += __shfl_xor(t.w, 32);
+    const int col = 4 * (l32 + 32 * k);
+    if (hw == 0 && col < d) *reinterpret_cast<float4*>(out + col) = t;
+  }
+}
+
 // One 4-wave block per key: keys with no rows (and the padding id) get zeros;
 // multi-chunk keys sum their partials, wave w taking chunks w, w+4, ... and
 // the four wave sums combined in a fixed order (bitwise reproducible).
@@ -155,7 +224,7 @@ int key_bits(int64_t V) {
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct EmbWs {
-  size_t keys_in, keys_out, vals_in, vals_out, seg, nch, choff, partial, sort_tmp, scan_tmp;
+  size_t keys_in, keys_out, vals_in, vals_out, seg, nch, choff, desc, partial, sort_tmp, scan_tmp;
   size_t sort_bytes, scan_bytes, total;
 };
 
@@ -171,6 +240,7 @@ EmbWs emb_layout(int64_t M, int64_t V, int64_t d) {
   w.nch = take((V + 1) * 4);
   w.choff = take((V + 1) * 4);
   const int64_t max_chunks = M / kChunk + V + 1;
+  w.desc = take((size_t)max_chunks * 16);
   w.partial = take((size_t)max_chunks * d * 4);
   w.sort_bytes = 0;
   rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (const int*)nullptr, (int*)nullptr,
@@ -192,10 +262,23 @@ int emb_sums(const EmbWs& w, char* ws, const float* grad, int64_t M, int64_t d, 
   const int* nch = reinterpret_cast<const int*>(ws + w.nch);
   const int* choff = reinterpret_cast<const int*>(ws + w.choff);
   float* partial = reinterpret_cast<float*>(ws + w.partial);
+  const int4* desc = reinterpret_cast<const int4*>(ws + w.desc);
   const int64_t max_chunks = M / kChunk + V + 1;
-  hipLaunchKernelGGL((k_emb_chunk_sum<NV>), dim3((unsigned)((max_chunks + 3) / 4)), dim3(256), 0,
-                     st, vals, seg, nch, choff, grad, (int)d, (int)V, (int)padding_idx, dw,
-                     partial);
+  const unsigned cblocks = (unsigned)((max_chunks + 3) / 4);
+  if (d % 4 == 0 && aligned16(grad) && aligned16(dw)) {
+    if (d <= 128)
+      hipLaunchKernelGGL((k_emb_chunk_sum4<1>), dim3(cblocks), dim3(256), 0, st, vals, choff, desc,
+                         grad, (int)d, (int)V, (int)padding_idx, dw, partial);
+    else if (d <= 256)
+      hipLaunchKernelGGL((k_emb_chunk_sum4<2>), dim3(cblocks), dim3(256), 0, st, vals, choff, desc,
+                         grad, (int)d, (int)V, (int)padding_idx, dw, partial);
+    else
+      hipLaunchKernelGGL((k_emb_chunk_sum4<4>), dim3(cblocks), dim3(256), 0, st, vals, choff, desc,
+                         grad, (int)d, (int)V, (int)padding_idx, dw, partial);
+  } else {
+    hipLaunchKernelGGL((k_emb_chunk_sum<NV>), dim3(cblocks), dim3(256), 0, st, vals, seg, nch,
+                       choff, grad, (int)d, (int)V, (int)padding_idx, dw, partial);
+  }
   hipLaunchKernelGGL((k_emb_finish<NV>), dim3((unsigned)V), dim3(256), 0, st, nch,
                      choff, partial, (int)d, (int)V, (int)padding_idx, dw);
   return launch_status("rb_embedding_bwd");
@@ -233,6 +316,8 @@ int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, v
   if (rocprim::exclusive_scan(ws + w.scan_tmp, scb, nch, choff, 0, (size_t)(V + 1),
                               rocprim::plus<int>(), st) != hipSuccess)
     return fail("rb_embedding_bwd: scan failed");
+  hipLaunchKernelGGL(k_emb_chunk_desc, dim3(vb), dim3(256), 0, st, seg, nch, choff, (int)V,
+                     reinterpret_cast<int4*>(ws + w.desc));
   return launch_status("rb_embedding_plan");
 }
 
