@@ -30,7 +30,16 @@ __device__ __forceinline__ float row_sum(float v) {
   return v;
 }
 
-constexpr int kRowBlocks = 1024;   // 4 waves each; grid-stride over rows
+// 4 waves each; grid-stride over rows.  The backward kernels' grid is also
+// their partial count (dgamma/dbeta/dbias rows); the forward kernels take
+// 4x the blocks (more rows in flight: add_ln_fwd 0.67 -> 0.69, silu fwd
+// 0.67 -> 0.70 of HBM; the same for the backward kernels lost 1-2% to
+// the larger partial sums; tools/ab_bench.sh, profiles/r02_ab_row_blocks.log)
+#ifndef RB_ROW_BLOCKS
+#define RB_ROW_BLOCKS 1024
+#endif
+constexpr int kRowBlocks = RB_ROW_BLOCKS;
+constexpr int kRowBlocksFwd = 4 * RB_ROW_BLOCKS;
 
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
@@ -336,17 +345,18 @@ __global__ void k_dropout_mask(DropSpec drop, uint8_t* __restrict__ out, int64_t
   }
 }
 
-template <int LPR>
+template <int LPR, int MAXB = kRowBlocks>
 int64_t row_blocks(int64_t rows) {
   constexpr int RPB = 4 * (kWave / LPR);
-  return std::max<int64_t>(1, std::min<int64_t>(kRowBlocks, (rows + RPB - 1) / RPB));
+  return std::max<int64_t>(1, std::min<int64_t>(MAXB, (rows + RPB - 1) / RPB));
 }
 
 template <int NV, int LPR>
 int add_ln_fwd_t(const float* a, const int64_t* idx, int64_t nidx, const DropSpec& drop,
                  const float* r, const float* gamma, const float* beta, float eps, float* y,
                  float* s_out, float* mean, float* rstd, int64_t rows, hipStream_t st) {
-  hipLaunchKernelGGL((k_add_ln_fwd<NV, LPR>), dim3((unsigned)row_blocks<LPR>(rows)), dim3(256), 0,
+  hipLaunchKernelGGL((k_add_ln_fwd<NV, LPR>), dim3((unsigned)row_blocks<LPR, kRowBlocksFwd>(rows)),
+                     dim3(256), 0,
                      st, a, idx, nidx, drop, r, gamma, beta, eps, y, s_out, mean, rstd, rows);
   return launch_status("rb_add_ln_fwd");
 }
@@ -364,7 +374,8 @@ int add_ln_bwd_t(const float* dy, const float* dy2, const float* s, const float*
 template <int NV, int LPR>
 int silu_fwd_t(const float* a, const float* bias, const DropSpec& drop, float* u, int64_t rows,
                hipStream_t st) {
-  hipLaunchKernelGGL((k_silu_dropout_fwd<NV, LPR>), dim3((unsigned)(2 * row_blocks<LPR>(rows))),
+  hipLaunchKernelGGL((k_silu_dropout_fwd<NV, LPR>),
+                     dim3((unsigned)(row_blocks<LPR, 2 * kRowBlocksFwd>(rows))),
                      dim3(256), 0, st, a, bias, drop, u, rows);
   return launch_status("rb_silu_dropout_fwd");
 }
