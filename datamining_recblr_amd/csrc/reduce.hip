@@ -6,7 +6,8 @@
 // these shapes costs a hipMemset of a semaphore buffer plus a reduction
 // launch, and fixes the summation order independently of the device:
 //   out[m, c] = ((S_0 + S_1) + ...) + S_{RG-1},  S_g = sum_{p = g, g+RG, ...} in[m, p, c]
-// with RG = 4 (P <= 256) or 16 row groups, each S_g summed in increasing p.
+// with RG = 4 (P <= 256) or 16 row groups, each S_g summed in increasing p
+// (16 for the wide weight-gradient partials, read four columns per thread).
 #include "common.h"
 
 namespace rb {
@@ -41,10 +42,56 @@ __global__ __launch_bounds__(64 * RG) void k_colsum(const float* __restrict__ in
   }
 }
 
+// The same sums, four adjacent columns per thread (16-B loads; C, rs, ms
+// multiples of 4 and 16-B aligned operands): per column the identical order,
+// so the results are bitwise those of k_colsum.
+template <int RG>
+__global__ __launch_bounds__(64 * RG) void k_colsum4(const float* __restrict__ in, int64_t P,
+                                                     int64_t C, int64_t rs, int64_t ms,
+                                                     int64_t cblocks, float* __restrict__ out) {
+  __shared__ float4 red[RG][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t m = blockIdx.x / cblocks;
+  const int64_t c = ((blockIdx.x - m * cblocks) * 64 + tx) * 4;
+  const float* base = in + m * ms + c;
+  float4 s = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  auto add = [](float4& acc, const float4& v) {
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  };
+  if (c < C) {
+    int64_t p = ty;
+    for (; p + 3 * RG < P; p += 4 * RG) {
+      const float4 a = *reinterpret_cast<const float4*>(base + p * rs);
+      const float4 b = *reinterpret_cast<const float4*>(base + (p + RG) * rs);
+      const float4 d = *reinterpret_cast<const float4*>(base + (p + 2 * RG) * rs);
+      const float4 e = *reinterpret_cast<const float4*>(base + (p + 3 * RG) * rs);
+      add(s, a); add(s, b); add(s, d); add(s, e);
+    }
+    for (; p < P; p += RG) add(s, *reinterpret_cast<const float4*>(base + p * rs));
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    float4 t = red[0][tx];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) add(t, red[g][tx]);
+    *reinterpret_cast<float4*>(out + m * C + c) = t;
+  }
+}
+
 }  // namespace
 
 int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
                   float* out, hipStream_t st) {
+  // wide partials (the weight gradients' [S, N*K] row-chunk sums): 16-B
+  // loads, 16 row groups (64 KB in flight per CU)
+  if (C >= 8192 && P >= 64 && C % 4 == 0 && rs % 4 == 0 && ms % 4 == 0 && aligned16(in) &&
+      aligned16(out)) {
+    const int64_t cb4 = (C / 4 + 63) / 64;
+    hipLaunchKernelGGL(k_colsum4<16>, dim3((unsigned)(M * cb4)), dim3(1024), 0, st, in, P, C, rs,
+                       ms, cb4, out);
+    return launch_status("rb_colsum");
+  }
   const int64_t cblocks = (C + 63) / 64;
   const unsigned grid = (unsigned)(M * cblocks);
   if (P <= 256)

@@ -267,7 +267,8 @@ def test_pad_prefix_kernels_match_torch(cuda, H, pads):
         assert err < 2e-5, (n, err.item())
 
 
-@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 131072), (1024, 128), (300, 65),
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3), (64, 131072), (128, 65536), (512, 16384),
+                                   (1024, 128), (300, 65),
                                    (3, 2048, 256), (2048, 1024), (2048, 256), (2000, 256)])
 def test_colsum_fixed_order(cuda, shape):
     from datamining_recblr_amd import kernels
@@ -280,11 +281,12 @@ def test_colsum_fixed_order(cuda, shape):
     close(out, ref, atol=1e-5, rtol=1e-5, what="colsum")
     assert torch.equal(out, kernels.colsum(x))
     # restated order: RG interleaved partials in increasing p, combined in order
-    # (RG = 4 for P <= 256, else 16); few columns with many rows: 64-row
-    # chunk sums first, then the chunk sums (kernels.colsum)
+    # (RG = 4 for P <= 256, else 16; 16 for wide partials, C >= 8192 and
+    # P >= 64); few columns with many rows: 64-row chunk sums first, then the
+    # chunk sums (kernels.colsum)
     def one_pass(xs):
-        P = xs.shape[1]
-        RG = 4 if P <= 256 else 16
+        P, C = xs.shape[1], xs.shape[2]
+        RG = 16 if (C >= 8192 and P >= 64 and C % 4 == 0) else (4 if P <= 256 else 16)
         parts = [torch.zeros(xs.shape[0], xs.shape[2]) for _ in range(RG)]
         for p in range(P):
             parts[p % RG] = parts[p % RG] + xs[:, p]
