@@ -441,7 +441,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         quad_transpose(v, lane);
         f32x4* o = (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane);
         if (pend_full || pend_r0 + 8 * g + 4 * (lane >> 5) + (lane & 3) < M)
+#ifdef HN_PLAIN_STORE
+          *o = f32x4{v[0], v[1], v[2], v[3]};
+#else
           __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, o);
+#endif
       }
     } else {
 #pragma unroll
