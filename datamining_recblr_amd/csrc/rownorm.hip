@@ -6,9 +6,8 @@
 //   s = A[row] * keep * scale + r[row]      (A[row] = table[idx[row]] if idx)
 //   y = (s - mean) * rstd * gamma + beta,   rstd = 1 / sqrt(var + eps)
 //
-// The LayerNorm kernels keep the default cache policy (ldc/stc): their rows
-// are re-read at once by the next GEMM, and measured in the training step nt
-// accesses cost them 0.69 -> 0.63 of HBM; the SiLU kernels stream (ldv/stv).
+// The LayerNorm kernels load with the default cache policy (ldc) and store
+// per direction (st_ln below); the SiLU kernels stream (ldv/stv).
 //
 // Rows of D floats are spread over LPR lanes holding NV float4s each
 // (LPR * NV * 4 = D), so one wave covers 64/LPR rows per step; row statistics
@@ -22,6 +21,24 @@
 
 namespace rb {
 namespace {
+
+// Store policy of the LayerNorm outputs: the forward's (y, s) nontemporal
+// (its consumers, the in-projection GEMM and through it the conv, read
+// faster: conv forward 0.65 -> 0.69), the backward's (ds, da) default (nt
+// cost the backward kernel 0.68 -> 0.61); tools/ab_bench.sh,
+// profiles/r02_ab_ln_store_policy.log.  RB_LN_NT / RB_LN_PLAIN: all nt /
+// all default, for A/B.
+#if defined(RB_LN_NT)
+constexpr bool kLnFwdNT = true, kLnBwdNT = true;
+#elif defined(RB_LN_PLAIN)
+constexpr bool kLnFwdNT = false, kLnBwdNT = false;
+#else
+constexpr bool kLnFwdNT = true, kLnBwdNT = false;
+#endif
+template <bool NT, int V>
+__device__ __forceinline__ void st_ln(float* p, const float (&o)[V]) {
+  if constexpr (NT) stv(p, o); else stc(p, o);
+}
 
 template <int LPR>
 __device__ __forceinline__ float row_sum(float v) {
@@ -105,8 +122,8 @@ k_add_ln_fwd(const float* __restrict__ a, const int64_t* __restrict__ idx, int64
         float o[4];
 #pragma unroll
         for (int v = 0; v < 4; ++v) o[v] = (s[k][v] - mu) * rs * gm[k][v] + bt[k][v];
-        stc(y + row * D + c, o);
-        if (s_out) stc(s_out + row * D + c, s[k]);
+        st_ln<kLnFwdNT>(y + row * D + c, o);
+        if (s_out) st_ln<kLnFwdNT>(s_out + row * D + c, s[k]);
       }
       if (l == 0) {
         if (mean_out) mean_out[row] = mu;
@@ -183,7 +200,7 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ dy2,
       float d[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) d[v] = ok ? rs * (g[k][v] - mg - xh[k][v] * mgx) : 0.0f;
-      if (ok && ds_out) stc(ds_out + row * D + c, d);
+      if (ok && ds_out) st_ln<kLnBwdNT>(ds_out + row * D + c, d);
       if (da_out || dbias_part) {
         float m[4];
         drop.get4(rr * D + c, m);
@@ -192,7 +209,7 @@ k_add_ln_bwd(const float* __restrict__ dy, const float* __restrict__ dy2,
           d[v] = d[v] * m[v];
           acca[k][v] += d[v];
         }
-        if (ok && da_out) stc(da_out + row * D + c, d);
+        if (ok && da_out) st_ln<kLnBwdNT>(da_out + row * D + c, d);
       }
     }
   }
