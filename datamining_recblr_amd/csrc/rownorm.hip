@@ -329,7 +329,11 @@ k_silu_dropout_bwd(const float* __restrict__ a, const float* __restrict__ bias, 
         o[v] = (g[v] * m[v]) * fdsilu(x[v] + bv[k][v]);
         acc[k][v] += o[v];
       }
+#ifdef RB_SILU_BWD_PLAIN
+      stc(da + e, o);
+#else
       stv(da + e, o);
+#endif
     }
   }
   if (dbias_part == nullptr) return;   // grid-uniform
