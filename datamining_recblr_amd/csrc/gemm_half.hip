@@ -340,13 +340,27 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       a_off[q] = (int)(r * lda * 4) + lc * 16;
     }
   };
+#ifdef HN_A_NT
+  // A/B: the A stream with the nontemporal hint when every A row is read
+  // once (a single column tile)
+  const bool a_nt = nct == 1;
+#else
+  constexpr bool a_nt = false;
+#endif
   auto issueA = [&]() {
     char* st = smem + a_slot * N_A_STAGE + wave * 4096;
     const char* b = a_base + a_kt * (N_BK * 4);
+    if (a_nt) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024), 16,
-                                       0, 0);
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024),
+                                         16, 0, 2);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024),
+                                         16, 0, 0);
+    }
     a_slot = a_slot + 1 == N_NSA ? 0 : a_slot + 1;
     if (++a_kt == KT) {
       a_kt = 0;
