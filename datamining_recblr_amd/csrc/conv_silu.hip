@@ -328,10 +328,20 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
       // weight's own [c, k] order, then dbias — one column sum gives both,
       // already in parameter layout
       float* row = dw_part + b * (K + 1) * H;
+      if constexpr (K == 4 && VEC == 4) {
+        // a lane's 4 channels x 4 taps are 16 consecutive floats: 16-B stores
+        // (the vector path checked dw_part's alignment; H % 4 == 0)
 #pragma unroll
-      for (int v = 0; v < VEC; ++v)
+        for (int v = 0; v < VEC; ++v) {
+          const float o[4] = {accw[0][v], accw[1][v], accw[2][v], accw[3][v]};
+          stv(row + (c0 + v) * K, o);
+        }
+      } else {
 #pragma unroll
-        for (int k = 0; k < K; ++k) row[(c0 + v) * K + k] = accw[k][v];
+        for (int v = 0; v < VEC; ++v)
+#pragma unroll
+          for (int k = 0; k < K; ++k) row[(c0 + v) * K + k] = accw[k][v];
+      }
       stv(row + K * H + c0, accb);
     } else {
 #pragma unroll
