@@ -970,84 +970,6 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     }
   };
 
-#ifdef HN_TN_INTERLEAVE
-  // Measured and dropped (tools/gemmbench_h.hip: 570-585 -> 673-690 us for
-  // the four dW shapes; 256 VGPRs): m-step t's MFMAs (buffer t & 1)
-  // interleaved with the conversion of step t + 1 into the other buffer (one
-  // column group after each 32 x 32 block's three products), then the load
-  // of step t + 3, one barrier per m-step.
-  auto mma_conv = [&](int buf, f32x4 (&r)[8], int tc, bool conv) {
-    const uint32_t iy = smem_base + buf * CF::STAGE;
-    const uint32_t ix = iy + 2 * CF::YPLANE;
-    const int cb = buf ^ 1;
-    const uint32_t img = smem_base + cb * CF::STAGE + (op == 0 ? 0 : 2 * CF::YPLANE);
-    const uint32_t plane = op == 0 ? CF::YPLANE : CF::XPLANE;
-    conv = conv && loader;
-    if (conv) {
-      const int64_t row0 = r_begin + (int64_t)tc * 32 + rg * 8;
-      if (row0 + 8 > r_end) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (row0 + q >= r_end) r[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      }
-    }
-    auto conv_col = [&](int c) {
-      f16x8 h0, h1;
-#pragma unroll
-      for (int q = 0; q < 8; q += 2) {
-        f16x2 p0, p1;
-        split2h(f32x2{r[q][c], r[q + 1][c]} * sc, p0, p1);
-        h0[q] = p0[0]; h0[q + 1] = p0[1];
-        h1[q] = p1[0]; h1[q + 1] = p1[1];
-      }
-      const uint32_t off = tn_off(4 * cc + c, rg);
-      hds_write16(img + off, h0);
-      hds_write16(img + plane + off, h1);
-    };
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      f16x8 a[2][2], b[2][2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint32_t oa = tn_off(64 * wm + 32 * i + (lane & 31), 2 * st + h);
-        const uint32_t ob = tn_off(64 * wk + 32 * i + (lane & 31), 2 * st + h);
-        a[i][0] = hds_read16<f16x8>(iy + oa);
-        a[i][1] = hds_read16<f16x8>(iy + CF::YPLANE + oa);
-        b[i][0] = hds_read16<f16x8>(ix + ob);
-        b[i][1] = hds_read16<f16x8>(ix + CF::XPLANE + ob);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0][0]),
-                     "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]));
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mfma_h(a[i][1], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_h(a[i][0], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_h(a[i][0], b[j][0], acc[i][j]);
-          if (st == 0 && conv) conv_col(2 * i + j);
-        }
-    }
-  };
-  if (T > 0) load(0, raw0);
-  if (T > 1) load(1, raw1);
-  if (T > 0) {
-    convert(raw0, 0, 0);
-    if (T > 2) load(2, raw0);
-  }
-  __syncthreads();
-  for (int t = 0; t < T; t += 2) {
-    mma_conv(0, raw1, t + 1, t + 1 < T);
-    if (t + 3 < T) load(t + 3, raw1);
-    __syncthreads();
-    if (t + 1 < T) {
-      mma_conv(1, raw0, t + 2, t + 2 < T);
-      if (t + 4 < T) load(t + 4, raw0);
-      __syncthreads();
-    }
-  }
-#else
   if (T > 0) load(0, raw0);
   if (T > 1) load(1, raw1);
   for (int t = 0; t < T; t += 2) {
@@ -1062,7 +984,6 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
       mma(1);
     }
   }
-#endif
 
   // un-scale and store the partial tile (every split writes its slot, empty
   // chunks zeros)
