@@ -275,6 +275,64 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
                                     "kernels": kern}}
 
 
+def gemm_pattern(args, batch, dev, rounds=7):
+    """Each projection GEMM shape beside its streaming floor: the f16x3 NT
+    GEMM (linear.mm_nt at the batch's packed row count) alternated on this
+    lease with rb_probe_gemm_pattern, which reads the same A rows once and
+    writes the same outputs with trivial arithmetic (16-B accesses, the
+    epilogue's nontemporal stores).  Median per launch; kernel_over_pattern
+    is the GEMM's time in units of that floor."""
+    from datamining_recblr_amd import _lib, linear
+    from datamining_recblr_amd.kernels import _stream
+    d, H = args.hidden, 2 * args.hidden
+    M = int(batch["item_length"].sum())
+    shapes = {"in.fwd": (d, 2 * H), "in.dX": (2 * H, d), "gates.fwd": (H, 2 * H),
+              "gates.dX": (2 * H, H), "out.fwd": (H, d), "out.dX": (d, H),
+              "w2.fwd": (4 * d, d), "w2.dX": (d, 4 * d)}
+    g = torch.Generator(device=dev).manual_seed(6)
+    rmax_r = max(r for r, _ in shapes.values())
+    rmax_c = max(c for _, c in shapes.values())
+    a_all = torch.randn(M, rmax_r, device=dev, generator=g)
+    out = torch.empty(M, rmax_c, device=dev)
+    res, tot_k, tot_p = {}, 0.0, 0.0
+    for name, (R, C) in shapes.items():
+        a = a_all[:, :R].contiguous()
+        w = torch.randn(C, R, device=dev, generator=g) * R ** -0.5
+        o = out[:, :C]
+        st = _stream(a)
+
+        def real():
+            linear.mm_nt(a, w)
+
+        def pattern():
+            _lib.call("rb_probe_gemm_pattern", a.data_ptr(), M, R, o.data_ptr(), C, st)
+
+        real(), pattern()
+        torch.cuda.synchronize()
+        ts = {"kernel": [], "pattern": []}
+        for _ in range(rounds):
+            for key, fn in (("kernel", real), ("pattern", pattern)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn()
+                e1.record()
+                e1.synchronize()
+                ts[key].append(e0.elapsed_time(e1) * 1e3)
+        ku = sorted(ts["kernel"])[rounds // 2]
+        pu = sorted(ts["pattern"])[rounds // 2]
+        tot_k, tot_p = tot_k + ku, tot_p + pu
+        gbs = M * (R + C) * 4 / (pu * 1e-6) / 1e9
+        res[name] = {"R": R, "C": C, "kernel_us": round(ku, 1), "pattern_us": round(pu, 1),
+                     "pattern_frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "kernel_over_pattern": round(ku / pu, 3)}
+        del a, w
+    return {"rows": M, "shapes": res, "kernel_us": round(tot_k, 1), "pattern_us": round(tot_p, 1),
+            "kernel_over_pattern": round(tot_k / tot_p, 3),
+            "note": "linear.mm_nt (rb_gemm_nt_h) vs rb_probe_gemm_pattern (the same A reads and "
+                    "output writes, trivial math), alternated on this lease; a ratio of 1 would "
+                    "be a GEMM at the streaming floor of its own bytes"}
+
+
 def gate_bwd_pattern(args, batch, dev, rounds=15):
     """The dominant kernel beside a trivial-math kernel with its exact memory
     access pattern (rb_probe_gate_bwd_pattern: the same 5 reads + 4 writes
@@ -625,6 +683,8 @@ def main():
 
     if roofline is not None and env.rank == 0 and args.hidden * 2 % 4 == 0:
         roofline["pattern"] = gate_bwd_pattern(args, batches[0], dev)
+    if gemm is not None and env.rank == 0 and fmt == "f16x3":
+        gemm["pattern"] = gemm_pattern(args, batches[0], dev)
     ddp_ab = None
     if env.world_size == 1 and not args.no_ddp_ab:
         ddp_ab = ddp_overhead(args, model, batches, dev)

@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 24
+ABI_VERSION = 25
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -50,6 +50,7 @@ SIGNATURES = {
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
                                         _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
                                         _fp, _fp]),
+    "rb_probe_gemm_pattern": (ctypes.c_int, [_fp, _i64, _i64, _fp, _i64, _fp]),
     "rb_probe_gate_bwd_pattern": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64,
                                                  _fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp,
                                                  _fp]),

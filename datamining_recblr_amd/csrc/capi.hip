@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 24; }
+int rb_version(void) { return 25; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -175,6 +175,16 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
   return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, carries, dy, drg, drg_rs, dxc,
                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H,
                          seq_offsets, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_probe_gemm_pattern(const float* a, int64_t M, int64_t R, float* out, int64_t C,
+                          void* stream) {
+  if (!a || !out) return fail("rb_probe_gemm_pattern: null pointer");
+  if (M <= 0 || R <= 0 || C <= 0 || R % 4 || C % 4 || R > (1 << 20) || C > (1 << 20))
+    return fail("rb_probe_gemm_pattern: M, R, C must be positive, R and C multiples of 4");
+  if (!aligned16(a) || !aligned16(out))
+    return fail("rb_probe_gemm_pattern: operands must be 16-B aligned");
+  return launch_probe_gemm_pattern(a, M, R, out, C, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_probe_gate_bwd_pattern(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,

@@ -297,6 +297,8 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
                     int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
                     float* y_last = nullptr);
+int launch_probe_gemm_pattern(const float* A, int64_t M, int64_t R, float* out, int64_t C,
+                              hipStream_t st);
 int launch_probe_gate_bwd_pattern(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                                   const float* z, int64_t z_rs, const float* dy, float* drg,
                                   int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz,

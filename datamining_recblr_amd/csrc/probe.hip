@@ -96,4 +96,41 @@ int launch_probe_gate_bwd_pattern(const float* rg, int64_t rg_rs, const float* x
   return launch_status("rb_probe_gate_bwd_pattern");
 }
 
+// k_probe_gemm_pattern: the f16x3 NT GEMM's HBM bytes without the GEMM —
+// each row of A [M, R] read once (16-B loads), C outputs of that row written
+// (16-B nontemporal stores, the GEMM epilogue's policy); 8 lanes per row, a
+// wave 8 rows.  Its time is the streaming floor bench.py sets beside each
+// projection GEMM (gemm.pattern; tools/gemm_pattern.hip is the standalone
+// sweep).
+__global__ void __launch_bounds__(256)
+k_probe_gemm_pattern(const float* __restrict__ A, int64_t M, int R, float* __restrict__ out,
+                     int C) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t wrow = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8;
+  if (wrow >= M) return;
+  const int64_t row = wrow + (lane >> 3);
+  const int64_t r = row < M ? row : M - 1;
+  const rb_f32x4* a = reinterpret_cast<const rb_f32x4*>(A + r * R);
+  rb_f32x4 s = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int j = lane & 7; j < R / 4; j += 8) s += __builtin_nontemporal_load(a + j);
+  float t = s[0] + s[1] + s[2] + s[3];
+  t += __shfl_xor(t, 1);
+  t += __shfl_xor(t, 2);
+  t += __shfl_xor(t, 4);
+  if (row >= M) return;
+  rb_f32x4* o = reinterpret_cast<rb_f32x4*>(out + row * C);
+  for (int j = lane & 7; j < C / 4; j += 8)
+    __builtin_nontemporal_store(rb_f32x4{t, t + 1.0f, t + 2.0f, t + 3.0f}, o + j);
+}
+
+}  // namespace rb
+
+namespace rb {
+int launch_probe_gemm_pattern(const float* A, int64_t M, int64_t R, float* out, int64_t C,
+                              hipStream_t st) {
+  const int64_t blocks = (M + 31) / 32;
+  hipLaunchKernelGGL(k_probe_gemm_pattern, dim3((unsigned)blocks), dim3(256), 0, st, A, M, (int)R,
+                     out, (int)C);
+  return launch_status("rb_probe_gemm_pattern");
+}
 }  // namespace rb

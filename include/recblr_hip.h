@@ -480,6 +480,13 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
                  int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
                  void* stream);
 
+/* Measurement aid (bench.py gemm.pattern; not on the model's path): the HBM
+ * bytes of out[M, C] = a[M, R] W^T without the product — every row of a
+ * (contiguous, R % 4 == 0) read once, C floats per row written (C % 4 == 0),
+ * 16-B accesses, both 16-B aligned.  Replaces no reference interface. */
+int rb_probe_gemm_pattern(const float* a, int64_t M, int64_t R, float* out, int64_t C,
+                          void* stream);
+
 /* Measurement aid (bench.py, not the model's path; no reference counterpart):
  * the memory access pattern of rb_gate_scan_bwd (fp32) — the same reads of
  * r, i, xc, z, dy and writes of dr, di, dxc, dz with the same row strides,
