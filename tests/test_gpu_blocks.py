@@ -556,3 +556,21 @@ def test_gate_bwd_pattern_probe_covers_every_element(cuda):
     assert torch.equal(dz[:ntok], z * dy)
     assert torch.isnan(drg[ntok:]).all() and torch.isnan(dxc[ntok:]).all()
     assert torch.isnan(dxz[:, :H]).all() and torch.isnan(dxz[ntok:]).all()
+
+
+@pytest.mark.parametrize("M,R,C", [(1, 128, 512), (37, 512, 128), (1000, 256, 256)])
+def test_gemm_pattern_probe_covers_every_output(cuda, M, R, C):
+    """rb_probe_gemm_pattern (bench.py gemm.pattern) reads every A row and
+    writes every output of the GEMM it stands in for (out[m, 4j + i] =
+    rowsum(a[m]) + i), nothing past M rows."""
+    from datamining_recblr_amd import _lib
+    from datamining_recblr_amd.kernels import _stream
+
+    g = torch.Generator().manual_seed(M + R)
+    a = torch.randn(M, R, generator=g).to(cuda)
+    out = torch.full((M + 3, C), float("nan"), device=cuda)
+    _lib.call("rb_probe_gemm_pattern", a.data_ptr(), M, R, out.data_ptr(), C, _stream(a))
+    torch.cuda.synchronize()
+    ref = a.double().sum(1, keepdim=True) + (torch.arange(C, device=cuda) % 4).double()[None]
+    assert torch.allclose(out[:M].double(), ref, atol=1e-3, rtol=1e-5)
+    assert torch.isnan(out[M:]).all()
