@@ -18,14 +18,82 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_plan(gpus: int, environ: dict, argv: list, visible_gpus: int | None,
+                dry_run: bool = False):
+    """What `bench.py --gpus N` must do before anything touches a GPU.
+
+    Returns ("run", None) when this process is a rank of the right world (N = 1
+    and no WORLD_SIZE, or WORLD_SIZE == N from torchrun / the self-launch);
+    ("launch", cmd) when N > 1 and no WORLD_SIZE is set: cmd starts N rank
+    processes (torch.distributed.run, one per GPU, rendezvous on 127.0.0.1)
+    as a child of this process; ("error", message) for a world size that
+    disagrees with --gpus or more ranks than visible GPUs (never warn and
+    run a different world)."""
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", f"--gpus {gpus} but WORLD_SIZE={ws}: the launch disagrees with the request"
+        return "run", None
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1, got {gpus}"
+    if gpus == 1:
+        return "run", None
+    if not dry_run and (visible_gpus or 0) < gpus:
+        return "error", f"--gpus {gpus} but only {visible_gpus or 0} GPU(s) visible"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    return "launch", cmd
+
+
+def _gpus_arg(argv) -> tuple[int, bool]:
+    ap = argparse.ArgumentParser(add_help=False)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", action="store_true")
+    ns, _ = ap.parse_known_args(argv)
+    return ns.gpus, ns.dry_run
+
+
+def _launch_or_check() -> None:
+    """Run before any GPU call: self-launch N ranks when --gpus N > 1 came
+    without torchrun's env, exit non-zero on a world-size mismatch."""
+    gpus, dry = _gpus_arg(sys.argv[1:])
+    visible = None
+    if "WORLD_SIZE" not in os.environ and gpus > 1 and not dry:
+        import torch   # device_count() does not initialise the GPU on this image
+        visible = torch.cuda.device_count()
+    what, detail = launch_plan(gpus, os.environ, sys.argv[1:], visible, dry)
+    if what == "error":
+        print(f"bench.py: {detail}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if what == "launch":
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+            "HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+        sys.exit(subprocess.call(detail, env=env))
+
+
+if __name__ == "__main__":
+    _launch_or_check()
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
 
 from datamining_recblr_amd import kernels  # noqa: E402
 from datamining_recblr_amd.distributed import (barrier, init_from_env, max_over_ranks,  # noqa: E402
@@ -444,6 +512,65 @@ def ddp_overhead(args, model, batches, dev, rounds=3):
                     f"{rounds}x{args.steps} steps, best of each"}
 
 
+def dry_run_ranks(args):
+    """--dry-run: the launch plumbing without a GPU.  Every rank joins a gloo
+    group from the env torchrun (or the self-launch) set, all-gathers what it
+    sees, and rank 0 prints one JSON line; the world must equal --gpus."""
+    env = init_from_env(backend="gloo")
+    mine = torch.tensor([env.rank, env.local_rank, env.world_size], dtype=torch.int64)
+    if env.distributed:
+        got = [torch.empty_like(mine) for _ in range(env.world_size)]
+        dist.all_gather(got, mine)
+    else:
+        got = [mine]
+    ranks = [dict(zip(("rank", "local_rank", "world_size"), t.tolist())) for t in got]
+    ok = env.world_size == args.gpus and sorted(r["rank"] for r in ranks) == list(range(args.gpus))
+    if env.rank == 0:
+        print(json.dumps({"dry_run": True, "gpus": args.gpus, "world_size": env.world_size,
+                          "ranks": ranks, "ok": ok}), flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ok:
+        raise SystemExit(3)
+
+
+def allreduce_probe(model, env, dev, reps=20):
+    """The gradient exchange alone: one all-reduce (RCCL) of a flat fp32
+    buffer the size of all parameters, median of `reps` after 3 warm-ups,
+    max over ranks; bus bandwidth as nccl-tests defines it for all-reduce
+    (2 (N-1)/N x bytes / time)."""
+    n = sum(p.numel() for p in model.parameters())
+    buf = torch.ones(n, device=dev)
+    for _ in range(3):
+        dist.all_reduce(buf)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        barrier(env)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dist.all_reduce(buf)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    us = max_over_ranks(sorted(ts)[reps // 2], env, dev) * 1e6
+    nbytes = 4 * n
+    busbw = 2 * (env.world_size - 1) / env.world_size * nbytes / (us * 1e-6) / 1e9
+    return {"bytes": nbytes, "us": round(us, 1), "busbw_gbs": round(busbw, 1),
+            "note": "one dist.all_reduce of a flat fp32 buffer of every parameter (RCCL), median "
+                    "of 20, max over ranks; in the step DDP buckets it and overlaps it with the "
+                    "backward"}
+
+
+def per_rank_ms(ms: float, env, dev) -> list:
+    t = torch.tensor([ms], dtype=torch.float64, device=dev)
+    if not env.distributed:
+        return [round(ms, 3)]
+    got = [torch.empty_like(t) for _ in range(env.world_size)]
+    dist.all_gather(got, t)
+    return [round(float(x.item()), 3) for x in got]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -470,11 +597,20 @@ def main():
     ap.add_argument("--no-full-tail", action="store_true",
                     help="skip the comparison run that evaluates the last layer's "
                          "position-wise tail at every position")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch and rendezvous only: every rank joins a gloo group and rank 0 "
+                         "prints the ranks' (rank, local_rank, world_size); no GPU is touched")
     args = ap.parse_args()
 
+    if args.dry_run:
+        dry_run_ranks(args)
+        return
     env = init_from_env()
-    if env.world_size != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {env.world_size}", file=sys.stderr)
+    if env.world_size != args.gpus:   # _launch_or_check() exits first; belt and braces
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but world size {env.world_size}")
+    if env.world_size > 1 and torch.cuda.device_count() < env.world_size:
+        raise SystemExit(f"bench.py: world size {env.world_size} but "
+                         f"{torch.cuda.device_count()} GPU(s) visible")
     dev = torch.device("cuda", env.local_rank)
     torch.cuda.set_device(dev)
 
@@ -531,7 +667,40 @@ def main():
     elapsed = time.perf_counter() - t0
     if timing:
         timing.__exit__(None, None, None)
+    rank_ms = per_rank_ms(1000.0 * elapsed / args.steps, env, dev)
     elapsed = max_over_ranks(elapsed, env, dev)
+
+    # N > 1: the exchange on its own, and the same step without DDP on every
+    # rank at once (no collective: what each GPU does alone while its
+    # neighbours run) — the in-job reference for the scaling efficiency
+    multi = None
+    if env.world_size > 1:
+        from datamining_recblr_amd.distributed import LossModule
+        plain = LossModule(model)
+        for i in range(2):
+            opt.zero_grad(set_to_none=True)
+            plain(batches[i % len(batches)]).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        barrier(env)
+        t3 = time.perf_counter()
+        for i in range(args.steps):
+            opt.zero_grad(set_to_none=True)
+            plain(batches[i % len(batches)]).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        barrier(env)
+        plain_el = max_over_ranks(time.perf_counter() - t3, env, dev)
+        plain_value = env.world_size * args.batch * args.steps / plain_el
+        value_n = env.world_size * args.batch * args.steps / elapsed
+        multi = {"per_rank_ms_per_step": rank_ms,
+                 "allreduce": allreduce_probe(model, env, dev),
+                 "plain_local_ms_per_step": round(1000.0 * plain_el / args.steps, 3),
+                 "efficiency_vs_local_plain": round(value_n / plain_value, 4),
+                 "note": "efficiency_vs_local_plain = value / (the same step without DDP run "
+                         "concurrently on every rank, summed over ranks): the exchange's and "
+                         "DDP's cost at this N; value_N / (N value_1) across separate runs is "
+                         "computed by the driver from its own 1-GPU line"}
 
     # per-kernel / per-GEMM breakdown: a second pass with every launch timed
     timer = breakdown_ms = None
@@ -587,6 +756,18 @@ def main():
         fixed["note"] = (f"every sequence of full length {args.seq_len} (packed == dense "
                          "rows), the same step otherwise: a length-independent companion to "
                          "the headline, whose lengths are ~U{1..L}")
+    devlen = None
+    if not args.no_full_tail:
+        # run.py's path: RecBole hands item_length as a bare device tensor
+        # (RecBLR.py:86, run.py:84) — no host copy attached, so the packed
+        # forward reads the token count from the device (one sync per step)
+        saved = list(batches)
+        batches[:] = [dict(b, item_length=b["item_length"].clone()) for b in saved]
+        devlen = timed_variant(True, True)
+        batches[:] = saved
+        devlen["note"] = ("the headline's batches with item_length as a bare device tensor "
+                          "(no host lengths attached: run.py / RecBole's path); the packed "
+                          "forward syncs once per step for the token count")
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)
@@ -694,6 +875,8 @@ def main():
     if env.rank == 0 and env.world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, model.state_dict())
 
+    from datamining_recblr_amd.linear import gemm_format
+    gemm_format_name = gemm_format()
     if env.rank == 0:
         H = 2 * args.hidden
         line = {
@@ -701,7 +884,13 @@ def main():
             "n_gpus": env.world_size, "steps": args.steps, "warmup": args.warmup,
             "settle": {"seconds": args.settle_seconds, "steps": settle_steps},
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
+            "vs_baseline": None,
+            "dtype": ("f32 I/O, f16x3 split GEMM products" if gemm_format_name == "f16x3"
+                      else "f32"),
+            "lengths": {"headline": "packed, lengths ~U{1..L} (SURVEY §8(d))",
+                        "fixed_length_value": fixed["value"] if fixed else None,
+                        "fixed_length_ms_per_step": fixed["ms_per_step"] if fixed else None,
+                        "device_lengths_ms_per_step": (devlen or {}).get("ms_per_step")},
             "data": "synthetic RecBole-shaped batches (ids ~U{1..n_items-1}, lengths ~U{1..L}, "
                     "right-padded), reference init (seed 2020), resident in HBM",
             "config": {"workload": "RecBLR train step: calculate_loss(CE)+backward+Adam",
@@ -712,11 +901,13 @@ def main():
                        "seq_len": args.seq_len, "hidden_size": args.hidden, "inner_H": H,
                        "num_layers": args.layers, "n_items": args.n_items,
                        "dropout": args.dropout, "parallelism": f"dp{env.world_size}"},
+            "multi_gpu": multi,
             "roofline": roofline,
             "gemm": gemm,
             "optimizer": optimizer,
             "kernels": kernels_report,
             "fixed_length": fixed,
+            "device_lengths": devlen,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

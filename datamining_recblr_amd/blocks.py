@@ -20,6 +20,8 @@ projection's input gradient (ResidualGrad, rb_add_ln_bwd2's dy2).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -27,8 +29,8 @@ from . import kernels
 from ._lib import RecBLRNativeError
 from .linear import _timed, fire_hooks, has_hooks, linear, mm_nn, mm_nt, rmax_buffer, wgrad
 
-__all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm", "silu_dropout",
-           "feed_forward"]
+__all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm",
+           "silu_dropout", "feed_forward", "set_defer_residual", "defer_residual"]
 
 
 _GOLDEN = 0x9E3779B97F4A7C15   # odd 64-bit constant (2^64 / golden ratio)
@@ -42,11 +44,14 @@ def _rank() -> int:
 def draw_seed() -> int:
     """63-bit dropout seed from torch's default generator (host side, no sync).
 
-    The process-group rank is folded into the key: every rank seeds its
-    generator alike (RecBole seeds all processes with the same config seed),
-    so without it all data-parallel ranks would draw identical dropout masks
-    for their different batch shards.  Rank 0 (and a single process) keeps
-    the generator's value unchanged."""
+    The reference's driver re-seeds every process with seed + local_rank
+    before building the model (run.py:72), so under it the ranks' generators
+    already differ.  The process-group rank is folded in as a guard for
+    launchers that seed every rank alike (bench.py seeds 2020 everywhere, so
+    the ranks' weights start equal): without it all data-parallel ranks would
+    draw identical dropout masks for their different batch shards.  Rank 0
+    (and a single process) keeps the generator's value unchanged; rank r's
+    masks therefore differ from a single process seeded with seed + r."""
     s = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
     r = _rank()
     if r:
@@ -89,9 +94,30 @@ class ResidualGrad:
         self.taken = False
 
 
+# Deferred residual gradients change what autograd reports for the tensor in
+# between: its producer adds the residual term inside its own backward, so a
+# tensor hook, retain_grad() or torch.autograd.grad(loss, h) on h (a
+# RecurrentLayer output, the embedding LayerNorm output, a FeedForward input)
+# sees only the projection's term.  Parameter and input gradients are exact
+# either way.  RECBLR_DEFER_RESIDUAL=0 (or set_defer_residual(False)) makes the
+# consumer add the residual term to the gradient it returns, so every
+# intermediate gradient is the full one (one extra [rows, d] add per slot).
+_defer_residual = [os.environ.get("RECBLR_DEFER_RESIDUAL", "1") != "0"]
+
+
+def set_defer_residual(on: bool) -> None:
+    """Switch residual-gradient deferral (see _defer_residual) for models
+    run after this call."""
+    _defer_residual[0] = bool(on)
+
+
+def defer_residual() -> bool:
+    return _defer_residual[0]
+
+
 def _take(addend):
     """Register a producer for `addend` (it will add addend.ds itself)."""
-    if addend is not None and addend.rows is None:
+    if addend is not None and addend.rows is None and _defer_residual[0]:
         addend.taken = True
         return addend
     return None

@@ -33,7 +33,7 @@ def scan_fwd(gates: torch.Tensor, tokens: torch.Tensor) -> torch.Tensor:
 @scan_fwd.register_fake
 def _(gates, tokens):
     torch._check(gates.shape == tokens.shape, lambda: "gates and tokens must match")
-    return torch.empty_like(tokens)
+    return tokens.new_empty(tokens.shape)   # contiguous, like rb_scan_fwd's output
 
 
 @torch.library.custom_op("recblr::scan_bwd", mutates_args=())
@@ -45,7 +45,7 @@ def scan_bwd(gates: torch.Tensor, states: torch.Tensor,
 
 @scan_bwd.register_fake
 def _(gates, states, grad):
-    return torch.empty_like(gates), torch.empty_like(gates)
+    return gates.new_empty(gates.shape), gates.new_empty(gates.shape)
 
 
 def _scan_setup(ctx, inputs, output):
@@ -89,7 +89,9 @@ def linear_bwd(dy: torch.Tensor, x: torch.Tensor, weight: torch.Tensor,
 
 @linear_bwd.register_fake
 def _(dy, x, weight, has_bias):
-    return (torch.empty_like(x), torch.empty_like(weight),
+    # contiguous like the real outputs (mm_nn(...).view(x.shape), wgrad's [N, K]),
+    # whatever x's strides: empty_like would keep a transposed x's strides
+    return (x.new_empty(x.shape), weight.new_empty(weight.shape),
             dy.new_empty((weight.shape[0],) if has_bias else (0,)))
 
 

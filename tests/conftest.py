@@ -48,3 +48,22 @@ def split_gemm_calls(monkeypatch):
 
         monkeypatch.setattr(kernels, name, counted)
     return calls
+
+
+@pytest.fixture
+def tn_gemm_calls(monkeypatch):
+    """Records every launch of the f16 weight-gradient kernel
+    (kernels.gemm_tn_h / rb_gemm_tn_h) as (M, N, K) of dW[N, K] = dY[M, N]^T
+    X[M, K]: tests use it to assert the weight gradients they check ran on it
+    (it needs M >= linear.MIN_ROWS_FOR_SPLIT and the rmax side outputs)."""
+    from datamining_recblr_amd import kernels
+
+    calls = []
+    orig = kernels.gemm_tn_h
+
+    def counted(dy, x, ymax, xmax, *args, **kw):
+        calls.append((dy.shape[0], dy.shape[1], x.shape[1]))
+        return orig(dy, x, ymax, xmax, *args, **kw)
+
+    monkeypatch.setattr(kernels, "gemm_tn_h", counted)
+    return calls

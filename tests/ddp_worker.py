@@ -24,7 +24,17 @@ def main():
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
     from tests.ddp_common import CFG, batches, to_device
 
+    from datamining_recblr_amd import kernels
+
     linear.SPLIT_MIN_ROWS = 0          # every projection through rb_gemm_nt
+    tn_rows = []                       # M of every rb_gemm_tn_h launch (weight gradients)
+    _tn = kernels.gemm_tn_h
+
+    def counted(dy, x, *a, **kw):
+        tn_rows.append(dy.shape[0])
+        return _tn(dy, x, *a, **kw)
+
+    kernels.gemm_tn_h = counted
     env = init_from_env(backend=os.environ.get("RB_DDP_BACKEND", "gloo"))
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -46,6 +56,7 @@ def main():
     for n, p in model.named_parameters():
         rec[f"param.{n}"] = p.detach().cpu().clone()
     rec["dist"] = torch.tensor([int(dist.is_initialized()), env.world_size])
+    rec["tn_rows"] = torch.tensor(tn_rows, dtype=torch.int64)
     torch.save(rec, out)
     if dist.is_initialized():
         dist.barrier()

@@ -6,11 +6,12 @@ model trained on the full batch in one process.
 Both ranks share cuda:0 (one GPU per test box; RCCL refuses two ranks on one
 device, so the group uses gloo, which all-reduces the same DDP buckets).
 Exercises under DDP what no CPU test can: the custom autograd.Functions of
-the encoder, the ResidualGrad slot that adds the residual gradient inside
-the dX GEMM, the folded pad-prefix backward that adds into the conv-bias /
+the encoder, the ResidualGrad slots whose residual gradient the producing
+LayerNorm backward adds (rb_add_ln_bwd2), the folded pad-prefix backward that adds into the conv-bias /
 gate / Lambda gradients in place, the split-weight cache invalidated by the
 optimizer-step hook (3 Adam steps), and host-staged packing.  Every
-projection runs rb_gemm_nt (SPLIT_MIN_ROWS = 0 in the ranks and here).
+projection runs the split GEMM (SPLIT_MIN_ROWS = 0 in the ranks and here);
+at L = 200 the weight gradients run on rb_gemm_tn_h (asserted).
 
 Bar: each step's loss and every parameter gradient equal the full-batch
 run's within 1e-5 of the tensor's max (the only difference is the fp32
@@ -30,7 +31,12 @@ from tests.ddp_common import CFG, batches, to_device
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STEPS, GB, L, N_ITEMS = 3, 128, 100, 3000
+STEPS, N_ITEMS = 3, 3000
+# (global batch, L): the small case, and the bench's L = 200 with 192
+# sequences per rank, so every rank's ntok >= linear.MIN_ROWS_FOR_SPLIT and
+# the [ntok]-row weight gradients run on rb_gemm_tn_h (with the rmax side
+# outputs of the forward / input-gradient GEMMs) under DDP
+CASES = [(128, 100), (384, 200)]
 
 
 def _free_port():
@@ -41,7 +47,7 @@ def _free_port():
     return port
 
 
-def _run_ranks(tmp_path, world=2):
+def _run_ranks(tmp_path, GB, L, world=2):
     port = _free_port()
     procs, outs = [], []
     for r in range(world):
@@ -64,7 +70,7 @@ def _run_ranks(tmp_path, world=2):
     return [torch.load(o, weights_only=True) for o in outs]
 
 
-def _full_batch_reference(cuda):
+def _full_batch_reference(cuda, GB, L):
     from datamining_recblr_amd import linear
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
@@ -91,11 +97,17 @@ def _full_batch_reference(cuda):
     return rec
 
 
-def test_ddp_world2_recblr_matches_full_batch(cuda, tmp_path):
-    ranks = _run_ranks(tmp_path)
-    ref = _full_batch_reference(cuda)
+@pytest.mark.parametrize("GB,L", CASES, ids=[f"GB{g}_L{l}" for g, l in CASES])
+def test_ddp_world2_recblr_matches_full_batch(cuda, tmp_path, GB, L):
+    from datamining_recblr_amd import linear
+
+    ranks = _run_ranks(tmp_path, GB, L)
+    ref = _full_batch_reference(cuda, GB, L)
     for r in ranks:
         assert r["dist"].tolist() == [1, 2]
+        if L == 200:   # per step: layer 0 in/gates/out/w_1/w_2 + layer 1 in/gates
+            big = (r["tn_rows"] >= linear.MIN_ROWS_FOR_SPLIT).sum().item()
+            assert big >= 7 * STEPS, r["tn_rows"].tolist()
     for i in range(STEPS):
         # loss: each rank's shard mean; their average is the full-batch mean
         avg = sum(r[f"loss.{i}"] for r in ranks) / len(ranks)

@@ -41,7 +41,7 @@ def _cfg(L, loss_type="CE", d=128):
                 MAX_ITEM_LIST_LENGTH=L)
 
 
-def _run(cuda, B, L, packed, gather, seed, loss_type="CE"):
+def _run(cuda, B, L, packed, gather, seed, loss_type="CE", fixed_len=False):
     from datamining_recblr_amd.distributed import synthetic_interaction
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
@@ -50,7 +50,8 @@ def _run(cuda, B, L, packed, gather, seed, loss_type="CE"):
     torch.manual_seed(2020)
     model = RecBLR(cfg, SyntheticDataset(N_ITEMS)).to(cuda).eval()
     model.pack_sequences, model.gather_last_layer = packed, gather
-    inter = synthetic_interaction(B, L, N_ITEMS, cuda, seed=seed, with_neg=loss_type == "BPR")
+    inter = synthetic_interaction(B, L, N_ITEMS, cuda, seed=seed, with_neg=loss_type == "BPR",
+                                  fixed_len=fixed_len)
     loss = model.calculate_loss(inter)
     loss.backward()
     torch.cuda.synchronize()
@@ -87,6 +88,31 @@ def test_train_step_matches_oracle_with_split_gemm(cuda, split_gemm_calls, monke
         assert s in shapes, (s, shapes)
     if threshold == 0:
         assert any(c[0] == B for c in split_gemm_calls), "gathered tail not on the kernel"
+
+
+@pytest.mark.parametrize("fixed_len", [False, True], ids=["ragged", "fixed_len"])
+def test_timed_shape_weight_gradients_on_tn_kernel(cuda, split_gemm_calls, tn_gemm_calls,
+                                                   fixed_len):
+    """The bench's shape (d = 128, L = 200, n_items = 10,544, packed, gathered
+    tail) at B = 192: ntok >= linear.MIN_ROWS_FOR_SPLIT, so every [ntok]-row
+    weight gradient (RecBLR.py:162,165,167,213,214) runs on rb_gemm_tn_h with
+    the rmax side outputs of the forward / input-gradient GEMMs — the
+    configuration the benchmark times — and loss plus every gradient match
+    the oracle at 1e-4.  fixed_len: every sequence of length 200 (the bench's
+    fixed_length companion)."""
+    from datamining_recblr_amd import linear
+
+    B, L = 192, 200
+    ntok = _run(cuda, B, L, packed=True, gather=True, seed=11, fixed_len=fixed_len)
+    assert ntok >= linear.MIN_ROWS_FOR_SPLIT, ntok
+    big = [c for c in tn_gemm_calls if c[0] == ntok]
+    # layer 0: input, gates, output, w_1, w_2; layer 1: input, gates (its
+    # output projection and FFN run on the B gathered rows)
+    shapes = sorted((c[1], c[2]) for c in big)
+    assert len(big) >= 7, tn_gemm_calls
+    for s in ((512, 128), (512, 256), (128, 256), (512, 128), (128, 512)):
+        assert s in shapes, (s, shapes)
+    assert any(c[0] == ntok for c in split_gemm_calls)
 
 
 def test_all_positions_tail_matches_oracle(cuda, split_gemm_calls):

@@ -225,3 +225,31 @@ def test_weight_gradient_rows_decaying_over_2_to_the_60(cuda):
                         .view(S, -1)).view(N, K)
     ref = dy.double().t() @ x.double()
     assert _rel_err(dw, ref) < 4 * max(_rel_err(dy.t() @ x, ref), 1e-7)
+
+
+def test_weight_gradient_columns_spread_over_2_to_the_16(cuda):
+    """Column magnitudes of dY and X spread over 2^16 (the TN kernel keeps
+    one scale per operand and row chunk, shared by all columns: values within
+    2^17 of the chunk max keep all 22 bits).  Checked per
+    element at its own scale — dW[n, k] divided by the column scales
+    cy[n] cx[k], so the small columns cannot hide behind the large ones — at
+    the level of hipBLASLt's fp32 GEMM."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(9)
+    M, N, K, S = 40000, 256, 128, 64
+    cy = torch.exp2(-16.0 * torch.arange(N) / (N - 1))
+    cx = torch.exp2(-16.0 * torch.arange(K) / (K - 1))
+    dy = (torch.randn(M, N, generator=g) * cy).to(cuda)
+    x = (torch.randn(M, K, generator=g) * cx).to(cuda)
+    dw = kernels.colsum(kernels.gemm_tn_h(dy, x, _row_group_max(dy), _row_group_max(x), S)
+                        .view(S, -1)).view(N, K)
+    ref = dy.double().t() @ x.double()
+
+    scale = (cy[:, None] * cx[None, :]).double().to(cuda)
+
+    def scaled(out):
+        return ((out.double() - ref).abs() / scale).max().item() / (ref.abs() / scale).max().item()
+
+    e_h, e_t = scaled(dw), scaled(dy.t() @ x)
+    assert e_h < 1e-5 and e_h < 4 * max(e_t, 1e-7), (e_h, e_t)

@@ -213,3 +213,26 @@ def test_split_cache_counts_optimizer_steps():
     w.grad = torch.ones(4, 4)
     opt.step()
     assert linear._opt_steps[0] == n0 + 1
+
+
+def test_custom_op_fakes_are_contiguous_like_the_real_outputs():
+    """torch.compile / export trace the ops through their fake impls: the
+    fakes must give the real outputs' strides (contiguous) even for a
+    transposed input, or a compiled graph would assume a wrong layout."""
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    from datamining_recblr_amd import ops
+
+    with FakeTensorMode():
+        x = torch.empty(128, 300).t()          # [300, 128], strides (1, 300)
+        w = torch.empty(64, 128)
+        dy = torch.empty(300, 64)
+        dx, dw, db = ops.linear_bwd(dy, x, w, True)
+        y = ops.linear(x, w, None)
+        g = torch.empty(2, 4, 9)
+        s = ops.scan_fwd(g, g)
+        dg, dt = ops.scan_bwd(g, s, g)
+    assert dx.shape == x.shape and dx.is_contiguous() and not x.is_contiguous()
+    assert dw.shape == w.shape and dw.is_contiguous() and db.shape == (64,)
+    assert y.shape == (300, 64) and y.is_contiguous()
+    assert s.is_contiguous() and dg.is_contiguous() and dt.is_contiguous()
