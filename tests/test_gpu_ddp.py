@@ -14,8 +14,8 @@ projection runs the split GEMM (SPLIT_MIN_ROWS = 0 in the ranks and here);
 at L = 200 the weight gradients run on rb_gemm_tn_h (asserted).
 
 Bar: each step's loss and every parameter gradient equal the full-batch
-run's within 1e-5 of the tensor's max (the only difference is the fp32
-order of summing the two halves); the final parameters within 2e-5 (2% of
+run's within 1e-5 of the tensor's max at step 0 (the only difference is the
+fp32 order of summing the two halves), +1e-5 per Adam step taken before it; the final parameters within 2e-5 (2% of
 one Adam step at lr 1e-3: Adam divides by sqrt(v) + 1e-8, so on elements
 whose gradient is near zero it amplifies rounding-level differences)."""
 import os
@@ -116,7 +116,10 @@ def test_ddp_world2_recblr_matches_full_batch(cuda, tmp_path, GB, L):
             if not key.startswith(f"grad.{i}."):
                 continue
             want = ref[key]
-            tol = 1e-5 * want.abs().max().item() + 1e-8
+            # step i's gradients are taken at parameters that already differ by
+            # i Adam steps' rounding (see the bar above): 1e-5 of the max at
+            # step 0, +1e-5 per step taken
+            tol = 1e-5 * (1 + i) * want.abs().max().item() + 1e-8
             for r in ranks:   # DDP leaves the averaged gradient on every rank
                 err = (r[key] - want).abs().max().item()
                 assert err <= tol, (key, err, tol)
