@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 25
+ABI_VERSION = 26
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -111,6 +111,7 @@ SIGNATURES = {
                                     _fp, _fp]),
     "rb_gemm_tn_h": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _i64,
                                     _fp]),
+    "rb_gemm_tn_hs": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, ctypes.c_int, _fp]),
 }
 
 

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 25; }
+int rb_version(void) { return 26; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -659,12 +659,12 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
   if (!A || !Wf || !out) return fail("rb_gemm_nt_h: null pointer");
   if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt_h: empty shape");
   if (accumulate) return fail("rb_gemm_nt_h: accumulate is not supported (add the residual in its consumer)");
-  if (R % 32 || C % 128 || R > (1 << 16) || C > 1024)
-    return fail("rb_gemm_nt_h: R must be a multiple of 32 and C of 128 (C <= 1024)");
+  if (R % 32 || C % 32 || R > (1 << 16) || C > 1024)
+    return fail("rb_gemm_nt_h: R and C must be multiples of 32 (C <= 1024)");
   if (lda < R || lda % 4 || ldo < C || ldo % 2) return fail("rb_gemm_nt_h: bad row strides");
   if (!aligned16(A) || !aligned16(Wf) || (reinterpret_cast<uintptr_t>(out) & 7))
     return fail("rb_gemm_nt_h: A and Wf must be 16-byte aligned, out 8-byte aligned");
-  if ((M + 255) / 256 * (C / 128) > 0x7fffffffLL) return fail("rb_gemm_nt_h: grid too large");
+  if ((M + 31) / 32 > 0x7fffffffLL) return fail("rb_gemm_nt_h: grid too large");
   return launch_gemm_nt_h(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate, rmax,
                           reinterpret_cast<hipStream_t>(stream));
 }
@@ -683,6 +683,18 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
   if ((N / 128) * (K / 128) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_h: grid too large");
   return launch_gemm_tn_h(dY, ldy, X, ldx, M, (int)N, (int)K, ymax, xmax, parts, (int)splits,
                           reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
+                  int64_t K, float* dw, int accumulate, void* stream) {
+  if (!dY || !X || !dw) return fail("rb_gemm_tn_hs: null pointer");
+  if (M <= 0 || N <= 0 || K <= 0) return fail("rb_gemm_tn_hs: empty shape");
+  if (N % 32 || K % 32 || N > 65536 || K > 65536)
+    return fail("rb_gemm_tn_hs: N and K must be multiples of 32");
+  if (M > (1 << 24)) return fail("rb_gemm_tn_hs: M too large for the few-rows kernel");
+  if (ldy < N || ldx < K) return fail("rb_gemm_tn_hs: bad row strides");
+  return launch_gemm_tn_hs(dY, ldy, X, ldx, M, (int)N, (int)K, dw, accumulate,
+                           reinterpret_cast<hipStream_t>(stream));
 }
 
 }  // extern "C"

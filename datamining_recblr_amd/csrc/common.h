@@ -363,6 +363,10 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st);
+int launch_gemm_nt_hs(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                      const float* bias, float* out, int64_t ldo, float* rmax, hipStream_t st);
+int launch_gemm_tn_hs(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
+                      int K, float* dw, int accumulate, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
 int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, void* workspace,
                           int64_t ws_bytes, hipStream_t st);

@@ -1043,9 +1043,6 @@ int launch_split_weights_h(const rb_split_job* jobs, int n, hipStream_t st) {
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st) {
-  const int m_tiles = (int)((M + N_BM - 1) / N_BM);
-  const f16x8* wf = (const f16x8*)Wf;
-  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   (void)accumulate;  // rejected by rb_gemm_nt_h
 #ifdef HN_NARROW_STORE
   const bool wide = false;
@@ -1057,6 +1054,30 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
 #else
   const bool nb8 = wide && C % 256 == 0;
 #endif
+  // The persistent grid runs whole rounds of G tiles; the rows past the last
+  // whole round would run on a fraction of the chip (800 row tiles on 256
+  // CUs: a fourth round on 32 of them, +18% time for +4% rows), so they go
+  // to the few-rows kernel (gemm_small.hip) right behind, spread over the
+  // whole chip.  Below one round, or for C % 128 != 0, all rows go there.
+  const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
+  const int nct0 = C % 128 ? 0 : C / (nb8 ? 256 : 128);
+  const int64_t rows_round = nct0 ? (int64_t)(G0 / nct0) * N_BM : 0;
+#ifdef HN_NO_TAIL_SPLIT
+  const int64_t M_main = nct0 ? M : 0;
+#else
+  const int64_t M_main = (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
+                                                                   : (nct0 ? M : 0);
+#endif
+  if (M_main < M) {
+    const int rc = launch_gemm_nt_hs(A + M_main * lda, lda, M - M_main, R, Wf, C, bias,
+                                     out + M_main * ldo, ldo,
+                                     rmax ? rmax + M_main / 32 : nullptr, st);
+    if (rc || M_main == 0) return rc;
+  }
+  M = M_main;
+  const int m_tiles = (int)((M + N_BM - 1) / N_BM);
+  const f16x8* wf = (const f16x8*)Wf;
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / (nb8 ? 256 : 128));
   // persistent: one workgroup per CU (a multiple of 8: the XCD pairing above)
   const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8 * (8 / N_WAVES));

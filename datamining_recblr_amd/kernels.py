@@ -1043,3 +1043,25 @@ def gemm_tn_h(dy: torch.Tensor, x: torch.Tensor, ymax: torch.Tensor, xmax: torch
     _lib.call("rb_gemm_tn_h", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K,
               ymax.data_ptr(), xmax.data_ptr(), parts.data_ptr(), splits, _stream(dy))
     return parts
+
+
+def gemm_tn_hs(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
+               accumulate: bool = False) -> torch.Tensor:
+    """dW = dy^T x [N, K] for few rows on the f16 pipe (rb_gemm_tn_hs: exact
+    per-column scales, no rmax needed); with `out` and accumulate, added to it."""
+    for t, n in ((dy, "dy"), (x, "x")):
+        _check(t, n)
+    if dy.dim() != 2 or x.dim() != 2 or dy.stride(1) != 1 or x.stride(1) != 1:
+        raise ValueError("dy and x must be 2-D with unit inner stride")
+    M, N = dy.shape
+    K = x.shape[1]
+    if x.shape[0] != M:
+        raise ValueError("dy and x must have the same rows")
+    if out is None:
+        out = torch.empty((N, K), device=dy.device, dtype=torch.float32)
+        accumulate = False
+    elif out.shape != (N, K) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError("out must be a contiguous fp32 [N, K] tensor")
+    _lib.call("rb_gemm_tn_hs", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K,
+              out.data_ptr(), int(accumulate), _stream(dy))
+    return out

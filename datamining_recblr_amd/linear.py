@@ -132,10 +132,16 @@ def split_gemm_enabled() -> bool:
     return _split_on
 
 
+# f16x3: any row count (below one persistent round, and for the rows past the
+# last whole round, rb_gemm_nt_h runs its few-rows kernel, csrc/gemm_small.hip)
+HALF_MIN_ROWS = 1
+
+
 def _split_ok(a: torch.Tensor, C: int, R: int) -> bool:
-    return (_split_on and a.is_cuda and a.dim() == 2 and a.shape[0] >= SPLIT_MIN_ROWS
-            and C % 128 == 0 and R % 32 == 0 and a.stride(1) == 1 and a.stride(0) % 4 == 0
-            and a.data_ptr() % 16 == 0 and a.dtype == torch.float32
+    min_rows = HALF_MIN_ROWS if _half else SPLIT_MIN_ROWS
+    return (_split_on and a.is_cuda and a.dim() == 2 and a.shape[0] >= max(min_rows, 1)
+            and C % (32 if _half else 128) == 0 and R % 32 == 0 and a.stride(1) == 1
+            and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0 and a.dtype == torch.float32
             and (not _half or C <= 1024))
 
 
@@ -219,6 +225,11 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
         S = _tn_splits(dy2.device, (N // 128) * (K // 128))
         parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
         return kernels.colsum(parts.view(S, -1)).view(N, K)
+    if (_half and _split_on and _tn_on and M < MIN_ROWS_FOR_SPLIT and N % 32 == 0
+            and K % 32 == 0 and dy2.dtype == torch.float32 and x2.dtype == torch.float32
+            and dy2.is_cuda and dy2.stride(1) == 1 and x2.stride(1) == 1):
+        # few rows (the gathered last-layer tail): exact per-column scales
+        return kernels.gemm_tn_hs(dy2, x2)
     if M < MIN_ROWS_FOR_SPLIT or splits <= 1:
         return (dy2.t() @ x2).float()
     mk = M // splits

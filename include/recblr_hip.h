@@ -460,9 +460,14 @@ int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R);
  * rb_gemm_split_weights; each Wf rb_gemm_h_weight_bytes(C, R) bytes). */
 int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
 
-/* rb_gemm_nt's contract on the f16 image (R % 32 == 0, C % 128 == 0,
+/* rb_gemm_nt's contract on the f16 image (R % 32 == 0, C % 32 == 0,
  * C <= 1024; accumulate must be 0).  rmax (optional, [ceil(M/32)] floats): max |A| over each
- * 32-row group, the operand scale of rb_gemm_tn_h on the same rows. */
+ * 32-row group, the operand scale of rb_gemm_tn_h on the same rows.  Replaces
+ * nn.Linear's forward / input-gradient GEMM (RecBLR.py:162,165,167,213,214).
+ * Whole rounds of 256-row tiles run on the persistent kernel; the rows past
+ * the last whole round, and every row when M is below one round (the
+ * gathered last-layer tail, B rows) or C % 128 != 0, on the few-rows kernel
+ * (csrc/gemm_small.hip: exact per-row scales). */
 int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
                  const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                  void* stream);
@@ -479,6 +484,15 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
 int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
                  int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
                  void* stream);
+
+/* dW (+)= dY^T X for few rows M (F.linear's weight gradient on the gathered
+ * last-layer tail, RecBLR.py:167,213,214 at B rows; any M up to 2^24, fastest
+ * below ~16k): dW [N, K] row-major fp32, written (accumulate = 0) or added to
+ * (accumulate = 1); f16 two-part split with exact per-column scales over each
+ * eighth of the rows (no rmax needed); N % 32 == 0, K % 32 == 0; any row
+ * strides and alignment.  Deterministic (fixed-order partial sums). */
+int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
+                  int64_t K, float* dw, int accumulate, void* stream);
 
 /* Measurement aid (bench.py gemm.pattern; not on the model's path): the HBM
  * bytes of out[M, C] = a[M, R] W^T without the product — every row of a

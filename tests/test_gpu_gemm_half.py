@@ -253,3 +253,58 @@ def test_weight_gradient_columns_spread_over_2_to_the_16(cuda):
 
     e_h, e_t = scaled(dw), scaled(dy.t() @ x)
     assert e_h < 1e-5 and e_h < 4 * max(e_t, 1e-7), (e_h, e_t)
+
+
+@pytest.mark.parametrize("M,K,N", [(2048, 512, 128), (2048, 128, 512), (2048, 256, 128),
+                                   (77, 64, 32), (5000, 96, 96), (196608 + 8024, 256, 512),
+                                   (196608 + 8024, 512, 128), (65536 * 3 + 31, 128, 256)])
+def test_few_rows_kernel_and_round_remainder(cuda, M, K, N):
+    """The few-rows kernel (csrc/gemm_small.hip): the gathered last-layer tail
+    (B = 2048 rows), C % 128 != 0, and the rows past the persistent kernel's
+    last whole round (bench-sized M: 196,608 rows there + 8,024 here).  Every
+    row at fp32 level against fp64 (per-row error against the row's max), the
+    rmax side output equal to the exact 32-row-group maxima across the seam."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + 3 * K + N)
+    x = (torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-30, 30, (M, 1), generator=g)
+                                                      .float())).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda)
+    rmax = torch.empty((M + 31) // 32, device=cuda)
+    wf = kernels.gemm_h_weight(w)
+    y = kernels.gemm_nt_h(x, wf, N, rmax=rmax)
+    ref = x.double() @ w.double().t()
+    row_err = ((y.double() - ref).abs().amax(1) / ref.abs().amax(1)).max().item()
+    assert row_err < 4e-6, row_err
+    # the bias epilogue: exactly the un-biased output plus the bias, in fp32
+    assert torch.equal(kernels.gemm_nt_h(x, wf, N, bias=b), y + b)
+    want = torch.nn.functional.pad(x.abs().amax(1), (0, (-M) % 32)).view(-1, 32).amax(1)
+    assert torch.equal(rmax, want)
+
+
+@pytest.mark.parametrize("M", [1, 100, 2048, 16383])
+@pytest.mark.parametrize("N,K", [(128, 512), (512, 128), (128, 256), (64, 32)])
+def test_few_rows_weight_gradient(cuda, M, N, K):
+    """rb_gemm_tn_hs (the gathered tail's weight gradients, every M below
+    linear.MIN_ROWS_FOR_SPLIT): per-column scales over each eighth of the
+    rows, so columns spread over 2^±30 keep fp32-level accuracy per element
+    at their own scale; accumulate adds into an existing dW."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + N + 7 * K)
+    cy = torch.exp2(torch.randint(-30, 30, (N,), generator=g).float())
+    cx = torch.exp2(torch.randint(-30, 30, (K,), generator=g).float())
+    dy = (torch.randn(M, N, generator=g) * cy).to(cuda)
+    x = (torch.randn(M, K, generator=g) * cx).to(cuda)
+    dw = kernels.gemm_tn_hs(dy, x)
+    ref = dy.double().t() @ x.double()
+    scale = (cy[:, None] * cx[None, :]).double().to(cuda)
+    err = ((dw.double() - ref).abs() / scale).max().item() / max(
+        (ref.abs() / scale).max().item(), 1e-300)
+    assert err < 4e-6, err
+    base = torch.randn(N, K, generator=g).to(cuda)
+    acc = base.clone()
+    kernels.gemm_tn_hs(dy, x, out=acc, accumulate=True)
+    assert torch.equal(acc, base + dw)
+    assert torch.equal(kernels.gemm_tn_hs(dy, x), dw)   # deterministic

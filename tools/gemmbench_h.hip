@@ -9,6 +9,7 @@
 #include <cstdio>
 
 #include "../datamining_recblr_amd/csrc/gemm_half.hip"
+#include "../datamining_recblr_amd/csrc/gemm_small.hip"
 
 namespace rb {
 int launch_status(const char* what) {
