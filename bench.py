@@ -101,7 +101,7 @@ from datamining_recblr_amd.distributed import (barrier, init_from_env, max_over_
 from datamining_recblr_amd.gemm_tuning import tuned_gemms_active  # noqa: E402
 from datamining_recblr_amd.linear import split_gemm_enabled  # noqa: E402
 from datamining_recblr_amd.model import RecBLR  # noqa: E402
-from datamining_recblr_amd.recbole_compat import SyntheticDataset  # noqa: E402
+from datamining_recblr_amd.recbole_compat import Interaction, SyntheticDataset  # noqa: E402
 
 METRIC = "sequences/sec fwd+bwd at B=2048 L=200 d=128; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -623,7 +623,10 @@ def main():
 
     def step(i, opt_events=None):
         opt.zero_grad(set_to_none=True)
-        loss = step_mod(batches[i % len(batches)])
+        b = batches[i % len(batches)]
+        if isinstance(b, Interaction):   # a CPU batch, moved as RecBole's Trainer does
+            b = b.to(dev)
+        loss = step_mod(b)
         loss.backward()
         if opt_events is None:
             opt.step()
@@ -668,6 +671,16 @@ def main():
     if timing:
         timing.__exit__(None, None, None)
     rank_ms = per_rank_ms(1000.0 * elapsed / args.steps, env, dev)
+    # host side of a step: the time to queue one step's launches from an idle
+    # device (median of 5) — close to ms_per_step means the host paces the step
+    host_ms = []
+    for i in range(5):
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        step(i)
+        host_ms.append(1000.0 * (time.perf_counter() - t5))
+        torch.cuda.synchronize()
+    host_enqueue_ms = sorted(host_ms)[2]
     elapsed = max_over_ranks(elapsed, env, dev)
 
     # N > 1: the exchange on its own, and the same step without DDP on every
@@ -766,8 +779,18 @@ def main():
         devlen = timed_variant(True, True)
         batches[:] = saved
         devlen["note"] = ("the headline's batches with item_length as a bare device tensor "
-                          "(no host lengths attached: run.py / RecBole's path); the packed "
-                          "forward syncs once per step for the token count")
+                          "(no host lengths attached); the packed forward syncs once per "
+                          "step for the token count")
+        # run.py's path: CPU batches moved by Interaction.to(device) every step
+        # (the hook keeps the host lengths: no sync; pageable H2D copies of
+        # the batch inside the timed step, as RecBole's Trainer does)
+        batches[:] = [Interaction({k: v.cpu() for k, v in b.items()}) for b in saved]
+        recbole_path = timed_variant(True, True)
+        batches[:] = saved
+        recbole_path["note"] = ("CPU batches moved by Interaction.to(device) inside every step, "
+                                "as RecBole's Trainer (run.py) does; the hook on Interaction.to "
+                                "keeps the host lengths (recbole_compat.install_interaction_hook)")
+        devlen["recbole_interaction_path"] = recbole_path
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)
@@ -901,6 +924,7 @@ def main():
                        "seq_len": args.seq_len, "hidden_size": args.hidden, "inner_H": H,
                        "num_layers": args.layers, "n_items": args.n_items,
                        "dropout": args.dropout, "parallelism": f"dp{env.world_size}"},
+            "host_enqueue_ms_per_step": round(host_enqueue_ms, 3),
             "multi_gpu": multi,
             "roofline": roofline,
             "gemm": gemm,

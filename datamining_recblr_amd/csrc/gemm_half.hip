@@ -1060,13 +1060,17 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
   // to the few-rows kernel (gemm_small.hip) right behind, spread over the
   // whole chip.  Below one round, or for C % 128 != 0, all rows go there.
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
+  // (the few-rows kernel holds R <= 1024; beyond, the persistent kernel takes
+  // every row, a partial round included)
   const int nct0 = C % 128 ? 0 : C / (nb8 ? 256 : 128);
+  if (R > 1024 && nct0 == 0) return fail("rb_gemm_nt_h: C % 128 != 0 needs R <= 1024");
   const int64_t rows_round = nct0 ? (int64_t)(G0 / nct0) * N_BM : 0;
 #ifdef HN_NO_TAIL_SPLIT
   const int64_t M_main = nct0 ? M : 0;
 #else
-  const int64_t M_main = (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
-                                                                   : (nct0 ? M : 0);
+  const int64_t M_main = R > 1024 ? M
+                       : (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
+                                                                    : (nct0 ? M : 0);
 #endif
   if (M_main < M) {
     const int rc = launch_gemm_nt_hs(A + M_main * lda, lda, M - M_main, R, Wf, C, bias,

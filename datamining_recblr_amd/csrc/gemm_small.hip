@@ -5,15 +5,15 @@
 // chip), and weight gradients below linear.MIN_ROWS_FOR_SPLIT.
 //
 // k_gemm_nt_hs: out[M, C] = A[M, R] . Bm[C, R]^T (+ bias).  A 512-thread
-//   workgroup per (32 rows, 128 columns): wave w = (column block w & 3,
-//   K half w >> 2), one 32 x 32 accumulator; the two K halves meet in LDS
-//   (fixed order).  A rows are scaled by their EXACT max over R (found
-//   first, every wave scanning an eighth of the row), so no value can leave
-//   fp16's range and no recompute path is needed; the weights use the
-//   image's per-column scales.  Operands come straight from global memory
-//   (A rows re-read from L2 by the 4 column-block workgroups; 16-B loads,
-//   the weight fragments 1 KB per wave-instruction).  rmax (max |A| per
-//   32-row group) is written by the first column block.
+//   workgroup per 32 x 32 output block: the 8 waves split R into eighths,
+//   each loads its whole slice of both operands into registers at once (one
+//   memory round trip: these launches are latency-bound), and the eight
+//   partial accumulators meet in LDS (summed in wave order).  A rows are
+//   scaled by their EXACT max over R (the slices' maxima combined in LDS),
+//   so no value can leave fp16's range and no recompute path is needed; the
+//   weights use the image's per-column scales.  A rows are re-read from L2
+//   by the C/32 column-block workgroups.  rmax (max |A| per 32-row group) is
+//   written by the first column block.
 // k_gemm_tn_hs: dW[N, K] = dY[M, N]^T X[M, K] (+ dW when accumulate).  A
 //   512-thread workgroup per 32 x 32 block of dW: the 8 waves split the rows
 //   M, each scales its slice PER COLUMN of both operands (exact column max
@@ -67,26 +67,41 @@ __global__ void __launch_bounds__(512) k_gemm_nt_hs(const float* __restrict__ A,
                                                     const float* __restrict__ bias,
                                                     float* __restrict__ out, int64_t ldo,
                                                     float* __restrict__ rmax) {
+  constexpr int KMAX = 8;   // k16 blocks per wave held in registers (R <= 8 x 8 x 16 = 1024)
   __shared__ float s_max[8][32];
   __shared__ int s_er[32];
-  __shared__ f32x16s s_acc[4][64];
+  __shared__ f32x16s s_acc[8][64];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t r0 = (int64_t)blockIdx.x * 32;
-  const int cb = blockIdx.y * 4 + (wave & 3);   // 32-column block
-  const int kh = wave >> 2;                     // K half
+  const int cb = blockIdx.y;                    // 32-column block
   const int KB = R / 16;
+  // wave w: k16 blocks [kb0, kb1), an eighth of R (loaded once, into registers)
+  const int kb0 = KB * wave / 8, kb1 = KB * (wave + 1) / 8;
   int64_t row = r0 + (lane & 31);
   row = row < M ? row : M - 1;
   const float* arow = A + row * lda + 8 * (lane >> 5);
-
-  // exact row max over R: wave w scans k16 blocks w, w + 8, ...
+  const f16x8s* wb = Wf + (int64_t)cb * KB * 2 * 64 + lane;
+  f32x4s p[KMAX], q[KMAX];
+  f16x8s b0[KMAX], b1[KMAX];
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    if (kb0 + j < kb1) {
+      const int kb = kb0 + j;
+      p[j] = *reinterpret_cast<const f32x4s*>(arow + kb * 16);
+      q[j] = *reinterpret_cast<const f32x4s*>(arow + kb * 16 + 4);
+      b0[j] = wb[(kb * 2) * 64];
+      b1[j] = wb[(kb * 2 + 1) * 64];
+    }
+  }
+  // exact row max over R: each wave's slice, then the 8 slices in LDS
   float m = 0.0f;
-  for (int kb = wave; kb < KB; kb += 8) {
-    const f32x4s p = *reinterpret_cast<const f32x4s*>(arow + kb * 16);
-    const f32x4s q = *reinterpret_cast<const f32x4s*>(arow + kb * 16 + 4);
-    m = fmaxf(m, fmaxf(fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fmaxf(fabsf(p[2]), fabsf(p[3]))),
-                       fmaxf(fmaxf(fabsf(q[0]), fabsf(q[1])), fmaxf(fabsf(q[2]), fabsf(q[3])))));
+#pragma unroll
+  for (int j = 0; j < KMAX; ++j) {
+    if (kb0 + j < kb1) {
+      m = fmaxf(m, fmaxf(fmaxf(fmaxf(fabsf(p[j][0]), fabsf(p[j][1])), fmaxf(fabsf(p[j][2]), fabsf(p[j][3]))),
+                         fmaxf(fmaxf(fabsf(q[j][0]), fabsf(q[j][1])), fmaxf(fabsf(q[j][2]), fabsf(q[j][3])))));
+    }
   }
   m = fmaxf(m, __shfl_xor(m, 32));
   if (lane < 32) s_max[wave][lane] = m;
@@ -99,58 +114,43 @@ __global__ void __launch_bounds__(512) k_gemm_nt_hs(const float* __restrict__ A,
     s_max[0][tid] = mm;
   }
   __syncthreads();
-  if (rmax != nullptr && blockIdx.y == 0 && tid < 64) {
+  if (rmax != nullptr && cb == 0 && tid < 64) {
     float g = tid < 32 && r0 + tid < M ? s_max[0][tid] : 0.0f;
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) g = fmaxf(g, __shfl_xor(g, o));
     if (tid == 0) rmax[blockIdx.x] = g;
   }
   const float sc = __builtin_amdgcn_ldexpf(1.0f, kSW - s_er[lane & 31]);
-
   f32x16s acc;
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-  const bool active = cb * 32 < C;
-  if (active) {
-    const int kb0 = kh * (KB / 2), kb1 = kh ? KB : KB / 2;
-    const f16x8s* wb = Wf + (int64_t)cb * KB * 2 * 64 + lane;
-    // chunks of 8 k16 blocks: all 32 loads of a chunk issued before its
-    // MFMAs (these waves are latency-bound, not bandwidth-bound)
-    for (int kc = kb0; kc < kb1; kc += 8) {
-      f32x4s p[8], q[8];
-      f16x8s b0[8], b1[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int kb = kc + j < kb1 ? kc + j : kb1 - 1;
-        p[j] = *reinterpret_cast<const f32x4s*>(arow + kb * 16);
-        q[j] = *reinterpret_cast<const f32x4s*>(arow + kb * 16 + 4);
-        b0[j] = wb[(kb * 2) * 64];
-        b1[j] = wb[(kb * 2 + 1) * 64];
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (kc + j < kb1) {
-          f16x8s a0, a1;
-          split8(p[j], q[j], sc, a0, a1);
-          acc = mfma3(a0, a1, b0[j], b1[j], acc);
-        }
-      }
+  for (int j = 0; j < KMAX; ++j) {
+    if (kb0 + j < kb1) {
+      f16x8s a0, a1;
+      split8(p[j], q[j], sc, a0, a1);
+      acc = mfma3(a0, a1, b0[j], b1[j], acc);
     }
   }
-  if (kh == 1) s_acc[wave & 3][lane] = acc;
+  s_acc[wave][lane] = acc;
   __syncthreads();
-  if (kh == 1 || !active) return;
-  const f32x16s o = s_acc[wave & 3][lane];
+  if (wave >= 2) return;
+  // waves 0 and 1 each finish 8 of the 16 accumulator registers: the eight
+  // K slices summed in wave order
   const int col = cb * 32 + (lane & 31);
   const int ec = ew[col];
   const float bv = BIAS ? bias[col] : 0.0f;
 #pragma unroll
-  for (int e = 0; e < 16; ++e) {
+  for (int ee = 0; ee < 8; ++ee) {
+    const int e = wave * 8 + ee;
+    float v = s_acc[0][lane][e];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) v += s_acc[w][lane][e];
     const int rr = 8 * (e >> 2) + 4 * (lane >> 5) + (e & 3);
     const int64_t r = r0 + rr;
     if (r < M) {
-      const float v = __builtin_amdgcn_ldexpf(acc[e] + o[e], s_er[rr] + ec - 2 * kSW);
-      out[r * ldo + col] = BIAS ? v + bv : v;
+      const float o = __builtin_amdgcn_ldexpf(v, s_er[rr] + ec - 2 * kSW);
+      out[r * ldo + col] = BIAS ? o + bv : o;
     }
   }
 }
@@ -242,7 +242,8 @@ int launch_gemm_nt_hs(const float* A, int64_t lda, int64_t M, int R, const void*
   if (M <= 0) return 0;
   const f16x8s* wf = (const f16x8s*)Wf;
   const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
-  const dim3 grid((unsigned)((M + 31) / 32), (unsigned)((C + 127) / 128));
+  if (R > 8 * 8 * 16) return fail("rb_gemm_nt_h: the few-rows kernel needs R <= 1024");
+  const dim3 grid((unsigned)((M + 31) / 32), (unsigned)(C / 32));
   if (bias)
     k_gemm_nt_hs<true><<<grid, 512, 0, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax);
   else

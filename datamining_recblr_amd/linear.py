@@ -47,6 +47,10 @@ _half = _GEMM == "f16x3"
 # maxima are known (RECBLR_TN=0: hipBLASLt split-K, below)
 _tn_on = os.environ.get("RECBLR_TN", "1") != "0"
 _cache_on = os.environ.get("RECBLR_SPLIT_CACHE", "1") != "0"
+# few-rows weight gradients on rb_gemm_tn_hs (RECBLR_SMALL_TN=1); off by
+# default: at B = 2048 rows it measured 59 us against hipBLASLt's 18 us
+# (profiles/r03_v1_bench.log: 32-64 workgroups of column-strided loads)
+_small_tn = os.environ.get("RECBLR_SMALL_TN", "0") == "1"
 
 # Split images of the weights, kept across calls: (id(w), transpose) ->
 # [weakref(w), data_ptr, (version, optimizer steps), wf].  An entry is current
@@ -225,7 +229,7 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
         S = _tn_splits(dy2.device, (N // 128) * (K // 128))
         parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
         return kernels.colsum(parts.view(S, -1)).view(N, K)
-    if (_half and _split_on and _tn_on and M < MIN_ROWS_FOR_SPLIT and N % 32 == 0
+    if (_small_tn and _half and _split_on and _tn_on and M < MIN_ROWS_FOR_SPLIT and N % 32 == 0
             and K % 32 == 0 and dy2.dtype == torch.float32 and x2.dtype == torch.float32
             and dy2.is_cuda and dy2.stride(1) == 1 and x2.stride(1) == 1):
         # few rows (the gathered last-layer tail): exact per-column scales

@@ -32,7 +32,7 @@ from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_n
                      feed_forward)
 from .kernels import Packed, pack_plan
 from .linear import HipLinearForward, fire_hooks, has_hooks, linear
-from .recbole_compat import BPRLoss, SequentialRecommender
+from .recbole_compat import BPRLoss, SequentialRecommender, install_interaction_hook
 from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
@@ -248,6 +248,9 @@ class RecBLR(SequentialRecommender):
         # reference); identical outputs and gradients, see DESIGN.md
         self.pack_sequences = os.environ.get("RECBLR_PACKED", "1") != "0"
 
+        # run.py's Trainer moves each batch with Interaction.to(device): keep the
+        # host lengths on the device tensor (no per-step sync in the packed forward)
+        install_interaction_hook(self.ITEM_SEQ_LEN)
         self.item_embedding = nn.Embedding(self.n_items, self.hidden_size, padding_idx=0)
         self.layer_norm = nn.LayerNorm(self.hidden_size, eps=1e-12)
         self.dropout = nn.Dropout(self.dropout_prob)

@@ -74,6 +74,72 @@ except ImportError:
             return -torch.log(self.gamma + torch.sigmoid(pos_score - neg_score)).mean()
 
 
+def _attach_lengths(src: dict, out: dict, field: str) -> None:
+    """out[field] (a device tensor) gets the host copy src[field] attached
+    (model.HOST_LENGTHS): the packed forward then sizes its buffers without
+    a device sync."""
+    from .model import attach_host_lengths
+
+    s, o = src.get(field), out.get(field)
+    if (isinstance(s, torch.Tensor) and isinstance(o, torch.Tensor) and s.device.type == "cpu"
+            and o.device.type != "cpu"):
+        attach_host_lengths(o, s)
+
+
+def install_interaction_hook(field: str = "item_length") -> bool:
+    """Make RecBole's ``Interaction.to(device)`` keep a host copy of the
+    sequence lengths on the device tensor it returns (run.py's Trainer moves
+    every CPU batch to the GPU with it right before ``calculate_loss``,
+    RecBLR.py:86; recbole/data/interaction.py).  Without it the packed
+    forward reads the token count from the device: one sync per step, which
+    stops the host from queueing ahead (bench.py's device_lengths: +1.2 ms
+    per step).  Idempotent; returns False when RecBole is absent."""
+    try:  # pragma: no cover - RecBole is absent in this image
+        from recbole.data.interaction import Interaction as _RI  # type: ignore
+    except ImportError:
+        return False
+    if getattr(_RI.to, "_recblr_hooked", False):  # pragma: no cover
+        return True
+    orig = _RI.to
+
+    def to(self, device, selected_field=None):  # pragma: no cover
+        ret = orig(self, device, selected_field)
+        _attach_lengths(self.interaction, ret.interaction, field)
+        return ret
+
+    to._recblr_hooked = True  # pragma: no cover
+    _RI.to = to  # pragma: no cover
+    return True  # pragma: no cover
+
+
+class Interaction:
+    """Minimal stand-in for recbole.data.interaction.Interaction: a dict of
+    tensors with ``to(device)`` — which, like the installed hook on RecBole's
+    own class (install_interaction_hook), attaches the host copy of the
+    sequence lengths to the device tensor it creates."""
+
+    LENGTH_FIELD = "item_length"
+
+    def __init__(self, interaction: dict):
+        self.interaction = dict(interaction)
+
+    def __getitem__(self, key):
+        return self.interaction[key]
+
+    def __contains__(self, key):
+        return key in self.interaction
+
+    def keys(self):
+        return self.interaction.keys()
+
+    def to(self, device, selected_field=None):
+        keys = self.interaction.keys() if selected_field is None else selected_field
+        out = {k: (v.to(device) if k in keys and isinstance(v, torch.Tensor) else v)
+               for k, v in self.interaction.items()}
+        _attach_lengths(self.interaction, out, self.LENGTH_FIELD)
+        return Interaction(out)
+
+
 class SyntheticDataset:
     """Dataset stand-in exposing ``num(field)`` (all the model reads)."""
 

@@ -236,3 +236,22 @@ def test_custom_op_fakes_are_contiguous_like_the_real_outputs():
     assert dw.shape == w.shape and dw.is_contiguous() and db.shape == (64,)
     assert y.shape == (300, 64) and y.is_contiguous()
     assert s.is_contiguous() and dg.is_contiguous() and dt.is_contiguous()
+
+
+def test_interaction_to_keeps_host_lengths():
+    """run.py's Trainer moves each CPU batch with Interaction.to(device)
+    (RecBole); the stand-in (and the hook installed on RecBole's class) keeps
+    the host copy of item_length on the moved tensor, so the packed forward
+    needs no device sync for the token count."""
+    from datamining_recblr_amd.model import HOST_LENGTHS
+    from datamining_recblr_amd.recbole_compat import Interaction
+
+    lengths = torch.tensor([3, 1, 7])
+    inter = Interaction({"item_id_list": torch.zeros(3, 7, dtype=torch.int64),
+                         "item_length": lengths, "item_id": torch.ones(3, dtype=torch.int64)})
+    moved = inter.to("meta")
+    assert moved["item_length"].device.type == "meta"
+    assert torch.equal(getattr(moved["item_length"], HOST_LENGTHS), lengths)
+    assert not hasattr(moved["item_id"], HOST_LENGTHS)
+    # a CPU -> CPU move attaches nothing (the tensor is already on the host)
+    assert not hasattr(inter.to("cpu")["item_length"], HOST_LENGTHS)

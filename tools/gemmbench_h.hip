@@ -17,6 +17,10 @@ int launch_status(const char* what) {
   if (e != hipSuccess) fprintf(stderr, "%s: %s\n", what, hipGetErrorString(e));
   return (int)e;
 }
+int fail(const char* m) {
+  fprintf(stderr, "%s\n", m);
+  return -1;
+}
 int num_cus() {
   int n = 0;
   (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
