@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 26; }
+int rb_version(void) { return 27; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -683,6 +683,27 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
   if ((N / 128) * (K / 128) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_h: grid too large");
   return launch_gemm_tn_h(dY, ldy, X, ldx, M, (int)N, (int)K, ymax, xmax, parts, (int)splits,
                           reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
+               const float* conv_b, const void* wg_img, const float* gate_b, const float* lam,
+               const float* h0, const int32_t* pieces, int64_t B, int64_t G, int64_t ntok,
+               int64_t H, float* y, int64_t y_rs, float* y_last, float* xc, float* rg,
+               float* carries, int64_t n_tiles, float* xc_rmax, void* stream) {
+  if (!xz || !conv_w || !conv_b || !wg_img || !gate_b || !lam || !pieces)
+    return fail("rb_grl_fwd: null pointer");
+  if (H != 256) return fail("rb_grl_fwd: the fused kernel is built for H = 256");
+  if (kc < 2 || kc > 4) return fail("rb_grl_fwd: conv kernel size must be 2, 3 or 4");
+  if (B <= 0 || G <= 0 || ntok <= 0 || ntok >= (1LL << 31) || G > (1 << 20))
+    return fail("rb_grl_fwd: bad sizes");
+  if (!y == !y_last) return fail("rb_grl_fwd: exactly one of y / y_last");
+  if (xz_rs < 2 * H || xz_rs % 4 || !aligned16(xz)) return fail("rb_grl_fwd: xz layout");
+  if (y && y_rs < H) return fail("rb_grl_fwd: y row stride");
+  if (carries && n_tiles <= 0) return fail("rb_grl_fwd: carries need n_tiles");
+  if ((xc && !aligned16(xc)) || !aligned16(wg_img)) return fail("rb_grl_fwd: alignment");
+  return launch_grl_fwd(xz, xz_rs, conv_w, (int)kc, conv_b, wg_img, gate_b, lam, h0,
+                        reinterpret_cast<const int*>(pieces), B, G, ntok, y, y_rs, y_last, xc,
+                        rg, carries, n_tiles, xc_rmax, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,

@@ -183,7 +183,7 @@ class Packed:
     """Packed variable-length sequences: sequence b occupies rows
     offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
     right-padded batch without the padding; include/recblr_hip.h)."""
-    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv")
+    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv", "pieces", "G")
 
     def __init__(self, offsets: torch.Tensor, L: int, ntok: int,
                  pos: torch.Tensor | None = None):
@@ -201,6 +201,10 @@ class Packed:
         # positions gather_indexes reads (rb_gate_scan_*_last)
         self.last = None
         self.inv = None
+        # optional (grl_pieces): the fused GatedRecurrentLayer kernel's work
+        # lists (int32 [3B + G + 1] on the device) and their count G
+        self.pieces = None
+        self.G = 0
 
 
 def _layout(t: torch.Tensor, name: str, C: int, seq: "Packed | None"):
@@ -1065,3 +1069,61 @@ def gemm_tn_hs(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = Non
     _lib.call("rb_gemm_tn_hs", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K,
               out.data_ptr(), int(accumulate), _stream(dy))
     return out
+
+
+def grl_pieces(lens_packed: torch.Tensor, offs: torch.Tensor, G: int) -> torch.Tensor:
+    """Host-side work lists of the fused GatedRecurrentLayer kernel
+    (rb_grl_fwd): whole sequences dealt to G workgroups in serpentine order
+    (packed order is longest first: sequence k goes to span k % G on even
+    rounds, G - 1 - k % G on odd ones), which evens the spans' row counts to
+    within a fraction of a percent at the benchmark's lengths.
+    lens_packed, offs: CPU int64 [B], [B + 1] in packed order.  Returns CPU
+    int32 [3B + G + 1]: start row, length, packed index of each piece (in
+    span order), then the G + 1 span offsets into the piece list."""
+    B = lens_packed.numel()
+    k = torch.arange(B)
+    r, j = k // G, k % G
+    span_of = torch.where(r % 2 == 0, j, G - 1 - j)
+    order = torch.sort(span_of, stable=True).indices
+    counts = torch.bincount(span_of, minlength=G)
+    span = torch.zeros(G + 1, dtype=torch.int64)
+    torch.cumsum(counts, 0, out=span[1:])
+    return torch.cat([offs[:-1][order], lens_packed[order], order, span]).to(torch.int32)
+
+
+def grl_fwd(xz, conv_w, conv_b, wg_img, gate_b, lam, h0, seq: Packed, want_y=True,
+            want_train=True):
+    """The fused GatedRecurrentLayer core forward (rb_grl_fwd) on packed
+    sequences: returns (y [ntok, H] or y_last [B, H] when not want_y, carries,
+    xc, rg, xc_rmax) — the last four only with want_train (the three-launch
+    backward's operands: 16-step carries, xc, the gates GEMM's output without
+    its bias, xc's 32-row-group maxima)."""
+    for t, n in ((xz, "xz"), (conv_w, "conv weight"), (conv_b, "conv bias"),
+                 (gate_b, "gates bias"), (lam, "Lambda")):
+        _check(t, n)
+    ntok, H2 = xz.shape
+    H = H2 // 2
+    if seq.pieces is None or xz.stride(1) != 1 or ntok != seq.ntok:
+        raise ValueError("grl_fwd needs packed sequences with their work lists")
+    kc = conv_w.shape[-1]
+    cw = conv_w.reshape(H, kc).contiguous()
+    dev = xz.device
+    y = torch.empty((ntok, H), device=dev) if want_y else None
+    y_last = None if want_y else torch.empty((seq.B, H), device=dev)
+    carries = xc = rg = rmax = None
+    nT = num_tiles(seq.L)
+    if want_train:
+        carries = torch.empty((seq.B, nT, H), device=dev)
+        xc = torch.empty((ntok, H), device=dev)
+        rg = torch.empty((ntok, 2 * H), device=dev)
+        rmax = torch.zeros((ntok + 31) // 32, device=dev)
+    nbytes = (2 + (1 if want_y else 0) + (3 if want_train else 0)) * ntok * H * 4
+    _launch("rb_grl_fwd", nbytes, xz.data_ptr(), xz.stride(0), cw.data_ptr(), kc,
+            conv_b.contiguous().data_ptr(), wg_img.data_ptr(), gate_b.contiguous().data_ptr(),
+            lam.contiguous().data_ptr(), 0 if h0 is None else h0.contiguous().data_ptr(),
+            seq.pieces.data_ptr(), seq.B, seq.G, ntok, H,
+            0 if y is None else y.data_ptr(), H, 0 if y_last is None else y_last.data_ptr(),
+            0 if xc is None else xc.data_ptr(), 0 if rg is None else rg.data_ptr(),
+            0 if carries is None else carries.data_ptr(), nT,
+            0 if rmax is None else rmax.data_ptr(), _stream(xz))
+    return (y if want_y else y_last), carries, xc, rg, rmax

@@ -154,6 +154,11 @@ def gemm_format() -> str:
     return _GEMM if _split_on else "torch"
 
 
+def rmax_wanted() -> bool:
+    """Whether weight gradients take the f16 pipe's row-group maxima (rmax)."""
+    return _half and _tn_on and _split_on
+
+
 def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
     """A [ceil(M/32)] buffer for the row-group maxima of `a` that the f16 GEMM
     writes (the weight-gradient kernel's operand scale) — None when a's GEMM

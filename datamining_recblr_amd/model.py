@@ -30,10 +30,15 @@ from torch import nn
 from ._lib import RecBLRNativeError
 from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
                      feed_forward)
-from .kernels import Packed, pack_plan
+from .kernels import Packed, grl_pieces, pack_plan
 from .linear import HipLinearForward, fire_hooks, has_hooks, linear
 from .recbole_compat import BPRLoss, SequentialRecommender, install_interaction_hook
-from .recurrence import bd_lru, pow2_pad_len, row_pad_lens
+from .recurrence import bd_lru, fused_ok, pow2_pad_len, row_pad_lens
+
+
+class _FusedProbe:
+    """Stands in for a Packed with work lists in the fused-path check."""
+    pieces = True
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
 # RECBLR_CONV_ROWS=0: packed conv forward per sequence instead of per row tile
@@ -71,6 +76,15 @@ class _PinnedRing:
 
 
 _host_ring = _PinnedRing()
+_host_ring32 = _PinnedRing()   # int32 staging (the fused kernel's work lists)
+_ncus: dict = {}
+
+
+def _num_cus(dev) -> int:
+    n = _ncus.get(dev)
+    if n is None:
+        n = _ncus[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    return n
 
 # RECBLR_LAST_ONLY=0: the last layer's scan writes y at every position
 _LAST_ONLY = os.environ.get("RECBLR_LAST_ONLY", "1") != "0"
@@ -331,27 +345,31 @@ class RecBLR(SequentialRecommender):
         # sequences are packed longest first: the recurrence kernels give one
         # wave per sequence, so the short ones fill in behind the long ones
         host = getattr(item_seq_len, HOST_LENGTHS, None)
-        if host is not None and host.shape == item_seq_len.shape:
-            # lengths known on the host (the data path attaches them): no device sync
-            lens_h = host.to(torch.int64).clamp(1, L)
-            order_h = torch.argsort(lens_h, descending=True, stable=True)
-            offs_h = torch.zeros(B + 1, dtype=torch.int64)
-            torch.cumsum(lens_h[order_h], 0, out=offs_h[1:])
-            ntok = int(offs_h[-1])
-            both = _host_ring.stage(torch.cat([offs_h, order_h]), dev)
-            offsets, order = both[:B + 1], both[B + 1:]
-        else:
-            lens = item_seq_len.to(torch.int64).clamp(1, L)
-            order = torch.argsort(lens, descending=True, stable=True)
-            offsets = torch.zeros(B + 1, dtype=torch.int64, device=dev)
-            torch.cumsum(lens.index_select(0, order), 0, out=offsets[1:])
-            ntok = int(offsets[-1])   # one device sync
+        if host is None or host.shape != item_seq_len.shape:
+            # lengths only on the device: one sync (RecBole's Trainer path
+            # attaches them instead, recbole_compat.install_interaction_hook)
+            host = item_seq_len.to("cpu")
+        lens_h = host.to(torch.int64).clamp(1, L)
+        order_h = torch.argsort(lens_h, descending=True, stable=True)
+        offs_h = torch.zeros(B + 1, dtype=torch.int64)
+        lens_p = lens_h[order_h]
+        torch.cumsum(lens_p, 0, out=offs_h[1:])
+        ntok = int(offs_h[-1])
+        both = _host_ring.stage(torch.cat([offs_h, order_h]), dev)
+        offsets, order = both[:B + 1], both[B + 1:]
+        pieces = None
+        H = self.hidden_size * self.expand
+        if fused_ok(_FusedProbe, H, not self.disable_conv1d, self.d_conv, torch.float32):
+            G = _num_cus(dev)
+            pieces = _host_ring32.stage(grl_pieces(lens_p, offs_h, G), dev)
         # one launch (rb_pack_plan): the packed item ids, each token's position
         # in its sequence (lets the conv forward tile the packed rows), each
         # batch row's packed index and last token
         ids, pos, inv, last = pack_plan(item_seq.to(torch.int64), offsets, order, ntok)
         seq = Packed(offsets, L, ntok, pos if _CONV_ROWS else None)
         seq.last, seq.inv = last, inv
+        if pieces is not None and pad is None:   # per-row pad prefixes: three-launch path
+            seq.pieces, seq.G = pieces, G
         if pad is not None:
             pad = pad.index_select(0, order)
         n = len(self.recurrent_layers)

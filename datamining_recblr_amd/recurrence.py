@@ -30,6 +30,7 @@ import torch
 import torch.nn.functional as F
 
 from . import kernels
+from . import linear as linear_mod
 from .linear import _timed, mm_nn, mm_nt, rmax_buffer, wgrad
 
 __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDLRUCore",
@@ -37,6 +38,15 @@ __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDL
 
 
 _FOLD_PAD = os.environ.get("RECBLR_FOLD_PAD", "1") != "0"
+# RECBLR_FUSED_GRL=0: the three-launch forward (conv, gates GEMM, gate scan)
+# instead of the fused rb_grl_fwd on packed fp32 sequences with H = 256
+_FUSED = os.environ.get("RECBLR_FUSED_GRL", "1") != "0"
+
+
+def fused_ok(seq, H: int, use_conv: bool, kc: int, dtype) -> bool:
+    """Whether BDLRUCore's forward runs as one rb_grl_fwd launch."""
+    return (_FUSED and seq is not None and seq.pieces is not None and use_conv and H == 256
+            and kc in (2, 3, 4) and dtype == torch.float32 and linear_mod.gemm_format() == "f16x3")
 
 
 def pow2_pad_len(seq_len: int) -> int:
@@ -99,22 +109,31 @@ class BDLRUCore(torch.autograd.Function):
         H2 = xz.shape[-1]
         H = H2 // 2
         x, z = xz[..., :H], xz[..., H:]
-        if use_conv:
-            xc = kernels.conv_silu_fwd(x, conv_w, conv_b, seq=seq)
-        else:
-            xc = x
-        rows = xz.numel() // H2
-        gflops = 2 * rows * H * H2
-        # gates GEMM without its bias: the gate kernels add gate_b on the fly
-        xc2 = xc.reshape(rows, H)
-        r_xc = rmax_buffer(xc2, H2, H) if ctx.needs_input_grad[3] else None
-        rg = _timed("gemm", gflops, mm_nt, xc2, gate_w, rmax=r_xc).view(*xz.shape[:-1], H2)
-        ctx.r_xc = r_xc
-        if observe is not None:   # module hooks of the fused conv / gates (model.py)
-            observe(x, xc, rg)
         train = any(ctx.needs_input_grad)
-        y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train, gate_b=gate_b,
-                                           seq=seq, last_only=last_only)
+        if (observe is None and (h0 is None or h0.dim() == 1)
+                and fused_ok(seq, H, use_conv, conv_w.shape[-1], xz.dtype)):
+            # conv + gates GEMM + gate scan in one launch (rb_grl_fwd); xc,
+            # rg and the carries are kept for the backward
+            y, carries, xc, rg, r_xc = kernels.grl_fwd(
+                xz, conv_w, conv_b, linear_mod._weight_split(gate_w, False), gate_b, lam, h0,
+                seq, want_y=not last_only, want_train=train)
+            ctx.r_xc = r_xc if ctx.needs_input_grad[3] and linear_mod.rmax_wanted() else None
+        else:
+            if use_conv:
+                xc = kernels.conv_silu_fwd(x, conv_w, conv_b, seq=seq)
+            else:
+                xc = x
+            rows = xz.numel() // H2
+            gflops = 2 * rows * H * H2
+            # gates GEMM without its bias: the gate kernels add gate_b on the fly
+            xc2 = xc.reshape(rows, H)
+            r_xc = rmax_buffer(xc2, H2, H) if ctx.needs_input_grad[3] else None
+            rg = _timed("gemm", gflops, mm_nt, xc2, gate_w, rmax=r_xc).view(*xz.shape[:-1], H2)
+            ctx.r_xc = r_xc
+            if observe is not None:   # module hooks of the fused conv / gates (model.py)
+                observe(x, xc, rg)
+            y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train,
+                                               gate_b=gate_b, seq=seq, last_only=last_only)
         ctx.use_conv = use_conv
         ctx.last_only = last_only
         ctx.has_h0 = h0 is not None and pad_len is None

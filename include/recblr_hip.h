@@ -494,6 +494,28 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
 int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
                   int64_t K, float* dw, int accumulate, void* stream);
 
+/* GatedRecurrentLayer's core in one launch (RecBLR.py:182-206 between the
+ * in- and out-projections), forward, packed sequences, fp32, H == 256:
+ * xc = silu(causal depthwise conv(x) + b) (conv_w [H, kc], kc in 2..4),
+ * rg = xc W_g^T (W_g's f16 image: rb_gemm_h_split_weights, C = 2H, R = H;
+ * three fp16 products, fp32 accumulate) + gate_b, alpha / beta gates, the
+ * BD-LRU scan from h0 ([H], shared; NULL = zeros) and y = silu(z) h.
+ * xz [ntok, 2H] (x | z), row stride xz_rs.  pieces: int32 [3B + G + 1] =
+ * each work piece's start row, length and packed sequence index (whole
+ * sequences, B of them), then G + 1 offsets into the piece list, one span
+ * per workgroup.  Outputs: y [ntok, H] (y_rs) or y_last [B, H] (each
+ * sequence's last row, packed order) — exactly one; optional xc [ntok, H],
+ * rg [ntok, 2H] (the GEMM without gate_b), carries [B, n_tiles, H] (the
+ * state entering every 16-step tile: rb_gate_scan_bwd's checkpoints) and
+ * xc_rmax [ceil(ntok/32)] (max |xc| per 32-row group, the caller zeroes
+ * it).  Replaces the reference's conv / gates Linear / gate math /
+ * parallel_scan chain (RecBLR.py:173-206, parallel_scan.py:117). */
+int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
+               const float* conv_b, const void* wg_img, const float* gate_b, const float* lam,
+               const float* h0, const int32_t* pieces, int64_t B, int64_t G, int64_t ntok,
+               int64_t H, float* y, int64_t y_rs, float* y_last, float* xc, float* rg,
+               float* carries, int64_t n_tiles, float* xc_rmax, void* stream);
+
 /* Measurement aid (bench.py gemm.pattern; not on the model's path): the HBM
  * bytes of out[M, C] = a[M, R] W^T without the product — every row of a
  * (contiguous, R % 4 == 0) read once, C floats per row written (C % 4 == 0),
