@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 27
+ABI_VERSION = 28
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -113,7 +113,11 @@ SIGNATURES = {
                                     _fp]),
     "rb_gemm_tn_hs": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, ctypes.c_int, _fp]),
     "rb_grl_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp, _fp, _i64, _i64,
-                                  _i64, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _i64, _fp, _fp]),
+                                  _i64, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
+                                  _i64, _fp]),
+    "rb_grl_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp, _fp, _fp, _i64,
+                                  _i64, _i64, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp, _fp,
+                                  _fp, _fp, _fp, _fp, _fp]),
 }
 
 

@@ -370,7 +370,14 @@ int launch_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int KC,
                    const float* conv_b, const void* wf, const float* gate_b, const float* lam,
                    const float* h0, const int* pieces, int64_t B, int64_t G, int64_t ntok,
                    float* y, int64_t y_rs, float* y_last, float* xc_out, float* rg_out,
-                   float* carries, int64_t nTc, float* xc_rmax, hipStream_t st);
+                   float* carries, int64_t nTc, float* xc_rmax, float* tile_carries,
+                   int64_t max_tiles, hipStream_t st);
+int launch_grl_bwd(const float* xz, int64_t xz_rs, const float* conv_w, int KC,
+                   const float* conv_b, const void* wf, const void* wft, const float* gate_b,
+                   const float* lam, const float* h0, const int* pieces, int64_t B, int64_t G,
+                   int64_t ntok, const float* tile_carries, int64_t max_tiles, const float* dy,
+                   const float* dy_last, float* dxz, int64_t dxz_rs, float* drg, float* xc_out,
+                   float* drg_rmax, float* xc_rmax, float* part, float* cpart, hipStream_t st);
 int launch_gemm_tn_hs(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
                       int K, float* dw, int accumulate, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);

@@ -183,7 +183,7 @@ class Packed:
     """Packed variable-length sequences: sequence b occupies rows
     offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
     right-padded batch without the padding; include/recblr_hip.h)."""
-    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv", "pieces", "G")
+    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv", "pieces", "G", "max_tiles")
 
     def __init__(self, offsets: torch.Tensor, L: int, ntok: int,
                  pos: torch.Tensor | None = None):
@@ -205,6 +205,7 @@ class Packed:
         # lists (int32 [3B + G + 1] on the device) and their count G
         self.pieces = None
         self.G = 0
+        self.max_tiles = 0          # 64-row tiles of the longest work list
 
 
 def _layout(t: torch.Tensor, name: str, C: int, seq: "Packed | None"):
@@ -1091,13 +1092,26 @@ def grl_pieces(lens_packed: torch.Tensor, offs: torch.Tensor, G: int) -> torch.T
     return torch.cat([offs[:-1][order], lens_packed[order], order, span]).to(torch.int32)
 
 
+def grl_max_tiles(lens_packed: torch.Tensor, G: int) -> int:
+    """64-row tiles of grl_pieces' longest work list (the fused backward's
+    checkpoint rows per workgroup)."""
+    B = lens_packed.numel()
+    k = torch.arange(B)
+    r, j = k // G, k % G
+    span_of = torch.where(r % 2 == 0, j, G - 1 - j)
+    rows = torch.zeros(G, dtype=torch.int64).index_add_(0, span_of, lens_packed.to(torch.int64))
+    return max(1, (int(rows.max()) + 63) // 64)
+
+
 def grl_fwd(xz, conv_w, conv_b, wg_img, gate_b, lam, h0, seq: Packed, want_y=True,
-            want_train=True):
+            want_train=True, tile_carries=False):
     """The fused GatedRecurrentLayer core forward (rb_grl_fwd) on packed
     sequences: returns (y [ntok, H] or y_last [B, H] when not want_y, carries,
     xc, rg, xc_rmax) — the last four only with want_train (the three-launch
     backward's operands: 16-step carries, xc, the gates GEMM's output without
-    its bias, xc's 32-row-group maxima)."""
+    its bias, xc's 32-row-group maxima).  tile_carries (with want_train):
+    instead of those, carries = the state entering each workgroup's 64-row
+    tiles [G, max_tiles, H], the only operand grl_bwd needs besides xz."""
     for t, n in ((xz, "xz"), (conv_w, "conv weight"), (conv_b, "conv bias"),
                  (gate_b, "gates bias"), (lam, "Lambda")):
         _check(t, n)
@@ -1110,14 +1124,18 @@ def grl_fwd(xz, conv_w, conv_b, wg_img, gate_b, lam, h0, seq: Packed, want_y=Tru
     dev = xz.device
     y = torch.empty((ntok, H), device=dev) if want_y else None
     y_last = None if want_y else torch.empty((seq.B, H), device=dev)
-    carries = xc = rg = rmax = None
+    carries = xc = rg = rmax = tc = None
     nT = num_tiles(seq.L)
-    if want_train:
+    if want_train and tile_carries:
+        if seq.max_tiles <= 0:
+            raise ValueError("tile_carries needs seq.max_tiles (grl_max_tiles)")
+        tc = torch.empty((seq.G, seq.max_tiles, H), device=dev)
+    elif want_train:
         carries = torch.empty((seq.B, nT, H), device=dev)
         xc = torch.empty((ntok, H), device=dev)
         rg = torch.empty((ntok, 2 * H), device=dev)
         rmax = torch.zeros((ntok + 31) // 32, device=dev)
-    nbytes = (2 + (1 if want_y else 0) + (3 if want_train else 0)) * ntok * H * 4
+    nbytes = (2 + (1 if want_y else 0) + (3 if xc is not None else 0)) * ntok * H * 4
     _launch("rb_grl_fwd", nbytes, xz.data_ptr(), xz.stride(0), cw.data_ptr(), kc,
             conv_b.contiguous().data_ptr(), wg_img.data_ptr(), gate_b.contiguous().data_ptr(),
             lam.contiguous().data_ptr(), 0 if h0 is None else h0.contiguous().data_ptr(),
@@ -1125,5 +1143,52 @@ def grl_fwd(xz, conv_w, conv_b, wg_img, gate_b, lam, h0, seq: Packed, want_y=Tru
             0 if y is None else y.data_ptr(), H, 0 if y_last is None else y_last.data_ptr(),
             0 if xc is None else xc.data_ptr(), 0 if rg is None else rg.data_ptr(),
             0 if carries is None else carries.data_ptr(), nT,
-            0 if rmax is None else rmax.data_ptr(), _stream(xz))
+            0 if rmax is None else rmax.data_ptr(), _ptr(tc), seq.max_tiles if tc is not None else 0,
+            _stream(xz))
+    if tc is not None:
+        carries = tc
     return (y if want_y else y_last), carries, xc, rg, rmax
+
+
+def grl_bwd(xz, conv_w, conv_b, wg_img, wgt_img, gate_b, lam, h0, seq: Packed, tile_carries,
+            dy, last_only=False, want_rmax=False):
+    """Backward of grl_fwd in one launch (rb_grl_bwd) from the forward's
+    tile_carries.  dy: [ntok, H], or [B, H] at each sequence's last row when
+    last_only.  Returns (dxz [ntok, 2H], drg [ntok, 2H], xc [ntok, H],
+    drg_rmax, xc_rmax (or None), dlam [H], dgate_b [2H], dh0 [H],
+    dconv_w [H, kc], dconv_b [H])."""
+    for t, n in ((xz, "xz"), (conv_w, "conv weight"), (conv_b, "conv bias"),
+                 (gate_b, "gates bias"), (lam, "Lambda"), (dy, "dy")):
+        _check(t, n)
+    ntok, H2 = xz.shape
+    H = H2 // 2
+    if seq.pieces is None or xz.stride(1) != 1 or ntok != seq.ntok:
+        raise ValueError("grl_bwd needs packed sequences with their work lists")
+    if tile_carries.shape != (seq.G, seq.max_tiles, H) or not tile_carries.is_contiguous():
+        raise ValueError("tile_carries shape mismatch")
+    want = (seq.B, H) if last_only else (ntok, H)
+    if tuple(dy.shape) != want or not dy.is_contiguous():
+        raise ValueError(f"dy must be a contiguous fp32 {list(want)}")
+    kc = conv_w.shape[-1]
+    cw = conv_w.reshape(H, kc).contiguous()
+    dev = xz.device
+    dxz = torch.empty((ntok, H2), device=dev)
+    drg = torch.empty((ntok, H2), device=dev)
+    xc = torch.empty((ntok, H), device=dev)
+    nr = (ntok + 31) // 32
+    rmax = torch.zeros(2 * nr, device=dev) if want_rmax else None
+    part = torch.empty((seq.G, 4, H), device=dev)
+    cpart = torch.empty((seq.G * 8, H * kc + H), device=dev)
+    nbytes = (2 + (0 if last_only else 1) + 5) * ntok * H * 4
+    _launch("rb_grl_bwd", nbytes, xz.data_ptr(), xz.stride(0), cw.data_ptr(), kc,
+            conv_b.contiguous().data_ptr(), wg_img.data_ptr(), wgt_img.data_ptr(),
+            gate_b.contiguous().data_ptr(), lam.contiguous().data_ptr(), _ptr(h0),
+            seq.pieces.data_ptr(), seq.B, seq.G, ntok, H, tile_carries.data_ptr(), seq.max_tiles,
+            0 if last_only else dy.data_ptr(), dy.data_ptr() if last_only else 0,
+            dxz.data_ptr(), H2, drg.data_ptr(), xc.data_ptr(),
+            0 if rmax is None else rmax.data_ptr(), 0 if rmax is None else rmax[nr:].data_ptr(),
+            part.data_ptr(), cpart.data_ptr(), _stream(xz))
+    sums = colsum(part.view(seq.G, 4 * H)).view(4, H)
+    csum = colsum(cpart)
+    return (dxz, drg, xc, None if rmax is None else rmax[:nr], None if rmax is None else rmax[nr:],
+            sums[0], sums[1:3].reshape(-1), sums[3], csum[:H * kc].view(H, kc), csum[H * kc:])

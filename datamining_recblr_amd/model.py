@@ -30,7 +30,7 @@ from torch import nn
 from ._lib import RecBLRNativeError
 from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
                      feed_forward)
-from .kernels import Packed, grl_pieces, pack_plan
+from .kernels import Packed, grl_max_tiles, grl_pieces, pack_plan
 from .linear import HipLinearForward, fire_hooks, has_hooks, linear
 from .recbole_compat import BPRLoss, SequentialRecommender, install_interaction_hook
 from .recurrence import bd_lru, fused_ok, pow2_pad_len, row_pad_lens
@@ -362,6 +362,7 @@ class RecBLR(SequentialRecommender):
         if fused_ok(_FusedProbe, H, not self.disable_conv1d, self.d_conv, torch.float32):
             G = _num_cus(dev)
             pieces = _host_ring32.stage(grl_pieces(lens_p, offs_h, G), dev)
+            max_tiles = grl_max_tiles(lens_p, G)
         # one launch (rb_pack_plan): the packed item ids, each token's position
         # in its sequence (lets the conv forward tile the packed rows), each
         # batch row's packed index and last token
@@ -369,7 +370,7 @@ class RecBLR(SequentialRecommender):
         seq = Packed(offsets, L, ntok, pos if _CONV_ROWS else None)
         seq.last, seq.inv = last, inv
         if pieces is not None and pad is None:   # per-row pad prefixes: three-launch path
-            seq.pieces, seq.G = pieces, G
+            seq.pieces, seq.G, seq.max_tiles = pieces, G, max_tiles
         if pad is not None:
             pad = pad.index_select(0, order)
         n = len(self.recurrent_layers)

@@ -38,9 +38,14 @@ __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDL
 
 
 _FOLD_PAD = os.environ.get("RECBLR_FOLD_PAD", "1") != "0"
-# RECBLR_FUSED_GRL=0: the three-launch forward (conv, gates GEMM, gate scan)
-# instead of the fused rb_grl_fwd on packed fp32 sequences with H = 256
-_FUSED = os.environ.get("RECBLR_FUSED_GRL", "1") != "0"
+# RECBLR_FUSED_GRL=1: the fused rb_grl_fwd (and rb_grl_bwd) on packed fp32
+# sequences with H = 256 instead of the three-launch path (conv, gates GEMM,
+# gate scan); off by default until it is the faster path
+_FUSED = os.environ.get("RECBLR_FUSED_GRL", "0") != "0"
+# RECBLR_FUSED_GRL_BWD=0: with the fused forward, keep the three-launch
+# backward (the forward then writes xc, rg and the 16-step carries) instead
+# of rb_grl_bwd (the forward writes only the 64-row tile checkpoints)
+_FUSED_BWD = os.environ.get("RECBLR_FUSED_GRL_BWD", "1") != "0"
 
 
 def fused_ok(seq, H: int, use_conv: bool, kc: int, dtype) -> bool:
@@ -112,13 +117,19 @@ class BDLRUCore(torch.autograd.Function):
         train = any(ctx.needs_input_grad)
         if (observe is None and (h0 is None or h0.dim() == 1)
                 and fused_ok(seq, H, use_conv, conv_w.shape[-1], xz.dtype)):
-            # conv + gates GEMM + gate scan in one launch (rb_grl_fwd); xc,
-            # rg and the carries are kept for the backward
+            # conv + gates GEMM + gate scan in one launch (rb_grl_fwd).  Its
+            # backward is one launch too (rb_grl_bwd), from the 64-row tile
+            # checkpoints; or the three-launch backward from xc, rg, carries
+            ctx.fused_bwd = train and _FUSED_BWD and seq.max_tiles > 0
             y, carries, xc, rg, r_xc = kernels.grl_fwd(
                 xz, conv_w, conv_b, linear_mod._weight_split(gate_w, False), gate_b, lam, h0,
-                seq, want_y=not last_only, want_train=train)
+                seq, want_y=not last_only, want_train=train, tile_carries=ctx.fused_bwd)
             ctx.r_xc = r_xc if ctx.needs_input_grad[3] and linear_mod.rmax_wanted() else None
+            if ctx.fused_bwd:   # rb_grl_bwd writes xc and both operands' row maxima
+                ctx.h0 = h0
+                ctx.want_rmax = ctx.needs_input_grad[3] and linear_mod.rmax_wanted()
         else:
+            ctx.fused_bwd = False
             if use_conv:
                 xc = kernels.conv_silu_fwd(x, conv_w, conv_b, seq=seq)
             else:
@@ -145,6 +156,8 @@ class BDLRUCore(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.fused_bwd:
+            return BDLRUCore._backward_fused(ctx, dy)
         xz, xc, rg, carries, conv_w, conv_b, gate_w, gate_b, lam = ctx.saved_tensors
         seq = ctx.seq
         H2 = xz.shape[-1]
@@ -175,6 +188,30 @@ class BDLRUCore(torch.autograd.Function):
             torch.add(dxc, dxc_g, out=dxz[..., :H])
         if ctx.pad_len is not None:   # + the pad-prefix state's share, in place
             kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len, dh0.float(),
+                                   into=(dconv_b, dgate_w, dgate_b, dlam))
+        return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
+                dh0 if ctx.has_h0 else None, None, None, None, None, None)
+
+    @staticmethod
+    def _backward_fused(ctx, dy):
+        """rb_grl_bwd: conv, gates GEMM and the forward scan recomputed per
+        64-row tile from xz and the tile checkpoints; the adjoint scan, dz,
+        drg, dxc = drg W_g and the conv backward in the same launch.  Left
+        outside: dW_g = drg^T xc (rb_gemm_tn_h on the 32-row maxima the kernel
+        writes) and the column sums of the per-workgroup partials."""
+        xz, _, _, tile_carries, conv_w, conv_b, gate_w, gate_b, lam = ctx.saved_tensors
+        seq = ctx.seq
+        H = xz.shape[-1] // 2
+        rows = xz.shape[0]
+        want_rmax = ctx.want_rmax
+        (dxz, drg, xc, r_drg, r_xc, dlam, dgate_b, dh0, dconv_w, dconv_b) = kernels.grl_bwd(
+            xz, conv_w, conv_b, linear_mod._weight_split(gate_w, False),
+            linear_mod._weight_split(gate_w, True), gate_b, lam, ctx.h0, seq, tile_carries,
+            dy.contiguous(), last_only=ctx.last_only, want_rmax=want_rmax)
+        dgate_w = _timed("gemm", 2 * rows * H * 2 * H, wgrad, drg, xc, ymax=r_drg, xmax=r_xc)
+        dconv_w = dconv_w.view_as(conv_w)
+        if ctx.pad_len is not None:   # + the pad-prefix state's share, in place
+            kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len, dh0,
                                    into=(dconv_b, dgate_w, dgate_b, dlam))
         return (dxz, dconv_w, dconv_b, dgate_w, dgate_b, dlam,
                 dh0 if ctx.has_h0 else None, None, None, None, None, None)

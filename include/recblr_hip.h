@@ -508,13 +508,36 @@ int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int
  * rg [ntok, 2H] (the GEMM without gate_b), carries [B, n_tiles, H] (the
  * state entering every 16-step tile: rb_gate_scan_bwd's checkpoints) and
  * xc_rmax [ceil(ntok/32)] (max |xc| per 32-row group, the caller zeroes
- * it).  Replaces the reference's conv / gates Linear / gate math /
- * parallel_scan chain (RecBLR.py:173-206, parallel_scan.py:117). */
+ * it).  tile_carries [G, max_tiles, H] (optional): the state entering each
+ * of a workgroup's 64-row tiles, the checkpoints of rb_grl_bwd.  Replaces
+ * the reference's conv / gates Linear / gate math / parallel_scan chain
+ * (RecBLR.py:173-206, parallel_scan.py:117). */
 int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
                const float* conv_b, const void* wg_img, const float* gate_b, const float* lam,
                const float* h0, const int32_t* pieces, int64_t B, int64_t G, int64_t ntok,
                int64_t H, float* y, int64_t y_rs, float* y_last, float* xc, float* rg,
-               float* carries, int64_t n_tiles, float* xc_rmax, void* stream);
+               float* carries, int64_t n_tiles, float* xc_rmax, float* tile_carries,
+               int64_t max_tiles, void* stream);
+
+/* Backward of rb_grl_fwd in one launch (autograd of RecBLR.py:182-206 and
+ * parallel_scan.py:117's backward): the same pieces and 64-row tiles walked
+ * in reverse; conv, gates GEMM and the forward scan recomputed from xz and
+ * the forward's tile_carries; dy [ntok, H] or dy_last [B, H] (exactly one).
+ * Writes dxz [ntok, 2H] (dx | dz; row stride dxz_rs), drg [ntok, 2H] (the
+ * gates GEMM's output gradient), xc [ntok, H] (its input, for the weight
+ * gradient drg^T xc), optional drg_rmax / xc_rmax [ceil(ntok/32)] (32-row
+ * group maxima, zeroed by the caller), part [G, 4, H] (per workgroup:
+ * dLambda, d gate_b r and i halves, dh0) and cpart [8G, H kc + H] (per
+ * wave: d conv_w in [H, kc] order, d conv_b); column sums of part and cpart
+ * are the parameter gradients.  dxc = drg W_g runs inside on W_g^T's f16
+ * image (wgt_img: rb_gemm_h_split_weights of W_g^T, C = H, R = 2H). */
+int rb_grl_bwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
+               const float* conv_b, const void* wg_img, const void* wgt_img, const float* gate_b,
+               const float* lam, const float* h0, const int32_t* pieces, int64_t B, int64_t G,
+               int64_t ntok, int64_t H, const float* tile_carries, int64_t max_tiles,
+               const float* dy, const float* dy_last, float* dxz, int64_t dxz_rs, float* drg,
+               float* xc, float* drg_rmax, float* xc_rmax, float* part, float* cpart,
+               void* stream);
 
 /* Measurement aid (bench.py gemm.pattern; not on the model's path): the HBM
  * bytes of out[M, C] = a[M, R] W^T without the product — every row of a

@@ -76,16 +76,28 @@ def test_train_step_matches_oracle_with_split_gemm(cuda, split_gemm_calls, monke
 
     if threshold != "shipped":
         monkeypatch.setattr(linear, "SPLIT_MIN_ROWS", threshold)
+    from datamining_recblr_amd import kernels, recurrence
+
+    fused, fused_b = [], []
+    orig, orig_b = kernels.grl_fwd, kernels.grl_bwd
+    monkeypatch.setattr(kernels, "grl_fwd", lambda *a, **k: fused.append(1) or orig(*a, **k))
+    monkeypatch.setattr(kernels, "grl_bwd", lambda *a, **k: fused_b.append(1) or orig_b(*a, **k))
     ntok = _run(cuda, B, L, packed, True, seed=B + L)
     rows = ntok if packed else B * L
     big = [c for c in split_gemm_calls if c[0] == rows]
     # per layer and direction: in, gates, out (fwd) and their dX GEMMs; layer
-    # 0's FFN (the last layer's tail runs on the B gathered rows)
-    assert len(big) >= 12, (rows, split_gemm_calls)
-    # the five projection shapes of the encoder all went through the kernel
+    # 0's FFN (the last layer's tail runs on the B gathered rows).  Packed
+    # with RECBLR_FUSED_GRL=1, both gates GEMMs run inside the fused kernels
+    # (rb_grl_fwd / _bwd).
+    on = packed and recurrence._FUSED
+    assert len(big) >= (8 if on else 12), (rows, split_gemm_calls)
     shapes = {(c[1], c[2]) for c in big}
-    for s in ((128, 512), (256, 512), (256, 128), (512, 128), (512, 256)):
+    for s in ((128, 512), (256, 128), (512, 128), (128, 256)):
         assert s in shapes, (s, shapes)
+    if on:
+        assert len(fused) == 2 and len(fused_b) == 2, "fused GatedRecurrentLayer not engaged"
+    else:
+        assert (256, 512) in shapes and (512, 256) in shapes and not fused and not fused_b
     if threshold == 0:
         assert any(c[0] == B for c in split_gemm_calls), "gathered tail not on the kernel"
 

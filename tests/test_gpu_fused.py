@@ -1,8 +1,9 @@
-"""The fused GatedRecurrentLayer forward (csrc/grl_fused.hip, rb_grl_fwd):
-conv + SiLU, the behaviour-gate projection and the BD-LRU scan with the
-silu(z) merge in one launch (RecBLR.py:182-206), against the three-launch
-path it replaces (rb_conv_silu_fwd_rows, rb_gemm_nt_h, rb_gate_scan_fwd) on
-the same packed batch, and the whole model with it against the oracle.
+"""The fused GatedRecurrentLayer forward and backward (csrc/grl_fused.hip,
+rb_grl_fwd / rb_grl_bwd): conv + SiLU, the behaviour-gate projection and the
+BD-LRU scan with the silu(z) merge in one launch each way (RecBLR.py:182-206),
+against the three-launch path they replace (rb_conv_silu_fwd_rows,
+rb_gemm_nt_h, rb_gate_scan_fwd and the mirror-image backward) on the same
+packed batch, and the whole model with them against the unfused model.
 
 Bars: xc bit-identical (the same conv arithmetic); rg within fp32 level of
 the row's magnitude (both are f16x3 GEMMs; the scales differ); y, the
@@ -29,6 +30,7 @@ def _packed_batch(cuda, B, L, H, seed, fixed=False):
     seq = Packed(offs.to(cuda), L, ntok, pos.to(cuda))
     G = torch.cuda.get_device_properties(cuda).multi_processor_count
     seq.pieces, seq.G = grl_pieces(lens_p, offs, G).to(cuda), G
+    seq.max_tiles = kernels.grl_max_tiles(lens_p, G)
     xz = torch.randn(ntok, 2 * H, generator=g).to(cuda)
     conv_w = (torch.randn(H, 1, 4, generator=g) * 0.5).to(cuda)
     conv_b = (torch.randn(H, generator=g) * 0.1).to(cuda)
@@ -78,11 +80,68 @@ def test_fused_forward_matches_three_launch_path(cuda, B, L, fixed):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("last_only", [False, True], ids=["all_rows", "last_rows"])
+@pytest.mark.parametrize("B,L,fixed", [(2048, 200, False), (192, 200, True), (300, 50, False),
+                                       (7, 3, False), (64, 1, False), (1000, 130, False)])
+def test_fused_backward_matches_three_launch_path(cuda, B, L, fixed, last_only):
+    """rb_grl_bwd (from rb_grl_fwd's 64-row tile checkpoints) against
+    rb_gate_scan_bwd + the dxc GEMM + rb_conv_silu_bwd on the same batch:
+    xc bit-identical; dz, dx, drg and the parameter gradients within 1e-5 of
+    the tensor's max (the gates GEMM's f16x3 scales differ per row / tile;
+    the partial sums group differently); the 32-row maxima exact."""
+    kernels, seq, xz, conv_w, conv_b, gate_w, gate_b, lam, h0 = _packed_batch(cuda, B, L, 256,
+                                                                            7 * B + L, fixed)
+    H = 256
+    x, z = xz[:, :H], xz[:, H:]
+    g = torch.Generator().manual_seed(B)
+    dy = torch.randn((seq.B if last_only else seq.ntok, H), generator=g).to(cuda)
+    wf, wft = kernels.gemm_h_weight(gate_w), kernels.gemm_h_weight(gate_w.t().contiguous())
+    # the three-launch reference
+    xc_ref = kernels.conv_silu_fwd(x, conv_w, conv_b, seq=seq)
+    rg_ref = kernels.gemm_nt_h(xc_ref, wf, 2 * H)
+    _, car = kernels.gate_scan_fwd(rg_ref, xc_ref, z, lam, h0, gate_b=gate_b, seq=seq)
+    dxz_ref = torch.empty_like(xz)
+    drg_ref, dxc_ref, dlam_ref, dgb_ref, dh0_ref = kernels.gate_scan_bwd(
+        rg_ref, xc_ref, z, lam, car, dy, dxz_ref[:, H:], gate_b=gate_b, seq=seq,
+        last_only=last_only)
+    dxc_g = kernels.gemm_nt_h(drg_ref, wft, H)
+    dw_ref, db_ref = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc_ref, dxc_g, dxz_ref[:, :H],
+                                           seq=seq)
+    # fused
+    y, tc, *_ = kernels.grl_fwd(xz, conv_w, conv_b, wf, gate_b, lam, h0, seq,
+                                want_y=not last_only, tile_carries=True)
+    assert tc.shape == (seq.G, seq.max_tiles, H)
+    out = kernels.grl_bwd(xz, conv_w, conv_b, wf, wft, gate_b, lam, h0, seq, tc, dy,
+                          last_only=last_only, want_rmax=True)
+    dxz, drg, xc, r_drg, r_xc, dlam, dgb, dh0, dw, db = out
+    torch.cuda.synchronize()
+    assert torch.equal(xc, xc_ref)
+    for name, a, b in (("dz", dxz[:, H:], dxz_ref[:, H:]), ("dx", dxz[:, :H], dxz_ref[:, :H]),
+                       ("drg", drg, drg_ref), ("dlam", dlam, dlam_ref),
+                       ("dgate_b", dgb, dgb_ref), ("dh0", dh0, dh0_ref),
+                       ("dconv_w", dw.reshape(-1), dw_ref.reshape(-1)), ("dconv_b", db, db_ref)):
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))
+
+    def gmax(t):
+        m = torch.nn.functional.pad(t.abs().amax(1), (0, (-t.shape[0]) % 32)).view(-1, 32)
+        return m.amax(1)
+
+    assert torch.equal(r_xc, gmax(xc_ref))
+    assert torch.equal(r_drg, gmax(drg))
+    # deterministic
+    out2 = kernels.grl_bwd(xz, conv_w, conv_b, wf, wft, gate_b, lam, h0, seq, tc, dy,
+                           last_only=last_only, want_rmax=True)
+    for a, b in zip(out, out2):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("packed_len", ["ragged", "fixed"])
 def test_model_with_fused_forward_equals_three_launch(cuda, monkeypatch, packed_len):
     """RecBLR.calculate_loss + backward at d = 128 (H = 256): the fused
-    forward (default) and RECBLR_FUSED_GRL=0 give the same loss and
-    gradients within fp32 re-association, and the fused kernel ran."""
+    forward and backward (default), the fused forward with the three-launch
+    backward (RECBLR_FUSED_GRL_BWD=0) and RECBLR_FUSED_GRL=0 give the same
+    loss and gradients within fp32 re-association, and the fused kernels
+    ran."""
     from datamining_recblr_amd import kernels, recurrence
     from datamining_recblr_amd.distributed import synthetic_interaction
     from datamining_recblr_amd.model import RecBLR
@@ -102,17 +161,25 @@ def test_model_with_fused_forward_equals_three_launch(cuda, monkeypatch, packed_
         return orig(*a, **kw)
 
     monkeypatch.setattr(kernels, "grl_fwd", counted)
+    bwd = []
+    orig_b = kernels.grl_bwd
+    monkeypatch.setattr(kernels, "grl_bwd", lambda *a, **k: bwd.append(1) or orig_b(*a, **k))
     res = {}
-    for fused in (True, False):
+    for fused, fused_bwd in ((True, True), (True, False), (False, False)):
         monkeypatch.setattr(recurrence, "_FUSED", fused)
+        monkeypatch.setattr(recurrence, "_FUSED_BWD", fused_bwd)
+        calls.clear()
+        bwd.clear()
         model.zero_grad(set_to_none=True)
         loss = model.calculate_loss(inter)
         loss.backward()
-        res[fused] = (loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()
-                                    if p.grad is not None})
-        if fused:
-            assert len(calls) == 2, calls   # both layers
-    assert abs(res[True][0] - res[False][0]) < 1e-6 * max(1.0, abs(res[False][0]))
-    for n, gr in res[False][1].items():
-        err = (res[True][1][n] - gr).abs().max().item()
-        assert err <= 1e-6 + 1e-5 * gr.abs().max().item(), (n, err)
+        res[fused, fused_bwd] = (loss.item(), {n: p.grad.clone() for n, p in model.named_parameters()
+                                               if p.grad is not None})
+        assert len(calls) == (2 if fused else 0), calls   # both layers
+        assert len(bwd) == (2 if fused_bwd else 0), bwd
+    ref = res[False, False]
+    for key in ((True, True), (True, False)):
+        assert abs(res[key][0] - ref[0]) < 1e-6 * max(1.0, abs(ref[0]))
+        for n, gr in ref[1].items():
+            err = (res[key][1][n] - gr).abs().max().item()
+            assert err <= 1e-6 + 1e-5 * gr.abs().max().item(), (key, n, err)
