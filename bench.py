@@ -791,6 +791,22 @@ def main():
                                 "as RecBole's Trainer (run.py) does; the hook on Interaction.to "
                                 "keeps the host lengths (recbole_compat.install_interaction_hook)")
         devlen["recbole_interaction_path"] = recbole_path
+    fused_ab = None
+    if not args.no_full_tail:
+        # the fused GatedRecurrentLayer kernels (csrc/grl_fused.hip): the
+        # headline runs rb_grl_fwd + the three-launch backward; A/B against
+        # the one-launch backward and against no fusion, same batches
+        from datamining_recblr_amd import recurrence
+        saved_f = (recurrence._FUSED, recurrence._FUSED_BWD)
+        fused_ab = {}
+        for name, f, fb in (("fused_fwd_and_bwd", True, True), ("unfused", False, False)):
+            recurrence._FUSED, recurrence._FUSED_BWD = f, fb
+            fused_ab[name] = timed_variant(True, True)
+        recurrence._FUSED, recurrence._FUSED_BWD = saved_f
+        fused_ab["headline"] = {"fused_fwd": saved_f[0], "fused_bwd": saved_f[1]}
+        fused_ab["note"] = ("RECBLR_FUSED_GRL / RECBLR_FUSED_GRL_BWD A/B on the headline's "
+                            "batches: rb_grl_fwd (conv + gates GEMM + scan) with the "
+                            "three-launch backward is the default; rb_grl_bwd is opt-in")
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)
@@ -872,7 +888,7 @@ def main():
         tot_b = sum(d["bytes"] for d in hbm)
         tot_ms = sum(d["ms"] for d in hbm)
         core = [summ[n] for n in ("rb_conv_silu_fwd", "rb_gate_scan_fwd", "rb_gate_scan_bwd",
-                                  "rb_conv_silu_bwd") if n in summ]
+                                  "rb_conv_silu_bwd", "rb_grl_fwd", "rb_grl_bwd") if n in summ]
         if core:   # BASELINE's target: the fused scan + conv + gate path
             cb = sum(d["bytes"] for d in core)
             cms = sum(d["ms"] for d in core)
@@ -932,6 +948,7 @@ def main():
             "kernels": kernels_report,
             "fixed_length": fixed,
             "device_lengths": devlen,
+            "fused_grl": fused_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

@@ -701,7 +701,7 @@ int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
     return fail("rb_grl_fwd: bad sizes");
   if (!y == !y_last) return fail("rb_grl_fwd: exactly one of y / y_last");
   if (xz_rs < 2 * H || xz_rs % 4 || !aligned16(xz)) return fail("rb_grl_fwd: xz layout");
-  if (y && y_rs < H) return fail("rb_grl_fwd: y row stride");
+  if (y && (y_rs < H || y_rs % 4 || !aligned16(y))) return fail("rb_grl_fwd: y layout");
   if (ntok * (y && y_rs > xz_rs ? y_rs : xz_rs) >= (1LL << 31))   // 32-bit element offsets
     return fail("rb_grl_fwd: ntok * row stride must be < 2^31");
   if (carries && n_tiles <= 0) return fail("rb_grl_fwd: carries need n_tiles");

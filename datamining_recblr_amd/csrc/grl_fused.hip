@@ -54,15 +54,39 @@ constexpr int LDS_ROW = LDS_ER + GT * 4;       // per row: global row
 constexpr int LDS_POS = LDS_ROW + GT * 4;       //          position in its sequence (-1: none)
 constexpr int LDS_SEQ = LDS_POS + GT * 4;       //          packed sequence index
 constexpr int LDS_LAST = LDS_SEQ + GT * 4;      //          last row of its sequence
-constexpr int LDS_BYTES = LDS_LAST + GT * 4;
+constexpr int LDS_CW = LDS_LAST + GT * 4;       // conv weights [H][KC] and bias [H] (once)
+constexpr int LDS_BYTES = LDS_CW + GH * 4 * 4 + GH * 4;
 
 typedef int i32x4g __attribute__((ext_vector_type(4)));
 
 // Ablation switches of tools/grlbench.hip (wrong results; never set in the
 // library build): 1 weight fragments not loaded, 2 no gates GEMM at all,
-// 4 no x / xz row loads, 8 no per-channel z / dy loads and y / dz / drg stores
+// 4 no x / xz row loads, 8 no per-channel z / dy loads and y / dz / drg stores,
+// 16 no y stores (forward), 32 no xc / dx row stores (backward)
 #ifndef GRL_PROBE
 #define GRL_PROBE 0
+#endif
+// -DGRL_STAMPS (tools/grlbench.hip only): per-phase cycle sums of every wave
+// (the stamps' lgkmcnt(0) waits perturb the overlap: read shares)
+#ifdef GRL_STAMPS
+__device__ unsigned long long grl_stamps[2][20];
+#define GRL_STAMP(k)                                                           \
+  do {                                                                         \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    unsigned long long t_;                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                         \
+    if ((k) >= 0) st_acc[(k) < 0 ? 0 : (k)] += t_ - st_prev;                   \
+    st_prev = t_;                                                              \
+  } while (0)
+#define GRL_STAMP_DECL unsigned long long st_acc[20] = {}, st_prev = 0
+#define GRL_STAMP_FLUSH(w) \
+  if (lane == 0)           \
+    for (int k_ = 0; k_ < 20; ++k_) atomicAdd(&grl_stamps[w][k_], st_acc[k_])
+#else
+#define GRL_STAMP(k) do {} while (0)
+#define GRL_STAMP_DECL do {} while (0)
+#define GRL_STAMP_FLUSH(w) do {} while (0)
 #endif
 
 __device__ __forceinline__ f32x16g mfma_g(f16x8g a, f16x8g b, f32x16g c) {
@@ -76,6 +100,29 @@ __device__ __forceinline__ f32x16g mfma_g(f16x8g a, f16x8g b, f32x16g c) {
 __device__ __forceinline__ int opaque(int x) {
   asm volatile("" : "+v"(x));
   return x;
+}
+
+// The lane id again, from an instruction the compiler may neither hoist nor
+// reuse: per-phase lane-dependent bases are rebuilt (two VALU ops) instead of
+// being kept live across the whole tile loop, where they spilled
+__device__ __forceinline__ int fresh_lane() {
+  int x;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(x));
+  return x;
+}
+
+__device__ __forceinline__ float opaque_f(float x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// Workgroup barrier ordering LDS only: the kernels never read global memory
+// another wave wrote, so the row stores (y, dxz, drg, xc) stay in flight
+// across it (__syncthreads would drain them at every phase: vmcnt(0))
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -150,27 +197,88 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
   float carry = 0.0f;                      // state entering the tile (channel c)
   // virtual-row cursor over the pieces (wave-uniform)
   int cur_p = pb, cur_off = 0;
-
-  for (int v0 = 0; v0 < span_rows; v0 += GT) {
-    if (a.tile_carries && h == 0)
-      a.tile_carries[((int64_t)g * a.max_tiles + v0 / GT) * GH + c] = carry;
-    // ---- row map of the tile: lane r describes virtual row v0 + r
+  // row map of the tile at the cursor (lane r: virtual row r; row -1 past
+  // the span) and the cursor past it
+  int mrow, mpos, mseq, mlast;
+  auto row_map = [&]() {
     int rp = cur_p, roff = cur_off + lane;
     while (rp < pe && roff >= p_len[rp]) {
       roff -= p_len[rp];
       ++rp;
     }
     const bool rvalid = rp < pe;
-    const int rrow = rvalid ? p_row[rp] + roff : 0;          // global row
-    const int rpos = rvalid ? roff : -1;                     // position in its sequence
-    const int rseq = rvalid ? p_seq[rp] : 0;
-    const bool rlast = rvalid && roff == p_len[rp] - 1;
-    {  // advance the cursor past this tile (lane 63's row + 1)
-      int np = __builtin_amdgcn_readlane(rp, 63), noff = __builtin_amdgcn_readlane(roff, 63) + 1;
-      if (np < pe && noff >= p_len[np]) { ++np; noff = 0; }
-      cur_p = np;
-      cur_off = noff;
+    mrow = rvalid ? p_row[rp] + roff : 0;
+    mpos = rvalid ? roff : -1;
+    mseq = rvalid ? p_seq[rp] : 0;
+    mlast = rvalid && roff == p_len[rp] - 1;
+    int np = __builtin_amdgcn_readlane(rp, 63), noff = __builtin_amdgcn_readlane(roff, 63) + 1;
+    if (np < pe && noff >= p_len[np]) { ++np; noff = 0; }
+    cur_p = np;
+    cur_off = noff;
+  };
+  // Register prefetch, one tile ahead: phase A's x rows (this wave's 8 rows
+  // and the KC-1 rows before its first) are issued right after phase A has
+  // used the current ones, phase D's z values right after phase D; both
+  // land while the GEMM and the scan of the current tile run.
+  f32x4g xo[8], xh[KC - 1];
+  float zp[2][16];
+  auto load_x = [&]() {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int vr = 8 * wave + j;
+      const int grow = __builtin_amdgcn_readlane(mrow, vr);
+      const int pos = __builtin_amdgcn_readlane(mpos, vr);
+      xo[j] = pos >= 0 && !(GRL_PROBE & 4)
+                  ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)(grow * xzr + 4 * lane))
+                  : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
     }
+    const int g0 = __builtin_amdgcn_readlane(mrow, 8 * wave);
+    const int p0 = __builtin_amdgcn_readlane(mpos, 8 * wave);
+#pragma unroll
+    for (int i = 0; i < KC - 1; ++i) {   // row g0 - (KC - 1 - i)
+      const int l = KC - 1 - i;
+      xh[i] = p0 >= l && !(GRL_PROBE & 4)
+                  ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((g0 - l) * xzr + 4 * lane))
+                  : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+  };
+  auto load_z = [&](int rb) {   // C layout: row 32 rb + 8 (e / 4) + 4 h + e % 4
+    const int rv = mpos >= 0 ? mrow : -1;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
+        const int r0 = __builtin_amdgcn_readlane(rv, rc), r1 = __builtin_amdgcn_readlane(rv, rc + 4);
+        const int grow = h ? r1 : r0;
+        zp[rb][e] = grow >= 0 && !(GRL_PROBE & 8) ? a.xz[(uint32_t)(grow * xzr + GH + c)] : 0.0f;
+      }
+  };
+  // conv weights and bias -> LDS once (phase A then issues no global loads
+  // of its own: a vector-memory wait there would also wait for the prefetch)
+  for (int i = tid; i < GH * KC; i += 512)
+    reinterpret_cast<float*>(smem + LDS_CW)[(i / KC) * 4 + i % KC] = a.conv_w[i];
+  for (int i = tid; i < GH; i += 512) reinterpret_cast<float*>(smem + LDS_CW + GH * 16)[i] = a.conv_b[i];
+  row_map();
+  load_x();
+  load_z(0);
+  load_z(1);
+  lds_sync();
+  auto store_y = [&]() {
+    const char* yb = smem + opaque(LDS_XC + 16 * lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int vr = 8 * wave + j;
+      if (s_pos[vr] >= 0 && !(GRL_PROBE & 24))
+        __builtin_nontemporal_store(*reinterpret_cast<const f32x4g*>(yb + vr * XC_PITCH),
+                                    reinterpret_cast<f32x4g*>(a.y + (uint32_t)(s_row[vr] * yr + 4 * lane)));
+    }
+  };
+
+  GRL_STAMP_DECL;
+  GRL_STAMP(-1);
+  for (int v0 = 0; v0 < span_rows; v0 += GT) {
+    if (a.tile_carries && h == 0)
+      a.tile_carries[((int64_t)g * a.max_tiles + v0 / GT) * GH + c] = carry;
+    const bool more = v0 + GT < span_rows;
 
     // per-lane LDS bases of this tile (see opaque())
     // (region offsets inside opaque(): the per-row constants fold into the
@@ -181,35 +289,40 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
     char* const db = smem + opaque(LDS_ER + 16 * h);               // per-row int arrays
     char* const xb = smem + opaque(LDS_XC + 4 * h * XC_PITCH + 4 * c);   // s_xc[4h][c]
     char* const gb = smem + opaque(LDS_PLANE0 + lane * 16);         // GEMM A fragments
+    GRL_STAMP(0);
+    // the previous tile's y rows, whole 1 KB rows from LDS (phase D left
+    // them in the xc slots: per-lane 4-byte stores there cost 20 % more)
+    if (a.y && v0 > 0) store_y();
     // ---- phase A: conv + SiLU, LDS images (channels 4*lane .. 4*lane+3)
     float cw[KC][4], cb[4];
+    {
+      const char* cwp = smem + opaque(LDS_CW + 64 * lane);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
+      for (int v = 0; v < 4; ++v) {
+        const f32x4g w4 = *reinterpret_cast<const f32x4g*>(cwp + 16 * v);
 #pragma unroll
-      for (int k = 0; k < KC; ++k) cw[k][v] = a.conv_w[(4 * lane + v) * KC + k];
-      cb[v] = a.conv_b[4 * lane + v];
+        for (int k = 0; k < KC; ++k) cw[k][v] = w4[k];
+      }
+      const f32x4g b4 = *reinterpret_cast<const f32x4g*>(smem + opaque(LDS_CW + GH * 16 + 16 * lane));
+#pragma unroll
+      for (int v = 0; v < 4; ++v) cb[v] = b4[v];
     }
-#pragma unroll 2
+#pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int vr = 8 * wave + j;
-      const int grow = __builtin_amdgcn_readlane(rrow, vr);
-      const int pos = __builtin_amdgcn_readlane(rpos, vr);   // -1: past the span
+      const int grow = __builtin_amdgcn_readlane(mrow, vr);
+      const int pos = __builtin_amdgcn_readlane(mpos, vr);   // -1: past the span
       f32x4g xcv = {0.0f, 0.0f, 0.0f, 0.0f};
       if (pos >= 0) {
-        f32x4g xs[KC];
-#pragma unroll
-        for (int k = 0; k < KC; ++k) {
-          if (KC - 1 - k <= pos && !(GRL_PROBE & 4))
-            xs[k] = *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((grow - (KC - 1 - k)) * xzr + 4 * lane));
-          else
-            xs[k] = f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
-        }
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           float acc = cb[v];
 #pragma unroll
-          for (int k = 0; k < KC; ++k)   // lag KC-1-k: rows before the sequence start are zero
-            acc = acc + (KC - 1 - k <= pos ? cw[k][v] * xs[k][v] : 0.0f);
+          for (int k = 0; k < KC; ++k) {   // lag l: rows before the sequence start are zero
+            const int l = KC - 1 - k;
+            const float xv = j - l >= 0 ? xo[j - l >= 0 ? j - l : 0][v] : xh[j - l >= 0 ? 0 : KC - 1 + j - l][v];
+            acc = acc + (l <= pos ? cw[k][v] * xv : 0.0f);
+          }
           xcv[v] = fsilu(acc);
         }
         if (a.xc_out) __builtin_nontemporal_store(xcv, reinterpret_cast<f32x4g*>(a.xc_out + (uint32_t)(grow * GH + 4 * lane)));
@@ -223,8 +336,8 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
         s_er[vr] = e;
         s_row[vr] = grow;
         s_pos[vr] = pos;
-        s_seq[vr] = __builtin_amdgcn_readlane(rseq, vr);
-        s_last[vr] = __builtin_amdgcn_readlane((int)rlast, vr);
+        s_seq[vr] = __builtin_amdgcn_readlane(mseq, vr);
+        s_last[vr] = __builtin_amdgcn_readlane(mlast, vr);
       }
       const float sc = __builtin_amdgcn_ldexpf(1.0f, kSWg - e);
       f16x4g h0v, h1v;
@@ -242,7 +355,9 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
       *reinterpret_cast<f16x4g*>(ab_fr + fo) = h0v;
       *reinterpret_cast<f16x4g*>(ab_fr + PLANE_BYTES + fo) = h1v;
     }
-    __syncthreads();
+    GRL_STAMP(1);
+    lds_sync();
+    GRL_STAMP(2);
 
     // ---- phase C: r / i columns of channels 32w.. for the 64 rows
     f32x16g ar[2], ai[2];
@@ -259,13 +374,15 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
       return *reinterpret_cast<const f16x8g*>(base + kb * 2048 + p * 1024 + wl);
 #endif
     };
+    // weight fragments two k16 steps ahead (L2 latency over one step's MFMAs)
     f16x8g br0 = wfrag(wr, 0, 0), br1 = wfrag(wr, 0, 1), bi0 = wfrag(wi, 0, 0), bi1 = wfrag(wi, 0, 1);
+    f16x8g nr0 = wfrag(wr, 1, 0), nr1 = wfrag(wr, 1, 1), ni0 = wfrag(wi, 1, 0), ni1 = wfrag(wi, 1, 1);
 #pragma unroll 1
     for (int kb = 0; kb < ((GRL_PROBE & 2) ? 0 : KBG); ++kb) {
-      f16x8g nr0, nr1, ni0, ni1;
-      if (kb + 1 < KBG) {
-        nr0 = wfrag(wr, kb + 1, 0); nr1 = wfrag(wr, kb + 1, 1);
-        ni0 = wfrag(wi, kb + 1, 0); ni1 = wfrag(wi, kb + 1, 1);
+      f16x8g mr0, mr1, mi0, mi1;
+      if (kb + 2 < KBG) {
+        mr0 = wfrag(wr, kb + 2, 0); mr1 = wfrag(wr, kb + 2, 1);
+        mi0 = wfrag(wi, kb + 2, 0); mi1 = wfrag(wi, kb + 2, 1);
       }
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
@@ -279,7 +396,15 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
         ai[rb] = mfma_g(a0, bi1, ai[rb]);
         ai[rb] = mfma_g(a0, bi0, ai[rb]);
       }
-      if (kb + 1 < KBG) { br0 = nr0; br1 = nr1; bi0 = ni0; bi1 = ni1; }
+      br0 = nr0; br1 = nr1; bi0 = ni0; bi1 = ni1;
+      if (kb + 2 < KBG) { nr0 = mr0; nr1 = mr1; ni0 = mi0; ni1 = mi1; }
+    }
+    // the next tile's row map and x rows, issued behind the last weight loads
+    // (vector-memory waits are in order: a later weight wait would wait for
+    // them too) and landing under phase D and the next phase A
+    if (more) {
+      row_map();
+      load_x();
     }
 
 #define DROW(rc) (*reinterpret_cast<const int*>(db + (LDS_ROW - LDS_ER) + 4 * (rc)))
@@ -287,17 +412,12 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
 #define DSEQ(rc) (*reinterpret_cast<const int*>(db + (LDS_SEQ - LDS_ER) + 4 * (rc)))
 #define DLAST(rc) (*reinterpret_cast<const int*>(db + (LDS_LAST - LDS_ER) + 4 * (rc)))
 #define DER(rc) (*reinterpret_cast<const int*>(db + 4 * (rc)))
+    GRL_STAMP(3);
     // ---- phase D: gates, scan, merge (lane: channel c, rows of its C layout),
     // one 32-row block at a time; alpha -> ar, b' -> ai in place
     float run = carry;
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb) {
-      float zr[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);   // row = rc + 4h
-        zr[e] = DPOS(rc) >= 0 && !(GRL_PROBE & 8) ? a.xz[(uint32_t)(DROW(rc) * xzr + GH + c)] : 0.0f;
-      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);   // row = rc + 4h
@@ -359,13 +479,14 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
             a.carries[(uint32_t)((DSEQ(rc) * a.nTc + (pos >> 4)) * GH + c)] = hp;
           const float hn = hp * ar[rb][e] + ai[rb][e];
           hp = hn;
-          const float yv = fsilu(zr[e]) * hn;
-          if (pos >= 0 && !(GRL_PROBE & 8)) {
-            if (a.y) a.y[(uint32_t)(DROW(rc) * yr + c)] = yv;
-            else if (a.y_last && DLAST(rc)) a.y_last[(uint32_t)(DSEQ(rc) * GH + c)] = yv;
-          }
+          const float yv = fsilu(zp[rb][e]) * hn;
+          if (a.y)   // over this (row, channel)'s xc, read above
+            *reinterpret_cast<float*>(xb + rc * XC_PITCH) = yv;
+          else if (pos >= 0 && a.y_last && DLAST(rc) && !(GRL_PROBE & 24))
+            a.y_last[(uint32_t)(DSEQ(rc) * GH + c)] = yv;
         }
       }
+      if (more) load_z(rb);   // this block's z of the next tile (its row map is current)
     }
     carry = run;
 #undef DROW
@@ -373,45 +494,50 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
 #undef DSEQ
 #undef DLAST
 #undef DER
-    __syncthreads();   // LDS is rewritten by the next tile
+    GRL_STAMP(4);
+    lds_sync();   // LDS is rewritten by the next tile
+    GRL_STAMP(5);
   }
+  if (a.y) store_y();
+  GRL_STAMP_FLUSH(0);
 }
 
 // ---------------------------------------------------------------------------
 // Backward of k_grl_fwd, one launch per layer (RecBLR.py:182-206 reversed):
 // the same work lists, each workgroup walking its virtual rows in REVERSE
 // 64-row tiles, the adjoint state carried across tiles.  Per tile:
-//   A  row-wide: conv pre-activations recomputed from x (-> LDS R0, fp32),
-//      xc = silu(pre) to HBM (the gates weight gradient's operand) and as
-//      the f16 A planes of GEMM 1 (-> LDS R1)
+//   A  row-wide: xc = silu(conv(x)) recomputed (-> LDS R0, fp32; and to HBM,
+//      the gates weight gradient's operand), as the f16 A planes of GEMM 1
+//      (-> LDS R1)
 //   C  GEMM 1: r / i of channels 32w.. (as the forward)
 //   D  C layout: gates; the forward scan from the tile's checkpoint (the
-//      forward's tile_carries) gives h_{t-1} (-> LDS R1, the planes are
-//      spent) and dz; the reverse adjoint scan (e_t = a_t (gy_t + e_{t+1}),
-//      reset at each sequence's last row) gives d = dL/dh, then dr, di (to
-//      HBM), dxc's direct term, the partial sums of dLambda, d gate_b, dh0
-//   E  each row of drg scaled by its exact max over all 512 columns (a
-//      reduce-scatter inside the wave, then across waves in LDS)
-//   F  GEMM 2: dxc_g = drg W_g for channels 32w.. (W_g^T's image), in two
-//      K halves: dr's fp16 planes (row-major, LDS R0), then di's
-//   G  dpre = dxc_direct silu'(pre) (LDS R1, written in D) + dxc_g silu'(pre)
-//      (-> LDS R0)
-//   H  row-wide: the conv backward, dx (dpre of the next 3 rows: this tile
-//      or the later tile's first rows, kept in LDS), dW / dbias partials
-constexpr int DRG_PITCH = GH * 2 + 16;         // a row-major fp16 plane row of one drg half (dr or di)
-constexpr int B_R0_BYTES = 2 * GT * DRG_PITCH > GT * XC_PITCH ? 2 * GT * DRG_PITCH : GT * XC_PITCH;
-constexpr int B_R0 = 0;                        // pre / the drg half's planes / dpre
-constexpr int B_R1 = B_R0_BYTES;               // xc planes / h_{t-1} / dpre's direct term
+//      forward's tile_carries): dz (to HBM) and gy = dy silu(z) (-> R1, the
+//      planes are spent); the reverse adjoint scan (e_t = a_t (gy_t +
+//      e_{t+1}), reset at each sequence's last row) gives d = dL/dh, then
+//      dr, di, dxc's direct term (kept in registers) and the partial sums of
+//      dLambda, d gate_b, dh0
+//   E  dr -> R0, di -> R1 (fp32, row-major); then row-wide: each drg row to
+//      HBM in 1 KB pieces, its exact max over 512 columns, and in place its
+//      f16 planes (x = 2^-s (x0 + x1)) as GEMM 2's A operand
+//   F  GEMM 2: dxc_g = drg W_g for channels 32w.. (W_g^T's image), K = 512
+//   G  dxc = dxc_g + the direct term (-> R0, C layout)
+//   H  row-wide: H1 pre-activations again from x (the rows dW needs anyway),
+//      dpre = dxc silu'(pre) in place, dW / dbias partials; H2 dx from dpre of
+//      the row and the next KC-1 (later rows: R0 or the halo of the later tile)
+// Only the per-lane dz stores are 4-byte scattered; every other row stream is
+// written in 16-B lane pieces of whole rows.
+constexpr int B_R0 = 0;                        // xc / dr (fp32, then planes) / dxc, dpre
+constexpr int B_R1 = GT * XC_PITCH;            // xc planes / gy / di (fp32, then planes)
 constexpr int B_HALO = B_R1 + GT * XC_PITCH;   // 3 rows of dpre (the later tile's first rows)
 constexpr int B_ER = B_HALO + 3 * XC_PITCH;    // xc row exponents
 constexpr int B_ER2 = B_ER + GT * 4;           // drg row exponents
-constexpr int B_RMX = B_ER2 + GT * 4;          // drg row maxima
-constexpr int B_ROW = B_RMX + GT * 4;
+constexpr int B_ROW = B_ER2 + GT * 4;
 constexpr int B_POS = B_ROW + GT * 4;
 constexpr int B_SEQ = B_POS + GT * 4;
 constexpr int B_LAST = B_SEQ + GT * 4;         // rows left to the sequence's end (0: last)
-constexpr int B_PMAX = B_LAST + GT * 4;        // [8 waves][64 rows] partial drg row maxima
-constexpr int B_LDS_BYTES = B_PMAX + 8 * GT * 4;
+constexpr int B_CW = B_LAST + GT * 4;          // conv weights [H][4] and bias [H] (once)
+constexpr int B_LDS_BYTES = B_CW + GH * 16 + GH * 4;
+constexpr int PL_LO = GH * 2;                  // a drg half's lo plane, bytes into its row
 
 struct GrlBwdArgs {
   const float* xz;
@@ -467,7 +593,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
 
   const int c = 32 * wave + (lane & 31);
   const float lamc = a.lam[c];
-  const float nsp = -softplus_f(lamc);
+  const float nsp = -softplus_f(lamc), nsp_k = nsp;
   const float br = a.gate_b[c], bi = a.gate_b[GH + c];
   const int ec_r = a.ew[c], ec_i = a.ew[GH + c], ec_t = a.ewt[c];
   const float hz = a.h0 ? a.h0[c] : 0.0f;
@@ -476,6 +602,11 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
   const char* wr = reinterpret_cast<const char*>(a.wf) + (int64_t)wave * KBG * 2048;
   const char* wi = reinterpret_cast<const char*>(a.wf) + (int64_t)(8 + wave) * KBG * 2048;
   const char* wt = reinterpret_cast<const char*>(a.wft) + (int64_t)wave * (2 * KBG) * 2048;
+
+  // conv weights and bias -> LDS once
+  for (int i = tid; i < GH * KC; i += 512)
+    reinterpret_cast<float*>(smem + B_CW)[(i / KC) * 4 + i % KC] = a.conv_w[i];
+  for (int i = tid; i < GH; i += 512) reinterpret_cast<float*>(smem + B_CW + GH * 16)[i] = a.conv_b[i];
 
   float acc_v = 0.0f, acc_r = 0.0f, acc_i = 0.0f, acc_h = 0.0f;   // channel c
   float cw_acc[KC][4], cb_acc[4];                                  // channels 4*lane..
@@ -490,7 +621,25 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
   // cursor at the last tile's first virtual row
   int cur_p = pb, cur_off = (n_tiles - 1) * GT;
   while (cur_off >= p_len[cur_p]) { cur_off -= p_len[cur_p]; ++cur_p; }
+  lds_sync();
 
+  // conv weights of channels 4*lane.. from LDS (fresh bases: not kept live)
+  auto conv_weights = [&](float (&cw)[KC][4], float (&cbv)[4]) {
+    const int lf = fresh_lane();
+    const char* cwp = smem + (B_CW + 64 * lf);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const f32x4g w4 = *reinterpret_cast<const f32x4g*>(cwp + 16 * v);
+#pragma unroll
+      for (int k = 0; k < KC; ++k) cw[k][v] = w4[k];
+    }
+    const f32x4g b4 = *reinterpret_cast<const f32x4g*>(smem + (B_CW + GH * 16 + 16 * lf));
+#pragma unroll
+    for (int v = 0; v < 4; ++v) cbv[v] = b4[v];
+  };
+
+  GRL_STAMP_DECL;
+  GRL_STAMP(-1);
   for (int t = n_tiles - 1; t >= 0; --t) {
     if (t != n_tiles - 1) {   // move the cursor back by one tile
       cur_off -= GT;
@@ -504,33 +653,20 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
     const int rseq = rvalid ? p_seq[rp] : 0;
     const int rrem = rvalid ? p_len[rp] - 1 - roff : -1;     // rows to the sequence's end
 
-    // per-lane LDS bases; every region's offset is inside opaque() so the
-    // per-row constants stay below 64 KiB and fold into ds_* immediates
-    char* const ab_pre = smem + opaque(B_R0 + 16 * lane);
-    char* const ab_fr = smem + opaque(B_R1 + (lane >> 2) * FRAG_PITCH + 32 * ((lane >> 1) & 1) * 16 +
-                                      8 * (lane & 1));
-    char* const db = smem + opaque(B_ER + 16 * h);                 // per-row int arrays
-    char* const r0c = smem + opaque(B_R0 + 4 * h * XC_PITCH + 4 * c);   // R0 [4h][c]
-    char* const r1c = smem + opaque(B_R1 + 4 * h * XC_PITCH + 4 * c);   // R1 [4h][c]
-    char* const gb = smem + opaque(B_R1 + lane * 16);
-    // GEMM 2's A fragment of lane l: row l % 32, halfs 8 (l / 32) .. + 7 of a k16 block
-    char* const g2 = smem + B_R0 + opaque((lane & 31) * DRG_PITCH + 16 * (lane >> 5));
-
-    // ---- A: pre-activations, xc, its f16 planes
+    GRL_STAMP(0);
+    // ---- A: xc (fp32 -> R0, HBM), its f16 planes (-> R1)
     {
       float cw[KC][4], cbv[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-#pragma unroll
-        for (int k = 0; k < KC; ++k) cw[k][v] = a.conv_w[(4 * lane + v) * KC + k];
-        cbv[v] = a.conv_b[4 * lane + v];
-      }
+      conv_weights(cw, cbv);
+      char* const ab_xc = smem + opaque(B_R0 + 16 * lane);
+      char* const ab_fr = smem + opaque(B_R1 + (lane >> 2) * FRAG_PITCH + 32 * ((lane >> 1) & 1) * 16 +
+                                        8 * (lane & 1));
 #pragma unroll 2
       for (int j = 0; j < 8; ++j) {
         const int vr = 8 * wave + j;
         const int grow = __builtin_amdgcn_readlane(rrow, vr);
         const int pos = __builtin_amdgcn_readlane(rpos, vr);
-        f32x4g pre = {0.0f, 0.0f, 0.0f, 0.0f}, xcv = {0.0f, 0.0f, 0.0f, 0.0f};
+        f32x4g xcv = {0.0f, 0.0f, 0.0f, 0.0f};
         if (pos >= 0) {
           f32x4g xs[KC];
 #pragma unroll
@@ -544,12 +680,12 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
 #pragma unroll
             for (int k = 0; k < KC; ++k)
               acc = acc + (KC - 1 - k <= pos ? cw[k][v] * xs[k][v] : 0.0f);
-            pre[v] = acc;
             xcv[v] = fsilu(acc);
           }
+          if (!(GRL_PROBE & 32))
           __builtin_nontemporal_store(xcv, reinterpret_cast<f32x4g*>(a.xc_out + (uint32_t)(grow * GH + 4 * lane)));
         }
-        *reinterpret_cast<f32x4g*>(ab_pre + vr * XC_PITCH) = pre;
+        *reinterpret_cast<f32x4g*>(ab_xc + vr * XC_PITCH) = xcv;
         const float m = wave_max(fmaxf(fmaxf(fabsf(xcv[0]), fabsf(xcv[1])), fmaxf(fabsf(xcv[2]), fabsf(xcv[3]))));
         const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
         if (lane == 0) {
@@ -576,7 +712,9 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         *reinterpret_cast<f16x4g*>(ab_fr + PLANE_BYTES + fo) = h1v;
       }
     }
-    __syncthreads();
+    GRL_STAMP(1);
+    lds_sync();
+    GRL_STAMP(2);
 
     // ---- C: GEMM 1 (r, i)
     f32x16g ar[2], ai[2];
@@ -586,6 +724,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
       for (int e = 0; e < 16; ++e) { ar[rb][e] = 0.0f; ai[rb][e] = 0.0f; }
     {
       const int wl = opaque(lane * 16);
+      const char* const gb = smem + opaque(B_R1 + lane * 16);
       auto wfrag = [&](const char* base, int kb, int p) {
 #if GRL_PROBE & 1
         return f16x8g{} + (_Float16)(kb + p);
@@ -594,12 +733,13 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
 #endif
       };
       f16x8g br0 = wfrag(wr, 0, 0), br1 = wfrag(wr, 0, 1), bi0 = wfrag(wi, 0, 0), bi1 = wfrag(wi, 0, 1);
+      f16x8g nr0 = wfrag(wr, 1, 0), nr1 = wfrag(wr, 1, 1), ni0 = wfrag(wi, 1, 0), ni1 = wfrag(wi, 1, 1);
 #pragma unroll 1
       for (int kb = 0; kb < ((GRL_PROBE & 2) ? 0 : KBG); ++kb) {
-        f16x8g nr0, nr1, ni0, ni1;
-        if (kb + 1 < KBG) {
-          nr0 = wfrag(wr, kb + 1, 0); nr1 = wfrag(wr, kb + 1, 1);
-          ni0 = wfrag(wi, kb + 1, 0); ni1 = wfrag(wi, kb + 1, 1);
+        f16x8g mr0, mr1, mi0, mi1;
+        if (kb + 2 < KBG) {
+          mr0 = wfrag(wr, kb + 2, 0); mr1 = wfrag(wr, kb + 2, 1);
+          mi0 = wfrag(wi, kb + 2, 0); mi1 = wfrag(wi, kb + 2, 1);
         }
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb) {
@@ -613,18 +753,30 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
           ai[rb] = mfma_g(a0, bi1, ai[rb]);
           ai[rb] = mfma_g(a0, bi0, ai[rb]);
         }
-        if (kb + 1 < KBG) { br0 = nr0; br1 = nr1; bi0 = ni0; bi1 = ni1; }
+        br0 = nr0; br1 = nr1; bi0 = ni0; bi1 = ni1;
+        if (kb + 2 < KBG) { nr0 = mr0; nr1 = mr1; ni0 = mi0; ni1 = mi1; }
       }
     }
-    __syncthreads();   // R1's planes are spent: h_{t-1} goes there
+    GRL_STAMP(3);
+    lds_sync();   // R1's planes are spent: gy goes there
+    GRL_STAMP(4);
 
+// each phase takes fresh (opaque) bases: per-row values are re-read from
+// LDS, never kept in registers from one phase to the next
+#define GRL_BASES                                                                   \
+  const int lane_f = fresh_lane();                                                  \
+  const int h = lane_f >> 5;                                                        \
+  const int c = 32 * wave + (lane_f & 31);                                          \
+  const char* const db = smem + (B_ER + 16 * h);               /* per-row ints */   \
+  char* const r0c = smem + (B_R0 + 4 * h * XC_PITCH + 4 * c);  /* R0 [4h][c] */     \
+  char* const r1c = smem + (B_R1 + 4 * h * XC_PITCH + 4 * c)   /* R1 [4h][c] */
 #define BPOS(rc) (*reinterpret_cast<const int*>(db + (B_POS - B_ER) + 4 * (rc)))
 #define BROW(rc) (*reinterpret_cast<const int*>(db + (B_ROW - B_ER) + 4 * (rc)))
 #define BSEQ(rc) (*reinterpret_cast<const int*>(db + (B_SEQ - B_ER) + 4 * (rc)))
 #define BREM(rc) (*reinterpret_cast<const int*>(db + (B_LAST - B_ER) + 4 * (rc)))
 #define BER(rc) (*reinterpret_cast<const int*>(db + 4 * (rc)))
 #define BER2(rc) (*reinterpret_cast<const int*>(db + (B_ER2 - B_ER) + 4 * (rc)))
-#define PRE(rc) (*reinterpret_cast<const float*>(r0c + (rc) * XC_PITCH))
+#define XCV(rc) (*reinterpret_cast<const float*>(r0c + (rc) * XC_PITCH))
 #define HPV(rc) (*reinterpret_cast<float*>(r1c + (rc) * XC_PITCH))
     // ---- D (forward part): gates (ar <- sigmoid(r), ai <- sigmoid(i); alpha,
     // beta, b' recomputed from them where needed), the forward scan from the
@@ -632,12 +784,27 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
     // gy = dy silu(z) -> LDS R1
     float cin[2][4];
     {
+      GRL_BASES;
       float run = a.tile_carries[((int64_t)g * a.max_tiles + t) * GH + c];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) {
-        float bp[16], al[16];
+        float bp[16], al[16], zv[16], gv[16];
+        // this block's z and dy first: their latency hides under the gate math
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
+          if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+          const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
+          zv[e] = gv[e] = 0.0f;
+          if (BPOS(rc) >= 0 && !(GRL_PROBE & 8)) {
+            const int grow = BROW(rc);
+            zv[e] = a.xz[(uint32_t)(grow * xzr + GH + c)];
+            gv[e] = !LASTDY ? a.dy[(uint32_t)(grow * GH + c)]
+                            : (BREM(rc) == 0 ? a.dy_last[(uint32_t)(BSEQ(rc) * GH + c)] : 0.0f);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);
           const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
           const int er = BER(rc);
           const float r = __builtin_amdgcn_ldexpf(ar[rb][e], er + ec_r - 2 * kSWg) + br;
@@ -647,13 +814,14 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
           const float aa = ok ? fexp(nsp * sr) : 1.0f;
           const float si = fsigm(i);
           const float sq = fsqrt(1.0f - aa * aa + 1e-8f);
-          bp[e] = ok ? sq * si * fsilu(PRE(rc)) : 0.0f;
+          bp[e] = ok ? sq * si * XCV(rc) : 0.0f;
           ar[rb][e] = sr;
           ai[rb][e] = si;
           al[e] = aa;
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+          __builtin_amdgcn_sched_barrier(0);   // scheduling region: one 4-row group
           float A = 1.0f, X = 0.0f;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -677,6 +845,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
+          __builtin_amdgcn_sched_barrier(0);   // scheduling region: one 4-row group
           float hp = cin[rb][q];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
@@ -686,26 +855,22 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
             if (pos == 0) hp = hz;
             const float hn = hp * al[e] + bp[e];
             hp = hn;
-            float gsv = 0.0f;
-            if (pos >= 0 && !(GRL_PROBE & 8)) {
-              const int grow = BROW(rc);
-              const float zz = a.xz[(uint32_t)(grow * xzr + GH + c)];
-              const float gv = !LASTDY ? a.dy[(uint32_t)(grow * GH + c)]
-                                       : (BREM(rc) == 0 ? a.dy_last[(uint32_t)(BSEQ(rc) * GH + c)] : 0.0f);
-              const float sz = fsigm(zz);
-              a.dxz[(uint32_t)(grow * dxr + GH + c)] = (gv * hn) * (sz * (1.0f + zz * (1.0f - sz)));
-              gsv = gv * (zz * sz);
-            }
-            HPV(rc) = gsv;
+            const float zz = zv[e];
+            const float sz = fsigm(zz);
+            if (pos >= 0 && !(GRL_PROBE & 8))
+              a.dxz[(uint32_t)(BROW(rc) * dxr + GH + c)] = (gv[e] * hn) * (sz * (1.0f + zz * (1.0f - sz)));
+            HPV(rc) = gv[e] * (zz * sz);   // 0 past the span (gv = 0)
           }
         }
       }
     }
 
-    // ---- D (reverse part): adjoint, gate gradients; dr, di -> ar, ai;
-    // silu'(pre) stays in dsl, dxc_direct silu'(pre) goes to R1 (over gy)
-    float dsl[2][16];
+    GRL_STAMP(5);
+    // ---- D (reverse part): adjoint, gate gradients; dr, di -> ar, ai; dxc's
+    // direct term -> dxd
+    float dxd[2][16];
     {
+      GRL_BASES;
       float run = eadj;
 #pragma unroll
       for (int rbr = 0; rbr < 2; ++rbr) {
@@ -714,6 +879,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         float ein[4];
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
+          __builtin_amdgcn_sched_barrier(0);
           const int q = 3 - qq;
           float A = 1.0f, X = 0.0f;
 #pragma unroll
@@ -742,8 +908,12 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          // the group's 4 rows: gate values and the forward state again
+          __builtin_amdgcn_sched_barrier(0);   // scheduling region: one 4-row group
+          // the group's 4 rows: gate values and the forward state again (a
+          // fresh copy of nsp: the exps are recomputed, not kept from the
+          // aggregate pass)
           float ga[4], gq[4], gx[4], hpv[4];
+          const float nspq = opaque_f(nsp_k);
           {
             float hp = cin[rb][q];
 #pragma unroll
@@ -752,9 +922,9 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
               const int rc = 32 * rb + 8 * q + u;
               const int pos = BPOS(rc);
               const bool ok = pos >= 0;
-              const float aa = ok ? fexp(nsp * ar[rb][e]) : 1.0f;
+              const float aa = ok ? fexp(nspq * ar[rb][e]) : 1.0f;
               const float sq = fsqrt(1.0f - aa * aa + 1e-8f);
-              const float xcv = fsilu(PRE(rc));
+              const float xcv = XCV(rc);
               if (pos == 0) hp = hz;
               hpv[u] = hp;
               hp = hp * aa + (ok ? sq * ai[rb][e] * xcv : 0.0f);
@@ -778,20 +948,13 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
             const float du = (dbeta * si) * (0.5f * frcp(sq));
             const float da = hpv[u] * d + (-du) * (2.0f * aa);
             const float dv = da * aa;
-            const float dr = ok ? (dv * nsp) * ((1.0f - sr) * sr) : 0.0f;
+            const float dr = ok ? (dv * nspq) * ((1.0f - sr) * sr) : 0.0f;
             const float di = ok ? (dbeta * sq) * ((1.0f - si) * si) : 0.0f;
-            const float sl = fdsilu(PRE(rc));
-            dsl[rb][e] = sl;
-            HPV(rc) = ok ? (d * (sq * si)) * sl : 0.0f;
+            dxd[rb][e] = ok ? d * (sq * si) : 0.0f;
             if (ok) {
               acc_v += dv * sr;
               acc_r += dr;
               acc_i += di;
-            }
-            if (ok && !(GRL_PROBE & 8)) {
-              const int grow = BROW(rc);
-              a.drg[(uint32_t)(grow * (2 * GH) + c)] = dr;
-              a.drg[(uint32_t)(grow * (2 * GH) + GH + c)] = di;
             }
             E = d * aa;
             if (pos == 0) acc_h += E;
@@ -802,117 +965,169 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
       }
       eadj = run;
     }
+    GRL_STAMP(6);
+    lds_sync();   // every wave is past its reads of xc (R0) and gy (R1)
+    GRL_STAMP(7);
 
-    // ---- E: drg row maxima (reduce-scatter over the 32 lanes of a half:
-    // slot s = (rb, e) ends on lane (s & 31) of each half), across waves in LDS
+    // ---- E: dr -> R0, di -> R1 (fp32, row-major), then row-wide
     {
-      float v[32];
+      GRL_BASES;
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) v[16 * rb + e] = fmaxf(fabsf(ar[rb][e]), fabsf(ai[rb][e]));
-#pragma unroll
-      for (int m = 16, n = 32; m >= 1; m >>= 1, n >>= 1) {
-        const bool up = (lane & m) != 0;
-#pragma unroll
-        for (int j = 0; j < n / 2; ++j) {
-          const float send = up ? v[j] : v[j + n / 2];
-          const float keep = up ? v[j + n / 2] : v[j];
-          v[j] = fmaxf(keep, __shfl_xor(send, m));
+        for (int e = 0; e < 16; ++e) {
+          if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+          const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
+          *reinterpret_cast<float*>(r0c + rc * XC_PITCH) = ar[rb][e];
+          *reinterpret_cast<float*>(r1c + rc * XC_PITCH) = ai[rb][e];
         }
-      }
-      // lane l of half h now holds slot s = l & 31: rb = s >> 4, e = s & 15
-      const int s = lane & 31;
-      const int row = 32 * (s >> 4) + 8 * ((s & 15) >> 2) + 4 * h + (s & 3);
-      *reinterpret_cast<float*>(smem + B_PMAX + 4 * (wave * GT + row)) = v[0];
     }
-    __syncthreads();   // every wave is past its reads of R0 (pre)
-    if (wave == 0) {
-      float m = 0.0f;
+    lds_sync();
+    {
+      char* const e0 = smem + opaque(B_R0 + 16 * lane);
+      char* const e1 = smem + opaque(B_R1 + 16 * lane);
+#pragma unroll 2
+      for (int j = 0; j < 8; ++j) {
+        const int vr = 8 * wave + j;
+        const int pos = *reinterpret_cast<const int*>(smem + B_POS + 4 * vr);
+        const f32x4g dr4 = *reinterpret_cast<const f32x4g*>(e0 + vr * XC_PITCH);
+        const f32x4g di4 = *reinterpret_cast<const f32x4g*>(e1 + vr * XC_PITCH);
+        const int grow = *reinterpret_cast<const int*>(smem + B_ROW + 4 * vr);
+        if (pos >= 0 && !(GRL_PROBE & 8)) {
+          __builtin_nontemporal_store(dr4, reinterpret_cast<f32x4g*>(a.drg + (uint32_t)(grow * (2 * GH) + 4 * lane)));
+          __builtin_nontemporal_store(di4, reinterpret_cast<f32x4g*>(a.drg + (uint32_t)(grow * (2 * GH) + GH + 4 * lane)));
+        }
+        float m = 0.0f;
 #pragma unroll
-      for (int w = 0; w < 8; ++w) m = fmaxf(m, *reinterpret_cast<const float*>(smem + B_PMAX + 4 * (w * GT + lane)));
-      *reinterpret_cast<int*>(smem + B_ER2 + 4 * lane) = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
-      const int pos = *reinterpret_cast<const int*>(smem + B_POS + 4 * lane);
-      if (a.drg_rmax && pos >= 0)
-        atomicMax(reinterpret_cast<int*>(a.drg_rmax) + (*reinterpret_cast<const int*>(smem + B_ROW + 4 * lane) >> 5),
-                  __float_as_int(m));
+        for (int v = 0; v < 4; ++v) m = fmaxf(m, fmaxf(fabsf(dr4[v]), fabsf(di4[v])));
+        m = wave_max(m);
+        const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
+        if (lane == 0) {
+          *reinterpret_cast<int*>(smem + B_ER2 + 4 * vr) = e;
+          if (a.drg_rmax && pos >= 0)
+            atomicMax(reinterpret_cast<int*>(a.drg_rmax) + (grow >> 5), __float_as_int(m));
+        }
+        const float sc = __builtin_amdgcn_ldexpf(1.0f, kSWg - e);
+        // in place: the row's hi plane at +0, lo plane at +PL_LO (halfs)
+        f16x4g rh, rl, ih, il;
+#pragma unroll
+        for (int v = 0; v < 4; v += 2) {
+          const f32x2g xr = f32x2g{dr4[v], dr4[v + 1]} * sc;
+          const f16x2g r0 = __builtin_convertvector(xr, f16x2g);
+          const f16x2g r1 = __builtin_convertvector(xr - __builtin_convertvector(r0, f32x2g), f16x2g);
+          const f32x2g xi = f32x2g{di4[v], di4[v + 1]} * sc;
+          const f16x2g i0 = __builtin_convertvector(xi, f16x2g);
+          const f16x2g i1 = __builtin_convertvector(xi - __builtin_convertvector(i0, f32x2g), f16x2g);
+          rh[v] = r0[0]; rh[v + 1] = r0[1]; rl[v] = r1[0]; rl[v + 1] = r1[1];
+          ih[v] = i0[0]; ih[v + 1] = i0[1]; il[v] = i1[0]; il[v + 1] = i1[1];
+        }
+        // the wave's own row: its 16-B reads above are done before these writes
+        *reinterpret_cast<f16x4g*>(e0 - 8 * lane + vr * XC_PITCH) = rh;
+        *reinterpret_cast<f16x4g*>(e0 - 8 * lane + vr * XC_PITCH + PL_LO) = rl;
+        *reinterpret_cast<f16x4g*>(e1 - 8 * lane + vr * XC_PITCH) = ih;
+        *reinterpret_cast<f16x4g*>(e1 - 8 * lane + vr * XC_PITCH + PL_LO) = il;
+      }
     }
-    __syncthreads();
+    GRL_STAMP(8);
+    lds_sync();
+    GRL_STAMP(9);
 
-    // ---- F: GEMM 2, dxc_g for channels 32w.. (K = 512 in two halves)
+    // ---- F: GEMM 2, dxc_g for channels 32w.. (K = 512: dr's planes in R0,
+    // di's in R1)
     f32x16g ax[2];
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
       for (int e = 0; e < 16; ++e) ax[rb][e] = 0.0f;
+    {
+      const int wl = opaque(lane * 16);
+      // A fragment of lane l: row l % 32, halfs 8 (l / 32) .. + 7 of a k16 block
+      const char* const g2 = smem + opaque((lane & 31) * XC_PITCH + 16 * (lane >> 5));
+      auto tfrag = [&](int kk, int p) {
+#if GRL_PROBE & 1
+        return f16x8g{} + (_Float16)(kk + p);
+#else
+        return *reinterpret_cast<const f16x8g*>(wt + kk * 2048 + p * 1024 + wl);
+#endif
+      };
+      f16x8g b0 = tfrag(0, 0), b1 = tfrag(0, 1), n0 = tfrag(1, 0), n1 = tfrag(1, 1);
+#pragma unroll 1
+      for (int kk = 0; kk < ((GRL_PROBE & 2) ? 0 : 2 * KBG); ++kk) {
+        f16x8g m0, m1;
+        if (kk + 2 < 2 * KBG) { m0 = tfrag(kk + 2, 0); m1 = tfrag(kk + 2, 1); }
+        const char* const ga = g2 + (kk < KBG ? B_R0 + kk * 32 : B_R1 + (kk - KBG) * 32);
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      // this half's values (dr, then di) -> row-major fp16 planes in R0
+        for (int rb = 0; rb < 2; ++rb) {
+          const f16x8g a0 = *reinterpret_cast<const f16x8g*>(ga + rb * 32 * XC_PITCH);
+          const f16x8g a1 = *reinterpret_cast<const f16x8g*>(ga + rb * 32 * XC_PITCH + PL_LO);
+          ax[rb] = mfma_g(a1, b0, ax[rb]);
+          ax[rb] = mfma_g(a0, b1, ax[rb]);
+          ax[rb] = mfma_g(a0, b0, ax[rb]);
+        }
+        b0 = n0; b1 = n1;
+        if (kk + 2 < 2 * KBG) { n0 = m0; n1 = m1; }
+      }
+    }
+    GRL_STAMP(10);
+    lds_sync();   // the planes are spent: dxc goes to R0
+    GRL_STAMP(11);
+
+    // ---- G: dxc = dxc_g + the direct term -> R0 (C layout)
+    {
+      GRL_BASES;
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
+          if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);
           const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
-          const float sc = __builtin_amdgcn_ldexpf(1.0f, kSWg - BER2(rc));
-          const float xv = (half == 0 ? ar[rb][e] : ai[rb][e]) * sc;
-          const _Float16 v0 = (_Float16)xv;
-          const _Float16 v1 = (_Float16)(xv - (float)v0);
-          char* rowp = smem + B_R0 + opaque((rc + 4 * h) * DRG_PITCH + 2 * c);
-          *reinterpret_cast<_Float16*>(rowp) = v0;
-          *reinterpret_cast<_Float16*>(rowp + GT * DRG_PITCH) = v1;
+          *reinterpret_cast<float*>(r0c + rc * XC_PITCH) =
+              __builtin_amdgcn_ldexpf(ax[rb][e], BER2(rc) + ec_t - 2 * kSWg) + dxd[rb][e];
         }
-      __syncthreads();
-      {
-        const int wl = opaque(lane * 16);
-        const char* wth = wt + half * KBG * 2048;
-        auto tfrag = [&](int kb, int p) {
-#if GRL_PROBE & 1
-          return f16x8g{} + (_Float16)(kb + p);
-#else
-          return *reinterpret_cast<const f16x8g*>(wth + kb * 2048 + p * 1024 + wl);
-#endif
-        };
-        f16x8g b0 = tfrag(0, 0), b1 = tfrag(0, 1);
-#pragma unroll 1
-        for (int kb = 0; kb < ((GRL_PROBE & 2) ? 0 : KBG); ++kb) {
-          f16x8g n0, n1;
-          if (kb + 1 < KBG) { n0 = tfrag(kb + 1, 0); n1 = tfrag(kb + 1, 1); }
-#pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
-            const int fo = rb * 32 * DRG_PITCH + kb * 32;
-            const f16x8g a0 = *reinterpret_cast<const f16x8g*>(g2 + fo);
-            const f16x8g a1 = *reinterpret_cast<const f16x8g*>(g2 + GT * DRG_PITCH + fo);
-            ax[rb] = mfma_g(a1, b0, ax[rb]);
-            ax[rb] = mfma_g(a0, b1, ax[rb]);
-            ax[rb] = mfma_g(a0, b0, ax[rb]);
-          }
-          if (kb + 1 < KBG) { b0 = n0; b1 = n1; }
-        }
-      }
-      __syncthreads();   // the planes are spent (the next half, or dpre, reuses R0)
     }
+    GRL_STAMP(12);
+    lds_sync();
+    GRL_STAMP(13);
 
-    // ---- G: dpre = dxc_direct silu'(pre) (R1) + dxc_g silu'(pre) -> R0
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
-        const float dg = __builtin_amdgcn_ldexpf(ax[rb][e], BER2(rc) + ec_t - 2 * kSWg);
-        *reinterpret_cast<float*>(r0c + rc * XC_PITCH) =
-            BPOS(rc) >= 0 ? HPV(rc) + dg * dsl[rb][e] : 0.0f;
-      }
-    __syncthreads();
-
-    // ---- H: conv backward, row-wide (channels 4*lane..)
+    // ---- H: conv backward, row-wide (channels 4*lane..).  H1: the
+    // pre-activation again from x (the rows dW needs anyway), dpre = dxc
+    // silu'(pre) -> R0 in place, dW / dbias partials; H2: dx from dpre of
+    // this row and the next KC-1 (later rows: R0 or the halo)
     {
-      float cw[KC][4];
+      float cw[KC][4], cbv[4];
+      conv_weights(cw, cbv);
+      char* const dp = smem + opaque(B_R0 + 16 * lane);
+      const char* const dh = smem + opaque(B_HALO + 16 * lane);
+#pragma unroll 2
+      for (int j = 0; j < 8; ++j) {
+        const int vr = 8 * wave + j;
+        const int pos = *reinterpret_cast<const int*>(smem + B_POS + 4 * vr);
+        f32x4g dpv = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (pos >= 0) {
+          const int grow = *reinterpret_cast<const int*>(smem + B_ROW + 4 * vr);
+          f32x4g xs[KC];
 #pragma unroll
-      for (int v = 0; v < 4; ++v)
+          for (int k = 0; k < KC; ++k)
+            xs[k] = KC - 1 - k <= pos && !(GRL_PROBE & 4)
+                        ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((grow - (KC - 1 - k)) * xzr + 4 * lane))
+                        : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
+          const f32x4g g1 = *reinterpret_cast<const f32x4g*>(dp + vr * XC_PITCH);
 #pragma unroll
-        for (int k = 0; k < KC; ++k) cw[k][v] = a.conv_w[(4 * lane + v) * KC + k];
-      const char* dp = smem + B_R0 + opaque(16 * lane);
-      const char* dh = smem + B_HALO + opaque(16 * lane);
+          for (int v = 0; v < 4; ++v) {
+            float acc = cbv[v];
+#pragma unroll
+            for (int k = 0; k < KC; ++k) acc = acc + (KC - 1 - k <= pos ? cw[k][v] * xs[k][v] : 0.0f);
+            dpv[v] = g1[v] * fdsilu(acc);
+#pragma unroll
+            for (int k = 0; k < KC; ++k) cw_acc[k][v] = cw_acc[k][v] + dpv[v] * xs[k][v];
+            cb_acc[v] = cb_acc[v] + dpv[v];
+          }
+        }
+        *reinterpret_cast<f32x4g*>(dp + vr * XC_PITCH) = dpv;
+      }
+      GRL_STAMP(14);
+      lds_sync();
+      GRL_STAMP(15);
 #pragma unroll 2
       for (int j = 0; j < 8; ++j) {
         const int vr = 8 * wave + j;
@@ -920,7 +1135,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         if (pos < 0) continue;
         const int grow = *reinterpret_cast<const int*>(smem + B_ROW + 4 * vr);
         const int rem = *reinterpret_cast<const int*>(smem + B_LAST + 4 * vr);
-        const f32x4g dpv = *reinterpret_cast<const f32x4g*>(dp + vr * XC_PITCH);
         f32x4g dxv = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int k = 0; k < KC; ++k) {
@@ -932,33 +1146,31 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) dxv[v] = dxv[v] + cw[k][v] * dn[v];
           }
-          if (lag <= pos && !(GRL_PROBE & 4)) {   // dW[k] += dpre_vr x_{vr - lag}
-            const f32x4g xv = *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((grow - lag) * xzr + 4 * lane));
-#pragma unroll
-            for (int v = 0; v < 4; ++v) cw_acc[k][v] = cw_acc[k][v] + dpv[v] * xv[v];
-          }
         }
-#pragma unroll
-        for (int v = 0; v < 4; ++v) cb_acc[v] = cb_acc[v] + dpv[v];
-        __builtin_nontemporal_store(dxv, reinterpret_cast<f32x4g*>(a.dxz + (uint32_t)(grow * dxr + 4 * lane)));
+        if (!(GRL_PROBE & 32))
+          __builtin_nontemporal_store(dxv, reinterpret_cast<f32x4g*>(a.dxz + (uint32_t)(grow * dxr + 4 * lane)));
       }
     }
-    __syncthreads();
+    GRL_STAMP(16);
+    lds_sync();
     if (wave == 0) {   // this tile's first 3 rows of dpre: the halo of the next (earlier) tile
 #pragma unroll
       for (int j = 0; j < 3; ++j)
         *reinterpret_cast<f32x4g*>(smem + B_HALO + j * XC_PITCH + 16 * lane) =
             *reinterpret_cast<const f32x4g*>(smem + B_R0 + j * XC_PITCH + 16 * lane);
     }
+#undef GRL_BASES
 #undef BPOS
 #undef BROW
 #undef BSEQ
 #undef BREM
 #undef BER
 #undef BER2
-#undef PRE
+#undef XCV
 #undef HPV
+    GRL_STAMP(17);
   }
+  GRL_STAMP_FLUSH(1);
   // ---- partial sums of this workgroup
   acc_v += __shfl_xor(acc_v, 32);
   acc_r += __shfl_xor(acc_r, 32);

@@ -38,14 +38,14 @@ __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDL
 
 
 _FOLD_PAD = os.environ.get("RECBLR_FOLD_PAD", "1") != "0"
-# RECBLR_FUSED_GRL=1: the fused rb_grl_fwd (and rb_grl_bwd) on packed fp32
-# sequences with H = 256 instead of the three-launch path (conv, gates GEMM,
-# gate scan); off by default until it is the faster path
-_FUSED = os.environ.get("RECBLR_FUSED_GRL", "0") != "0"
-# RECBLR_FUSED_GRL_BWD=0: with the fused forward, keep the three-launch
-# backward (the forward then writes xc, rg and the 16-step carries) instead
-# of rb_grl_bwd (the forward writes only the 64-row tile checkpoints)
-_FUSED_BWD = os.environ.get("RECBLR_FUSED_GRL_BWD", "1") != "0"
+# RECBLR_FUSED_GRL=0: the three-launch forward (conv, gates GEMM, gate scan)
+# instead of the fused rb_grl_fwd on packed fp32 sequences with H = 256
+_FUSED = os.environ.get("RECBLR_FUSED_GRL", "1") != "0"
+# RECBLR_FUSED_GRL_BWD=1: with the fused forward, the one-launch backward
+# rb_grl_bwd from the forward's 64-row tile checkpoints instead of the
+# three-launch backward (from the xc, rg and 16-step carries the fused
+# forward then writes).  Off by default: slower on MI355X
+_FUSED_BWD = os.environ.get("RECBLR_FUSED_GRL_BWD", "0") != "0"
 
 
 def fused_ok(seq, H: int, use_conv: bool, kc: int, dtype) -> bool:

@@ -86,18 +86,18 @@ def test_train_step_matches_oracle_with_split_gemm(cuda, split_gemm_calls, monke
     rows = ntok if packed else B * L
     big = [c for c in split_gemm_calls if c[0] == rows]
     # per layer and direction: in, gates, out (fwd) and their dX GEMMs; layer
-    # 0's FFN (the last layer's tail runs on the B gathered rows).  Packed
-    # with RECBLR_FUSED_GRL=1, both gates GEMMs run inside the fused kernels
-    # (rb_grl_fwd / _bwd).
+    # 0's FFN (the last layer's tail runs on the B gathered rows).  Packed,
+    # the gates forward GEMM runs inside rb_grl_fwd (RECBLR_FUSED_GRL, on by
+    # default) and with RECBLR_FUSED_GRL_BWD=1 the gates dX GEMM inside
+    # rb_grl_bwd.
     on = packed and recurrence._FUSED
-    assert len(big) >= (8 if on else 12), (rows, split_gemm_calls)
+    on_b = on and recurrence._FUSED_BWD
+    assert len(big) >= 12 - 2 * on - 2 * on_b, (rows, split_gemm_calls)
     shapes = {(c[1], c[2]) for c in big}
     for s in ((128, 512), (256, 128), (512, 128), (128, 256)):
         assert s in shapes, (s, shapes)
-    if on:
-        assert len(fused) == 2 and len(fused_b) == 2, "fused GatedRecurrentLayer not engaged"
-    else:
-        assert (256, 512) in shapes and (512, 256) in shapes and not fused and not fused_b
+    assert len(fused) == 2 * on and len(fused_b) == 2 * on_b, (fused, fused_b)
+    assert ((256, 512) in shapes) != on and ((512, 256) in shapes) != on_b, shapes
     if threshold == 0:
         assert any(c[0] == B for c in split_gemm_calls), "gathered tail not on the kernel"
 

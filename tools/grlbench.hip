@@ -133,11 +133,32 @@ int main(int argc, char** argv) {
     return launch_grl_fwd(xz, 2 * H, conv_w, KC, conv_b, wf, gate_b, lam, h0, d_pieces, B, G, ntok,
                           y, H, nullptr, nullptr, nullptr, nullptr, 0, nullptr, tc, max_tiles, 0);
   };
+  const int nTc = (L + 15) / 16;
+  float* car = dalloc((int64_t)B * nTc * H, 16, 0.0f);
+  float* rgo = dalloc(ntok * 2 * H, 17, 0.0f);
+  auto fwd_legacy = [&]() {   // the three-launch backward's operands as side outputs
+    return launch_grl_fwd(xz, 2 * H, conv_w, KC, conv_b, wf, gate_b, lam, h0, d_pieces, B, G, ntok,
+                          y, H, nullptr, xc, rgo, car, nTc, rmax, nullptr, 0, 0);
+  };
   auto bwd = [&]() {
     return launch_grl_bwd(xz, 2 * H, conv_w, KC, conv_b, wf, wft, gate_b, lam, h0, d_pieces, B, G,
                           ntok, tc, max_tiles, dy, nullptr, dxz, 2 * H, drg, xc, rmax, rmax + nr,
                           part, cpart, 0);
   };
+#ifdef GRL_STAMPS
+  auto stamps = [&](int w, const char* const* names, int n) {
+    unsigned long long st[2][20];
+    CK(hipMemcpyFromSymbol(st, HIP_SYMBOL(grl_stamps), sizeof(st)));
+    double tot = 0;
+    for (int k = 0; k < n; ++k) tot += (double)st[w][k];
+    for (int k = 0; k < n; ++k) printf("    %-14s %5.1f%%\n", names[k], 100.0 * st[w][k] / tot);
+  };
+  auto zero = [&]() {
+    unsigned long long z[2][20] = {};
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(grl_stamps), z, sizeof(z)));
+  };
+  zero();
+#endif
   const double fwd_bytes = 3.0 * ntok * H * 4, bwd_bytes = 8.0 * ntok * H * 4;
   for (int w = 0; w < 3; ++w) { fwd(); bwd(); }
   CK(hipDeviceSynchronize());
@@ -148,6 +169,20 @@ int main(int argc, char** argv) {
   CK(hipEventSynchronize(e1));
   CK(hipEventElapsedTime(&ms, e0, e1));
   printf("fwd  %8.1f us  %6.0f GB/s (x, z, y)\n", 1e3 * ms / iters, fwd_bytes / (1e6 * ms / iters));
+#ifdef GRL_STAMPS
+  CK(hipDeviceSynchronize());
+  {
+    const char* names[] = {"rowmap", "A", "A.sync", "C.gemm", "D", "D.sync"};
+    stamps(0, names, 6);
+  }
+#endif
+  CK(hipEventRecord(e0));
+  for (int i = 0; i < iters; ++i) fwd_legacy();
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("fwd+ %8.1f us  (y + xc, rg, 16-step carries: the three-launch backward's operands)\n",
+         1e3 * ms / iters);
   CK(hipEventRecord(e0));
   for (int i = 0; i < iters; ++i) bwd();
   CK(hipEventRecord(e1));
@@ -156,5 +191,13 @@ int main(int argc, char** argv) {
   printf("bwd  %8.1f us  %6.0f GB/s (x, z, dy, dx, dz, dr, di, xc)\n", 1e3 * ms / iters,
          bwd_bytes / (1e6 * ms / iters));
   CK(hipDeviceSynchronize());
+#ifdef GRL_STAMPS
+  {
+    const char* names[] = {"rowmap", "A", "A.sync", "C.gemm1", "C.sync", "D.fwd", "D.rev",
+                           "D.sync", "E", "E.sync", "F.gemm2", "F.sync", "G", "G.sync", "H1",
+                           "H1.sync", "H2", "H2.sync+halo"};
+    stamps(1, names, 18);
+  }
+#endif
   return 0;
 }
