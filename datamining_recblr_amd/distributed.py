@@ -61,17 +61,24 @@ class LossModule(nn.Module):
         return self.model.calculate_loss(interaction)
 
 
-def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float = 32.0) -> nn.Module:
+def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float = 32.0,
+             static_graph: bool | None = None) -> nn.Module:
+    """DDP over the loss module.  static_graph (default: RECBLR_DDP_STATIC,
+    on): the train step uses the same parameters in the same order every
+    iteration, so the reducer skips its per-iteration graph bookkeeping."""
     step = LossModule(model)
     if not env.distributed:
         return step
+    if static_graph is None:
+        static_graph = os.environ.get("RECBLR_DDP_STATIC", "1") != "0"
     dev = next(model.parameters()).device
     kw = dict(device_ids=[dev.index]) if dev.type == "cuda" else {}
     # ablation flags (RecBLR.py:28-35) leave the conv / FFN parameters unused
     unused = bool(getattr(model, "disable_conv1d", False) or getattr(model, "disable_ffn", False))
     return nn.parallel.DistributedDataParallel(
         step, bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True,
-        broadcast_buffers=False, find_unused_parameters=unused, **kw)
+        broadcast_buffers=False, find_unused_parameters=unused and not static_graph,
+        static_graph=static_graph, **kw)
 
 
 def synthetic_interaction(batch: int, seq_len: int, n_items: int, device, seed: int,
