@@ -1072,16 +1072,35 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
                        : (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
                                                                     : (nct0 ? M : 0);
 #endif
+  const f16x8* wf = (const f16x8*)Wf;
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   if (M_main < M) {
-    const int rc = launch_gemm_nt_hs(A + M_main * lda, lda, M - M_main, R, Wf, C, bias,
-                                     out + M_main * ldo, ldo,
-                                     rmax ? rmax + M_main / 32 : nullptr, st);
-    if (rc || M_main == 0) return rc;
+#ifndef HN_TAIL_SMALL
+    // a partial round of 256 x 64 tiles: 4x (2x) the 256 x 256 (256 x 128)
+    // tiles of the main launch, each a quarter (half) of their time
+    if (M_main > 0 && wide && C % 64 == 0) {
+      const int64_t Mt = M - M_main;
+      const int mt_t = (int)((Mt + N_BM - 1) / N_BM);
+      const int64_t nt_t = (int64_t)((mt_t + 7) / 8) * 8 * (C / 64);
+      const unsigned grid_t = (unsigned)std::min<int64_t>(nt_t, (int64_t)num_cus() / 8 * 8 * (8 / N_WAVES));
+      const float* At = A + M_main * lda;
+      float* ot = out + M_main * ldo;
+      float* rt = rmax ? rmax + M_main / 32 : nullptr;
+      if (bias) run_nt_h<true, true, 2>(At, lda, Mt, R, wf, ew, C, bias, ot, ldo, rt, mt_t, grid_t, st);
+      else run_nt_h<false, true, 2>(At, lda, Mt, R, wf, ew, C, bias, ot, ldo, rt, mt_t, grid_t, st);
+      const int rc = launch_status("rb_gemm_nt_h");
+      if (rc) return rc;
+    } else
+#endif
+    {
+      const int rc = launch_gemm_nt_hs(A + M_main * lda, lda, M - M_main, R, Wf, C, bias,
+                                       out + M_main * ldo, ldo,
+                                       rmax ? rmax + M_main / 32 : nullptr, st);
+      if (rc || M_main == 0) return rc;
+    }
   }
   M = M_main;
   const int m_tiles = (int)((M + N_BM - 1) / N_BM);
-  const f16x8* wf = (const f16x8*)Wf;
-  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / (nb8 ? 256 : 128));
   // persistent: one workgroup per CU (a multiple of 8: the XCD pairing above)
   const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8 * (8 / N_WAVES));

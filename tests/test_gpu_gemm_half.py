@@ -259,9 +259,10 @@ def test_weight_gradient_columns_spread_over_2_to_the_16(cuda):
                                    (77, 64, 32), (5000, 96, 96), (196608 + 8024, 256, 512),
                                    (196608 + 8024, 512, 128), (65536 * 3 + 31, 128, 256)])
 def test_few_rows_kernel_and_round_remainder(cuda, M, K, N):
-    """The few-rows kernel (csrc/gemm_small.hip): the gathered last-layer tail
-    (B = 2048 rows), C % 128 != 0, and the rows past the persistent kernel's
-    last whole round (bench-sized M: 196,608 rows there + 8,024 here).  Every
+    """The few-rows kernel (csrc/gemm_small.hip: the gathered last-layer tail,
+    B = 2048 rows; C % 128 != 0) and the rows past the persistent kernel's
+    last whole round (bench-sized M: 196,608 rows there + 8,024 here, on the
+    256 x 64-tile launch of the same kernel).  Every
     row at fp32 level against fp64 (per-row error against the row's max), the
     rmax side output equal to the exact 32-row-group maxima across the seam."""
     from datamining_recblr_amd import kernels
