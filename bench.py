@@ -793,20 +793,22 @@ def main():
         devlen["recbole_interaction_path"] = recbole_path
     fused_ab = None
     if not args.no_full_tail:
-        # the fused GatedRecurrentLayer kernels (csrc/grl_fused.hip): the
-        # headline runs rb_grl_fwd + the three-launch backward; A/B against
-        # the one-launch backward and against no fusion, same batches
+        # the fused GatedRecurrentLayer kernels (csrc/grl_fused.hip, opt-in):
+        # A/B against the headline's three-launch path on the same batches
         from datamining_recblr_amd import recurrence
         saved_f = (recurrence._FUSED, recurrence._FUSED_BWD)
         fused_ab = {}
-        for name, f, fb in (("fused_fwd_and_bwd", True, True), ("unfused", False, False)):
+        for name, f, fb in (("fused_fwd", True, False), ("fused_fwd_and_bwd", True, True),
+                            ("unfused", False, False)):
+            if (f, fb) == saved_f:
+                continue
             recurrence._FUSED, recurrence._FUSED_BWD = f, fb
             fused_ab[name] = timed_variant(True, True)
         recurrence._FUSED, recurrence._FUSED_BWD = saved_f
         fused_ab["headline"] = {"fused_fwd": saved_f[0], "fused_bwd": saved_f[1]}
         fused_ab["note"] = ("RECBLR_FUSED_GRL / RECBLR_FUSED_GRL_BWD A/B on the headline's "
-                            "batches: rb_grl_fwd (conv + gates GEMM + scan) with the "
-                            "three-launch backward is the default; rb_grl_bwd is opt-in")
+                            "batches: rb_grl_fwd (conv + gates GEMM + scan in one launch) "
+                            "alone and with rb_grl_bwd, against the three-launch path")
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)

@@ -38,9 +38,11 @@ __all__ = ["pow2_pad_len", "row_pad_lens", "pad_prefix_state", "PadPrefix", "BDL
 
 
 _FOLD_PAD = os.environ.get("RECBLR_FOLD_PAD", "1") != "0"
-# RECBLR_FUSED_GRL=0: the three-launch forward (conv, gates GEMM, gate scan)
-# instead of the fused rb_grl_fwd on packed fp32 sequences with H = 256
-_FUSED = os.environ.get("RECBLR_FUSED_GRL", "1") != "0"
+# RECBLR_FUSED_GRL=1: the fused rb_grl_fwd (conv + gates GEMM + gate scan in
+# one launch) on packed fp32 sequences with H = 256 instead of the three
+# launches.  Off by default: not faster in the step on MI355X (DESIGN.md §4,
+# "Fused GatedRecurrentLayer kernels"; bench.py's fused_grl A/B)
+_FUSED = os.environ.get("RECBLR_FUSED_GRL", "0") != "0"
 # RECBLR_FUSED_GRL_BWD=1: with the fused forward, the one-launch backward
 # rb_grl_bwd from the forward's 64-row tile checkpoints instead of the
 # three-launch backward (from the xc, rg and 16-step carries the fused
