@@ -1056,9 +1056,11 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
 #endif
   // The persistent grid runs whole rounds of G tiles; the rows past the last
   // whole round would run on a fraction of the chip (800 row tiles on 256
-  // CUs: a fourth round on 32 of them, +18% time for +4% rows), so they go
-  // to the few-rows kernel (gemm_small.hip) right behind, spread over the
-  // whole chip.  Below one round, or for C % 128 != 0, all rows go there.
+  // CUs: a fourth round on 32 of them, +18% time for +4% rows), so they run
+  // as a second launch of 256 x 64 tiles (2-4x as many, each a fraction of
+  // the time).  Below one round, or for C % 128 != 0, every row goes to that
+  // launch, or to the few-rows kernel (gemm_small.hip) for the few-thousand-
+  // row shapes it wins, or for C % 64 != 0.
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
   // (the few-rows kernel holds R <= 1024; beyond, the persistent kernel takes
   // every row, a partial round included)
@@ -1078,7 +1080,11 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
 #ifndef HN_TAIL_SMALL
     // a partial round of 256 x 64 tiles: 4x (2x) the 256 x 256 (256 x 128)
     // tiles of the main launch, each a quarter (half) of their time
-    if (M_main > 0 && wide && C % 64 == 0) {
+    // below one round: the few-rows kernel only where it measured faster
+    // (a few thousand rows with K = 512, or C = 128; tools/gemmbench_h.hip,
+    // profiles/r03_gemmbench_small_m.log) — at 8,192 rows it is 2.7x slower
+    const bool few = M_main == 0 && M <= 4096 && (R > 256 || C < 256);
+    if (!few && wide && C % 64 == 0) {
       const int64_t Mt = M - M_main;
       const int mt_t = (int)((Mt + N_BM - 1) / N_BM);
       const int64_t nt_t = (int64_t)((mt_t + 7) / 8) * 8 * (C / 64);
@@ -1089,7 +1095,7 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
       if (bias) run_nt_h<true, true, 2>(At, lda, Mt, R, wf, ew, C, bias, ot, ldo, rt, mt_t, grid_t, st);
       else run_nt_h<false, true, 2>(At, lda, Mt, R, wf, ew, C, bias, ot, ldo, rt, mt_t, grid_t, st);
       const int rc = launch_status("rb_gemm_nt_h");
-      if (rc) return rc;
+      if (rc || M_main == 0) return rc;
     } else
 #endif
     {
