@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 28; }
+int rb_version(void) { return 29; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -541,7 +541,22 @@ int rb_item_ce_probs_h(const void* seq_img, const int* seq_exp, const void* item
   if (!target || !lse || !dloss || !probs) return fail("rb_item_ce_probs_h: null pointer");
   if (ld < V) return fail("rb_item_ce_probs_h: ld < V");
   return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
-                                item_offset, probs, ld, reinterpret_cast<hipStream_t>(stream));
+                                item_offset, probs, ld, nullptr,
+                                reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_ce_probs_h_t(const void* seq_img, const int* seq_exp, const void* item_img,
+                         const int* item_exp, const int64_t* target, const float* lse,
+                         const float* dloss, int64_t B, int64_t V, int64_t d, int64_t item_offset,
+                         float* probs_t, int64_t ldt, float* group_max, void* stream) {
+  if (int rc = check_items_h(seq_img, seq_exp, item_img, item_exp, B, V, d)) return rc;
+  if (!target || !lse || !dloss || !probs_t || !group_max)
+    return fail("rb_item_ce_probs_h_t: null pointer");
+  if (ldt < B || ldt % 4 || reinterpret_cast<uintptr_t>(probs_t) % 16)
+    return fail("rb_item_ce_probs_h_t: probs_t must be 16-B aligned with ldt >= B, ldt % 4 == 0");
+  return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
+                                item_offset, probs_t, ldt, group_max,
+                                reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,

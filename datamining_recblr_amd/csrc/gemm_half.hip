@@ -1070,9 +1070,15 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
 #ifdef HN_NO_TAIL_SPLIT
   const int64_t M_main = nct0 ? M : 0;
 #else
-  const int64_t M_main = R > 1024 ? M
-                       : (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
-                                                                    : (nct0 ? M : 0);
+  int64_t M_main = R > 1024 ? M
+                 : (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
+                                                              : (nct0 ? M : 0);
+#ifdef HN_TAIL_ROUNDS
+  // experiment: one more whole round into the 256 x 64-tile launch for
+  // single-column-tile shapes
+  if (nct0 == 1 && R <= 1024 && M_main >= (HN_TAIL_ROUNDS) * rows_round)
+    M_main -= (HN_TAIL_ROUNDS - 1) * rows_round;
+#endif
 #endif
   const f16x8* wf = (const f16x8*)Wf;
   const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);

@@ -854,8 +854,12 @@ __global__ __launch_bounds__(256) void k_ce_fwd_h(const _Float16* __restrict__ E
 }
 
 // k_item_scores<D, true> on the f16 pipe (the logits' gradient P): seq rows
-// in registers (A), item tiles streamed (B) with their exponents
-template <int D>
+// in registers (A), item tiles streamed (B) with their exponents.  TR: P^T
+// [V, ld] instead (each lane's 16 rows as four 16-B pieces of its item's
+// row) and every 32-item group's max |P| (atomicMax into gmax, zeroed by the
+// caller): the operands of the input gradients as f16x3 GEMMs
+// (scoring._bwd_slices)
+template <int D, bool TR>
 __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__ Ei,
                                                     const int* __restrict__ Ee,
                                                     const _Float16* __restrict__ Wi,
@@ -865,7 +869,7 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
                                                     const float* __restrict__ lse,
                                                     const int64_t* __restrict__ tgt,
                                                     const float* __restrict__ dloss, float inv_n,
-                                                    int64_t v_off) {
+                                                    int64_t v_off, float* __restrict__ gmax) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
   Place pl;
   if (!place(RB, NS, pl)) return;
@@ -893,15 +897,45 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
     const int v = (int)(t * kTile) + j;
     const f32x16 x = lds_dot_h<D, false>(tile, j, h, e0, e1);
     const int ev = reinterpret_cast<const int*>(ebuf)[j];
-    if (v < V) {
-      float* o = out + (b0 + 4 * h) * ld + v;
+    if constexpr (!TR) {
+      if (v < V) {
+        float* o = out + (b0 + 4 * h) * ld + v;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rr = crow(r, 0);   // row - b0 - 4h
-        const float xs = __builtin_amdgcn_ldexpf(x[r], ev + er[r]);
-        const float val = (fexp(xs - lr[r]) - (v == tr[r] ? 1.0f : 0.0f)) * g;
-        if (full || b0 + 4 * h + rr < B) o[rr * ld] = val;
+        for (int r = 0; r < 16; ++r) {
+          const int rr = crow(r, 0);   // row - b0 - 4h
+          const float xs = __builtin_amdgcn_ldexpf(x[r], ev + er[r]);
+          const float val = (fexp(xs - lr[r]) - (v == tr[r] ? 1.0f : 0.0f)) * g;
+          if (full || b0 + 4 * h + rr < B) o[rr * ld] = val;
+        }
       }
+    } else {
+      float m = 0.0f;
+      if (v < V) {
+        float* o = out + (int64_t)v * ld + b0 + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {   // rows b0 + 8q + 4h + 0..3
+          rb_f32x4 val4;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = 4 * q + u;
+            const float xs = __builtin_amdgcn_ldexpf(x[r], ev + er[r]);
+            const bool in = full || b0 + 8 * q + 4 * h + u < B;
+            val4[u] = in ? (fexp(xs - lr[r]) - (v == tr[r] ? 1.0f : 0.0f)) * g : 0.0f;
+            m = fmaxf(m, fabsf(val4[u]));
+          }
+          if (full) {
+            *reinterpret_cast<rb_f32x4*>(o + 8 * q) = val4;
+          } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (b0 + 8 * q + 4 * h + u < B) o[8 * q + u] = val4[u];
+          }
+        }
+      }
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh));
+      if (lane == 0)   // non-negative floats order as their bit patterns
+        atomicMax(reinterpret_cast<int*>(gmax) + t, __float_as_int(m));
     }
   });
 }
@@ -1035,10 +1069,15 @@ void ce_fwd_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, co
 template <int D>
 void probs_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, int64_t B, int64_t V,
                const Grid2& g, float* out, int64_t ld, const float* lse, const int64_t* tgt,
-               const float* dloss, float inv_n, int64_t v_off, hipStream_t st) {
-  hipLaunchKernelGGL(k_ce_probs_h<D>, dim3(g.wgs()), dim3(256), 0, st, (const _Float16*)Ei, Ee,
-                     (const _Float16*)Wi, We, B, V, g.per, g.blocks, g.splits, out, ld, lse, tgt,
-                     dloss, inv_n, v_off);
+               const float* dloss, float inv_n, int64_t v_off, float* gmax, hipStream_t st) {
+  if (gmax)
+    hipLaunchKernelGGL((k_ce_probs_h<D, true>), dim3(g.wgs()), dim3(256), 0, st,
+                       (const _Float16*)Ei, Ee, (const _Float16*)Wi, We, B, V, g.per, g.blocks,
+                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax);
+  else
+    hipLaunchKernelGGL((k_ce_probs_h<D, false>), dim3(g.wgs()), dim3(256), 0, st,
+                       (const _Float16*)Ei, Ee, (const _Float16*)Wi, We, B, V, g.per, g.blocks,
+                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax);
 }
 
 void sum_parts(const float* parts, int64_t P, int64_t n, float* out, hipStream_t st) {
@@ -1152,12 +1191,12 @@ int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const in
 int launch_item_ce_probs_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                            const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
                            int64_t V, int64_t D, int64_t v_off, float* out, int64_t ld,
-                           hipStream_t st) {
+                           float* gmax, hipStream_t st) {
   const Grid2 g = plan(B, ntiles(V));
   const float inv_n = 1.0f / (float)B;
   RB_ITEM_DISPATCH(D, probs_h_t, Ei, Ee, Wi, We, B, V, g, out, ld, lse, tgt, dloss, inv_n, v_off,
-                   st);
-  return launch_status("rb_item_ce_probs_h");
+                   gmax, st);
+  return launch_status(gmax ? "rb_item_ce_probs_h_t" : "rb_item_ce_probs_h");
 }
 
 int launch_item_scores(const float* E, const float* W, int64_t B, int64_t V, int64_t D,

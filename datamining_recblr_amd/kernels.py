@@ -797,6 +797,24 @@ def item_ce_probs_h(seq: SplitRows, items: SplitRows, target, lse, dloss, item_o
     return out
 
 
+def item_ce_probs_h_t(seq: SplitRows, items: SplitRows, target, lse, dloss, item_offset=0):
+    """item_ce_probs_h transposed (rb_item_ce_probs_h_t): (P^T [V, B], gmax
+    [ceil(V/32)]) with gmax the max |P| of every 32-item group — the operands
+    of dseq = P W (rb_gemm_tn_h) and ditems = P^T seq (rb_gemm_nt_h)."""
+    B, V, d, target = _split_operands(seq, items, target)
+    _check(lse, "lse")
+    _check(dloss, "dloss")
+    dev = seq.img.device
+    ldt = (B + 3) // 4 * 4
+    pt = torch.empty((V, ldt), device=dev, dtype=torch.float32)[:, :B]
+    gmax = torch.zeros((V + 31) // 32, device=dev, dtype=torch.float32)
+    _launch("rb_item_ce_probs_h_t", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
+            items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
+            lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
+            int(item_offset), pt.data_ptr(), ldt, gmax.data_ptr(), _stream(seq.img))
+    return pt, gmax
+
+
 def item_rank(seq, items, target, first_item=1, want_equal=True):
     """(n_greater, n_equal) int64 [B]: items in [first_item, V) other than the
     target scoring above / equal to it (-1 for an out-of-range target)."""

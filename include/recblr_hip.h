@@ -342,6 +342,16 @@ int rb_item_ce_probs_h(const void* seq_img, const int* seq_exp, const void* item
                        const float* dloss, int64_t B, int64_t V, int64_t d, int64_t item_offset,
                        float* probs, int64_t ld, void* stream);
 
+/* rb_item_ce_probs_h transposed: probs_t [V, ldt] = P^T (ldt >= B, a
+ * multiple of 4, 16-B aligned) and group_max [ceil(V/32)] = max |P| over
+ * each 32-item group (atomic max: zeroed by the caller) — the operands of
+ * dL/dseq = P W and dL/ditems = P^T seq (RecBLR.py:100-102's backward) as
+ * the f16x3 weight-gradient / NT GEMMs (rb_gemm_tn_h, rb_gemm_nt_h). */
+int rb_item_ce_probs_h_t(const void* seq_img, const int* seq_exp, const void* item_img,
+                         const int* item_exp, const int64_t* target, const float* lse,
+                         const float* dloss, int64_t B, int64_t V, int64_t d, int64_t item_offset,
+                         float* probs_t, int64_t ldt, float* group_max, void* stream);
+
 /* Workspace bytes of rb_item_rank. */
 int64_t rb_item_rank_workspace(int64_t B, int64_t V, int64_t d);
 

@@ -329,3 +329,51 @@ def test_item_ce_f16_engaged_in_training_loss(cuda):
         model.calculate_loss(inter).backward()
     names = {r[0] for r in t.records}
     assert {"rb_item_split_h", "rb_item_ce_fwd_h", "rb_item_ce_probs_h"} <= names, names
+
+
+def test_item_ce_f16_probs_transposed(cuda):
+    """rb_item_ce_probs_h_t: P^T bit-identical to the row-major kernel's P,
+    partial batch tile included, and the exact max |P| of every 32-item group."""
+    from datamining_recblr_amd import kernels
+
+    seq, W, tgt = _data(200, 1000, 128, cuda, seed=14)
+    ss, sw = kernels.item_split_h(seq), kernels.item_split_h(W)
+    _, lse = kernels.item_ce_fwd_h(ss, sw, tgt)
+    dl = torch.full((), 1.5, device=cuda)
+    p = kernels.item_ce_probs_h(ss, sw, tgt, lse, dl)
+    pt, gmax = kernels.item_ce_probs_h_t(ss, sw, tgt, lse, dl)
+    assert torch.equal(pt, p.t())
+    want = torch.nn.functional.pad(p.abs().amax(0), (0, (-1000) % 32)).view(-1, 32).amax(1)
+    assert torch.equal(gmax, want)
+    # a slice of the table
+    pt2, g2 = kernels.item_ce_probs_h_t(ss, sw.rows(320, 1000), tgt, lse, dl, item_offset=320)
+    assert torch.equal(pt2, p[:, 320:].t())
+    assert torch.equal(g2, want[10:])
+
+
+@pytest.mark.parametrize("B,V,slice_bytes", [(2048, 10544, 1 << 30), (256, 515, 256 * 4 * 96),
+                                             (128, 33, 1 << 30)])
+def test_item_ce_f16_grads_vs_fp64(cuda, monkeypatch, B, V, slice_bytes):
+    """RECBLR_CE_GRADS=f16: the sliced backward's products on the f16 GEMM
+    kernels (P^T from rb_item_ce_probs_h_t; dseq on rb_gemm_tn_h, ditems on
+    rb_gemm_nt_h) at the bench's shape (B = 2048, n_items = 10,544, d = 128)
+    and on multi-slice tables, against torch fp64; no library GEMM runs."""
+    from datamining_recblr_amd import kernels, scoring
+
+    monkeypatch.setattr(scoring, "PROBS_SLICE_BYTES", slice_bytes)
+    monkeypatch.setattr(scoring, "CE_GRADS", "f16")
+    seq, W, tgt = _data(B, V, 128, cuda, seed=15, scale=0.5)
+    s1 = seq.clone().requires_grad_()
+    w1 = W.clone().requires_grad_()
+    mm = []
+    orig = torch.mm
+    monkeypatch.setattr(torch, "mm", lambda *a, **k: mm.append(1) or orig(*a, **k))
+    with kernels.kernel_timing() as t:
+        (0.7 * scoring.item_cross_entropy(s1, w1, tgt)).backward()
+    names = {r[0] for r in t.records}
+    assert "rb_item_ce_probs_h_t" in names and not mm, (names, len(mm))
+    s2 = seq.double().requires_grad_()
+    w2 = W.double().requires_grad_()
+    (0.7 * F.cross_entropy(s2 @ w2.t(), tgt)).backward()
+    normwise(s1.grad, s2.grad, 2e-5, "dseq")
+    normwise(w1.grad, w2.grad, 2e-5, "ditems")
