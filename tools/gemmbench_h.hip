@@ -150,7 +150,8 @@ int main(int argc, char** argv) {
   double ttot = 0;
   for (const TShape& t : tsh) {
     const int nt = (t.N / 128) * (t.K / 128);
-    const int S = std::max(8, (2 * num_cus() / nt) / 8 * 8);
+    const int S = getenv("GB_TN_S") ? atoi(getenv("GB_TN_S"))
+                                     : std::max(8, (2 * num_cus() / nt) / 8 * 8);
     std::vector<float> ts;
     for (int rep = 0; rep < 12; ++rep) {
       CK(hipEventRecord(e0, 0));
