@@ -1004,6 +1004,219 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
 
 
 
+// k_gemm_tn_pc: the same product and partials as k_gemm_tn_h on the 512-
+// thread tiles (256 x 128 or 128 x 256), with the work divided by role:
+// waves 0-3 only multiply (each a 64-wide slice of the tile's longer side
+// against all of the shorter: 8 blocks of 32 x 32, 128 accumulators), waves
+// 4-7 only load, scale, split and write the next m-step's column-major
+// images.  The two roles share each SIMD (waves w and w + 4), so the
+// conversion's VALU and LDS writes run beside the MFMAs instead of between
+// them; one barrier per 32-row m-step separates the two LDS stages.
+template <int NBN, int NBK>
+__global__ void __launch_bounds__(512, 1)
+k_gemm_tn_pc(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X, int64_t ldx,
+             int64_t M, int N, int K, const float* __restrict__ ymax,
+             const float* __restrict__ xmax, float* __restrict__ parts, int S, int64_t mk,
+             int nt_k) {
+  static_assert(NBN * NBK == 2, "512-thread tiles only");
+  using CF = TnCfg<NBN, NBK>;
+  constexpr int YC = CF::YC, XC = CF::XC;
+  constexpr bool SPLIT_N = YC >= XC;          // MFMA waves split the longer side
+  constexpr int BN = SPLIT_N ? 2 : YC / 32;   // n blocks per MFMA wave
+  constexpr int BK = SPLIT_N ? XC / 32 : 2;   // k blocks per MFMA wave
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int idx = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
+  const int nt = (N / YC) * nt_k;
+  const int tile = idx % nt, s = idx / nt;
+  const int n0 = (tile / nt_k) * YC, k0 = (tile % nt_k) * XC;
+  const int64_t r_begin = (int64_t)s * mk;
+  const int64_t r_end = r_begin + mk < M ? r_begin + mk : M;
+  const int64_t nrows = r_end > r_begin ? r_end - r_begin : 0;
+  const int T = (int)((nrows + 31) / 32);
+
+  // chunk scales from the 32-row group maxima
+  float my = 0.0f, mx = 0.0f;
+  for (int64_t g = r_begin / 32 + tid; g * 32 < r_end; g += 512) {
+    my = fmaxf(my, ymax[g]);
+    mx = fmaxf(mx, xmax[g]);
+  }
+  float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    my = fmaxf(my, __shfl_xor(my, o));
+    mx = fmaxf(mx, __shfl_xor(mx, o));
+  }
+  if (lane == 0) { red[wave] = my; red[8 + wave] = mx; }
+  __syncthreads();
+  my = 0.0f;
+  mx = 0.0f;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    my = fmaxf(my, red[w]);
+    mx = fmaxf(mx, red[8 + w]);
+  }
+  const int ey = my > 0.0f ? __builtin_amdgcn_frexp_expf(my) : 0;
+  const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;
+  __syncthreads();
+  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+
+  if (wave >= 4) {
+    // ---- converters: YC + XC roles of 4 columns x 8 rows over 256 threads
+    // (role r = ct, then ct + 256 where that exists)
+    const int ct = tid - 256;
+    auto role = [&](int r, const float*& src, int64_t& ld, float& sc, uint32_t& img_off,
+                    uint32_t& plane, int& cc, int& rg) {
+      const int op = r < YC ? 0 : 1;
+      const int lt = op == 0 ? r : r - YC;
+      const int ncg = (op == 0 ? YC : XC) / 4;
+      cc = lt % ncg;
+      rg = lt / ncg;
+      src = op == 0 ? Y + n0 + 4 * cc : X + k0 + 4 * cc;
+      ld = op == 0 ? ldy : ldx;
+      sc = __builtin_amdgcn_ldexpf(1.0f, kTT - (op == 0 ? ey : ex));
+      img_off = op == 0 ? 0u : (uint32_t)(2 * CF::YPLANE);
+      plane = op == 0 ? (uint32_t)CF::YPLANE : (uint32_t)CF::XPLANE;
+    };
+    constexpr int NROLE = (YC + XC + 255) / 256;   // 2
+    const bool two = ct + 256 < YC + XC;           // wave-uniform (waves 4, 5)
+    const float* src[NROLE];
+    int64_t ld[NROLE];
+    float sc[NROLE];
+    uint32_t img_off[NROLE], plane[NROLE];
+    int cc[NROLE], rg[NROLE];
+    role(ct, src[0], ld[0], sc[0], img_off[0], plane[0], cc[0], rg[0]);
+    role(two ? ct + 256 : ct, src[1], ld[1], sc[1], img_off[1], plane[1], cc[1], rg[1]);
+    // two register stages, named (a runtime index would put them in scratch)
+    f32x4 raw0[NROLE][8], raw1[NROLE][8];
+    auto load = [&](int t, f32x4 (&r)[NROLE][8]) {
+#pragma unroll
+      for (int k = 0; k < NROLE; ++k) {
+        if (k == 1 && !two) break;
+        const int64_t row0 = r_begin + (int64_t)t * 32 + rg[k] * 8;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          int64_t row = row0 + q;
+          row = row < r_end ? row : r_end - 1;
+          r[k][q] = *reinterpret_cast<const f32x4*>(src[k] + row * ld[k]);
+        }
+      }
+    };
+    auto convert = [&](int t, f32x4 (&r)[NROLE][8]) {
+      const uint32_t stage = smem_base + (t & 1) * CF::STAGE;
+#pragma unroll
+      for (int k = 0; k < NROLE; ++k) {
+        if (k == 1 && !two) break;
+        const int64_t row0 = r_begin + (int64_t)t * 32 + rg[k] * 8;
+        if (row0 + 8 > r_end) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (row0 + q >= r_end) r[k][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          f16x8 h0, h1;
+#pragma unroll
+          for (int q = 0; q < 8; q += 2) {
+            f16x2 p0, p1;
+            split2h(f32x2{r[k][q][c], r[k][q + 1][c]} * sc[k], p0, p1);
+            h0[q] = p0[0]; h0[q + 1] = p0[1];
+            h1[q] = p1[0]; h1[q + 1] = p1[1];
+          }
+          const uint32_t off = stage + img_off[k] + tn_off(4 * cc[k] + c, rg[k]);
+          hds_write16(off, h0);
+          hds_write16(off + plane[k], h1);
+        }
+      }
+    };
+    // step t's operands live in raw0 (t even) / raw1 (t odd), loaded two
+    // steps ahead
+    if (T > 0) load(0, raw0);
+    if (T > 1) load(1, raw1);
+    if (T > 0) {
+      convert(0, raw0);
+      if (T > 2) load(2, raw0);
+    }
+    __syncthreads();
+    for (int t = 0; t < T; t += 2) {
+      if (t + 1 < T) {
+        convert(t + 1, raw1);
+        if (t + 3 < T) load(t + 3, raw1);
+      }
+      __syncthreads();
+      if (t + 1 < T) {
+        if (t + 2 < T) {
+          convert(t + 2, raw0);
+          if (t + 4 < T) load(t + 4, raw0);
+        }
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  // ---- MFMA waves: a 64-wide slice of the longer side each
+  f32x16 acc[BN][BK];
+#pragma unroll
+  for (int a = 0; a < BN; ++a)
+#pragma unroll
+    for (int b = 0; b < BK; ++b)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
+  const int h = lane >> 5;
+  const int nb0 = SPLIT_N ? 64 * wave : 0;   // the wave's first n / k of the tile
+  const int kb0 = SPLIT_N ? 0 : 64 * wave;
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    const uint32_t iy = smem_base + (t & 1) * CF::STAGE;
+    const uint32_t ix = iy + 2 * CF::YPLANE;
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      f16x8 a[BN][2], b[BK][2];
+#pragma unroll
+      for (int i = 0; i < BN; ++i) {
+        const uint32_t oa = tn_off(nb0 + 32 * i + (lane & 31), 2 * st + h);
+        a[i][0] = *reinterpret_cast<const f16x8*>(smem + (iy - smem_base) + oa);
+        a[i][1] = *reinterpret_cast<const f16x8*>(smem + (iy - smem_base) + CF::YPLANE + oa);
+      }
+#pragma unroll
+      for (int j = 0; j < BK; ++j) {
+        const uint32_t ob = tn_off(kb0 + 32 * j + (lane & 31), 2 * st + h);
+        b[j][0] = *reinterpret_cast<const f16x8*>(smem + (ix - smem_base) + ob);
+        b[j][1] = *reinterpret_cast<const f16x8*>(smem + (ix - smem_base) + CF::XPLANE + ob);
+      }
+#pragma unroll
+      for (int i = 0; i < BN; ++i)
+#pragma unroll
+        for (int j = 0; j < BK; ++j) {
+          acc[i][j] = mfma_h(a[i][1], b[j][0], acc[i][j]);
+          acc[i][j] = mfma_h(a[i][0], b[j][1], acc[i][j]);
+          acc[i][j] = mfma_h(a[i][0], b[j][0], acc[i][j]);
+        }
+    }
+    __syncthreads();
+  }
+
+  // un-scale and store the partial tile (every split writes its slot, empty
+  // chunks zeros)
+  const int sh = ey + ex - 2 * kTT;
+  float* out = parts + (int64_t)s * N * K;
+#pragma unroll
+  for (int i = 0; i < BN; ++i)
+#pragma unroll
+    for (int j = 0; j < BK; ++j) {
+      const int col = k0 + kb0 + 32 * j + (lane & 31);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = n0 + nb0 + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+        out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
+      }
+    }
+}
+
 template <bool BIAS, bool WIDE, int NB>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
               const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
@@ -1156,6 +1369,19 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
     }
     const int nt_k = K / CF::XC;
     const int nt = (N / CF::YC) * nt_k;
+#ifdef HN_TN_PC
+    if constexpr (NBN * NBK == 2) {
+      static bool done_pc = false;
+      if (!done_pc) {
+        (void)hipFuncSetAttribute((const void*)k_gemm_tn_pc<NBN, NBK>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS);
+        done_pc = true;
+      }
+      k_gemm_tn_pc<NBN, NBK><<<(unsigned)(nt * S), 512, CF::LDS, st>>>(
+          Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
+      return;
+    }
+#endif
     k_gemm_tn_h<NBN, NBK><<<(unsigned)(nt * S), CF::THREADS, CF::LDS, st>>>(
         Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
   };
