@@ -932,6 +932,43 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     }
   };
 
+#ifdef HN_TN_16
+  // v_mfma_f32_16x16x32_f16 (one 32-row m-step per product): 4 x 4 blocks of
+  // 16 x 16 per wave
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto mma = [&](int buf) {
+    const uint32_t iy = smem_base + buf * CF::STAGE;
+    const uint32_t ix = iy + 2 * CF::YPLANE;
+    f16x8 a[4][2], b[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t oa = tn_off(64 * wm + 16 * i + (lane & 15), lane >> 4);
+      const uint32_t ob = tn_off(64 * wk + 16 * i + (lane & 15), lane >> 4);
+      a[i][0] = hds_read16<f16x8>(iy + oa);
+      a[i][1] = hds_read16<f16x8>(iy + CF::YPLANE + oa);
+      b[i][0] = hds_read16<f16x8>(ix + ob);
+      b[i][1] = hds_read16<f16x8>(ix + CF::XPLANE + ob);
+    }
+    // the reads are inline asm: tie every fragment to the wait
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
+                   "+v"(a[2][1]), "+v"(a[3][0]), "+v"(a[3][1]), "+v"(b[0][0]), "+v"(b[0][1]),
+                   "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[3][0]),
+                   "+v"(b[3][1]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+      }
+  };
+#else
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -970,6 +1007,7 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     }
   };
 
+#endif
   if (T > 0) load(0, raw0);
   if (T > 1) load(1, raw1);
   for (int t = 0; t < T; t += 2) {
@@ -989,6 +1027,19 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
   // chunks zeros)
   const int sh = ey + ex - 2 * kTT;
   float* out = parts + (int64_t)s * N * K;
+#ifdef HN_TN_16
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = k0 + 64 * wk + 16 * j + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = n0 + 64 * wm + 16 * i + 4 * (lane >> 4) + e;
+        out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
+      }
+    }
+#else
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1000,6 +1051,7 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
         out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
       }
     }
+#endif
 }
 
 
