@@ -164,3 +164,37 @@ def test_grl_bf16_vs_oracle(cuda, B, L, d):
     for n, p in layer.named_parameters():
         assert p.grad.dtype == torch.float32
         assert rel(p.grad, params[n].grad) < tol, n
+
+
+@pytest.mark.parametrize("B,L,H", [(3, 2048, 512), (5, 64, 256)])
+def test_gate_bwd_bf16_dense_equals_packed(cuda, B, L, H):
+    """The bf16 gate backward on dense rows (whole tiles, 64-channel spans:
+    the rows the LDS-DMA ring variant takes when built with
+    -DRB_GATE_BWD_DMA=1) and on the same rows as a packed batch of equal
+    lengths (the register-prefetch path): the same per-tile arithmetic, so
+    dz, drg and dxc are bit-identical and the partial sums equal to 1e-6."""
+    from datamining_recblr_amd import kernels
+    from datamining_recblr_amd.kernels import Packed
+
+    g = torch.Generator().manual_seed(B * L + H)
+    rg = torch.randn(B, L, 2 * H, generator=g).to(BF).to(cuda)
+    xc = torch.randn(B, L, H, generator=g).to(BF).to(cuda)
+    z = torch.randn(B, L, H, generator=g).to(BF).to(cuda)
+    dy = torch.randn(B, L, H, generator=g).to(BF).to(cuda)
+    lam = torch.linspace(-2.2, -6.9, H).to(cuda)
+    gb = (0.1 * torch.randn(2 * H, generator=g)).to(cuda)
+    _, car = kernels.gate_scan_fwd(rg, xc, z, lam, None, gate_b=gb)
+    dz_d = torch.empty_like(z)
+    dense = kernels.gate_scan_bwd(rg, xc, z, lam, car, dy, dz_d, gate_b=gb)
+    offs = torch.arange(B + 1, dtype=torch.int64) * L
+    seq = Packed(offs.to(cuda), L, B * L)
+    flat = lambda t: t.reshape(B * L, -1)   # noqa: E731
+    dz_p = torch.empty_like(flat(z))
+    packed = kernels.gate_scan_bwd(flat(rg), flat(xc), flat(z), lam, car, flat(dy), dz_p,
+                                   gate_b=gb, seq=seq)
+    torch.cuda.synchronize()
+    assert torch.equal(flat(dz_d).view(torch.int16), dz_p.view(torch.int16)), "dz"
+    assert torch.equal(flat(dense[0]).view(torch.int16), packed[0].view(torch.int16)), "drg"
+    assert torch.equal(flat(dense[1]).view(torch.int16), packed[1].view(torch.int16)), "dxc"
+    for k, n in ((2, "dLambda"), (3, "dgate_b"), (4, "dh0")):
+        _close(dense[k], packed[k], rtol=1e-6, what=n)

@@ -18,6 +18,8 @@
 #include "../datamining_recblr_amd/csrc/gemm_half.hip"
 #include "../datamining_recblr_amd/csrc/pack.hip"
 #include "../datamining_recblr_amd/csrc/probe.hip"
+#include "../datamining_recblr_amd/csrc/gemm_small.hip"
+#include "../datamining_recblr_amd/csrc/grl_fused.hip"
 
 #include <algorithm>
 #include <cstdio>
@@ -403,6 +405,22 @@ int main(int argc, char** argv) {
                            (int64_t)B, L, H, ncw);
       }, {}});
     }
+    {
+      auto bp = [](float* p) { return reinterpret_cast<bf16_t*>(p); };
+      cs.push_back({"gate_bwd bf16 v4 q4 tc4 dma", 9 * N * 2, [=] {
+        gate_bwd_v<bf16_t, 4, 4, 4, false, true>(bp(rg), 2 * H, bp(xc), H, bp(xz + H), 2 * H, lam,
+                                                 nullptr, car, bp(dy), bp(drg), 2 * H, bp(dxc), H,
+                                                 bp(dz + H), 2 * H, part, dh0, B, L, H, nullptr, 0,
+                                                 nullptr);
+      }, {}});
+      cs.push_back({"gate_bwd bf16 v4 q4 tc4 pf (shipped)", 9 * N * 2, [=] {
+        gate_bwd_v<bf16_t, 4, 4, 4, true>(bp(rg), 2 * H, bp(xc), H, bp(xz + H), 2 * H, lam,
+                                          nullptr, car, bp(dy), bp(drg), 2 * H, bp(dxc), H,
+                                          bp(dz + H), 2 * H, part, dh0, B, L, H, nullptr, 0,
+                                          nullptr);
+      }, {}});
+    }
+    if (getenv("KB_DMA_ONLY")) goto timed;
     add_gate<bf16_t, 4, 4, 4, true>(cs, "bf16 v4 q4 tc4 pf", B, L, H, sep, N, 1);
     add_gate<bf16_t, 4, 4, 4, false>(cs, "bf16 v4 q4 tc4", B, L, H, sep, N, 1);
     add_gate<bf16_t, 8, 8, 2, true>(cs, "bf16 v8 q8 tc2 pf", B, L, H, sep, N, 1);
@@ -498,6 +516,7 @@ int main(int argc, char** argv) {
   }, {}});
   }
 
+timed:
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
