@@ -205,6 +205,13 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
 
 SPLIT_K = 64
 MIN_ROWS_FOR_SPLIT = 16384
+# few-thousand-row weight gradients (the gathered last-layer tail, B rows)
+# with both operands' row-group maxima known: rb_gemm_tn_h with one 32-row
+# group per split (S = M / 32 <= 64) plus the column sum (RECBLR_TN_FEW=1).
+# Off by default: in the step at B = 2,048 the three tail shapes took 19-22 us
+# against hipBLASLt's 18.5-19 us (profiles/r03_tnfew_bench.log)
+TN_FEW_MIN_ROWS = 2048
+_tn_few = os.environ.get("RECBLR_TN_FEW", "0") == "1"
 
 
 _ncus = {}
@@ -227,11 +234,15 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
     the parameter."""
     M = dy2.shape[0]
     N, K = dy2.shape[1], x2.shape[1]
-    if (ymax is not None and xmax is not None and M >= MIN_ROWS_FOR_SPLIT and N % 128 == 0
+    if (ymax is not None and xmax is not None
+            and (M >= MIN_ROWS_FOR_SPLIT or (_tn_few and M >= TN_FEW_MIN_ROWS))
+            and N % 128 == 0
             and K % 128 == 0 and dy2.stride(1) == 1 and x2.stride(1) == 1
             and dy2.stride(0) % 4 == 0 and x2.stride(0) % 4 == 0
             and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0):
         S = _tn_splits(dy2.device, (N // 128) * (K // 128))
+        if M < MIN_ROWS_FOR_SPLIT:   # at least one 32-row group per split
+            S = max(8, min(S, M // 32 // 8 * 8))
         parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
         return kernels.colsum(parts.view(S, -1)).view(N, K)
     if (_small_tn and _half and _split_on and _tn_on and M < MIN_ROWS_FOR_SPLIT and N % 32 == 0

@@ -209,6 +209,37 @@ def test_weight_gradient_tn_matches_fp64(cuda, M, N, K, S):
     assert torch.equal(kernels.gemm_tn_h(dy, x, ymax, xmax, S), parts)
 
 
+@pytest.mark.parametrize("M,N,K", [(2048, 128, 512), (2048, 512, 128), (2048, 128, 256),
+                                   (2500, 512, 256)])
+def test_few_thousand_rows_weight_gradient_on_tn_kernel(cuda, monkeypatch, M, N, K):
+    """linear.wgrad at the gathered last-layer tail's row counts (B = 2,048
+    sequences), RECBLR_TN_FEW=1: with both operands' rmax from the f16 GEMMs that read them
+    (here the few-rows / 256 x 64-tile launches of rb_gemm_nt_h), the weight
+    gradient runs on rb_gemm_tn_h with one 32-row group per split, at the
+    same fp32-level error next to hipBLASLt."""
+    from datamining_recblr_amd import kernels, linear
+
+    monkeypatch.setattr(linear, "_tn_few", True)   # RECBLR_TN_FEW=1
+    calls = []
+    orig = kernels.gemm_tn_h
+    monkeypatch.setattr(kernels, "gemm_tn_h", lambda *a, **k: calls.append(a[4]) or orig(*a, **k))
+    g = torch.Generator().manual_seed(M + N + K)
+    dy = (torch.randn(M, N, generator=g) * torch.rand(M, 1, generator=g) * 1e-3).to(cuda)
+    x = (torch.randn(M, K, generator=g) * 3).to(cuda)
+    ymax = torch.empty((M + 31) // 32, device=cuda)
+    xmax = torch.empty((M + 31) // 32, device=cuda)
+    kernels.gemm_nt_h(dy, kernels.gemm_h_weight(torch.randn(128, N, device=cuda)), 128, rmax=ymax)
+    kernels.gemm_nt_h(x, kernels.gemm_h_weight(torch.randn(256, K, device=cuda)), 256, rmax=xmax)
+    assert torch.equal(ymax, _row_group_max(dy)) and torch.equal(xmax, _row_group_max(x))
+    dw = linear.wgrad(dy, x, ymax=ymax, xmax=xmax)
+    assert len(calls) == 1 and calls[0] * 32 <= M, calls
+    ref = dy.double().t() @ x.double()
+    e_h = _rel_err(dw, ref)
+    e_t = _rel_err(dy.t() @ x, ref)
+    assert e_h < 2e-6 and e_h < 4 * max(e_t, 1e-7), (e_h, e_t)
+    assert torch.equal(linear.wgrad(dy, x, ymax=ymax, xmax=xmax), dw)
+
+
 def test_weight_gradient_rows_decaying_over_2_to_the_60(cuda):
     """Rows whose magnitudes decay by 2^60 along the chunk (the BD-LRU's
     alpha^t gradients): the per-chunk scale keeps the dominant rows exact and
