@@ -178,6 +178,43 @@ __global__ void __launch_bounds__(256) k_seq(Bufs b, int64_t B, int L, int H, in
   }
 }
 
+// the kernel layout with W waves per workgroup (W = 8: the workgroup spans
+// whole 1-KB rows of one sequence) and optionally a barrier after each tile
+// (the workgroup's stores of a tile issued together)
+template <int NT, int Q, int TC, int W, bool BAR>
+__global__ void __launch_bounds__(64 * W) k_seqw(Bufs b, int64_t B, int L, int H, int ncw) {
+  constexpr int G = 64 / Q, TILE = Q * TC;
+  const int lane = threadIdx.x & 63, q = lane & (Q - 1), g = lane / Q;
+  const int64_t wid = (int64_t)blockIdx.x * W + (threadIdx.x >> 6);
+  const int64_t s = wid / ncw;
+  if (s >= B) return;   // whole workgroups (B * ncw % W == 0 here)
+  const int c = (int)(wid - s * ncw) * (G * 4) + g * 4;
+  const int nT = (L + TILE - 1) / TILE;
+  for (int tile = nT - 1; tile >= 0; --tile) {
+    const int t0 = tile * TILE + q * TC;
+    f4 r[TC], i[TC], x[TC], z[TC], d[TC];
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const int64_t t = s * L + min(t0 + j, L - 1);
+      r[j] = ld((const f4*)(b.rg + t * 2 * H + c));
+      i[j] = ld((const f4*)(b.rg + t * 2 * H + H + c));
+      x[j] = ld((const f4*)(b.xc + t * H + c));
+      z[j] = ld((const f4*)(b.xz + t * 2 * H + H + c));
+      d[j] = ld((const f4*)(b.dy + t * H + c));
+    }
+    if (BAR) __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      if (t0 + j >= L) continue;
+      const int64_t t = s * L + t0 + j;
+      st(r[j] * d[j], (f4*)(b.drg + t * 2 * H + c));
+      st(i[j] * d[j], (f4*)(b.drg + t * 2 * H + H + c));
+      st(x[j] * d[j], (f4*)(b.dxc + t * H + c));
+      st(z[j] * d[j], (f4*)(b.dxz + t * 2 * H + H + c));
+    }
+  }
+}
+
 __global__ void fill(float* p, int64_t n, uint32_t seed) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -247,9 +284,29 @@ int main(int argc, char** argv) {
   const int ncw8 = H / 32;
   const unsigned g8 = (unsigned)(((int64_t)B * ncw8 + 3) / 4);
   all4("seq q8 tc2 (kernel layout)", 9 * S, DISPATCH(K_SEQ8, g8, b, (int64_t)B, L, H, ncw8));
+  // workgroup width and per-tile barriers (policy: nt, the kernel's)
+#define SEQW(W, BAR)                                                                         \
+  cs.push_back({"seq q8 tc2 wg" #W " bar" #BAR " nt", 9 * S, [=] {                          \
+    hipLaunchKernelGGL((k_seqw<1, 8, 2, W, BAR>), dim3((unsigned)(((int64_t)B * ncw8 + W - 1) / W)), \
+                       dim3(64 * W), 0, 0, b, (int64_t)B, L, H, ncw8);                       \
+  }, {}})
+  SEQW(4, false);
+  SEQW(4, true);
+  SEQW(8, false);
+  SEQW(8, true);
+  SEQW(2, false);
+  SEQW(16, true);
   const int ncw1 = H / 256;
   const unsigned g1 = (unsigned)(((int64_t)B * ncw1 + 3) / 4);
   all4("seq q1 tc4 (row-wide)", 9 * S, DISPATCH(K_SEQ1, g1, b, (int64_t)B, L, H, ncw1));
+  if (getenv("F54_WG_ONLY")) {   // the workgroup-width sweep only (+ references)
+    std::vector<Case> keep;
+    for (auto& c : cs)
+      if (c.name.find("wg") != std::string::npos || c.name.find("copy 1R1W nt") != std::string::npos ||
+          c.name == "seq q8 tc2 (kernel layout) nt")
+        keep.push_back(c);
+    cs.swap(keep);
+  }
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
