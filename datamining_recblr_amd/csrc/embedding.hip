@@ -25,6 +25,9 @@ namespace rb {
 namespace {
 
 constexpr int kChunk = 64;
+#ifndef RB_EMB_MERGE_LIMIT
+#define RB_EMB_MERGE_LIMIT 0   // rocPRIM's default: 1 << 20
+#endif
 
 __global__ void k_emb_prep(const int64_t* __restrict__ idx, int* __restrict__ keys,
                            int* __restrict__ vals, int64_t M) {
@@ -215,6 +218,13 @@ k_emb_finish(const int* __restrict__ nch, const int* __restrict__ choff,
     dw[(int64_t)v * d + col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
 }
 
+// rocPRIM picks its block-sort + merge-sort path below 2^20 items (~100 us
+// for the bench's ~205k packed positions: block sort plus 14 merge passes);
+// a merge-sort limit of 0 selects Onesweep, the LSD radix sort (stable: the
+// positions of one key stay in order), two 8-bit passes over the 14 key bits
+using EmbSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, RB_EMB_MERGE_LIMIT>;
+
 int key_bits(int64_t V) {
   int b = 1;
   while ((int64_t(1) << b) < V) ++b;
@@ -243,7 +253,7 @@ EmbWs emb_layout(int64_t M, int64_t V, int64_t d) {
   w.desc = take((size_t)max_chunks * 16);
   w.partial = take((size_t)max_chunks * d * 4);
   w.sort_bytes = 0;
-  rocprim::radix_sort_pairs(nullptr, w.sort_bytes, (const int*)nullptr, (int*)nullptr,
+  rocprim::radix_sort_pairs<EmbSortCfg>(nullptr, w.sort_bytes, (const int*)nullptr, (int*)nullptr,
                             (const int*)nullptr, (int*)nullptr, (size_t)M, 0, key_bits(V));
   w.sort_tmp = take(w.sort_bytes);
   w.scan_bytes = 0;
@@ -306,7 +316,7 @@ int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, v
   hipLaunchKernelGGL(k_emb_prep, dim3((unsigned)pblocks), dim3(256), 0, st, idx, keys_in, vals_in,
                      M);
   size_t sb = w.sort_bytes;
-  if (rocprim::radix_sort_pairs(ws + w.sort_tmp, sb, keys_in, keys_out, vals_in, vals_out,
+  if (rocprim::radix_sort_pairs<EmbSortCfg>(ws + w.sort_tmp, sb, keys_in, keys_out, vals_in, vals_out,
                                 (size_t)M, 0, key_bits(V), st) != hipSuccess)
     return fail("rb_embedding_bwd: radix sort failed");
   const unsigned vb = (unsigned)((V + 256) / 256);
