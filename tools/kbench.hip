@@ -375,6 +375,31 @@ int main(int argc, char** argv) {
     cs.push_back(bwd("bwd packed regs", offs_sorted, false, 9 * NP * 4));
     cs.push_back(bwd("bwd packed dma", offs_sorted, true, 9 * NP * 4));
     cs.push_back(bwd("bwd packed-unsorted dma", offs_unsorted, true, 9 * NP * 4));
+    // conv backward on the packed batch: 3 reads (x, the two dxc terms) + 1
+    // write (dx) per element; chunk layouts, prefetch
+    auto cbp = [&](const char* nm, auto kern, int Q, int VEC) {
+      const int span = (64 / Q) * VEC;
+      const int ncw = (H + span - 1) / span;
+      const int64_t blocks = ((int64_t)B * ncw + 3) / 4;
+      cs.push_back({nm, 4 * NP * 4, [=] {
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, 0, (const float*)xz, 2 * H,
+                           w, bias, (const float*)g1, (const float*)dy, dxo, 2 * H, dwp,
+                           (float*)nullptr, (int64_t)B, L, H, ncw, offs_sorted);
+      }, {}});
+    };
+    cbp("conv_bwd packed q4 tc4 (shipped)", k_conv_silu_bwd<float, 4, 4, 4, 4, false>, 4, 4);
+    cbp("conv_bwd packed q4 tc4 pf", k_conv_silu_bwd<float, 4, 4, 4, 4, true>, 4, 4);
+    cbp("conv_bwd packed q8 tc4", k_conv_silu_bwd<float, 4, 4, 8, 4, false>, 8, 4);
+    cbp("conv_bwd packed q4 tc8", k_conv_silu_bwd<float, 4, 4, 4, 8, false>, 4, 4);
+    cbp("conv_bwd packed q2 tc8", k_conv_silu_bwd<float, 4, 4, 2, 8, false>, 2, 4);
+    cbp("conv_bwd packed v2 q4 tc4", k_conv_silu_bwd<float, 4, 2, 4, 4, false>, 4, 2);
+    cbp("conv_bwd packed q4 tc4 (shipped, again)", k_conv_silu_bwd<float, 4, 4, 4, 4, false>, 4, 4);
+    cbp("conv_bwd packed q8 tc4 (again)", k_conv_silu_bwd<float, 4, 4, 8, 4, false>, 8, 4);
+    cs.push_back({"copy4 (1R+1W float4)", 2 * NP * 4, [=] {
+      hipLaunchKernelGGL(copy4, dim3(8192), dim3(256), 0, 0, (const float4*)xc, (float4*)dxc,
+                         (int64_t)(NP / 4));
+    }, {}});
+    if (getenv("KB_CONV_ONLY")) goto timed;
     cs.push_back({"gate_fwd packed", 5 * NP * 4, [=] {
       launch_gate_fwd(rg, 2 * H, xc, H, xz + H, 2 * H, lam, nullptr, nullptr, 0, y, H, car, B, L,
                       H, offs_sorted, 0);
