@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 29
+ABI_VERSION = 30
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -84,6 +84,9 @@ SIGNATURES = {
                                           _i64, _fp, _i64, _fp]),
     "rb_item_ce_probs_h_t": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64,
                                             _i64, _fp, _i64, _fp, _fp]),
+    "rb_item_ce_probs_h_both": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _fp, _i64, _i64,
+                                               _i64, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp]),
+    "rb_group_absmax": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _fp]),
     "rb_item_rank_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
     "rb_item_rank": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _i64,
                                     _fp]),

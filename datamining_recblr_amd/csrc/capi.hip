@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 29; }
+int rb_version(void) { return 30; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -541,7 +541,7 @@ int rb_item_ce_probs_h(const void* seq_img, const int* seq_exp, const void* item
   if (!target || !lse || !dloss || !probs) return fail("rb_item_ce_probs_h: null pointer");
   if (ld < V) return fail("rb_item_ce_probs_h: ld < V");
   return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
-                                item_offset, probs, ld, nullptr,
+                                item_offset, probs, ld, nullptr, nullptr, 0, nullptr,
                                 reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -555,8 +555,31 @@ int rb_item_ce_probs_h_t(const void* seq_img, const int* seq_exp, const void* it
   if (ldt < B || ldt % 4 || reinterpret_cast<uintptr_t>(probs_t) % 16)
     return fail("rb_item_ce_probs_h_t: probs_t must be 16-B aligned with ldt >= B, ldt % 4 == 0");
   return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
-                                item_offset, probs_t, ldt, group_max,
+                                item_offset, probs_t, ldt, group_max, nullptr, 0, nullptr,
                                 reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_ce_probs_h_both(const void* seq_img, const int* seq_exp, const void* item_img,
+                            const int* item_exp, const int64_t* target, const float* lse,
+                            const float* dloss, int64_t B, int64_t V, int64_t d,
+                            int64_t item_offset, float* probs, int64_t ld, float* probs_t,
+                            int64_t ldt, float* row_group_max, float* item_group_max,
+                            void* stream) {
+  if (int rc = check_items_h(seq_img, seq_exp, item_img, item_exp, B, V, d)) return rc;
+  if (!target || !lse || !dloss || !probs || !probs_t || !row_group_max || !item_group_max)
+    return fail("rb_item_ce_probs_h_both: null pointer");
+  if (ld < V) return fail("rb_item_ce_probs_h_both: ld < V");
+  if (ldt < B || ldt % 4 || reinterpret_cast<uintptr_t>(probs_t) % 16)
+    return fail("rb_item_ce_probs_h_both: probs_t must be 16-B aligned with ldt >= B, ldt % 4 == 0");
+  return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
+                                item_offset, probs_t, ldt, item_group_max, probs, ld,
+                                row_group_max, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out, void* stream) {
+  if (!x || !out) return fail("rb_group_absmax: null pointer");
+  if (n <= 0 || c <= 0 || ld < c) return fail("rb_group_absmax: bad shape");
+  return launch_group_absmax(x, n, c, ld, out, reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_item_scores(const float* seq, const float* items, int64_t B, int64_t V, int64_t d,
@@ -689,8 +712,8 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
                  void* stream) {
   if (!dY || !X || !ymax || !xmax || !parts) return fail("rb_gemm_tn_h: null pointer");
   if (M <= 0 || N <= 0 || K <= 0) return fail("rb_gemm_tn_h: empty shape");
-  if (N % 128 || K % 128 || N > 8192 || K > 8192)
-    return fail("rb_gemm_tn_h: N and K must be multiples of 128 (<= 8192)");
+  if (N % 128 || K % 128 || N > 65536 || K > 65536)
+    return fail("rb_gemm_tn_h: N and K must be multiples of 128 (<= 65536)");
   if (splits < 8 || splits % 8 || splits > 65536)
     return fail("rb_gemm_tn_h: splits must be a positive multiple of 8");
   if (ldy < N || ldx < K || ldy % 4 || ldx % 4) return fail("rb_gemm_tn_h: bad row strides");

@@ -412,7 +412,9 @@ int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const in
 int launch_item_ce_probs_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                            const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
                            int64_t V, int64_t D, int64_t v_off, float* out, int64_t ld,
-                           float* gmax, hipStream_t st);
+                           float* gmax, float* out2, int64_t ld2, float* bmax, hipStream_t st);
+int launch_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out,
+                        hipStream_t st);
 int launch_pad_prefix_fwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                           int64_t H, float* h0, float* ws, hipStream_t st);

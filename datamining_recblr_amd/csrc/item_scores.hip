@@ -858,8 +858,11 @@ __global__ __launch_bounds__(256) void k_ce_fwd_h(const _Float16* __restrict__ E
 // [V, ld] instead (each lane's 16 rows as four 16-B pieces of its item's
 // row) and every 32-item group's max |P| (atomicMax into gmax, zeroed by the
 // caller): the operands of the input gradients as f16x3 GEMMs
-// (scoring._bwd_slices)
-template <int D, bool TR>
+// (scoring._bwd_slices).  MODE 0: P; 1: P^T + gmax; 2: both layouts (P into
+// out2 [B, ld2]), gmax and every 32-row group's max |P| (bmax, atomicMax) —
+// the operands of both input gradients as rb_gemm_tn_h products
+// (scoring._bwd_f16).
+template <int D, int MODE>
 __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__ Ei,
                                                     const int* __restrict__ Ee,
                                                     const _Float16* __restrict__ Wi,
@@ -869,7 +872,10 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
                                                     const float* __restrict__ lse,
                                                     const int64_t* __restrict__ tgt,
                                                     const float* __restrict__ dloss, float inv_n,
-                                                    int64_t v_off, float* __restrict__ gmax) {
+                                                    int64_t v_off, float* __restrict__ gmax,
+                                                    float* __restrict__ out2, int64_t ld2,
+                                                    float* __restrict__ bmax) {
+  constexpr bool TR = MODE != 0;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
   Place pl;
   if (!place(RB, NS, pl)) return;
@@ -891,6 +897,7 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
     er[r] = Ee[row] - 2 * kTS;
   }
   const bool full = b0 + kTile <= B;
+  float mb = 0.0f;   // MODE 2: max |P| over the wave's rows and tiles
   stream_tiles<D, 2>(reinterpret_cast<const float*>(Wi), V, per, pl.split,
                      reinterpret_cast<const float*>(We), nullptr,
                      [&](int64_t t, const float* tile, const float* ebuf, const int64_t*) {
@@ -930,14 +937,26 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
             for (int u = 0; u < 4; ++u)
               if (b0 + 8 * q + 4 * h + u < B) o[8 * q + u] = val4[u];
           }
+          if constexpr (MODE == 2) {   // the same values row-major: out2[b][v]
+            float* o2 = out2 + (b0 + 8 * q + 4 * h) * ld2 + v;
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+              if (full || b0 + 8 * q + 4 * h + u < B) o2[u * ld2] = val4[u];
+          }
         }
       }
+      if constexpr (MODE == 2) mb = fmaxf(mb, m);
 #pragma unroll
       for (int sh = 32; sh >= 1; sh >>= 1) m = fmaxf(m, __shfl_xor(m, sh));
       if (lane == 0)   // non-negative floats order as their bit patterns
         atomicMax(reinterpret_cast<int*>(gmax) + t, __float_as_int(m));
     }
   });
+  if constexpr (MODE == 2) {
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) mb = fmaxf(mb, __shfl_xor(mb, sh));
+    if (lane == 0 && b0 < B) atomicMax(reinterpret_cast<int*>(bmax) + b0 / kTile, __float_as_int(mb));
+  }
 }
 
 // ---- host side ---------------------------------------------------------------------
@@ -1069,15 +1088,22 @@ void ce_fwd_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, co
 template <int D>
 void probs_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, int64_t B, int64_t V,
                const Grid2& g, float* out, int64_t ld, const float* lse, const int64_t* tgt,
-               const float* dloss, float inv_n, int64_t v_off, float* gmax, hipStream_t st) {
-  if (gmax)
-    hipLaunchKernelGGL((k_ce_probs_h<D, true>), dim3(g.wgs()), dim3(256), 0, st,
+               const float* dloss, float inv_n, int64_t v_off, float* gmax, float* out2,
+               int64_t ld2, float* bmax, hipStream_t st) {
+  if (out2)
+    hipLaunchKernelGGL((k_ce_probs_h<D, 2>), dim3(g.wgs()), dim3(256), 0, st,
                        (const _Float16*)Ei, Ee, (const _Float16*)Wi, We, B, V, g.per, g.blocks,
-                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax);
+                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax, out2, ld2, bmax);
+  else if (gmax)
+    hipLaunchKernelGGL((k_ce_probs_h<D, 1>), dim3(g.wgs()), dim3(256), 0, st,
+                       (const _Float16*)Ei, Ee, (const _Float16*)Wi, We, B, V, g.per, g.blocks,
+                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax, nullptr,
+                       (int64_t)0, nullptr);
   else
-    hipLaunchKernelGGL((k_ce_probs_h<D, false>), dim3(g.wgs()), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_ce_probs_h<D, 0>), dim3(g.wgs()), dim3(256), 0, st,
                        (const _Float16*)Ei, Ee, (const _Float16*)Wi, We, B, V, g.per, g.blocks,
-                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax);
+                       g.splits, out, ld, lse, tgt, dloss, inv_n, v_off, gmax, nullptr,
+                       (int64_t)0, nullptr);
 }
 
 void sum_parts(const float* parts, int64_t P, int64_t n, float* out, hipStream_t st) {
@@ -1191,12 +1217,13 @@ int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const in
 int launch_item_ce_probs_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                            const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
                            int64_t V, int64_t D, int64_t v_off, float* out, int64_t ld,
-                           float* gmax, hipStream_t st) {
+                           float* gmax, float* out2, int64_t ld2, float* bmax, hipStream_t st) {
   const Grid2 g = plan(B, ntiles(V));
   const float inv_n = 1.0f / (float)B;
   RB_ITEM_DISPATCH(D, probs_h_t, Ei, Ee, Wi, We, B, V, g, out, ld, lse, tgt, dloss, inv_n, v_off,
-                   gmax, st);
-  return launch_status(gmax ? "rb_item_ce_probs_h_t" : "rb_item_ce_probs_h");
+                   gmax, out2, ld2, bmax, st);
+  return launch_status(out2 ? "rb_item_ce_probs_h_both"
+                            : gmax ? "rb_item_ce_probs_h_t" : "rb_item_ce_probs_h");
 }
 
 int launch_item_scores(const float* E, const float* W, int64_t B, int64_t V, int64_t D,

@@ -79,7 +79,53 @@ __global__ __launch_bounds__(64 * RG) void k_colsum4(const float* __restrict__ i
   }
 }
 
+// out[g] = max |x[r][c]| over the rows r of 32-row group g (a partial last
+// group too) and all c < C: the row-group maxima rb_gemm_tn_h takes as operand
+// scales, for tensors no f16 GEMM has read.  One 256-thread workgroup per
+// group: the group's rows x 16-B pieces (or single columns) spread over the
+// threads, every load independent, then a workgroup max.
+__global__ __launch_bounds__(256) void k_group_absmax(const float* __restrict__ x, int64_t n,
+                                                      int64_t c, int64_t ld,
+                                                      float* __restrict__ out, int vec4) {
+  __shared__ float red[4];
+  const int64_t g = blockIdx.x;
+  const int64_t r0 = g * 32;
+  const int nr = (int)((r0 + 32 < n ? r0 + 32 : n) - r0);
+  float m = 0.0f;
+  if (vec4) {
+    const int c4 = (int)(c / 4);
+    const int tot = nr * c4;
+#pragma unroll 4
+    for (int e = threadIdx.x; e < tot; e += 256) {
+      const int r = e / c4, k = e - r * c4;
+      const float4 v = *reinterpret_cast<const float4*>(x + (r0 + r) * ld + 4 * k);
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+  } else {
+    const int64_t tot = (int64_t)nr * c;
+    for (int64_t e = threadIdx.x; e < tot; e += 256) {
+      const int64_t r = e / c, k = e - r * c;
+      m = fmaxf(m, fabsf(x[(r0 + r) * ld + k]));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) out[g] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
 }  // namespace
+
+int launch_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out,
+                        hipStream_t st) {
+  const int64_t ng = (n + 31) / 32;
+  const int vec4 = c % 4 == 0 && ld % 4 == 0 && aligned16(x) && c <= (int64_t)1 << 24;
+  if (ng > 0x7fffffffLL || (!vec4 && c > ((int64_t)1 << 40)))
+    return fail("rb_group_absmax: too many groups");
+  hipLaunchKernelGGL(k_group_absmax, dim3((unsigned)ng), dim3(256), 0, st, x, n, c, ld, out, vec4);
+  return launch_status("rb_group_absmax");
+}
 
 int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
                   float* out, hipStream_t st) {
@@ -89,6 +135,14 @@ int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, 
       aligned16(out)) {
     const int64_t cb4 = (C / 4 + 63) / 64;
     hipLaunchKernelGGL(k_colsum4<16>, dim3((unsigned)(M * cb4)), dim3(1024), 0, st, in, P, C, rs,
+                       ms, cb4, out);
+    return launch_status("rb_colsum");
+  }
+  if (C >= 8192 && P <= 256 && C % 4 == 0 && rs % 4 == 0 && ms % 4 == 0 && aligned16(in) &&
+      aligned16(out)) {
+    // few wide partials (split-K GEMM slices): the k_colsum<4> order, 16-B loads
+    const int64_t cb4 = (C / 4 + 63) / 64;
+    hipLaunchKernelGGL(k_colsum4<4>, dim3((unsigned)(M * cb4)), dim3(256), 0, st, in, P, C, rs,
                        ms, cb4, out);
     return launch_status("rb_colsum");
   }

@@ -815,6 +815,44 @@ def item_ce_probs_h_t(seq: SplitRows, items: SplitRows, target, lse, dloss, item
     return pt, gmax
 
 
+def item_ce_probs_h_both(seq: SplitRows, items: SplitRows, target, lse, dloss, item_offset=0,
+                        pad_to: int = 1):
+    """Both layouts of the logits' gradient in one pass
+    (rb_item_ce_probs_h_both): (P [B, Vp], P^T [V, B], bmax [ceil(B/32)],
+    gmax [ceil(V/32)]) — P's columns padded with zeros to Vp = V rounded up to
+    pad_to; bmax / gmax the max |P| of every 32-row / 32-item group."""
+    B, V, d, target = _split_operands(seq, items, target)
+    _check(lse, "lse")
+    _check(dloss, "dloss")
+    dev = seq.img.device
+    Vp = (V + pad_to - 1) // pad_to * pad_to
+    p = torch.empty((B, Vp), device=dev, dtype=torch.float32)
+    if Vp > V:
+        p[:, V:].zero_()
+    ldt = (B + 3) // 4 * 4
+    pt = torch.empty((V, ldt), device=dev, dtype=torch.float32)[:, :B]
+    maxes = torch.zeros((B + 31) // 32 + (V + 31) // 32, device=dev, dtype=torch.float32)
+    bmax, gmax = maxes[:(B + 31) // 32], maxes[(B + 31) // 32:]
+    _launch("rb_item_ce_probs_h_both", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
+            items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
+            lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
+            int(item_offset), p.data_ptr(), Vp, pt.data_ptr(), ldt, bmax.data_ptr(),
+            gmax.data_ptr(), _stream(seq.img))
+    return p, pt, bmax, gmax
+
+
+def group_absmax(x: torch.Tensor) -> torch.Tensor:
+    """[ceil(n/32)] max |x| over each 32-row group of a 2-D x (rb_group_absmax)."""
+    _check(x, "x")
+    if x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be 2-D with unit column stride")
+    n, c = x.shape
+    out = torch.empty(((n + 31) // 32,), device=x.device, dtype=torch.float32)
+    _launch("rb_group_absmax", 4 * n * c, x.data_ptr(), n, c, x.stride(0), out.data_ptr(),
+            _stream(x))
+    return out
+
+
 def item_rank(seq, items, target, first_item=1, want_equal=True):
     """(n_greater, n_equal) int64 [B]: items in [first_item, V) other than the
     target scoring above / equal to it (-1 for an out-of-range target)."""

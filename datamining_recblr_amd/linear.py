@@ -207,11 +207,13 @@ SPLIT_K = 64
 MIN_ROWS_FOR_SPLIT = 16384
 # few-thousand-row weight gradients (the gathered last-layer tail, B rows)
 # with both operands' row-group maxima known: rb_gemm_tn_h with one 32-row
-# group per split (S = M / 32 <= 64) plus the column sum (RECBLR_TN_FEW=1).
-# Off by default: in the step at B = 2,048 the three tail shapes took 19-22 us
-# against hipBLASLt's 18.5-19 us (profiles/r03_tnfew_bench.log)
+# group per split (S = M / 32 <= 64) plus the column sum; at B = 2,048 the
+# three tail shapes take 16-22 us each, 55.6 us together against hipBLASLt's
+# 56.4 us (profiles/r03_ceb_bench_tnfew.log, r03_tnfew_bench.log: 19-22 us on
+# another lease) — the step then runs no library GEMM (RECBLR_TN_FEW=0:
+# hipBLASLt)
 TN_FEW_MIN_ROWS = 2048
-_tn_few = os.environ.get("RECBLR_TN_FEW", "0") == "1"
+_tn_few = os.environ.get("RECBLR_TN_FEW", "1") != "0"
 
 
 _ncus = {}

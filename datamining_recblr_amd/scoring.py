@@ -43,21 +43,25 @@ PROBS_SLICE_BYTES = 1 << 30
 # Logits pipe of the CE forward and of the sliced backward's P: "f16" (two-part
 # split operands on the f16 MFMA, fp32-level accuracy; default) or "f32".
 CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
-# The sliced backward's two products dseq = P W, ditems = P^T seq: "torch"
-# (hipBLASLt fp32 on P, default) or "f16" (the f16x3 GEMM kernels on a
-# transposed P: 2.2x slower at the bench shape — the NT kernel's 42 row tiles
-# with K = 2048 and online row scales that P^T's rows outgrow;
-# tools/ce_grads_probe.py, profiles/r03_ce_grads_probe.log).
-CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "torch")
+# The backward's two products dseq = P W, ditems = P^T seq: "f16" (default:
+# P written in both layouts, both products on the f16x3 weight-gradient
+# kernel, _bwd_f16) or "torch" (hipBLASLt fp32 on P, sliced).  An earlier f16
+# variant ran ditems as the NT kernel on P^T: 2.2x slower (42 row tiles with
+# K = 2048 and online row scales that P^T's rows outgrow;
+# profiles/r03_ce_grads_probe.log).
+CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "f16")
 
 
 def _f16_grads_ok(seq, table) -> bool:
     """The logits' input gradients as f16x3 GEMMs (_bwd_f16): B a multiple of
-    128 (the weight-gradient kernel's N) and of 32, d of 128."""
+    256 (the weight-gradient kernel's N; its row splits), d of 128, both
+    layouts of P within twice PROBS_SLICE_BYTES."""
     from . import linear
     B, d = seq.shape
-    return (CE_GRADS == "f16" and linear.gemm_format() == "f16x3" and B % 128 == 0
-            and d % 128 == 0 and table.stride(1) == 1 and table.data_ptr() % 16 == 0)
+    V = table.shape[0]
+    return (CE_GRADS == "f16" and linear.gemm_format() == "f16x3" and B % 256 == 0
+            and d % 128 == 0 and table.stride(1) == 1 and table.data_ptr() % 16 == 0
+            and 8 * B * V <= 2 * PROBS_SLICE_BYTES)
 
 
 def _group_max(x: torch.Tensor) -> torch.Tensor:
@@ -68,34 +72,31 @@ def _group_max(x: torch.Tensor) -> torch.Tensor:
 
 
 def _bwd_f16(seq, table, target, lse, dloss, want_seq, want_items, split):
-    """Sliced like _bwd_slices, but the logits' gradient is written transposed
-    (P^T [vc, B], rb_item_ce_probs_h_t, with its 32-item group maxima) and both
-    products run on the f16 pipe: ditems = P^T seq (rb_gemm_nt_h against
-    seq^T's image) and dseq = P W (rb_gemm_tn_h over the item rows, partials
-    summed in a fixed order) — no library GEMM."""
+    """The logits' gradient in both layouts from one pass
+    (rb_item_ce_probs_h_both: P [B, Vp] with its 32-row group maxima, P^T
+    [V, B] with its 32-item group maxima) and both products as the f16x3
+    weight-gradient GEMM (rb_gemm_tn_h, fixed-order row-chunk partials, a
+    column sum): ditems = P^T seq reduced over P's batch rows, dseq = P W over
+    P^T's item rows — no library GEMM."""
     from .linear import _timed, _tn_splits
 
     B, d = seq.shape
     V = table.shape[0]
-    vc = max(32, min(V, PROBS_SLICE_BYTES // (4 * B)) // 32 * 32)
     s_seq, s_tab = split
+    p, pt, bmax, gmax = kernels.item_ce_probs_h_both(s_seq, s_tab, target, lse, dloss,
+                                                     pad_to=256)
+    fl = 2 * B * V * d
     dseq = dtable = None
     if want_items:
-        dtable = torch.empty_like(table)
-        seq_img = kernels.gemm_h_weight(seq, transpose=True)   # Bm = seq^T [d, B]
-    S = _tn_splits(seq.device, (B // 128) * (d // 128)) // 2
-    for v0 in range(0, V, vc):
-        v1 = min(V, v0 + vc)
-        pt, gmax = kernels.item_ce_probs_h_t(s_seq, s_tab.rows(v0, v1), target, lse, dloss,
-                                             item_offset=v0)
-        fl = 2 * B * (v1 - v0) * d
-        if want_items:
-            _timed("gemm", fl, kernels.gemm_nt_h, pt, seq_img, d, out=dtable[v0:v1])
-        if want_seq:
-            rows = table[v0:v1]
-            parts = _timed("gemm", fl, kernels.gemm_tn_h, pt, rows, gmax, _group_max(rows), S)
-            part = kernels.colsum(parts.view(S, -1)).view(B, d)
-            dseq = part if dseq is None else dseq.add_(part)
+        Vp = p.shape[1]
+        S1 = max(8, min(_tn_splits(seq.device, (Vp // 256) * (d // 128)), B // 256 // 8 * 8))
+        parts = _timed("gemm", fl, kernels.gemm_tn_h, p, seq, bmax, kernels.group_absmax(seq), S1)
+        dtable = kernels.colsum(parts.view(S1, -1)).view(Vp, d)[:V]
+    if want_seq:
+        S2 = max(8, _tn_splits(seq.device, (B // 256) * (d // 128)) // 2)
+        parts = _timed("gemm", fl, kernels.gemm_tn_h, pt, table, gmax,
+                       kernels.group_absmax(table), S2)
+        dseq = kernels.colsum(parts.view(S2, -1)).view(B, d)
     return dseq, dtable
 
 

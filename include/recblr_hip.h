@@ -352,6 +352,23 @@ int rb_item_ce_probs_h_t(const void* seq_img, const int* seq_exp, const void* it
                          const float* dloss, int64_t B, int64_t V, int64_t d, int64_t item_offset,
                          float* probs_t, int64_t ldt, float* group_max, void* stream);
 
+/* Both layouts in one pass: probs [B, ld] = P (as rb_item_ce_probs_h) and
+ * probs_t [V, ldt] = P^T with item_group_max (as rb_item_ce_probs_h_t), plus
+ * row_group_max [ceil(B/32)] = max |P| over each 32-row group (atomic max:
+ * both maxima zeroed by the caller).  dL/ditems = P^T seq then runs as the
+ * weight-gradient GEMM over P's rows and dL/dseq = P W over P^T's rows
+ * (rb_gemm_tn_h, RecBLR.py:100-102's backward) with no library GEMM. */
+int rb_item_ce_probs_h_both(const void* seq_img, const int* seq_exp, const void* item_img,
+                            const int* item_exp, const int64_t* target, const float* lse,
+                            const float* dloss, int64_t B, int64_t V, int64_t d,
+                            int64_t item_offset, float* probs, int64_t ld, float* probs_t,
+                            int64_t ldt, float* row_group_max, float* item_group_max,
+                            void* stream);
+
+/* out [ceil(n/32)] = max |x| over each 32-row group of x [n, c] (row stride
+ * ld): rb_gemm_tn_h's operand scales for a tensor no f16 GEMM has read. */
+int rb_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out, void* stream);
+
 /* Workspace bytes of rb_item_rank. */
 int64_t rb_item_rank_workspace(int64_t B, int64_t V, int64_t d);
 

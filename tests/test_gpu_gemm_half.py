@@ -213,13 +213,13 @@ def test_weight_gradient_tn_matches_fp64(cuda, M, N, K, S):
                                    (2500, 512, 256)])
 def test_few_thousand_rows_weight_gradient_on_tn_kernel(cuda, monkeypatch, M, N, K):
     """linear.wgrad at the gathered last-layer tail's row counts (B = 2,048
-    sequences), RECBLR_TN_FEW=1: with both operands' rmax from the f16 GEMMs that read them
+    sequences): with both operands' rmax from the f16 GEMMs that read them
     (here the few-rows / 256 x 64-tile launches of rb_gemm_nt_h), the weight
     gradient runs on rb_gemm_tn_h with one 32-row group per split, at the
     same fp32-level error next to hipBLASLt."""
     from datamining_recblr_amd import kernels, linear
 
-    monkeypatch.setattr(linear, "_tn_few", True)   # RECBLR_TN_FEW=1
+    monkeypatch.setattr(linear, "_tn_few", True)   # RECBLR_TN_FEW (default on)
     calls = []
     orig = kernels.gemm_tn_h
     monkeypatch.setattr(kernels, "gemm_tn_h", lambda *a, **k: calls.append(a[4]) or orig(*a, **k))

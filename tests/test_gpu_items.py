@@ -351,13 +351,43 @@ def test_item_ce_f16_probs_transposed(cuda):
     assert torch.equal(g2, want[10:])
 
 
-@pytest.mark.parametrize("B,V,slice_bytes", [(2048, 10544, 1 << 30), (256, 515, 256 * 4 * 96),
-                                             (128, 33, 1 << 30)])
-def test_item_ce_f16_grads_vs_fp64(cuda, monkeypatch, B, V, slice_bytes):
-    """RECBLR_CE_GRADS=f16: the sliced backward's products on the f16 GEMM
-    kernels (P^T from rb_item_ce_probs_h_t; dseq on rb_gemm_tn_h, ditems on
-    rb_gemm_nt_h) at the bench's shape (B = 2048, n_items = 10,544, d = 128)
-    and on multi-slice tables, against torch fp64; no library GEMM runs."""
+def test_item_ce_f16_probs_both_layouts(cuda):
+    """rb_item_ce_probs_h_both: P (zero-padded columns) and P^T bit-identical
+    to the one-layout kernels, the 32-item group maxima equal to
+    rb_item_ce_probs_h_t's and the 32-row group maxima exact, partial batch
+    tile included; rb_group_absmax exact."""
+    from datamining_recblr_amd import kernels
+
+    seq, W, tgt = _data(200, 1000, 128, cuda, seed=16)
+    ss, sw = kernels.item_split_h(seq), kernels.item_split_h(W)
+    _, lse = kernels.item_ce_fwd_h(ss, sw, tgt)
+    dl = torch.full((), 0.8, device=cuda)
+    p_ref = kernels.item_ce_probs_h(ss, sw, tgt, lse, dl)
+    pt_ref, g_ref = kernels.item_ce_probs_h_t(ss, sw, tgt, lse, dl)
+    p, pt, bmax, gmax = kernels.item_ce_probs_h_both(ss, sw, tgt, lse, dl, pad_to=256)
+    assert p.shape == (200, 1024) and torch.equal(p[:, :1000], p_ref)
+    assert not p[:, 1000:].any()
+    assert torch.equal(pt, pt_ref) and torch.equal(gmax, g_ref)
+    want = torch.nn.functional.pad(p_ref.abs().amax(1), (0, (-200) % 32)).view(-1, 32).amax(1)
+    assert torch.equal(bmax, want)
+    x = torch.randn(1000, 96, device=cuda)
+    want_x = torch.nn.functional.pad(x.abs().amax(1), (0, (-1000) % 32)).view(-1, 32).amax(1)
+    assert torch.equal(kernels.group_absmax(x), want_x)
+    assert torch.equal(kernels.group_absmax(x[:, 1:95]),
+                       torch.nn.functional.pad(x[:, 1:95].abs().amax(1), (0, 24)).view(-1, 32).amax(1))
+
+
+@pytest.mark.parametrize("B,V,slice_bytes,on", [(2048, 10544, 1 << 30, True),
+                                                (512, 1000, 1 << 30, True),
+                                                (256, 515, 256 * 4 * 96, False),
+                                                (128, 33, 1 << 30, False)])
+def test_item_ce_f16_grads_vs_fp64(cuda, monkeypatch, B, V, slice_bytes, on):
+    """RECBLR_CE_GRADS=f16 (default): the logits' gradient in both layouts
+    (rb_item_ce_probs_h_both) and both products on the f16 weight-gradient
+    kernel (rb_gemm_tn_h) at the bench's shape (B = 2048, n_items = 10,544,
+    d = 128) — no library GEMM runs — against torch fp64; shapes outside its
+    conditions (B % 256, both layouts within the slice budget) take the sliced
+    library path, same tolerance."""
     from datamining_recblr_amd import kernels, scoring
 
     monkeypatch.setattr(scoring, "PROBS_SLICE_BYTES", slice_bytes)
@@ -371,7 +401,10 @@ def test_item_ce_f16_grads_vs_fp64(cuda, monkeypatch, B, V, slice_bytes):
     with kernels.kernel_timing() as t:
         (0.7 * scoring.item_cross_entropy(s1, w1, tgt)).backward()
     names = {r[0] for r in t.records}
-    assert "rb_item_ce_probs_h_t" in names and not mm, (names, len(mm))
+    if on:
+        assert "rb_item_ce_probs_h_both" in names and not mm, (names, len(mm))
+    else:
+        assert "rb_item_ce_probs_h_both" not in names and mm, (names, len(mm))
     s2 = seq.double().requires_grad_()
     w2 = W.double().requires_grad_()
     (0.7 * F.cross_entropy(s2 @ w2.t(), tgt)).backward()

@@ -52,3 +52,29 @@ res = {
 }
 for k, v in res.items():
     print(f"{k:32s} {v:8.1f} us")
+
+# the both-layouts plan: ditems = TN over the batch rows of P [B, Vp] (Vp = V
+# rounded to 256), dseq = TN over the item rows of P^T, each + column sum
+Vp = (V + 255) // 256 * 256
+pbuf = torch.zeros(B, Vp, device=dev)
+kernels.item_ce_probs_h(ss, sw, tgt, lse, dl, out=pbuf[:, :V])
+bmax = scoring._group_max(pbuf)
+smax = scoring._group_max(seq)
+res2 = {}
+for S1 in (8, 16):
+    res2[f"TN ditems on P (S={S1})"] = t(lambda: kernels.gemm_tn_h(pbuf, seq, bmax, smax, S1))
+    res2[f"colsum [{S1}, Vp*d]"] = t(lambda: kernels.colsum(torch.empty(S1, Vp * d, device=dev)))
+for S2 in (16, 32, 64):
+    res2[f"TN dseq on P^T (S={S2})"] = t(lambda: kernels.gemm_tn_h(pt, W, gmax, xm, S2))
+    res2[f"colsum [{S2}, B*d]"] = t(lambda: kernels.colsum(torch.empty(S2, B * d, device=dev)))
+for k, v in res2.items():
+    print(f"{k:32s} {v:8.1f} us")
+# accuracy of the two products against fp64 on the same P
+ref_items = (p.double().t() @ seq.double())
+ref_seq = (p.double() @ W.double())
+di = kernels.colsum(kernels.gemm_tn_h(pbuf, seq, bmax, smax, 8).view(8, -1)).view(Vp, d)[:V]
+ds = kernels.colsum(kernels.gemm_tn_h(pt, W, gmax, xm, 32).view(32, -1)).view(B, d)
+for nm, a, r in (("ditems", di, ref_items), ("dseq", ds, ref_seq)):
+    e = ((a.double() - r).abs().max() / r.abs().max()).item()
+    et = (((p.t() @ seq if nm == "ditems" else p @ W).double() - r).abs().max() / r.abs().max()).item()
+    print(f"{nm}: rel err {e:.3e} (torch fp32 {et:.3e})")
