@@ -97,6 +97,35 @@ def test_rows_across_the_fp32_range(cuda, N):
     assert (y[5] == 0).all()
 
 
+@pytest.mark.parametrize("N", [128, 512])
+def test_non_finite_rows(cuda, N):
+    """An inf or NaN entry of A: the outputs an fp32 GEMM makes non-finite
+    are non-finite here too (NaN where torch gives ±inf: the split's low part
+    of an infinite value is inf - inf), and every other row is unaffected —
+    at fp32 accuracy, as without the bad rows."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(13)
+    M, K = 4096 + 77, 256
+    a = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    bad = [3, 300, 301, 4100]
+    a_bad = a.clone()
+    a_bad[3, 7] = float("inf")
+    a_bad[300, 0] = -float("inf")
+    a_bad[301, 200] = float("nan")
+    a_bad[4100, 255] = float("inf")
+    wi = kernels.gemm_h_weight(w.to(cuda))
+    y = kernels.gemm_nt_h(a_bad.to(cuda), wi, N)
+    yt = a_bad.to(cuda) @ w.to(cuda).t()
+    assert torch.equal(torch.isfinite(y), torch.isfinite(yt))
+    good = torch.ones(M, dtype=torch.bool)
+    good[bad] = False
+    assert not torch.isfinite(y[bad]).any()
+    ref = (a.double() @ w.double().t())[good].to(cuda)
+    assert _rel_err(y[good.to(cuda)], ref) < 2e-6
+
+
 def test_row_strided_operand_and_output(cuda):
     """A as a column slice of a wider activation (the x half of xz), out as a
     row-strided view — the layouts the encoder hands over."""
