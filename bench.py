@@ -809,6 +809,23 @@ def main():
         fused_ab["note"] = ("RECBLR_FUSED_GRL / RECBLR_FUSED_GRL_BWD A/B on the headline's "
                             "batches: rb_grl_fwd (conv + gates GEMM + scan in one launch) "
                             "alone and with rb_grl_bwd, against the three-launch path")
+    ffn_act_ab = None
+    if not args.no_full_tail:
+        # the FeedForward's activation in w_1's GEMM epilogue (rb_gemm_nt_h_act)
+        # against the GEMM + rb_silu_dropout_fwd, alternated 3x on the lease
+        from datamining_recblr_amd import linear as _lin
+        saved_a = _lin.set_ffn_act_fused(True)
+        runs = {"fused": [], "two_launches": []}
+        for _ in range(3):
+            for name, on in (("fused", True), ("two_launches", False)):
+                _lin.set_ffn_act_fused(on)
+                runs[name].append(timed_variant(True, True)["ms_per_step"])
+        _lin.set_ffn_act_fused(saved_a)
+        ffn_act_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
+        ffn_act_ab["headline"] = "fused" if saved_a else "two_launches"
+        ffn_act_ab["note"] = ("RECBLR_FFN_ACT A/B on the headline's batches: w_1 with "
+                              "dropout(silu(.)) in its epilogue vs the GEMM and "
+                              "rb_silu_dropout_fwd, best of 3 alternated runs each")
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)
@@ -951,6 +968,7 @@ def main():
             "fixed_length": fixed,
             "device_lengths": devlen,
             "fused_grl": fused_ab,
+            "ffn_act": ffn_act_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

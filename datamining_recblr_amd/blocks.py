@@ -27,7 +27,8 @@ import torch.nn.functional as F
 
 from . import kernels
 from ._lib import RecBLRNativeError
-from .linear import _timed, fire_hooks, has_hooks, linear, mm_nn, mm_nt, rmax_buffer, wgrad
+from .linear import (_timed, fire_hooks, has_hooks, linear, mm_nn, mm_nn_dact, mm_nn_dact_ok, mm_nt,
+                     mm_nt_act, mm_nt_act_ok, rmax_buffer, wgrad)
 
 __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm",
            "silu_dropout", "feed_forward", "set_defer_residual", "defer_residual"]
@@ -242,18 +243,26 @@ class _FeedForward(torch.autograd.Function):
         # row-group maxima of the GEMM inputs: the weight gradients' operand scales
         want = ctx.needs_input_grad[1] or ctx.needs_input_grad[3]
         r_x = rmax_buffer(x2, inner, d) if want else None
-        a1 = _timed("gemm", f, mm_nt, x2, w1, rmax=r_x)
-        u = kernels.silu_dropout_fwd(a1, seed=seed1, p=p, bias=b1)
+        # a1 = x W1^T + b1 and u = dropout(silu(a1)) from one GEMM epilogue
+        # where it applies (b1 then lives in a1: the backward gets no bias)
+        if mm_nt_act_ok(x2, w1):
+            (a1, u), a1_bias = _timed("gemm", f, mm_nt_act, x2, w1, b1, seed1, p, rmax=r_x), None
+        else:
+            a1 = _timed("gemm", f, mm_nt, x2, w1, rmax=r_x)
+            u = kernels.silu_dropout_fwd(a1, seed=seed1, p=p, bias=b1)
+            a1_bias = b1
         r_u = rmax_buffer(u, d, inner) if want else None
         a2 = _timed("gemm", f, mm_nt, u, w2, b2, rmax=r_u)
         ctx.r_x, ctx.r_u = r_x, r_u
         if observe is not None:   # module hooks of w_1 / w_2 (feed_forward)
-            observe(x2.view(x.shape), (a1 + b1).view(*x.shape[:-1], inner), u.view(*x.shape[:-1], inner),
+            pre = a1 if a1_bias is None else a1 + a1_bias
+            observe(x2.view(x.shape), pre.view(*x.shape[:-1], inner), u.view(*x.shape[:-1], inner),
                     a2.view(x.shape))
         save = any(ctx.needs_input_grad)
         y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
                                               p=p, save=save)
         ctx.seed1, ctx.seed2, ctx.p = seed1, seed2, p
+        ctx.a1_has_bias = a1_bias is None
         # in_addend: x's producer takes the residual's gradient (see ResidualGrad)
         ctx.in_addend = in_addend if in_addend is not None and in_addend.taken else None
         ctx.out_addend = _take(out_addend)
@@ -269,10 +278,15 @@ class _FeedForward(torch.autograd.Function):
             dy, s, gamma, mean, rstd, seed=ctx.seed2, p=ctx.p, want_ds=True, want_da=True,
             want_dbias=True, dy2=_pop(ctx.out_addend))
         r_da2 = rmax_buffer(da2, w2.shape[1], d) if ctx.r_u is not None else None
-        du = _timed("gemm", f, mm_nn, da2, w2, rmax=r_da2)
-        dw2 = _timed("gemm", f, wgrad, da2, u, ymax=r_da2, xmax=ctx.r_u)
-        da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True,
-                                            bias=b1)
+        if ctx.a1_has_bias and mm_nn_dact_ok(da2, w2):
+            # du never stored: the activation backward in the GEMM epilogue
+            da1, db1 = _timed("gemm", f, mm_nn_dact, da2, w2, a1, ctx.seed1, ctx.p, rmax=r_da2)
+            dw2 = _timed("gemm", f, wgrad, da2, u, ymax=r_da2, xmax=ctx.r_u)
+        else:
+            du = _timed("gemm", f, mm_nn, da2, w2, rmax=r_da2)
+            dw2 = _timed("gemm", f, wgrad, da2, u, ymax=r_da2, xmax=ctx.r_u)
+            da1, db1 = kernels.silu_dropout_bwd(a1, du, seed=ctx.seed1, p=ctx.p, want_dbias=True,
+                                                bias=None if ctx.a1_has_bias else b1)
         r_da1 = rmax_buffer(da1, d, w1.shape[0]) if ctx.r_x is not None else None
         dx = _timed("gemm", f, mm_nn, da1, w1, rmax=r_da1)
         if ctx.in_addend is not None:   # x's producer adds the residual's gradient

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 30; }
+int rb_version(void) { return 31; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -705,6 +705,42 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
   if ((M + 31) / 32 > 0x7fffffffLL) return fail("rb_gemm_nt_h: grid too large");
   return launch_gemm_nt_h(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate, rmax,
                           reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                     const float* bias, float* out, int64_t ldo, float* rmax, float* act,
+                     uint64_t seed, float p, void* stream) {
+  if (!A || !Wf || !out || !act) return fail("rb_gemm_nt_h_act: null pointer");
+  if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt_h_act: empty shape");
+  if (R % 32 || C % 32 || R > 1024 || C > 1024)
+    return fail("rb_gemm_nt_h_act: R and C must be multiples of 32 (R, C <= 1024)");
+  if (lda < R || lda % 4 || ldo < C || ldo % 4) return fail("rb_gemm_nt_h_act: bad row strides");
+  if (!aligned16(A) || !aligned16(Wf) || !aligned16(out) || !aligned16(act) ||
+      (bias && !aligned16(bias)))
+    return fail("rb_gemm_nt_h_act: A, Wf, out, act and bias must be 16-byte aligned");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_gemm_nt_h_act: dropout p must be in [0, 1)");
+  if ((M + 31) / 32 > 0x7fffffffLL) return fail("rb_gemm_nt_h_act: grid too large");
+  return launch_gemm_nt_h_act(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, rmax, act,
+                              make_drop(nullptr, seed, p), reinterpret_cast<hipStream_t>(stream));
+}
+
+int64_t rb_gemm_nt_h_dact_parts(void) { return nt_h_dact_parts(); }
+
+int rb_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                      float* out, int64_t ldo, float* rmax, const float* pre, uint64_t seed,
+                      float p, float* dpart, int64_t n_parts, void* stream) {
+  if (!A || !Wf || !out || !pre || !dpart) return fail("rb_gemm_nt_h_dact: null pointer");
+  if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt_h_dact: empty shape");
+  if (R % 32 || C % 32 || R > 1024 || C > 512)
+    return fail("rb_gemm_nt_h_dact: R and C must be multiples of 32 (R <= 1024, C <= 512)");
+  if (lda < R || lda % 4 || ldo < C || ldo % 4) return fail("rb_gemm_nt_h_dact: bad row strides");
+  if (!aligned16(A) || !aligned16(Wf) || !aligned16(out) || !aligned16(pre) || !aligned16(dpart))
+    return fail("rb_gemm_nt_h_dact: A, Wf, out, pre and dpart must be 16-byte aligned");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_gemm_nt_h_dact: dropout p must be in [0, 1)");
+  if ((M + 31) / 32 > 0x7fffffffLL) return fail("rb_gemm_nt_h_dact: grid too large");
+  return launch_gemm_nt_h_dact(A, lda, M, (int)R, Wf, (int)C, out, ldo, rmax, pre,
+                               make_drop(nullptr, seed, p), dpart, n_parts,
+                               reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,

@@ -363,6 +363,13 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st);
+int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                         const float* bias, float* out, int64_t ldo, float* rmax, float* act,
+                         DropSpec drop, hipStream_t st);
+int64_t nt_h_dact_parts();
+int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                          float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
+                          float* dpart, int64_t n_parts, hipStream_t st);
 int launch_gemm_nt_hs(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                       const float* bias, float* out, int64_t ldo, float* rmax, hipStream_t st);
 int grl_fwd_lds_bytes();

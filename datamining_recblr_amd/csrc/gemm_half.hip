@@ -272,20 +272,47 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int lane) {
   }
 }
 
-template <bool BIAS, bool WIDE, int NB>
+// ACT (the FeedForward's first projection, RecBLR.py:219-221): a second
+// output act = dropout(silu(out)) — out with the bias, i.e. the activation's
+// input — written beside out by the same epilogue (same row stride ldo);
+// the dropout keep-flags are DropSpec's Philox stream at element index
+// e_base + row * C + col, exactly the flags k_silu_dropout_fwd draws for
+// that element, so act equals the separate kernel's output bit for bit.
+//
+// DACT (the same activation's backward, fused into the input-gradient GEMM
+// dU = dA2 W_2 of the FeedForward's second projection): the tile's dU values
+// never reach HBM; the epilogue loads the activation's input `pre` at the
+// same positions and stores dA1 = dU * keep * scale * silu'(pre) — what
+// k_silu_dropout_bwd computes from dU, bit for bit — and sums dA1 over the
+// tile's rows into per-wave LDS column sums (fixed order, deterministic),
+// written at the end as the workgroup's row of dpart [gridDim.x, C] (the
+// w_1 bias gradient's partials).  Rows of a tile flagged for the cold
+// recompute tail are summed there instead, from their recomputed values.
+constexpr int N_DACT_MAXC = 512;   // LDS column sums: 8 waves x C floats
+template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>
 __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restrict__ A, int64_t lda,
                                                           int64_t M, int R,
                                                           const f16x8* __restrict__ Wf,
                                                           const int* __restrict__ ew, int C,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ out, int64_t ldo,
-                                                          float* __restrict__ rmax, int m_tiles) {
+                                                          float* __restrict__ rmax, int m_tiles,
+                                                          float* __restrict__ act, DropSpec drop,
+                                                          int64_t e_base,
+                                                          const float* __restrict__ pre,
+                                                          float* __restrict__ dpart) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   using CF = NtCfg<NB>;
   constexpr int N_BN = CF::BN, N_NB = NB, N_BDMA = CF::BDMA, N_NSA = CF::NSA, N_LA = N_NSA - 1;
   constexpr int N_B_STAGE = CF::B_STAGE, N_RING = CF::RING;
-  constexpr bool DEFER = NB == 4;   // deferred epilogue (NB = 8: stored at the tile's end)
+  // deferred epilogue for NB = 4 (NB = 8 and DACT: stored at the tile's end)
+  constexpr bool DEFER = NB == 4 && !DACT;
   static_assert(!(NB == 8) || WIDE, "256-column tiles store through the wide epilogue");
+  static_assert(!ACT || (WIDE && !DEFER), "the activation output rides the tile-end wide epilogue");
+  static_assert(!DACT || (WIDE && !DEFER && !ACT && !BIAS), "DACT: tile-end wide epilogue, no bias");
+  const int64_t act_delta = ACT ? (reinterpret_cast<char*>(act) - reinterpret_cast<char*>(out)) : 0;
+  const int64_t pre_delta =
+      DACT ? (reinterpret_cast<const char*>(pre) - reinterpret_cast<const char*>(out)) : 0;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -296,7 +323,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   const int G = gridDim.x;
   const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
   const int U = my_tiles * KT;  // k-steps of this workgroup
-  if (U == 0) return;
+  if (U == 0) {
+    if (DACT)
+      for (int c = tid; c < C; c += N_THREADS) dpart[(int64_t)blockIdx.x * C + c] = 0.0f;
+    return;
+  }
 
   // column exponents and bias into LDS (before any DMA: ordinary loads)
   int* s_ew = reinterpret_cast<int*>(smem + N_RING);
@@ -305,6 +336,10 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     s_ew[c] = ew[c];
     if (BIAS) s_bias[c] = bias[c];
   }
+  // DACT: per-wave column sums of dA1 (wave-private: no atomics)
+  float* s_col = reinterpret_cast<float*>(smem + CF::LDS) + wave * N_DACT_MAXC;
+  if (DACT)
+    for (int c = lane; c < C; c += 64) s_col[c] = 0.0f;
   __syncthreads();
 
   // tile T = blockIdx.x + i*G: the column tiles of one row tile are
@@ -439,6 +474,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   bool pend_on = false, pend_full = true;
   const char* pend_base = nullptr;  // the wave's first row of the pending tile
   int64_t pend_r0 = 0;
+  int pend_c0 = 0;                  // its first column (ACT's dropout element index)
   // narrow stores: lane = one column, 16 dword stores per block (2 rows of
   // 128 B each); wide stores (WIDE: out 16-B aligned, ldo % 4 == 0): each
   // group of 4 registers transposed inside the lane quads, so a lane holds 4
@@ -454,12 +490,22 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         for (int r = 0; r < 4; ++r) v[r] = BIAS ? blk[4 * g + r] + pbias[n] : blk[4 * g + r];
         quad_transpose(v, lane);
         f32x4* o = (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane);
-        if (pend_full || pend_r0 + 8 * g + 4 * (lane >> 5) + (lane & 3) < M)
+        const int64_t row = pend_r0 + 8 * g + 4 * (lane >> 5) + (lane & 3);
+        if (pend_full || row < M)
 #ifdef HN_PLAIN_STORE
           *o = f32x4{v[0], v[1], v[2], v[3]};
 #else
           __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, o);
 #endif
+        if constexpr (ACT) {
+          float m[4];
+          drop.get4(e_base + row * C + pend_c0 + n * 32 + (lane & 28), m);
+          f32x4 a;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) a[r] = fsilu(v[r]) * m[r];
+          if (pend_full || row < M)
+            __builtin_nontemporal_store(a, (f32x4*)(reinterpret_cast<char*>(o) + act_delta));
+        }
       }
     } else {
 #pragma unroll
@@ -481,6 +527,65 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     }
     return pend_full;
   };
+  // DACT tile end: acc[n] holds the tile's un-scaled dU blocks.  The next
+  // block's `pre` values load behind the current block's math (ordinary
+  // loads: the compiler places their waits); rows past M load row M - 1 and
+  // store nothing.  skip_sums: the wave's rows of this tile will be redone
+  // (and summed) by the cold tail.
+  auto dact_epilogue = [&](bool skip_sums) {
+    if constexpr (DACT) {
+      const int rq = 4 * (lane >> 5) + (lane & 3);
+      f32x4 pq[2][4];
+      auto ld_pre = [&](int n, f32x4 (&q)[4]) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int64_t row = pend_r0 + 8 * g + rq;
+          int64_t off = (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane + pre_delta;
+          if (!pend_full && row >= M) off -= (row - (M - 1)) * ldo * 4;
+          q[g] = *reinterpret_cast<const f32x4*>(pend_base + off);
+        }
+      };
+      ld_pre(0, pq[0]);
+#pragma unroll
+      for (int n = 0; n < N_NB; ++n) {
+        if (n + 1 < N_NB) ld_pre(n + 1, pq[(n + 1) & 1]);
+        float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[n][4 * g + r];
+          quad_transpose(v, lane);
+          const int64_t row = pend_r0 + 8 * g + rq;
+          const bool ok = pend_full || row < M;
+          float mk[4];
+          drop.get4(e_base + row * C + pend_c0 + n * 32 + (lane & 28), mk);
+          const f32x4 pv = pq[n & 1][g];
+          f32x4 d;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[r] = (v[r] * mk[r]) * fdsilu(pv[r] + 0.0f);
+          if (ok) {
+            __builtin_nontemporal_store(
+                d, (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane));
+#pragma unroll
+            for (int r = 0; r < 4; ++r) cs[r] += d[r];
+          }
+        }
+        if (!skip_sums) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            cs[r] += dpp_xor1(cs[r]);
+            cs[r] += dpp_xor2(cs[r]);
+            cs[r] += __shfl_xor(cs[r], 32);
+          }
+          if ((lane & 3) == 0 && lane < 32) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s_col[pend_c0 + n * 32 + (lane & 28) + r] += cs[r];
+          }
+        }
+      }
+    }
+  };
   bool stored_prev = false;
 
   int i = 0, kt = 0, c_slot_a = 0, c_slot_b = 0;
@@ -498,8 +603,10 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     {
       const bool ya = u > 0 && u - 1 + N_LA < U;
       // stores after the DMAs: one block per step (DEFER), or the whole
-      // tile at its end (NB = 8)
-      constexpr int NST = DEFER ? (WIDE ? 4 : 16) : 4 * NB;
+      // tile at its end (NB = 8; ACT: twice as many).  vmcnt counts to 63: a
+      // larger allowance is clamped, which only waits for more
+      constexpr int NST_ = DEFER ? (WIDE ? 4 : 16) : (ACT ? 8 : 4) * NB;
+      constexpr int NST = NST_ > 59 ? 59 : NST_;
       if constexpr (N_LA == 1) {
         // A(u) itself was issued in step u-1 (after B(u)): only the stores
         // issued after it may stay in flight
@@ -664,6 +771,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         if (cur_mt < m_tiles) {
           pend_base = reinterpret_cast<const char*>(out + r0 * ldo + cur_ct * N_BN);
           pend_r0 = r0;
+          pend_c0 = cur_ct * N_BN;
           pend_full = full;
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
@@ -671,8 +779,12 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
 #pragma unroll
             for (int n = 0; n < N_NB; ++n) acc[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
           }
+          if constexpr (DACT) {
+            dact_epilogue(flag_tile);
+          } else {
 #pragma unroll
-          for (int n = 0; n < N_NB; ++n) store_block(acc[n], n);
+            for (int n = 0; n < N_NB; ++n) store_block(acc[n], n);
+          }
           stored_prev = full;
         }
 #pragma unroll
@@ -722,6 +834,9 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   if (nflag > 0) {
     hwait_vm<0>();
     const int ntodo = nflag > N_MAXFLAG ? my_tiles : nflag;
+    // DACT, every tile redone: the wave's column sums start over
+    if (DACT && nflag > N_MAXFLAG)
+      for (int c = lane; c < C; c += 64) s_col[c] = 0.0f;
     for (int f = 0; f < ntodo; ++f) {
       const int ii = nflag > N_MAXFLAG ? f : s_flag[f];
       int mt, ct;
@@ -739,46 +854,77 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       m = fmaxf(m, __shfl_xor(m, 32));
       const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
       const float sc = __builtin_amdgcn_ldexpf(1.0f, kTW - e);  // row max < 2^14
-      f32x16 c[N_NB];
-#pragma unroll
-      for (int n = 0; n < N_NB; ++n)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) c[n][j] = 0.0f;
-      for (int kb = 0; kb < KB16; ++kb) {
-        const f32x4 p = *reinterpret_cast<const f32x4*>(arow + kb * 16);
-        const f32x4 q = *reinterpret_cast<const f32x4*>(arow + kb * 16 + 4);
-        f16x8 a0, a1;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          const f32x2 v = (t < 2 ? f32x2{p[2 * t], p[2 * t + 1]} : f32x2{q[2 * t - 4], q[2 * t - 3]}) * sc;
-          f16x2 h0, h1;
-          split2h(v, h0, h1);
-          a0[2 * t] = h0[0]; a0[2 * t + 1] = h0[1];
-          a1[2 * t] = h1[0]; a1[2 * t + 1] = h1[1];
-        }
-#pragma unroll
-        for (int n = 0; n < N_NB; ++n) {
-          const f16x8* bp = Wf + ((int64_t)((ct * N_NB + n) * KB16 + kb) * 2) * 64 + lane;
-          const f16x8 b0 = bp[0], b1 = bp[64];
-          c[n] = mfma_h(a1, b0, c[n]);
-          c[n] = mfma_h(a0, b1, c[n]);
-          c[n] = mfma_h(a0, b0, c[n]);
-        }
-      }
       int erow[16];  // the exact exponent of each C-layout row
 #pragma unroll
       for (int j = 0; j < 16; ++j) erow[j] = __shfl(e, crow(j)) - 2 * kTW;
-#pragma unroll
+      // one column block at a time (the A row is re-read per block from L2:
+      // a cold path, kept to one accumulator block of registers)
       for (int n = 0; n < N_NB; ++n) {
+        f32x16 c;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) c[j] = 0.0f;
+        for (int kb = 0; kb < KB16; ++kb) {
+          const f32x4 p = *reinterpret_cast<const f32x4*>(arow + kb * 16);
+          const f32x4 q = *reinterpret_cast<const f32x4*>(arow + kb * 16 + 4);
+          f16x8 a0, a1;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const f32x2 v = (t < 2 ? f32x2{p[2 * t], p[2 * t + 1]} : f32x2{q[2 * t - 4], q[2 * t - 3]}) * sc;
+            f16x2 h0, h1;
+            split2h(v, h0, h1);
+            a0[2 * t] = h0[0]; a0[2 * t + 1] = h0[1];
+            a1[2 * t] = h1[0]; a1[2 * t + 1] = h1[1];
+          }
+          const f16x8* bp = Wf + ((int64_t)((ct * N_NB + n) * KB16 + kb) * 2) * 64 + lane;
+          const f16x8 b0 = bp[0], b1 = bp[64];
+          c = mfma_h(a1, b0, c);
+          c = mfma_h(a0, b1, c);
+          c = mfma_h(a0, b0, c);
+        }
         const int col = ct * N_BN + n * 32 + ccol;
         const int ecol = s_ew[col];
         const float bv = BIAS ? s_bias[col] : 0.0f;
+        float csum = 0.0f;   // DACT: this lane's rows of the column
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
           const int64_t r = (int64_t)mt * N_BM + wave * 32 + crow(j);
-          if (r < M) out[r * ldo + col] = __builtin_amdgcn_ldexpf(c[n][j], erow[j] + ecol) + bv;
+          if (r < M) {
+            float v = __builtin_amdgcn_ldexpf(c[j], erow[j] + ecol) + bv;
+            if constexpr (DACT) {
+              float mk[4];
+              const int64_t ei = e_base + r * C + col;
+              drop.get4(ei & ~(int64_t)3, mk);
+              const int q = (int)(ei & 3);
+              v = (v * (q == 0 ? mk[0] : q == 1 ? mk[1] : q == 2 ? mk[2] : mk[3])) *
+                  fdsilu(pre[r * ldo + col] + 0.0f);
+              csum += v;
+            }
+            out[r * ldo + col] = v;
+            if constexpr (ACT) {
+              float mk[4];
+              const int64_t ei = e_base + r * C + col;
+              drop.get4(ei & ~(int64_t)3, mk);
+              const int q = (int)(ei & 3);   // (no dynamic register indexing)
+              act[r * ldo + col] = fsilu(v) * (q == 0 ? mk[0] : q == 1 ? mk[1] : q == 2 ? mk[2] : mk[3]);
+            }
+          }
+        }
+        if constexpr (DACT) {
+          csum += __shfl_xor(csum, 32);
+          if (lane < 32) s_col[col] += csum;
         }
       }
+    }
+  }
+  if constexpr (DACT) {
+    // the workgroup's column sums, waves in a fixed order
+    __syncthreads();
+    const float* s_all = reinterpret_cast<const float*>(smem + CF::LDS);
+    for (int c = tid; c < C; c += N_THREADS) {
+      float t = s_all[c];
+#pragma unroll
+      for (int w = 1; w < N_WAVES; ++w) t += s_all[w * N_DACT_MAXC + c];
+      dpart[(int64_t)blockIdx.x * C + c] = t;
     }
   }
 }
@@ -1269,19 +1415,21 @@ k_gemm_tn_pc(const float* __restrict__ Y, int64_t ldy, const float* __restrict__
     }
 }
 
-template <bool BIAS, bool WIDE, int NB>
+template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
               const float* bias, float* out, int64_t ldo, float* rmax, int m_tiles, unsigned grid,
-              hipStream_t st) {
-  constexpr int lds = NtCfg<NB>::LDS;
+              hipStream_t st, float* act = nullptr, DropSpec drop = DropSpec{}, int64_t e_base = 0,
+              const float* pre = nullptr, float* dpart = nullptr) {
+  constexpr int lds = NtCfg<NB>::LDS + (DACT ? N_WAVES * N_DACT_MAXC * 4 : 0);
+  static_assert(lds <= 160 * 1024, "LDS");
   static bool done = false;  // benign race: idempotent
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS, WIDE, NB>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h<BIAS, WIDE, NB, ACT, DACT>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     done = true;
   }
-  k_gemm_nt_h<BIAS, WIDE, NB><<<grid, N_THREADS, lds, st>>>(A, lda, M, R, wf, ew, C, bias, out, ldo,
-                                                                rmax, m_tiles);
+  k_gemm_nt_h<BIAS, WIDE, NB, ACT, DACT><<<grid, N_THREADS, lds, st>>>(
+      A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, act, drop, e_base, pre, dpart);
 }
 
 }  // namespace
@@ -1391,6 +1539,105 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
     else run_nt_h<false, false, 4>(A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st);
   }
   return launch_status("rb_gemm_nt_h");
+}
+
+// out = A Bm^T + bias and act = dropout(silu(out)) in one pass (the
+// FeedForward's first projection + its activation, RecBLR.py:219-221).  The
+// same row split as launch_gemm_nt_h; only the shapes whose every row runs on
+// a wide-epilogue launch are taken (16-B aligned out / act, ldo % 4 == 0,
+// C % 256 == 0, not the few-rows kernel's shapes): nt_h_act_ok says which.
+bool nt_h_act_ok(int64_t M, int R, int C, const float* out, const float* act, int64_t ldo) {
+  const bool wide = (reinterpret_cast<uintptr_t>(out) & 15) == 0 &&
+                    (reinterpret_cast<uintptr_t>(act) & 15) == 0 && ldo % 4 == 0;
+  const bool few = M <= 4096 && (R > 256 || C < 256);
+  return wide && C % 256 == 0 && C <= N_MAXC && R <= 1024 && !few;
+}
+
+int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                         const float* bias, float* out, int64_t ldo, float* rmax, float* act,
+                         DropSpec drop, hipStream_t st) {
+  if (!nt_h_act_ok(M, R, C, out, act, ldo))
+    return fail("rb_gemm_nt_h_act: shape or alignment without a wide-epilogue launch");
+  const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
+  const int nct0 = C / 256;
+  const int64_t rows_round = (int64_t)(G0 / nct0) * N_BM;
+  const int64_t M_main = (G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round : M;
+  const f16x8* wf = (const f16x8*)Wf;
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
+  if (M_main < M) {   // the rows past the last whole round: 256 x 64 tiles
+    const int64_t Mt = M - M_main;
+    const int mt_t = (int)((Mt + N_BM - 1) / N_BM);
+    const int64_t nt_t = (int64_t)((mt_t + 7) / 8) * 8 * (C / 64);
+    const unsigned grid_t = (unsigned)std::min<int64_t>(nt_t, (int64_t)G0);
+    const float* At = A + M_main * lda;
+    float* ot = out + M_main * ldo;
+    float* at = act + M_main * ldo;
+    float* rt = rmax ? rmax + M_main / 32 : nullptr;
+    if (bias) run_nt_h<true, true, 2, true>(At, lda, Mt, R, wf, ew, C, bias, ot, ldo, rt, mt_t, grid_t, st, at, drop, M_main * C);
+    else run_nt_h<false, true, 2, true>(At, lda, Mt, R, wf, ew, C, bias, ot, ldo, rt, mt_t, grid_t, st, at, drop, M_main * C);
+    const int rc = launch_status("rb_gemm_nt_h_act");
+    if (rc || M_main == 0) return rc;
+  }
+  const int m_tiles = (int)((M_main + N_BM - 1) / N_BM);
+  const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * nct0;
+  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)G0);
+  if (bias) run_nt_h<true, true, 8, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
+  else run_nt_h<false, true, 8, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
+  return launch_status("rb_gemm_nt_h_act");
+}
+
+// The backward of launch_gemm_nt_h_act's activation fused into the
+// input-gradient GEMM that produces its output gradient: dU = A Bm^T is
+// never stored; out = dU * keep * scale * silu'(pre) (pre: the activation's
+// input, [M, C] with row stride ldo) and dpart [n_parts, C] receives the
+// workgroups' column sums of out (rows past the launches' grids zeroed).
+// The same row split and shape contract as the forward (nt_h_act_ok), C <=
+// 512.
+// DACT's main launch: 256 x 128 tiles stored at the tile's end (the 256 x 256
+// tile's 128 accumulators leave no registers for the epilogue's operands)
+#ifndef HN_DACT_NB
+#define HN_DACT_NB 4
+#endif
+int64_t nt_h_dact_parts() { return 2 * (int64_t)(num_cus() / 8 * 8 * (8 / N_WAVES)); }
+
+int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
+                          float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
+                          float* dpart, int64_t n_parts, hipStream_t st) {
+  if (!nt_h_act_ok(M, R, C, out, pre, ldo) || C > N_DACT_MAXC)
+    return fail("rb_gemm_nt_h_dact: shape or alignment without a wide-epilogue launch");
+  const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
+  const int nct0 = C / (32 * HN_DACT_NB);
+  const int64_t rows_round = (int64_t)(G0 / nct0) * N_BM;
+  const int64_t M_main = (G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round : M;
+  const f16x8* wf = (const f16x8*)Wf;
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
+  const int m_tiles = (int)((M_main + N_BM - 1) / N_BM);
+  const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * nct0;
+  const unsigned grid = M_main > 0 ? (unsigned)std::min<int64_t>(n_tiles, (int64_t)G0) : 0u;
+  const int64_t Mt = M - M_main;
+  const int mt_t = (int)((Mt + N_BM - 1) / N_BM);
+  const int64_t nt_t = (int64_t)((mt_t + 7) / 8) * 8 * (C / 64);
+  const unsigned grid_t = Mt > 0 ? (unsigned)std::min<int64_t>(nt_t, (int64_t)G0) : 0u;
+  if ((int64_t)grid + grid_t > n_parts) return fail("rb_gemm_nt_h_dact: dpart has too few rows");
+  if (Mt > 0) {   // the rows past the last whole round: 256 x 64 tiles
+    run_nt_h<false, true, 2, false, true>(A + M_main * lda, lda, Mt, R, wf, ew, C, nullptr,
+                                          out + M_main * ldo, ldo, rmax ? rmax + M_main / 32 : nullptr,
+                                          mt_t, grid_t, st, nullptr, drop, M_main * C,
+                                          pre + M_main * ldo, dpart + (int64_t)grid * C);
+    const int rc = launch_status("rb_gemm_nt_h_dact");
+    if (rc) return rc;
+  }
+  if (M_main > 0) {
+    run_nt_h<false, true, HN_DACT_NB, false, true>(A, lda, M_main, R, wf, ew, C, nullptr, out, ldo, rmax,
+                                          m_tiles, grid, st, nullptr, drop, 0, pre, dpart);
+    const int rc = launch_status("rb_gemm_nt_h_dact");
+    if (rc) return rc;
+  }
+  const int64_t used = (int64_t)grid + grid_t;
+  if (used < n_parts &&
+      hipMemsetAsync(dpart + used * C, 0, (size_t)(n_parts - used) * C * 4, st) != hipSuccess)
+    return fail("rb_gemm_nt_h_dact: hipMemsetAsync failed");
+  return 0;
 }
 
 // dW tile: 256 x 128 when N % 256 == 0 (2), else 128 x 256 when K % 256 == 0

@@ -1085,6 +1085,74 @@ def gemm_nt_h(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | No
     return out
 
 
+def gemm_nt_h_act_ok(a: torch.Tensor, C: int) -> bool:
+    """Whether gemm_nt_h_act takes a [M, R] operand with C outputs (freshly
+    allocated contiguous outputs): rb_gemm_nt_h_act's shape contract."""
+    M, R = a.shape
+    return C % 256 == 0 and C <= 1024 and R % 32 == 0 and R <= 1024 and not (
+        M <= 4096 and (R > 256 or C < 256))
+
+
+def gemm_nt_h_act(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None,
+                  seed: int, p: float, rmax: torch.Tensor | None = None):
+    """(out, act): out = a @ Bm^T + bias and act = dropout(silu(out)) from one
+    GEMM epilogue (rb_gemm_nt_h_act) — act equals silu_dropout_fwd(out,
+    seed=seed, p=p) bit for bit."""
+    _check(a, "a")
+    _check_p(p)
+    if a.dim() != 2 or a.stride(1) != 1:
+        raise ValueError("a must be a 2-D tensor with unit inner stride")
+    if not gemm_nt_h_act_ok(a, C):
+        raise ValueError(f"gemm_nt_h_act: no fused launch for {tuple(a.shape)} -> {C}")
+    M, R = a.shape
+    out = torch.empty((M, C), device=a.device, dtype=torch.float32)
+    act = torch.empty_like(out)
+    if bias is not None:
+        _check(bias, "bias")
+    if rmax is not None:
+        _check(rmax, "rmax")
+        if rmax.numel() < (M + 31) // 32:
+            raise ValueError("rmax needs ceil(M/32) entries")
+    _lib.call("rb_gemm_nt_h_act", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
+              0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0),
+              0 if rmax is None else rmax.data_ptr(), act.data_ptr(), int(seed), float(p),
+              _stream(a))
+    return out, act
+
+
+_dact_parts = None
+
+
+def gemm_nt_h_dact(a: torch.Tensor, wf: torch.Tensor, C: int, pre: torch.Tensor, seed: int,
+                   p: float, rmax: torch.Tensor | None = None, want_dbias: bool = True):
+    """(da, dbias or None): du = a @ Bm^T never stored; da = dropout-backward
+    (du) * silu'(pre) (rb_gemm_nt_h_dact) — silu_dropout_bwd(pre, du, seed=seed,
+    p=p) bit for bit — and dbias = da's column sums (fixed-order partials)."""
+    global _dact_parts
+    _check(a, "a")
+    _check(pre, "pre")
+    _check_p(p)
+    if a.dim() != 2 or a.stride(1) != 1:
+        raise ValueError("a must be a 2-D tensor with unit inner stride")
+    M, R = a.shape
+    if not gemm_nt_h_act_ok(a, C) or C > 512:
+        raise ValueError(f"gemm_nt_h_dact: no fused launch for {tuple(a.shape)} -> {C}")
+    if pre.shape != (M, C) or not pre.is_contiguous():
+        raise ValueError("pre must be a contiguous [M, C] tensor")
+    if rmax is not None:
+        _check(rmax, "rmax")
+        if rmax.numel() < (M + 31) // 32:
+            raise ValueError("rmax needs ceil(M/32) entries")
+    if _dact_parts is None:
+        _dact_parts = int(_lib.load().rb_gemm_nt_h_dact_parts())
+    out = torch.empty((M, C), device=a.device, dtype=torch.float32)
+    part = torch.empty((_dact_parts, C), device=a.device, dtype=torch.float32)
+    _lib.call("rb_gemm_nt_h_dact", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
+              out.data_ptr(), out.stride(0), 0 if rmax is None else rmax.data_ptr(),
+              pre.data_ptr(), int(seed), float(p), part.data_ptr(), _dact_parts, _stream(a))
+    return out, (colsum(part) if want_dbias else None)
+
+
 def gemm_tn_h(dy: torch.Tensor, x: torch.Tensor, ymax: torch.Tensor, xmax: torch.Tensor,
               splits: int) -> torch.Tensor:
     """Row-chunk partials of dW = dy^T x on the f16 pipe (rb_gemm_tn_h):

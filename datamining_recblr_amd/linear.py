@@ -184,6 +184,55 @@ def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
     return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
 
 
+# The FeedForward's first projection with dropout(silu(.)) in its epilogue
+# (rb_gemm_nt_h_act): the activation kernel's re-read of the GEMM output is
+# gone.  RECBLR_FFN_ACT=0: the GEMM and rb_silu_dropout_fwd as two launches.
+_act_fused = os.environ.get("RECBLR_FFN_ACT", "1") != "0"
+# below one persistent round (the gathered last-layer tail, B = 2,048 rows)
+# the fused launches run on a few dozen workgroups and measured slower than
+# the two launches (mm_nn_dact 30.7 us at 2,048 rows; profiles/r03_ffnact_bench.log)
+ACT_MIN_ROWS = 16384
+
+
+def set_ffn_act_fused(on: bool) -> bool:
+    """Switch the fused FeedForward activation (A/B in bench.py); returns the
+    previous setting."""
+    global _act_fused
+    prev, _act_fused = _act_fused, bool(on)
+    return prev
+
+
+def mm_nt_act_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether mm_nt_act applies to a [M, K] @ w [N, K]^T (else: the GEMM and
+    the activation kernel as two launches)."""
+    N, K = w.shape
+    return (_act_fused and _half and a.dtype == w.dtype and a.shape[0] >= ACT_MIN_ROWS
+            and _split_ok(a, N, K) and kernels.gemm_nt_h_act_ok(a, N))
+
+
+def mm_nt_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, seed: int, p: float,
+              rmax: torch.Tensor | None = None):
+    """(a @ w^T + bias, dropout(silu(a @ w^T + bias))) from one f16x3 GEMM
+    launch (where mm_nt_act_ok)."""
+    return kernels.gemm_nt_h_act(a, _weight_split(w, False), w.shape[0], bias, seed, p, rmax=rmax)
+
+
+def mm_nn_dact_ok(dy: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether mm_nn_dact applies to dy [M, N] @ w [N, K]."""
+    N, K = w.shape
+    return (_act_fused and _half and dy.dtype == w.dtype and K <= 512
+            and dy.shape[0] >= ACT_MIN_ROWS and _split_ok(dy, K, N)
+            and kernels.gemm_nt_h_act_ok(dy, K))
+
+
+def mm_nn_dact(dy: torch.Tensor, w: torch.Tensor, pre: torch.Tensor, seed: int, p: float,
+               rmax: torch.Tensor | None = None):
+    """(da, dbias): the activation backward of mm_nt_act's act fused into the
+    input-gradient GEMM du = dy @ w (du never stored; where mm_nn_dact_ok)."""
+    return kernels.gemm_nt_h_dact(dy, _weight_split(w, True), w.shape[1], pre, seed, p,
+                                  rmax=rmax)
+
+
 def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
           rmax: torch.Tensor | None = None) -> torch.Tensor:
     """dy [M, N] @ w [N, K] (the input gradient of F.linear); with `out`,
@@ -272,9 +321,9 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
 def _label(fn, args) -> str:
     """GEMM label for the bench's per-shape breakdown: op[M x K -> N]."""
     name = getattr(fn, "__name__", "gemm")
-    if name in ("mm_nt", "mm_nn") and len(args) >= 2:
+    if name in ("mm_nt", "mm_nn", "mm_nt_act", "mm_nn_dact") and len(args) >= 2:
         a, w = args[0], args[1]
-        n_out = w.shape[0] if name == "mm_nt" else w.shape[1]
+        n_out = w.shape[1] if name.startswith("mm_nn") else w.shape[0]
         return f"{name}[{a.shape[0]}x{a.shape[1]}->{n_out}]"
     if name == "wgrad" and len(args) >= 2:
         return f"wgrad[{args[0].shape[0]}:{args[0].shape[1]}x{args[1].shape[1]}]"

@@ -499,6 +499,32 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
                  const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                  void* stream);
 
+/* rb_gemm_nt_h with the FeedForward's activation in its epilogue
+ * (RecBLR.py:219-221, w_1 then dropout(silu(.))): out = A Bm^T + bias and
+ * act = dropout(silu(out)), both [M, C] with row stride ldo — act equals
+ * rb_silu_dropout_fwd(out, NULL, NULL, seed, p) bit for bit (same Philox
+ * flags per element).  Taken only where every row runs on a wide-epilogue
+ * launch: out and act 16-B aligned, ldo % 4 == 0, C % 256 == 0, R <= 1024 and
+ * not (M <= 4096 and (R > 256 or C < 256)); other shapes fail (use
+ * rb_gemm_nt_h + rb_silu_dropout_fwd). */
+int rb_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                     const float* bias, float* out, int64_t ldo, float* rmax, float* act,
+                     uint64_t seed, float p, void* stream);
+
+/* The backward of rb_gemm_nt_h_act's activation fused into the FeedForward's
+ * input-gradient GEMM dU = dA2 W_2 (RecBLR.py:219-222 backward): dU is not
+ * stored; out = dropout-backward(dU) * silu'(pre) — rb_silu_dropout_bwd(pre,
+ * NULL, NULL, seed, p, dU) bit for bit — with pre the activation's input
+ * (rb_gemm_nt_h_act's out), [M, C] at row stride ldo like out; dpart
+ * [n_parts, C] receives column sums of out per workgroup in a fixed order
+ * (the w_1 bias gradient's partials; sum them, e.g. rb_colsum; unused rows
+ * zeroed).  n_parts >= rb_gemm_nt_h_dact_parts().  Shape contract of
+ * rb_gemm_nt_h_act, C <= 512; no bias. */
+int64_t rb_gemm_nt_h_dact_parts(void);
+int rb_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                      float* out, int64_t ldo, float* rmax, const float* pre, uint64_t seed,
+                      float p, float* dpart, int64_t n_parts, void* stream);
+
 /* Weight gradient of F.linear, dW = dY^T X, as `splits` fixed-order row-chunk
  * partials on the f16 pipe (two-part split, three products):
  * parts[s][n, k] = sum over the rows m of chunk s of dY[m, n] X[m, k]

@@ -189,6 +189,42 @@ def test_fused_feed_forward(cuda, p, split_gemm_calls):
         close(a.grad, b.grad, atol=1e-4, rtol=1e-4, what=name)
 
 
+@pytest.mark.parametrize("M", [20000, 204632])
+def test_feed_forward_fused_activation_bitwise(cuda, M):
+    """The FeedForward with w_1's activation in the forward GEMM's epilogue
+    and its backward in the dU GEMM's (RECBLR_FFN_ACT, linear.mm_nt_act /
+    mm_nn_dact) == the GEMMs + rb_silu_dropout_fwd/bwd path, bit for bit: the
+    output and every gradient but db1 (the w_1 bias gradient: the same
+    values summed in another fixed order, within fp32 re-association)."""
+    from datamining_recblr_amd import linear
+    from datamining_recblr_amd.blocks import _FeedForward
+
+    g = torch.Generator(device="cpu").manual_seed(22)
+    d = 128
+    base = [torch.randn(M, d, generator=g), 0.05 * torch.randn(4 * d, d, generator=g),
+            0.1 * torch.randn(4 * d, generator=g), 0.05 * torch.randn(d, 4 * d, generator=g),
+            0.1 * torch.randn(d, generator=g), 1 + 0.1 * torch.randn(d, generator=g),
+            0.1 * torch.randn(d, generator=g)]
+    dy = torch.randn(M, d, generator=g).to(cuda)
+    res = []
+    for fused in (True, False):
+        prev = linear.set_ffn_act_fused(fused)
+        try:
+            leaves = [t.to(cuda).requires_grad_() for t in base]
+            assert linear.mm_nt_act_ok(leaves[0], leaves[1]) == fused
+            assert linear.mm_nn_dact_ok(dy, leaves[3]) == fused
+            y = _FeedForward.apply(*leaves, 41, 42, 0.2, 1e-12)
+            y.backward(dy)
+            res.append([y.detach()] + [t.grad for t in leaves])
+        finally:
+            linear.set_ffn_act_fused(prev)
+    for name, u, v in zip(("y", "dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta"), *res):
+        if name == "db1":
+            close(u, v, atol=1e-6 * v.abs().max().item(), rtol=1e-5, what=name)
+        else:
+            assert torch.equal(u, v), name
+
+
 def test_train_mode_dropout(cuda):
     """Train-mode model: fresh dropout per call (outputs differ run to run),
     reproducible under torch.manual_seed, and p = 0 in train mode == eval."""

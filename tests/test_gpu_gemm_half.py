@@ -126,6 +126,93 @@ def test_non_finite_rows(cuda, N):
     assert _rel_err(y[good.to(cuda)], ref) < 2e-6
 
 
+@pytest.mark.parametrize("M", [5000, 70001, 196608 + 8024])
+@pytest.mark.parametrize("p,bias", [(0.0, True), (0.2, True), (0.2, False)])
+def test_fused_activation_epilogue(cuda, M, p, bias):
+    """rb_gemm_nt_h_act (the FeedForward's w_1 with dropout(silu(.)) in the
+    epilogue, RecBLR.py:219-221): out bit-identical to rb_gemm_nt_h with the
+    bias, act bit-identical to rb_silu_dropout_fwd(out) with the same seed —
+    on the persistent 256 x 256 launch, the 256 x 64 launch of the rows past
+    the last whole round (Philox element index offset) and below one round;
+    rows 7-9 and a wave's rows with zero prefixes force the cold recompute
+    tail; the rmax side output equals the unfused GEMM's."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + int(10 * p))
+    R, C = 128, 512
+    a = torch.randn(M, R, generator=g)
+    a[7, :16] = 0
+    a[8, :16] *= 1e-12
+    a[9] *= torch.exp2(torch.arange(R).float() / 4)
+    a[300:340, :16] = 0
+    a = a.to(cuda)
+    w = (torch.randn(C, R, generator=g) / R ** 0.5).to(cuda)
+    b = (0.1 * torch.randn(C, generator=g)).to(cuda) if bias else None
+    wi = kernels.gemm_h_weight(w)
+    nr = (M + 31) // 32
+    r1 = torch.full((nr,), -1.0, device=cuda)
+    r2 = torch.full((nr,), -1.0, device=cuda)
+    out, act = kernels.gemm_nt_h_act(a, wi, C, b, seed=1234567, p=p, rmax=r1)
+    ref = kernels.gemm_nt_h(a, wi, C, bias=b, rmax=r2)
+    assert torch.equal(out, ref)
+    assert torch.equal(act, kernels.silu_dropout_fwd(ref, seed=1234567, p=p))
+    assert torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("M", [5000, 70001, 196608 + 8024])
+@pytest.mark.parametrize("p", [0.0, 0.2])
+def test_fused_activation_backward_epilogue(cuda, M, p):
+    """rb_gemm_nt_h_dact (dU = dA2 W_2 with the activation's backward in the
+    epilogue; dU never stored): da bit-identical to rb_gemm_nt_h +
+    rb_silu_dropout_bwd with the same seed, on both launches (the 256 x 64 one
+    with the Philox element offset) and below one round; rows 7-9 and a
+    wave's rows with zero prefixes go through the cold recompute tail (their
+    column sums from the recomputed values); dbias within fp32
+    re-association of the unfused column partials, and deterministic; rmax
+    as the unfused GEMM's."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + 3 + int(10 * p))
+    R, C = 128, 512
+    a = torch.randn(M, R, generator=g)
+    a[7, :16] = 0
+    a[8, :16] *= 1e-12
+    a[9] *= torch.exp2(torch.arange(R).float() / 4)
+    a[300:340, :16] = 0
+    a = a.to(cuda)
+    w = (torch.randn(R, C, generator=g) / R ** 0.5).to(cuda)   # mm_nn's w [N=R, K=C]
+    pre = torch.randn(M, C, generator=g).to(cuda)
+    wi = kernels.gemm_h_weight(w, transpose=True)
+    nr = (M + 31) // 32
+    r1 = torch.full((nr,), -1.0, device=cuda)
+    r2 = torch.full((nr,), -1.0, device=cuda)
+    da, db = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p, rmax=r1)
+    du = kernels.gemm_nt_h(a, wi, C, rmax=r2)
+    da_ref, db_ref = kernels.silu_dropout_bwd(pre, du, seed=7654321, p=p, want_dbias=True)
+    assert torch.equal(da, da_ref)
+    assert torch.equal(r1, r2)
+    ref64 = da_ref.double().sum(0)
+    tol = 1e-6 * da_ref.double().abs().sum(0).max().item()
+    assert (db.double() - ref64).abs().max().item() < tol
+    assert (db_ref.double() - ref64).abs().max().item() < tol
+    da2, db2 = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p)
+    assert torch.equal(da2, da) and torch.equal(db2, db)
+
+
+def test_fused_activation_rejects_other_shapes(cuda):
+    """The fused launch takes only shapes whose rows all run on a wide-epilogue
+    launch (C % 256 == 0, not the few-rows kernel's shapes)."""
+    from datamining_recblr_amd import kernels
+
+    a = torch.randn(5000, 128, device=cuda)
+    assert not kernels.gemm_nt_h_act_ok(a, 128)
+    assert not kernels.gemm_nt_h_act_ok(a[:2048, :], 128)
+    assert kernels.gemm_nt_h_act_ok(a, 512)
+    with pytest.raises(ValueError):
+        kernels.gemm_nt_h_act(a, kernels.gemm_h_weight(torch.randn(128, 128, device=cuda)), 128,
+                              None, seed=1, p=0.1)
+
+
 def test_row_strided_operand_and_output(cuda):
     """A as a column slice of a wider activation (the x half of xz), out as a
     row-strided view — the layouts the encoder hands over."""
