@@ -306,10 +306,16 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   constexpr int N_BN = CF::BN, N_NB = NB, N_BDMA = CF::BDMA, N_NSA = CF::NSA, N_LA = N_NSA - 1;
   constexpr int N_B_STAGE = CF::B_STAGE, N_RING = CF::RING;
   // deferred epilogue for NB = 4 (NB = 8 and DACT: stored at the tile's end)
-  constexpr bool DEFER = NB == 4 && !DACT;
+#ifdef HN_DACT_DEFER
+  // A/B build: DACT's blocks deferred a k-step each (256 VGPRs, 12 spilled:
+  // 1,068 vs 295 us at 204,632 rows, profiles/r03_ffn_probe.txt)
+  constexpr bool DEFER = NB == 4;
+#else
+  constexpr bool DEFER = NB == 4 && !DACT;   // DACT: stored at the tile's end
+#endif
   static_assert(!(NB == 8) || WIDE, "256-column tiles store through the wide epilogue");
-  static_assert(!ACT || (WIDE && !DEFER), "the activation output rides the tile-end wide epilogue");
-  static_assert(!DACT || (WIDE && !DEFER && !ACT && !BIAS), "DACT: tile-end wide epilogue, no bias");
+  static_assert(!ACT || WIDE, "the activation output rides the wide epilogue");
+  static_assert(!DACT || (WIDE && !ACT && !BIAS), "DACT: wide epilogue, no bias");
   const int64_t act_delta = ACT ? (reinterpret_cast<char*>(act) - reinterpret_cast<char*>(out)) : 0;
   const int64_t pre_delta =
       DACT ? (reinterpret_cast<const char*>(pre) - reinterpret_cast<const char*>(out)) : 0;
@@ -517,9 +523,74 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       }
     }
   };
+  // DACT: the activation's backward on one un-scaled dU block of the pending
+  // tile (pend_*): dA1 = dU * keep * scale * silu'(pre) stored, and summed
+  // over the block's rows into the wave's LDS column sums unless the cold
+  // tail will redo the tile (skip_sums).  ld_pre loads a block's `pre`
+  // values (ordinary loads: the compiler places their waits); rows past M
+  // load row M - 1 and store nothing.
+  const int rq = 4 * (lane >> 5) + (lane & 3);   // a lane's row in an 8-row group (wide layout)
+  auto ld_pre = [&](int n, f32x4 (&q)[4]) {
+    if constexpr (DACT) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int64_t row = pend_r0 + 8 * g + rq;
+        int64_t off = (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane + pre_delta;
+        if (!pend_full && row >= M) off -= (row - (M - 1)) * ldo * 4;
+        q[g] = *reinterpret_cast<const f32x4*>(pend_base + off);
+      }
+    }
+  };
+  auto dact_block = [&](const f32x16& blk, int n, const f32x4 (&pq)[4], bool skip_sums) {
+    if constexpr (DACT) {
+      float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = blk[4 * g + r];
+        quad_transpose(v, lane);
+        const int64_t row = pend_r0 + 8 * g + rq;
+        const bool ok = pend_full || row < M;
+        float mk[4];
+        drop.get4(e_base + row * C + pend_c0 + n * 32 + (lane & 28), mk);
+        const f32x4 pv = pq[g];
+        f32x4 d;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r] = (v[r] * mk[r]) * fdsilu(pv[r] + 0.0f);
+        if (ok) {
+          __builtin_nontemporal_store(
+              d, (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane));
+#pragma unroll
+          for (int r = 0; r < 4; ++r) cs[r] += d[r];
+        }
+      }
+      if (!skip_sums) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          cs[r] += dpp_xor1(cs[r]);
+          cs[r] += dpp_xor2(cs[r]);
+          cs[r] += __shfl_xor(cs[r], 32);
+        }
+        if ((lane & 3) == 0 && lane < 32) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s_col[pend_c0 + n * 32 + (lane & 28) + r] += cs[r];
+        }
+      }
+    }
+  };
+  // DEFER + DACT: the pending block's `pre` values, loaded one k-step ahead
+  f32x4 pq1[4];
+  bool pend_skip = false;
   auto store_quarter = [&]() {
     const int q = pend_q++;
-    if constexpr (DEFER) {
+    if constexpr (DEFER && DACT) {
+      if (q == 0) dact_block(pend[0], 0, pq1, pend_skip);
+      else if (q == 1) dact_block(pend[1], 1, pq1, pend_skip);
+      else if (q == 2) dact_block(pend[2], 2, pq1, pend_skip);
+      else dact_block(pend[3], 3, pq1, pend_skip);
+      if (q + 1 < N_NB) ld_pre(q + 1, pq1);
+    } else if constexpr (DEFER) {
       if (q == 0) store_block(pend[0], 0);
       else if (q == 1) store_block(pend[1], 1);
       else if (q == 2) store_block(pend[2], 2);
@@ -527,62 +598,16 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     }
     return pend_full;
   };
-  // DACT tile end: acc[n] holds the tile's un-scaled dU blocks.  The next
-  // block's `pre` values load behind the current block's math (ordinary
-  // loads: the compiler places their waits); rows past M load row M - 1 and
-  // store nothing.  skip_sums: the wave's rows of this tile will be redone
-  // (and summed) by the cold tail.
+  // DACT tile end (no DEFER): acc[n] holds the tile's un-scaled dU blocks;
+  // the next block's `pre` values load behind the current block's math
   auto dact_epilogue = [&](bool skip_sums) {
-    if constexpr (DACT) {
-      const int rq = 4 * (lane >> 5) + (lane & 3);
+    if constexpr (DACT && !DEFER) {
       f32x4 pq[2][4];
-      auto ld_pre = [&](int n, f32x4 (&q)[4]) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int64_t row = pend_r0 + 8 * g + rq;
-          int64_t off = (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane + pre_delta;
-          if (!pend_full && row >= M) off -= (row - (M - 1)) * ldo * 4;
-          q[g] = *reinterpret_cast<const f32x4*>(pend_base + off);
-        }
-      };
       ld_pre(0, pq[0]);
 #pragma unroll
       for (int n = 0; n < N_NB; ++n) {
         if (n + 1 < N_NB) ld_pre(n + 1, pq[(n + 1) & 1]);
-        float cs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = acc[n][4 * g + r];
-          quad_transpose(v, lane);
-          const int64_t row = pend_r0 + 8 * g + rq;
-          const bool ok = pend_full || row < M;
-          float mk[4];
-          drop.get4(e_base + row * C + pend_c0 + n * 32 + (lane & 28), mk);
-          const f32x4 pv = pq[n & 1][g];
-          f32x4 d;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) d[r] = (v[r] * mk[r]) * fdsilu(pv[r] + 0.0f);
-          if (ok) {
-            __builtin_nontemporal_store(
-                d, (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane));
-#pragma unroll
-            for (int r = 0; r < 4; ++r) cs[r] += d[r];
-          }
-        }
-        if (!skip_sums) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            cs[r] += dpp_xor1(cs[r]);
-            cs[r] += dpp_xor2(cs[r]);
-            cs[r] += __shfl_xor(cs[r], 32);
-          }
-          if ((lane & 3) == 0 && lane < 32) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s_col[pend_c0 + n * 32 + (lane & 28) + r] += cs[r];
-          }
-        }
+        dact_block(acc[n], n, pq[n & 1], skip_sums);
       }
     }
   };
@@ -605,7 +630,9 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       // stores after the DMAs: one block per step (DEFER), or the whole
       // tile at its end (NB = 8; ACT: twice as many).  vmcnt counts to 63: a
       // larger allowance is clamped, which only waits for more
-      constexpr int NST_ = DEFER ? (WIDE ? 4 : 16) : (ACT ? 8 : 4) * NB;
+      // (DEFER + DACT: each step's 4 stores are followed by the next block's
+      // 4 `pre` loads)
+      constexpr int NST_ = DEFER ? (WIDE ? (DACT || ACT ? 8 : 4) : 16) : (ACT ? 8 : 4) * NB;
       constexpr int NST = NST_ > 59 ? 59 : NST_;
       if constexpr (N_LA == 1) {
         // A(u) itself was issued in step u-1 (after B(u)): only the stores
@@ -802,6 +829,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         if (lane == 0 && grp * 32 < M) rmax[grp] = w;
       }
       tmax = 0.0f;
+      const bool tile_flagged = flag_tile;
       if (flag_tile) {
         if (nflag < N_MAXFLAG) s_flag[nflag] = i;
         ++nflag;
@@ -810,9 +838,14 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       if constexpr (DEFER) {
         pend_on = cur_mt < m_tiles;
         pend_r0 = (int64_t)cur_mt * N_BM + wave * 32;
+        pend_c0 = cur_ct * N_BN;
         pend_full = pend_r0 + 32 <= M;
         pend_base = reinterpret_cast<const char*>(out + pend_r0 * ldo + cur_ct * N_BN);
         pend_q = 0;
+        if (DACT && pend_on) {   // the first block's `pre`, stored during the next step
+          pend_skip = tile_flagged;
+          ld_pre(0, pq1);
+        }
       }
       kt = 0;
       ++i;
@@ -1553,13 +1586,20 @@ bool nt_h_act_ok(int64_t M, int R, int C, const float* out, const float* act, in
   return wide && C % 256 == 0 && C <= N_MAXC && R <= 1024 && !few;
 }
 
+// ACT's main launch: 256 x 256 tiles stored at the tile's end (8; 264 us at
+// 204,632 rows against 140 + 135-142 us for the GEMM and the activation
+// kernel), or, as an A/B build, 256 x 128 tiles with the deferred epilogue
+// (4: 995 us, profiles/r03_ffn_probe2.txt)
+#ifndef HN_ACT_NB
+#define HN_ACT_NB 8
+#endif
 int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                          const float* bias, float* out, int64_t ldo, float* rmax, float* act,
                          DropSpec drop, hipStream_t st) {
   if (!nt_h_act_ok(M, R, C, out, act, ldo))
     return fail("rb_gemm_nt_h_act: shape or alignment without a wide-epilogue launch");
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
-  const int nct0 = C / 256;
+  const int nct0 = C / (32 * HN_ACT_NB);
   const int64_t rows_round = (int64_t)(G0 / nct0) * N_BM;
   const int64_t M_main = (G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round : M;
   const f16x8* wf = (const f16x8*)Wf;
@@ -1581,8 +1621,8 @@ int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const vo
   const int m_tiles = (int)((M_main + N_BM - 1) / N_BM);
   const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * nct0;
   const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)G0);
-  if (bias) run_nt_h<true, true, 8, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
-  else run_nt_h<false, true, 8, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
+  if (bias) run_nt_h<true, true, HN_ACT_NB, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
+  else run_nt_h<false, true, HN_ACT_NB, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
   return launch_status("rb_gemm_nt_h_act");
 }
 
