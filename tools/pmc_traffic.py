@@ -33,8 +33,20 @@ def load(d, counter):
     return out
 
 
+def demangle(name):
+    """rocprofv3 leaves some template instances mangled (_ZN2rb...)."""
+    if not name.startswith("_Z"):
+        return name
+    import subprocess
+    try:
+        return subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-cxxfilt", name], capture_output=True,
+                              text=True, check=True).stdout.strip() or name
+    except (OSError, subprocess.SubprocessError):
+        return name
+
+
 def short(name):
-    n = name.replace("void ", "").replace("rb::(anonymous namespace)::", "")
+    n = demangle(name).replace("void ", "").replace("rb::(anonymous namespace)::", "")
     return n.split("(")[0]
 
 
@@ -59,7 +71,8 @@ def main():
                            "note": "algorithmic bytes / counted bytes on the calibration kernel"},
            "kernels": {}}
     for name in sorted(set(fetch) | set(write)):
-        if not (name.startswith("void rb::") or name.startswith("rb::")):
+        if not (name.startswith("void rb::") or name.startswith("rb::")
+                or name.startswith("_ZN2rb")):
             continue
         fv = [v for _, v in fetch.get(name, [])]
         wv = [v for _, v in write.get(name, [])]
