@@ -617,7 +617,13 @@ def main():
     torch.manual_seed(2020)  # the reference run's seed (LOG51:6); same on every rank
     model = RecBLR(make_cfg(args), SyntheticDataset(args.n_items)).to(dev).train()
     step_mod = wrap_ddp(model, env)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    # the optimizer update: rb_adam_step over every parameter in one launch
+    # (datamining_recblr_amd.optim.Adam); RECBLR_ADAM=torch: torch's fused Adam
+    if os.environ.get("RECBLR_ADAM", "native") == "torch":
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+    else:
+        from datamining_recblr_amd.optim import Adam as NativeAdam
+        opt = NativeAdam(model.parameters(), lr=1e-3)
     batches = [synthetic_interaction(args.batch, args.seq_len, args.n_items, dev,
                                      seed=1000 * env.rank + i) for i in range(4)]
 
@@ -729,8 +735,10 @@ def main():
     if opt_events:
         optimizer = {"ms_per_step": round(sum(a.elapsed_time(b) for a, b in opt_events)
                                           / len(opt_events), 4),
-                     "note": "torch.optim.Adam(fused=True) over all parameters; inside every "
-                             "timed step, timed on its own in the breakdown pass"}
+                     "impl": type(opt).__module__ + "." + type(opt).__name__,
+                     "note": "Adam over all parameters (rb_adam_step, one launch; RECBLR_ADAM="
+                             "torch: torch.optim.Adam(fused=True)); inside every timed step, "
+                             "timed on its own in the breakdown pass"}
     ms = 1000.0 * elapsed / args.steps
     value = env.world_size * args.batch * args.steps / elapsed
     if not torch.isfinite(loss):

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 31; }
+int rb_version(void) { return 32; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -722,6 +722,25 @@ int rb_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int64_t R, const vo
   if ((M + 31) / 32 > 0x7fffffffLL) return fail("rb_gemm_nt_h_act: grid too large");
   return launch_gemm_nt_h_act(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, rmax, act,
                               make_drop(nullptr, seed, p), reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_adam_step(const rb_adam_job* jobs, int64_t n, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, double bc1, double bc2, void* stream) {
+  if (!jobs || n <= 0 || n > RB_MAX_ADAM_JOBS) return fail("rb_adam_step: 1..RB_MAX_ADAM_JOBS jobs");
+  int64_t blocks = 0;
+  for (int64_t j = 0; j < n; ++j) {
+    const rb_adam_job& b = jobs[j];
+    if (!b.param || !b.grad || !b.exp_avg || !b.exp_avg_sq || b.n <= 0)
+      return fail("rb_adam_step: null pointer or empty tensor");
+    if (!aligned16(b.param) || !aligned16(b.grad) || !aligned16(b.exp_avg) ||
+        !aligned16(b.exp_avg_sq))
+      return fail("rb_adam_step: tensors must be 16-byte aligned");
+    blocks += (b.n + 1023) / 1024;
+  }
+  if (blocks > 0x7fffffffLL) return fail("rb_adam_step: too many elements");
+  if (!(bc1 > 0.0 && bc2 > 0.0)) return fail("rb_adam_step: bias corrections must be > 0");
+  return launch_adam(jobs, (int)n, lr, beta1, beta2, eps, weight_decay, bc1, bc2,
+                     reinterpret_cast<hipStream_t>(stream));
 }
 
 int64_t rb_gemm_nt_h_dact_parts(void) { return nt_h_dact_parts(); }

@@ -370,6 +370,8 @@ int64_t nt_h_dact_parts();
 int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                           float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
                           float* dpart, int64_t n_parts, hipStream_t st);
+int launch_adam(const rb_adam_job* jobs, int n, double lr, double beta1, double beta2, double eps,
+                double weight_decay, double bc1, double bc2, hipStream_t st);
 int launch_gemm_nt_hs(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                       const float* bias, float* out, int64_t ldo, float* rmax, hipStream_t st);
 int grl_fwd_lds_bytes();

@@ -450,6 +450,25 @@ int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_off
                  const int64_t* order, int64_t B, int64_t L, int64_t* ids, int64_t* row_pos,
                  int64_t* inv, int64_t* last, void* stream);
 
+/* One Adam step (torch.optim.Adam semantics, L2 weight decay, no amsgrad)
+ * over up to RB_MAX_ADAM_JOBS fp32 tensors in one launch — the optimizer of
+ * the reference's training loop (run.py: RecBole's Trainer, learner
+ * 'adam').  jobs: a HOST array; param / grad / exp_avg / exp_avg_sq of each
+ * job are n contiguous floats, 16-B aligned.  bc1 = 1 - beta1^t and bc2 =
+ * 1 - beta2^t for the step t being taken (t >= 1).  The scalars are the
+ * host's doubles: lr / bc1, 1 - beta and sqrt(bc2) are formed in double and
+ * rounded to fp32 once, as torch's Adam does. */
+#define RB_MAX_ADAM_JOBS 48
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t n;
+} rb_adam_job;
+int rb_adam_step(const rb_adam_job* jobs, int64_t n, double lr, double beta1, double beta2,
+                 double eps, double weight_decay, double bc1, double bc2, void* stream);
+
 /* rb_gemm_split_weight for up to RB_MAX_SPLIT_JOBS weights in one launch
  * (jobs: a HOST array of n descriptors, each with rb_gemm_split_weight's
  * arguments and constraints).  The host side refreshes every split image a
