@@ -617,9 +617,10 @@ def main():
     torch.manual_seed(2020)  # the reference run's seed (LOG51:6); same on every rank
     model = RecBLR(make_cfg(args), SyntheticDataset(args.n_items)).to(dev).train()
     step_mod = wrap_ddp(model, env)
-    # the optimizer update: rb_adam_step over every parameter in one launch
-    # (datamining_recblr_amd.optim.Adam); RECBLR_ADAM=torch: torch's fused Adam
-    if os.environ.get("RECBLR_ADAM", "native") == "torch":
+    # the optimizer update: torch's fused Adam, or RECBLR_ADAM=native:
+    # rb_adam_step over every parameter in one launch (datamining_recblr_amd.
+    # optim.Adam; default once measured on the GPU)
+    if os.environ.get("RECBLR_ADAM", "torch") != "native":
         opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     else:
         from datamining_recblr_amd.optim import Adam as NativeAdam
@@ -736,9 +737,9 @@ def main():
         optimizer = {"ms_per_step": round(sum(a.elapsed_time(b) for a, b in opt_events)
                                           / len(opt_events), 4),
                      "impl": type(opt).__module__ + "." + type(opt).__name__,
-                     "note": "Adam over all parameters (rb_adam_step, one launch; RECBLR_ADAM="
-                             "torch: torch.optim.Adam(fused=True)); inside every timed step, "
-                             "timed on its own in the breakdown pass"}
+                     "note": "Adam over all parameters (torch.optim.Adam(fused=True); "
+                             "RECBLR_ADAM=native: rb_adam_step, one launch); inside every timed "
+                             "step, timed on its own in the breakdown pass"}
     ms = 1000.0 * elapsed / args.steps
     value = env.world_size * args.batch * args.steps / elapsed
     if not torch.isfinite(loss):
