@@ -263,6 +263,64 @@ def gemm_bytes(by_shape):
     return total
 
 
+def kernel_report(summ, steps, ntok_step=None, H=None, layers=None):
+    """Per-kernel report from a KernelTimer summary: MFMA kernels (FLOP_KERNELS:
+    their launches count algorithmic FLOPs) against the f16x3 or fp32 MFMA
+    peak, every other kernel's algorithmic bytes against 8 TB/s; the fused
+    scan + conv + gate path both by its kernels' own byte counts and against
+    SURVEY §8(d)'s fixed model, 20 * ntok * H * 4 B per layer and step
+    (ntok = the packed tokens per step).  An HBM fraction above 1 means a
+    byte count is wrong: listed under "anomalies" (tests keep it empty)."""
+    rep, anomalies = {}, []
+    for name, d in summ.items():
+        if name in kernels.FLOP_KERNELS:
+            tf = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e12
+            pk = F16X3_PEAK_TFS if kernels.f16_split_kernel(name) else FP32_MFMA_PEAK_TFS
+            rep[name] = {"launches_per_step": d["launches"] / steps,
+                         "avg_us": round(d["avg_ms"] * 1e3, 2),
+                         "algo_flops": int(d["avg_bytes"]),
+                         "achieved_tflops": round(tf, 1),
+                         "peak_tflops": round(pk, 1),
+                         "frac": round(tf / pk, 4)}
+            continue
+        gbs = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
+        rep[name] = {"launches_per_step": d["launches"] / steps,
+                     "avg_us": round(d["avg_ms"] * 1e3, 2),
+                     "algo_bytes": int(d["avg_bytes"]),
+                     "achieved_gbs": round(gbs, 1),
+                     "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        if gbs > HBM_PEAK_GBS:
+            anomalies.append(name)
+    hbm = [d for n, d in summ.items() if n not in kernels.FLOP_KERNELS]
+    tot_b = sum(d["bytes"] for d in hbm)
+    tot_ms = sum(d["ms"] for d in hbm)
+    core = [summ[n] for n in ("rb_conv_silu_fwd", "rb_gate_scan_fwd", "rb_gate_scan_bwd",
+                              "rb_conv_silu_bwd", "rb_grl_fwd", "rb_grl_bwd") if n in summ]
+    if core:   # BASELINE's target: the fused scan + conv + gate path
+        cb = sum(d["bytes"] for d in core)
+        cms = sum(d["ms"] for d in core)
+        path = {"ms_per_step": round(cms / steps, 4),
+                "achieved_gbs": round(cb / (cms * 1e-3) / 1e9, 1),
+                "frac": round(cb / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if ntok_step and H and layers:
+            mb = 20.0 * ntok_step * H * 4 * layers
+            path["model_bytes_per_step"] = int(mb)
+            path["model_frac"] = round(mb / (cms / steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            path["model"] = ("SURVEY §8(d): 20 * ntok * H * 4 B per layer (fwd 7N + bwd 13N), "
+                             "ntok = packed tokens per step, against the path kernels' time")
+        rep["scan_conv_gate_path"] = path
+    if tot_ms:
+        rep["fused_path_total"] = {
+            "ms_per_step": round(tot_ms / steps, 4),
+            "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
+            "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "every HIP kernel counted in bytes (FLOP_KERNELS excluded)"}
+    if anomalies:
+        rep["anomalies"] = anomalies
+    return rep
+
+
+
 def scan_microbench(args, dev, reps=20):
     """BASELINE configs[1]: forward-only parallel_scan at B=2048, C=H=256,
     T=L=200 on the reference layout [B, C, T] (the reference pads T to 256;
@@ -620,11 +678,15 @@ def main():
     # the optimizer update: torch's fused Adam, or RECBLR_ADAM=native:
     # rb_adam_step over every parameter in one launch (datamining_recblr_amd.
     # optim.Adam; default once measured on the GPU)
-    if os.environ.get("RECBLR_ADAM", "torch") != "native":
-        opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
-    else:
-        from datamining_recblr_amd.optim import Adam as NativeAdam
-        opt = NativeAdam(model.parameters(), lr=1e-3)
+    from datamining_recblr_amd.optim import Adam as NativeAdam
+
+    def make_opt(kind):
+        if kind == "native":
+            return NativeAdam(model.parameters(), lr=1e-3)
+        return torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
+
+    adam_kind = os.environ.get("RECBLR_ADAM", "torch")
+    opt = make_opt(adam_kind)
     batches = [synthetic_interaction(args.batch, args.seq_len, args.n_items, dev,
                                      seed=1000 * env.rank + i) for i in range(4)]
 
@@ -835,6 +897,25 @@ def main():
         ffn_act_ab["note"] = ("RECBLR_FFN_ACT A/B on the headline's batches: w_1 with "
                               "dropout(silu(.)) in its epilogue vs the GEMM and "
                               "rb_silu_dropout_fwd, best of 3 alternated runs each")
+    adam_ab = None
+    if not args.no_full_tail:
+        # the optimizer update: rb_adam_step (one launch over every parameter)
+        # against torch's fused Adam, alternated 3x on the lease (each with its
+        # own state; the step's other work is the same)
+        saved_opt = opt
+        arms = {adam_kind: saved_opt,
+                ("torch" if adam_kind == "native" else "native"):
+                    make_opt("torch" if adam_kind == "native" else "native")}
+        runs = {k: [] for k in arms}
+        for _ in range(3):
+            for name, o in arms.items():
+                opt = o
+                runs[name].append(timed_variant(True, True)["ms_per_step"])
+        opt = saved_opt
+        adam_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
+        adam_ab["headline"] = adam_kind
+        adam_ab["note"] = ("RECBLR_ADAM A/B on the headline's batches: rb_adam_step (native, one "
+                           "launch) vs torch.optim.Adam(fused=True), best of 3 alternated runs")
     dense = full_tail = None
     if not args.no_full_tail:
         dense = timed_variant(False, True)
@@ -882,25 +963,9 @@ def main():
                     "mfma_busy": pmc_mfma(args),
                     "by_shape": by_shape,
                     "breakdown_pass_ms_per_step": round(breakdown_ms, 3)}
-        kernels_report = {}
-        for name, d in summ.items():
-            if name in kernels.FLOP_KERNELS:   # MFMA kernels: algorithmic FLOPs
-                tf = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e12
-                # the _h kernels run fp32-level products as three f16 MFMAs
-                pk = F16X3_PEAK_TFS if name.endswith("_h") else FP32_MFMA_PEAK_TFS
-                kernels_report[name] = {"launches_per_step": d["launches"] / args.steps,
-                                        "avg_us": round(d["avg_ms"] * 1e3, 2),
-                                        "algo_flops": int(d["avg_bytes"]),
-                                        "achieved_tflops": round(tf, 1),
-                                        "peak_tflops": round(pk, 1),
-                                        "frac": round(tf / pk, 4)}
-                continue
-            gbs = d["avg_bytes"] / (d["avg_ms"] * 1e-3) / 1e9
-            kernels_report[name] = {"launches_per_step": d["launches"] / args.steps,
-                                    "avg_us": round(d["avg_ms"] * 1e3, 2),
-                                    "algo_bytes": int(d["avg_bytes"]),
-                                    "achieved_gbs": round(gbs, 1),
-                                    "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        ntok_step = sum(int(batches[i % len(batches)]["item_length"].sum())
+                        for i in range(args.steps)) / args.steps
+        kernels_report = kernel_report(summ, args.steps, ntok_step, 2 * args.hidden, args.layers)
         dsumm = dom_timer.summary() if dom_timer is not None else {}
         if DOMINANT in dsumm:
             d = dsumm[DOMINANT]
@@ -912,23 +977,6 @@ def main():
                         "algo_bytes_per_launch": int(d["avg_bytes"]),
                         "avg_launch_us": round(d["avg_ms"] * 1e3, 2),
                         "timed": "HIP events on the launch stream, inside the timed region"}
-        hbm = [d for n, d in summ.items() if n not in kernels.FLOP_KERNELS]
-        tot_b = sum(d["bytes"] for d in hbm)
-        tot_ms = sum(d["ms"] for d in hbm)
-        core = [summ[n] for n in ("rb_conv_silu_fwd", "rb_gate_scan_fwd", "rb_gate_scan_bwd",
-                                  "rb_conv_silu_bwd", "rb_grl_fwd", "rb_grl_bwd") if n in summ]
-        if core:   # BASELINE's target: the fused scan + conv + gate path
-            cb = sum(d["bytes"] for d in core)
-            cms = sum(d["ms"] for d in core)
-            kernels_report["scan_conv_gate_path"] = {
-                "ms_per_step": round(cms / args.steps, 4),
-                "achieved_gbs": round(cb / (cms * 1e-3) / 1e9, 1),
-                "frac": round(cb / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        kernels_report["fused_path_total"] = {
-            "ms_per_step": round(tot_ms / args.steps, 4),
-            "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
-            "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-
     if roofline is not None and env.rank == 0 and args.hidden * 2 % 4 == 0:
         roofline["pattern"] = gate_bwd_pattern(args, batches[0], dev)
     if gemm is not None and env.rank == 0 and fmt == "f16x3":
@@ -978,6 +1026,7 @@ def main():
             "device_lengths": devlen,
             "fused_grl": fused_ab,
             "ffn_act": ffn_act_ab,
+            "adam": adam_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

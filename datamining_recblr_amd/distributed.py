@@ -61,14 +61,27 @@ class LossModule(nn.Module):
         return self.model.calculate_loss(interaction)
 
 
-def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float = 32.0,
+# Gradient bucket size.  DDP starts with one bucket and (static_graph) rebuilds
+# its buckets at the third iteration in the order the gradients became ready;
+# at 1 MB the ~2.9 MB of encoder gradients (d = 128, the later layer first)
+# fill two or more buckets whose all-reduces start while the backward is still
+# running; the 5.4 MB item-table gradient, finished last (the embedding
+# gather's backward adds to the CE's), closes the last one.  32 MB put all
+# 8.3 MB into one all-reduce after the backward (round 3).
+DDP_BUCKET_MB = float(os.environ.get("RECBLR_DDP_BUCKET_MB", "1"))
+
+
+def wrap_ddp(model: nn.Module, env: DistEnv, bucket_cap_mb: float | None = None,
              static_graph: bool | None = None) -> nn.Module:
     """DDP over the loss module.  static_graph (default: RECBLR_DDP_STATIC,
     on): the train step uses the same parameters in the same order every
-    iteration, so the reducer skips its per-iteration graph bookkeeping."""
+    iteration, so the reducer skips its per-iteration graph bookkeeping.
+    bucket_cap_mb: DDP_BUCKET_MB unless given."""
     step = LossModule(model)
     if not env.distributed:
         return step
+    if bucket_cap_mb is None:
+        bucket_cap_mb = DDP_BUCKET_MB
     if static_graph is None:
         static_graph = os.environ.get("RECBLR_DDP_STATIC", "1") != "0"
     dev = next(model.parameters()).device

@@ -75,12 +75,18 @@ def kernel_timing(only=None):
         _timer = prev
 
 
-def _launch(name: str, nbytes: int, *args, _fn: str | None = None) -> None:
-    """Call C-ABI entry point `_fn or name`; timed under `name` in bench runs."""
+def _launch(name: str, nbytes: int, *args, _fn: str | None = None, _flops: bool = False) -> None:
+    """Call C-ABI entry point `_fn or name`; timed under `name` in bench runs.
+    `nbytes` is the launch's algorithmic HBM bytes, or its algorithmic FLOPs
+    where `_flops` is set — exactly the names in FLOP_KERNELS (checked when
+    timed, and statically by tests/test_host_logic.py)."""
     t = _timer
     if t is None or (t.only is not None and name not in t.only):
         _lib.call(_fn or name, *args)
         return
+    if _flops != (name in FLOP_KERNELS):
+        raise AssertionError(f"{name}: counted in {'FLOPs' if _flops else 'bytes'} but "
+                             f"{'not ' if _flops else ''}listed in FLOP_KERNELS")
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -637,7 +643,14 @@ def embedding_plan(idx, num_rows, d, stream=None):
 # Launches timed in FLOPs rather than bytes (bench.py reports them against the
 # MFMA roofline).
 FLOP_KERNELS = frozenset({"rb_item_ce_fwd", "rb_item_ce_bwd", "rb_item_ce_probs", "rb_item_rank",
-                          "rb_item_scores", "rb_item_ce_fwd_h", "rb_item_ce_probs_h"})
+                          "rb_item_scores", "rb_item_ce_fwd_h", "rb_item_ce_probs_h",
+                          "rb_item_ce_probs_h_t", "rb_item_ce_probs_h_both"})
+
+
+def f16_split_kernel(name: str) -> bool:
+    """Kernels whose products run as three f16 MFMAs on two-part split
+    operands (their FLOP peak is a third of the f16 pipe's)."""
+    return name.endswith("_h") or "_h_" in name
 ITEM_DIMS = (16, 32, 64, 128, 256)
 
 
@@ -671,7 +684,7 @@ def item_ce_fwd(seq, items, target):
     lse = torch.empty((B,), device=seq.device, dtype=torch.float32)
     loss = torch.empty((), device=seq.device, dtype=torch.float32)
     _launch("rb_item_ce_fwd", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), target.data_ptr(),
-            B, V, d, lse.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws_bytes, _stream(seq))
+            B, V, d, lse.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws_bytes, _stream(seq), _flops=True)
     return loss, lse
 
 
@@ -693,7 +706,7 @@ def item_ce_bwd(seq, items, target, lse, dloss, want_seq=True, want_items=True):
             lse.contiguous().data_ptr(), dloss.data_ptr(), B, V, d,
             dseq.data_ptr() if dseq is not None else None,
             ditems.data_ptr() if ditems is not None else None, ws.data_ptr(), ws_bytes,
-            _stream(seq))
+            _stream(seq), _flops=True)
     return dseq, ditems
 
 
@@ -712,7 +725,7 @@ def item_ce_probs(seq, items, target, lse, dloss, item_offset=0, out=None):
         raise ValueError("probs must be [B, V] with unit column stride")
     _launch("rb_item_ce_probs", 2 * B * V * d, seq.data_ptr(), items.data_ptr(),
             target.data_ptr(), lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(),
-            B, V, d, int(item_offset), out.data_ptr(), out.stride(0), _stream(seq))
+            B, V, d, int(item_offset), out.data_ptr(), out.stride(0), _stream(seq), _flops=True)
     return out
 
 
@@ -773,7 +786,7 @@ def item_ce_fwd_h(seq: SplitRows, items: SplitRows, target):
     loss = torch.empty((), device=dev, dtype=torch.float32)
     _launch("rb_item_ce_fwd_h", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
             items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(), B, V, d,
-            lse.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws_bytes, _stream(seq.img))
+            lse.data_ptr(), loss.data_ptr(), ws.data_ptr(), ws_bytes, _stream(seq.img), _flops=True)
     return loss, lse
 
 
@@ -793,7 +806,7 @@ def item_ce_probs_h(seq: SplitRows, items: SplitRows, target, lse, dloss, item_o
     _launch("rb_item_ce_probs_h", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
             items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
             lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
-            int(item_offset), out.data_ptr(), out.stride(0), _stream(seq.img))
+            int(item_offset), out.data_ptr(), out.stride(0), _stream(seq.img), _flops=True)
     return out
 
 
@@ -811,7 +824,7 @@ def item_ce_probs_h_t(seq: SplitRows, items: SplitRows, target, lse, dloss, item
     _launch("rb_item_ce_probs_h_t", 2 * B * V * d, seq.img.data_ptr(), seq.exps.data_ptr(),
             items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
             lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
-            int(item_offset), pt.data_ptr(), ldt, gmax.data_ptr(), _stream(seq.img))
+            int(item_offset), pt.data_ptr(), ldt, gmax.data_ptr(), _stream(seq.img), _flops=True)
     return pt, gmax
 
 
@@ -837,7 +850,7 @@ def item_ce_probs_h_both(seq: SplitRows, items: SplitRows, target, lse, dloss, i
             items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
             lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
             int(item_offset), p.data_ptr(), Vp, pt.data_ptr(), ldt, bmax.data_ptr(),
-            gmax.data_ptr(), _stream(seq.img))
+            gmax.data_ptr(), _stream(seq.img), _flops=True)
     return p, pt, bmax, gmax
 
 
@@ -866,7 +879,7 @@ def item_rank(seq, items, target, first_item=1, want_equal=True):
     eq = torch.empty((B,), device=seq.device, dtype=torch.int64) if want_equal else None
     _launch("rb_item_rank", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), target.data_ptr(),
             B, V, d, int(first_item), gt.data_ptr(), eq.data_ptr() if eq is not None else None,
-            ws.data_ptr(), ws_bytes, _stream(seq))
+            ws.data_ptr(), ws_bytes, _stream(seq), _flops=True)
     return gt, eq
 
 
@@ -877,7 +890,7 @@ def item_scores(seq, items):
     V = items.shape[0]
     out = torch.empty((B, V), device=seq.device, dtype=torch.float32)
     _launch("rb_item_scores", 2 * B * V * d, seq.data_ptr(), items.data_ptr(), B, V, d,
-            out.data_ptr(), _stream(seq))
+            out.data_ptr(), _stream(seq), _flops=True)
     return out
 
 

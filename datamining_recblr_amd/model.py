@@ -36,9 +36,6 @@ from .recbole_compat import BPRLoss, SequentialRecommender, install_interaction_
 from .recurrence import bd_lru, fused_ok, pow2_pad_len, row_pad_lens
 
 
-class _FusedProbe:
-    """Stands in for a Packed with work lists in the fused-path check."""
-    pieces = True
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
 
 # RECBLR_CONV_ROWS=0: packed conv forward per sequence instead of per row tile
@@ -359,7 +356,7 @@ class RecBLR(SequentialRecommender):
         offsets, order = both[:B + 1], both[B + 1:]
         pieces = None
         H = self.hidden_size * self.expand
-        if fused_ok(_FusedProbe, H, not self.disable_conv1d, self.d_conv, torch.float32):
+        if fused_ok(True, H, not self.disable_conv1d, self.d_conv, torch.float32):
             G = _num_cus(dev)
             pieces = _host_ring32.stage(grl_pieces(lens_p, offs_h, G), dev)
             max_tiles = grl_max_tiles(lens_p, G)

@@ -51,8 +51,8 @@ class Adam(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             by_step = {}
             for p in group["params"]:
-                if p.grad is None:
-                    continue
+                if p.grad is None or p.numel() == 0:
+                    continue   # torch.optim.Adam leaves an empty parameter as it is
                 if (p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous()
                         or p.grad.dtype != torch.float32 or not p.grad.is_contiguous()):
                     raise ValueError("rb Adam: parameters and gradients must be contiguous fp32 "
@@ -64,7 +64,9 @@ class Adam(torch.optim.Optimizer):
                     st["step"] = 0
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
-                st["step"] += 1
+                # a state loaded from torch.optim.Adam holds `step` as a tensor
+                # (which hashes by identity): group launches by its value
+                st["step"] = int(st["step"]) + 1
                 by_step.setdefault(st["step"], []).append(p)
             for t, ps in by_step.items():
                 bc1, bc2 = 1.0 - b1 ** t, 1.0 - b2 ** t

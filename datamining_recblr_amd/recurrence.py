@@ -50,9 +50,10 @@ _FUSED = os.environ.get("RECBLR_FUSED_GRL", "0") != "0"
 _FUSED_BWD = os.environ.get("RECBLR_FUSED_GRL_BWD", "0") != "0"
 
 
-def fused_ok(seq, H: int, use_conv: bool, kc: int, dtype) -> bool:
-    """Whether BDLRUCore's forward runs as one rb_grl_fwd launch."""
-    return (_FUSED and seq is not None and seq.pieces is not None and use_conv and H == 256
+def fused_ok(has_pieces: bool, H: int, use_conv: bool, kc: int, dtype) -> bool:
+    """Whether BDLRUCore's forward runs as one rb_grl_fwd launch (has_pieces:
+    the packed batch carries the kernel's work lists)."""
+    return (_FUSED and has_pieces and use_conv and H == 256
             and kc in (2, 3, 4) and dtype == torch.float32 and linear_mod.gemm_format() == "f16x3")
 
 
@@ -118,7 +119,7 @@ class BDLRUCore(torch.autograd.Function):
         x, z = xz[..., :H], xz[..., H:]
         train = any(ctx.needs_input_grad)
         if (observe is None and (h0 is None or h0.dim() == 1)
-                and fused_ok(seq, H, use_conv, conv_w.shape[-1], xz.dtype)):
+                and fused_ok(seq is not None and seq.pieces is not None, H, use_conv, conv_w.shape[-1], xz.dtype)):
             # conv + gates GEMM + gate scan in one launch (rb_grl_fwd).  Its
             # backward is one launch too (rb_grl_bwd), from the 64-row tile
             # checkpoints; or the three-launch backward from xc, rg, carries

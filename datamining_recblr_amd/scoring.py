@@ -52,16 +52,30 @@ CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
 CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "f16")
 
 
+# rb_gemm_tn_h's largest N and K (include/recblr_hip.h); ditems runs with N =
+# the item count rounded up to 256
+GEMM_TN_MAX_N = 65536
+
+
+def _tn_splits8(dev, nt: int, div: int = 1) -> int:
+    """linear._tn_splits(dev, nt) // div rounded down to a multiple of 8
+    (rb_gemm_tn_h takes row splits in multiples of 8), at least 8."""
+    from .linear import _tn_splits
+    return max(8, _tn_splits(dev, nt) // div // 8 * 8)
+
+
 def _f16_grads_ok(seq, table) -> bool:
     """The logits' input gradients as f16x3 GEMMs (_bwd_f16): B a multiple of
     256 (the weight-gradient kernel's N; its row splits), d of 128, both
-    layouts of P within twice PROBS_SLICE_BYTES."""
+    layouts of P within twice PROBS_SLICE_BYTES, the padded item count within
+    the weight-gradient kernel's N limit."""
     from . import linear
     B, d = seq.shape
     V = table.shape[0]
     return (CE_GRADS == "f16" and linear.gemm_format() == "f16x3" and B % 256 == 0
             and d % 128 == 0 and table.stride(1) == 1 and table.data_ptr() % 16 == 0
-            and 8 * B * V <= 2 * PROBS_SLICE_BYTES)
+            and 8 * B * V <= 2 * PROBS_SLICE_BYTES
+            and (V + 255) // 256 * 256 <= GEMM_TN_MAX_N)
 
 
 def _group_max(x: torch.Tensor) -> torch.Tensor:
@@ -78,7 +92,7 @@ def _bwd_f16(seq, table, target, lse, dloss, want_seq, want_items, split):
     weight-gradient GEMM (rb_gemm_tn_h, fixed-order row-chunk partials, a
     column sum): ditems = P^T seq reduced over P's batch rows, dseq = P W over
     P^T's item rows — no library GEMM."""
-    from .linear import _timed, _tn_splits
+    from .linear import _timed
 
     B, d = seq.shape
     V = table.shape[0]
@@ -89,11 +103,11 @@ def _bwd_f16(seq, table, target, lse, dloss, want_seq, want_items, split):
     dseq = dtable = None
     if want_items:
         Vp = p.shape[1]
-        S1 = max(8, min(_tn_splits(seq.device, (Vp // 256) * (d // 128)), B // 256 // 8 * 8))
+        S1 = max(8, min(_tn_splits8(seq.device, (Vp // 256) * (d // 128)), B // 256 // 8 * 8))
         parts = _timed("gemm", fl, kernels.gemm_tn_h, p, seq, bmax, kernels.group_absmax(seq), S1)
         dtable = kernels.colsum(parts.view(S1, -1)).view(Vp, d)[:V]
     if want_seq:
-        S2 = max(8, _tn_splits(seq.device, (B // 256) * (d // 128)) // 2)
+        S2 = _tn_splits8(seq.device, (B // 256) * (d // 128), div=2)
         parts = _timed("gemm", fl, kernels.gemm_tn_h, pt, table, gmax,
                        kernels.group_absmax(table), S2)
         dseq = kernels.colsum(parts.view(S2, -1)).view(B, d)

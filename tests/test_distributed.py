@@ -113,3 +113,83 @@ def test_dropout_keys_differ_across_ranks():
     assert got[0] == single
     assert all(a != b for a, b in zip(got[0], got[1]))
     assert all(0 <= s < 2 ** 62 for s in got[1])
+
+
+class ParamShapedRec(nn.Module):
+    """RecBLR's parameters (d = 128, n_items = 10,544, two layers: the bench's
+    model, built on the CPU) behind a CPU loss that uses each of them once in
+    module order, so the backward finishes them in reverse order as the real
+    step does — the item table last."""
+
+    def __init__(self):
+        super().__init__()
+        from datamining_recblr_amd.model import RecBLR
+        from datamining_recblr_amd.recbole_compat import SyntheticDataset
+        self.inner = RecBLR(dict(hidden_size=128, loss_type="CE", num_layers=2, dropout_prob=0.2,
+                                 expand=2, d_conv=4, bd_lru_only=False, disable_conv1d=False,
+                                 disable_ffn=False, MAX_ITEM_LIST_LENGTH=200),
+                            SyntheticDataset(10544))
+
+    def calculate_loss(self, inter):
+        s = inter["item_id"].float().mean()
+        h = torch.zeros(())
+        for i, p in enumerate(self.inner.parameters()):
+            h = h * 0.5 + (p * (s + i)).square().mean()
+        return h
+
+
+def _bucket_worker(rank, world, port, queue):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from datamining_recblr_amd.distributed import init_from_env, wrap_ddp
+
+    env = init_from_env(backend="gloo")
+    torch.manual_seed(0)
+    model = ParamShapedRec()
+    step = wrap_ddp(model, env)
+    full = {"item_id": torch.arange(1, 9)}
+    shard = {"item_id": full["item_id"][4 * rank:4 * rank + 4]}
+    for _ in range(3):   # static_graph: buckets are rebuilt at the third forward
+        model.zero_grad(set_to_none=True)
+        step(shard).backward()
+    buckets = step.reducer._get_zeros_like_grad_buckets()
+    sizes = [b.buffer().numel() * 4 for b in buckets]
+    emb = model.inner.item_embedding.weight
+    last = [any(p.shape == emb.shape for p in b.parameters()) for b in buckets]
+    grads = {n: p.grad.detach().numpy().copy() for n, p in model.named_parameters()}
+    queue.put((rank, sizes, last, grads))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_buckets_overlap_the_backward():
+    """wrap_ddp's bucket size gives the bench's model >= 3 gradient buckets
+    (all-reduces that can start during the backward), the item table, whose
+    gradient is finished last, in the last one; gradients equal the
+    single-process ones averaged."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bucket_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    torch.manual_seed(0)
+    ref = ParamShapedRec()
+    ga = {}
+    for r in range(world):
+        ref.zero_grad(set_to_none=True)
+        ref.calculate_loss({"item_id": torch.arange(1, 9)[4 * r:4 * r + 4]}).backward()
+        for n, p in ref.named_parameters():
+            ga[n] = ga.get(n, 0) + p.grad / world
+    for rank, sizes, last, grads in results:
+        assert len(sizes) >= 3, sizes
+        assert sum(sizes) == 4 * sum(p.numel() for p in ref.parameters())
+        assert last == [False] * (len(sizes) - 1) + [True], (sizes, last)
+        for n in ga:
+            torch.testing.assert_close(torch.from_numpy(grads[n]), ga[n], atol=1e-6, rtol=1e-5)
