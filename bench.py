@@ -431,7 +431,7 @@ def gemm_pattern(args, batch, dev, rounds=7):
             linear.mm_nt(a, w)
 
         def pattern():
-            _lib.call("rb_probe_gemm_pattern", a.data_ptr(), M, R, o.data_ptr(), C, st)
+            _lib.call_probe("rb_probe_gemm_pattern", a.data_ptr(), M, R, o.data_ptr(), C, st)
 
         real(), pattern()
         torch.cuda.synchronize()
@@ -497,7 +497,7 @@ def gate_bwd_pattern(args, batch, dev, rounds=15):
                   B, args.seq_len, H, offs.data_ptr(), st)
 
     def pattern():
-        _lib.call("rb_probe_gate_bwd_pattern", rg.data_ptr(), 2 * H, xc.data_ptr(), H,
+        _lib.call_probe("rb_probe_gate_bwd_pattern", rg.data_ptr(), 2 * H, xc.data_ptr(), H,
                   z.data_ptr(), 2 * H, dy.data_ptr(), drg.data_ptr(), 2 * H, dxc.data_ptr(), H,
                   dz.data_ptr(), 2 * H, B, args.seq_len, H, offs.data_ptr(), st)
 

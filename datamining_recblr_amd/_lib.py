@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 32
+ABI_VERSION = 33
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -50,10 +50,6 @@ SIGNATURES = {
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
                                         _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
                                         _fp, _fp]),
-    "rb_probe_gemm_pattern": (ctypes.c_int, [_fp, _i64, _i64, _fp, _i64, _fp]),
-    "rb_probe_gate_bwd_pattern": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64,
-                                                 _fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp,
-                                                 _fp]),
     "rb_pad_prefix_fwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp]),
     "rb_pad_prefix_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
                                          _fp, _fp, _fp, ctypes.c_int, _fp]),
@@ -138,8 +134,17 @@ class RecBLRNativeError(RuntimeError):
     """The HIP extension is missing, failed to load, or a kernel call failed."""
 
 
+# the probe library (probes/recblr_probe.h: bench.py's measurement aids)
+PROBE_SIGNATURES = {
+    "rb_probe_gemm_pattern": (ctypes.c_int, [_fp, _i64, _i64, _fp, _i64, _fp]),
+    "rb_probe_gate_bwd_pattern": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64,
+                                                 _fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp,
+                                                 _fp]),
+}
+
 _lock = threading.Lock()
 _lib = None
+_probe = None
 
 
 def load(path: str | None = None) -> ctypes.CDLL:
@@ -185,3 +190,33 @@ def call(name: str, *args) -> None:
         msg = msg.decode() if msg else ""
         kind = "invalid argument" if rc == RB_EINVAL else f"hipError {rc}"
         raise RecBLRNativeError(f"{name} failed ({kind}): {msg}")
+
+
+def load_probe() -> ctypes.CDLL:
+    """The probe library (lib/libdmrecblr_probe.so): measurement aids for
+    bench.py, never on the model's path."""
+    global _probe
+    with _lock:
+        if _probe is not None:
+            return _probe
+        p = os.path.join(os.path.dirname(LIB_PATH), "libdmrecblr_probe.so")
+        if not os.path.exists(p):
+            raise RecBLRNativeError(f"probe library not built: {p} is missing. Run "
+                                    "`python -m datamining_recblr_amd.build`.")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in PROBE_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        lib.rb_probe_last_error_string.restype = ctypes.c_char_p
+        _probe = lib
+        return lib
+
+
+def call_probe(name: str, *args) -> None:
+    """Invoke a probe-library entry point and raise on a non-zero status."""
+    lib = load_probe()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.rb_probe_last_error_string()
+        raise RecBLRNativeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")

@@ -18,6 +18,11 @@ SOURCES = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.hip")))
 HEADERS = sorted(glob.glob(os.path.join(_HERE, "csrc", "*.h"))) + [
     os.path.join(ROOT, "include", "recblr_hip.h")]
 OUT = os.path.join(_HERE, "lib", "libdmrecblr.so")
+# measurement aids for bench.py (probes/recblr_probe.h): their own library,
+# hidden visibility, never loaded by the model's path
+PROBE_SOURCES = sorted(glob.glob(os.path.join(_HERE, "probes", "*.hip")))
+PROBE_HEADERS = HEADERS + sorted(glob.glob(os.path.join(_HERE, "probes", "*.h")))
+PROBE_OUT = os.path.join(_HERE, "lib", "libdmrecblr_probe.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 # -ffp-contract=off: the reference scan is compiled with enable_fp_fusion=False
@@ -34,26 +39,32 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (expected /opt/rocm/bin/hipcc)")
 
 
-def _stale() -> bool:
-    if not os.path.exists(OUT):
+def _stale(out, deps) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
-    deps = SOURCES + HEADERS
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(s) > t for s in deps)
 
 
-def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
-    if not force and not _stale():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [hipcc(), *FLAGS, "-I", os.path.join(ROOT, "include"), "-o", tmp, *SOURCES]
+def _compile(out, sources, extra, verbose, jobs):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
+    cmd = [hipcc(), *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-o", tmp, *sources]
     if jobs > 1:
         cmd.insert(1, f"-parallel-jobs={jobs}")
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
+    os.replace(tmp, out)
+
+
+def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
+    """Build the product library (and the probe library beside it); returns
+    the product library's path."""
+    if force or _stale(OUT, SOURCES + HEADERS):
+        _compile(OUT, SOURCES, [], verbose, jobs)
+    if PROBE_SOURCES and (force or _stale(PROBE_OUT, PROBE_SOURCES + PROBE_HEADERS)):
+        _compile(PROBE_OUT, PROBE_SOURCES, ["-fvisibility=hidden"], verbose, jobs)
     return OUT
 
 

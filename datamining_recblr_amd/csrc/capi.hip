@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 32; }
+int rb_version(void) { return 33; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -175,37 +175,6 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc
   return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, carries, dy, drg, drg_rs, dxc,
                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H,
                          seq_offsets, reinterpret_cast<hipStream_t>(stream));
-}
-
-int rb_probe_gemm_pattern(const float* a, int64_t M, int64_t R, float* out, int64_t C,
-                          void* stream) {
-  if (!a || !out) return fail("rb_probe_gemm_pattern: null pointer");
-  if (M <= 0 || R <= 0 || C <= 0 || R % 4 || C % 4 || R > (1 << 20) || C > (1 << 20))
-    return fail("rb_probe_gemm_pattern: M, R, C must be positive, R and C multiples of 4");
-  if (!aligned16(a) || !aligned16(out))
-    return fail("rb_probe_gemm_pattern: operands must be 16-B aligned");
-  return launch_probe_gemm_pattern(a, M, R, out, C, reinterpret_cast<hipStream_t>(stream));
-}
-
-int rb_probe_gate_bwd_pattern(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                              const float* z, int64_t z_rs, const float* dy, float* drg,
-                              int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz,
-                              int64_t dz_rs, int64_t B, int64_t L, int64_t H,
-                              const int64_t* seq_offsets, void* stream) {
-  if (!rg || !xc || !z || !dy || !drg || !dxc || !dz)
-    return fail("rb_probe_gate_bwd_pattern: null pointer");
-  if (rg_rs < 2 * H || xc_rs < H || z_rs < H || drg_rs < 2 * H || dxc_rs < H || dz_rs < H)
-    return fail("rb_probe_gate_bwd_pattern: row stride too small");
-  if (H % 4 || rg_rs % 4 || xc_rs % 4 || z_rs % 4 || drg_rs % 4 || dxc_rs % 4 || dz_rs % 4 ||
-      !aligned16(rg) || !aligned16(xc) || !aligned16(z) || !aligned16(dy) || !aligned16(drg) ||
-      !aligned16(dxc) || !aligned16(dz))
-    return fail("rb_probe_gate_bwd_pattern: 16-B aligned rows of a multiple of 4 floats only");
-  if (int r = check_dims("rb_probe_gate_bwd_pattern", B, L, H,
-                         max4(max4(rg_rs, xc_rs, z_rs, drg_rs), dz_rs, dxc_rs, H)))
-    return r;
-  return launch_probe_gate_bwd_pattern(rg, rg_rs, xc, xc_rs, z, z_rs, dy, drg, drg_rs, dxc, dxc_rs,
-                                       dz, dz_rs, B, L, H, seq_offsets,
-                                       reinterpret_cast<hipStream_t>(stream));
 }
 
 // ---- bf16 storage variants (fp32 arithmetic; same checks as the fp32 forms) ----

@@ -64,9 +64,6 @@ __device__ __forceinline__ float fdsilu(float x) {
 // carry the nontemporal hint (global_load/store ... nt): on this chip a plain
 // 1R+1W float4 copy runs at 0.76 of 8 TB/s with default-policy accesses and
 // 0.83 with nt ones (tools/copyprobe2.hip, profiles/r01_copyprobe2.log).
-#ifndef RB_STREAM_NT
-#define RB_STREAM_NT 1
-#endif
 typedef float rb_f32x4 __attribute__((ext_vector_type(4)));
 typedef float rb_f32x2v __attribute__((ext_vector_type(2)));
 typedef uint32_t rb_u32x4 __attribute__((ext_vector_type(4)));
@@ -82,7 +79,7 @@ __device__ __forceinline__ void st_pol(T v, T* p) {
   if constexpr (NT) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
-constexpr bool kNT = RB_STREAM_NT != 0;
+constexpr bool kNT = true;
 
 // ldv / stv: once-touched activation streams (nt); ldc / stc: default policy,
 // for small operands many workgroups re-read (parameters, carries) and for
@@ -297,13 +294,6 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
                     int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
                     float* y_last = nullptr);
-int launch_probe_gemm_pattern(const float* A, int64_t M, int64_t R, float* out, int64_t C,
-                              hipStream_t st);
-int launch_probe_gate_bwd_pattern(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
-                                  const float* z, int64_t z_rs, const float* dy, float* drg,
-                                  int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz,
-                                  int64_t dz_rs, int64_t B, int64_t L, int64_t H,
-                                  const int64_t* offs, hipStream_t st);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,

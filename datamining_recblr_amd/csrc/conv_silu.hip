@@ -6,22 +6,12 @@
 // and one wave-instruction touches Q contiguous 256-B row segments.
 #include "common.h"
 
-// the input rows are re-read by the neighbouring time tile (K-1 halo rows), so
-// they keep the default cache policy unless RB_CONV_X_NT is set
-#ifndef RB_CONV_X_NT
-#define RB_CONV_X_NT 0
-#endif
-#if RB_CONV_X_NT
-#define RB_CONV_LDX ldv
-#else
-#define RB_CONV_LDX ldc
-#endif
-
+// the input rows are re-read by the neighbouring time tile (K-1 halo rows):
+// default cache policy (ldc)
+//
 // steps per lane of the row-tiled packed forward at K = 4 (tile = 4 x TC rows;
 // each tile re-fetches K-1 halo rows its predecessor loaded)
-#ifndef RB_CONV_ROWS_TC
-#define RB_CONV_ROWS_TC 4
-#endif
+constexpr int kConvRowsTC = 4;
 
 namespace rb {
 namespace {
@@ -72,7 +62,7 @@ k_conv_silu_fwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
   for (int m = 0; m < NX; ++m) {
     const int t = t0 - (K - 1) + m;
     const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
-    RB_CONV_LDX(xs[m], xb + tc * x_rs);
+    ldc(xs[m], xb + tc * x_rs);
     if (t < 0) {
 #pragma unroll
       for (int v = 0; v < VEC; ++v) xs[m][v] = 0.0f;
@@ -128,7 +118,7 @@ k_conv_silu_fwd_rows(const T* __restrict__ x, int x_rs, const float* __restrict_
   for (int m = 0; m < NX; ++m) {
     int64_t r = r0 - (K - 1) + m;
     r = r < 0 ? 0 : (r >= ntok ? ntok - 1 : r);
-    RB_CONV_LDX(xs[m], x + r * x_rs + cc);
+    ldc(xs[m], x + r * x_rs + cc);
   }
   int64_t pj[TC];
 #pragma unroll
@@ -222,7 +212,7 @@ k_conv_silu_bwd(const T* __restrict__ x, int x_rs, const float* __restrict__ w,
     for (int m = 0; m < NX; ++m) {
       const int t = t0 - (K - 1) + m;
       const int tc = t < 0 ? 0 : (t >= L ? L - 1 : t);
-      ld_raw<RB_CONV_X_NT != 0>(in.xs[m], xb + tc * x_rs);
+      ld_raw<false>(in.xs[m], xb + tc * x_rs);
     }
 #pragma unroll
     for (int j = 0; j < TC; ++j) {
@@ -463,7 +453,7 @@ int conv_fwd_rows_k(const T* x, int64_t x_rs, const float* w, const float* bias,
     case 1: return conv_fwd_rows_t<T, 1, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 2: return conv_fwd_rows_t<T, 2, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 3: return conv_fwd_rows_t<T, 3, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
-    case 4: return conv_fwd_rows_t<T, 4, RB_CONV_ROWS_TC>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
+    case 4: return conv_fwd_rows_t<T, 4, kConvRowsTC>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 5: return conv_fwd_rows_t<T, 5, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 6: return conv_fwd_rows_t<T, 6, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);
     case 7: return conv_fwd_rows_t<T, 7, 4>(x, x_rs, w, bias, xc, xc_rs, ntok, H, vec, pos, st);

@@ -25,9 +25,7 @@ namespace rb {
 namespace {
 
 constexpr int kChunk = 64;
-#ifndef RB_EMB_MERGE_LIMIT
-#define RB_EMB_MERGE_LIMIT 0   // rocPRIM's default: 1 << 20
-#endif
+constexpr unsigned kEmbMergeLimit = 0;   // rocPRIM's default: 1 << 20
 
 __global__ void k_emb_prep(const int64_t* __restrict__ idx, int* __restrict__ keys,
                            int* __restrict__ vals, int64_t M) {
@@ -223,7 +221,7 @@ k_emb_finish(const int* __restrict__ nch, const int* __restrict__ choff,
 // a merge-sort limit of 0 selects Onesweep, the LSD radix sort (stable: the
 // positions of one key stay in order), two 8-bit passes over the 14 key bits
 using EmbSortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                              rocprim::default_config, RB_EMB_MERGE_LIMIT>;
+                                              rocprim::default_config, kEmbMergeLimit>;
 
 int key_bits(int64_t V) {
   int b = 1;
@@ -253,11 +251,11 @@ EmbWs emb_layout(int64_t M, int64_t V, int64_t d) {
   w.desc = take((size_t)max_chunks * 16);
   w.partial = take((size_t)max_chunks * d * 4);
   w.sort_bytes = 0;
-  rocprim::radix_sort_pairs<EmbSortCfg>(nullptr, w.sort_bytes, (const int*)nullptr, (int*)nullptr,
+  (void)rocprim::radix_sort_pairs<EmbSortCfg>(nullptr, w.sort_bytes, (const int*)nullptr, (int*)nullptr,
                             (const int*)nullptr, (int*)nullptr, (size_t)M, 0, key_bits(V));
   w.sort_tmp = take(w.sort_bytes);
   w.scan_bytes = 0;
-  rocprim::exclusive_scan(nullptr, w.scan_bytes, (const int*)nullptr, (int*)nullptr, 0,
+  (void)rocprim::exclusive_scan(nullptr, w.scan_bytes, (const int*)nullptr, (int*)nullptr, 0,
                           (size_t)(V + 1), rocprim::plus<int>());
   w.scan_tmp = take(w.scan_bytes);
   w.total = off;

@@ -240,50 +240,7 @@ __device__ __forceinline__ void scan_from_upper(float& A, float& E, int q) {
   }
 }
 
-// DMA (bf16, configs[4]): the operands of the next kDmaSlots - 1 tiles move
-// by LDS-DMA (global_load_lds_dwordx4) into a per-wave LDS ring instead of
-// register buffers, so a wave keeps three tiles of loads in flight under the
-// same register budget (one wave per SIMD at L = 2048).  Ring slot: the five
-// operand streams as [step j][chunk q][channel group g] 8-B entries (a tile's
-// reads of one step are one linear, conflict-free 512-B sweep), then the
-// tile's 256-B carry checkpoint.  Each wave owns its ring: its own counted
-// vmcnt orders its LDS reads behind its DMAs, no barriers.
-constexpr int kDmaSlots = 3;
-constexpr int kDmaSlot = 5 * 2048 + 256;
-constexpr int kDmaLds = 4 * kDmaSlots * kDmaSlot;
-#ifndef RB_GATE_DMA_AUX
-#define RB_GATE_DMA_AUX 2   // nontemporal (once-read streams)
-#endif
-typedef __attribute__((address_space(3))) void* gs_lds_ptr_t;
-typedef uint32_t gs_u32x2 __attribute__((ext_vector_type(2)));
-typedef float gs_f32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ gs_u32x2 gs_ds_read_b64(uint32_t addr) {
-  gs_u32x2 r;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
-__device__ __forceinline__ gs_f32x4 gs_ds_read_b128(uint32_t addr) {
-  gs_f32x4 r;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
-  return r;
-}
-// wait until at most 11 * nb + 16 * ns vector-memory ops are outstanding
-// (nb DMA batches of 11 and ns tiles' 16 stores issued after the awaited batch)
-__device__ __forceinline__ void gs_wait_ring(int nb, int ns) {
-  switch (nb * 3 + ns) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(32)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(27)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(43)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(38)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(54)" ::: "memory"); break;
-  }
-}
-
-template <typename T, int VEC, int Q, int TC, bool PF, bool DMA = false>
+template <typename T, int VEC, int Q, int TC, bool PF>
 __global__ void __launch_bounds__(256)
 k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, int xc_rs,
                 const T* __restrict__ z, int z_rs, const float* __restrict__ lam,
@@ -368,12 +325,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   };
   auto process = [&](const BwdIn<T, VEC, TC>& raw, int tile, const float (&hc)[VEC]) {
     float hcar[VEC];
-    if constexpr (DMA) {
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) hcar[v] = hc[v];
-    } else {
-      ldc(hcar, carries + (b * nTc + tile) * H + cc);
-    }
+    ldc(hcar, carries + (b * nTc + tile) * H + cc);
     struct {
       float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC], g[TC][VEC];
     } in;
@@ -502,76 +454,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
     const int nT = (L + TILE - 1) / TILE;          // tiles of this row
 #pragma unroll
     for (int v = 0; v < VEC; ++v) ecarry[v] = 0.0f;
-    if constexpr (DMA) {
-      // dense rows, L % TILE == 0, every lane's channels valid, dy at every
-      // position (the host checks): every tile issues exactly 16 stores, so
-      // the counted waits below are exact
-      static_assert(sizeof(T) == 2 && VEC == 4 && Q == 4 && TC == 4,
-                    "the LDS-DMA ring serves the bf16 4 x 4 x 4 layout");
-      extern __shared__ __attribute__((aligned(16))) char gs_smem[];
-      char* ring = gs_smem + (threadIdx.x >> 6) * (kDmaSlots * kDmaSlot);
-      const uint32_t ring_addr = (uint32_t)(uintptr_t)(gs_lds_ptr_t)ring;
-      const int cw0 = c0 - g * VEC;                 // the wave's first channel
-      // DMA lane l -> LDS entry l*16 of a 1-KB piece: step 2h + (l >> 5),
-      // chunk (l >> 3) & 3, 8 channels from cw0 + 8 (l & 7)
-      const int dj = lane >> 5, dq = (lane >> 3) & 3, dc = (lane & 7) * 8;
-      const int drow0 = dq * TC + dj;
-      const T* sbase[5] = {rg + row0 * rg_rs + cw0, rg + row0 * rg_rs + H + cw0,
-                           xc + row0 * xc_rs + cw0, z + row0 * z_rs + cw0, dy + row0 * H + cw0};
-      const int srs[5] = {rg_rs, rg_rs, xc_rs, z_rs, H};
-      auto issue = [&](int tile, int slot) {
-        char* dst = ring + slot * kDmaSlot;
-#pragma unroll
-        for (int s_ = 0; s_ < 5; ++s_)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const T* src = sbase[s_] + (int64_t)(tile * TILE + drow0 + 2 * h) * srs[s_] + dc;
-            __builtin_amdgcn_global_load_lds((const void*)src,
-                                             (gs_lds_ptr_t)(dst + s_ * 2048 + h * 1024), 16, 0,
-                                             RB_GATE_DMA_AUX);
-          }
-        if (lane < 16)
-          __builtin_amdgcn_global_load_lds(
-              (const void*)(carries + (b * nTc + tile) * H + cw0 + lane * 4),
-              (gs_lds_ptr_t)(dst + 10240), 16, 0, 0);
-      };
-      for (int k = 0; k < kDmaSlots - 1 && k < nT; ++k) issue(nT - 1 - k, k);
-      int slot = 0;
-      for (int k = 0; k < nT; ++k) {
-        const int tile = nT - 1 - k;
-        if (k + kDmaSlots - 1 < nT) {
-          // its slot was read by the previous tile (consumed: lgkmcnt drained)
-          const int ns_ = slot == 0 ? kDmaSlots - 1 : slot - 1;
-          issue(tile - (kDmaSlots - 1), ns_);
-        }
-        gs_wait_ring(min(k + kDmaSlots - 1, nT - 1) - k, k - max(0, k - kDmaSlots + 1));
-        const uint32_t rd = ring_addr + slot * kDmaSlot + q * 128 + g * 8;
-        BwdIn<T, VEC, TC> raw;
-        gs_u32x2 w[5][TC];
-#pragma unroll
-        for (int s_ = 0; s_ < 5; ++s_)
-#pragma unroll
-          for (int j = 0; j < TC; ++j) w[s_][j] = gs_ds_read_b64(rd + s_ * 2048 + j * 512);
-        gs_f32x4 hv = gs_ds_read_b128(ring_addr + slot * kDmaSlot + 10240 + g * 16);
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[0][2]), "+v"(w[0][3]),
-                       "+v"(w[1][0]), "+v"(w[1][1]), "+v"(w[1][2]), "+v"(w[1][3]),
-                       "+v"(w[2][0]), "+v"(w[2][1]), "+v"(w[2][2]), "+v"(w[2][3]),
-                       "+v"(w[3][0]), "+v"(w[3][1]), "+v"(w[3][2]), "+v"(w[3][3]),
-                       "+v"(w[4][0]), "+v"(w[4][1]), "+v"(w[4][2]), "+v"(w[4][3]), "+v"(hv));
-#pragma unroll
-        for (int j = 0; j < TC; ++j) {
-          raw.r[j].w[0] = w[0][j][0]; raw.r[j].w[1] = w[0][j][1];
-          raw.i[j].w[0] = w[1][j][0]; raw.i[j].w[1] = w[1][j][1];
-          raw.x[j].w[0] = w[2][j][0]; raw.x[j].w[1] = w[2][j][1];
-          raw.z[j].w[0] = w[3][j][0]; raw.z[j].w[1] = w[3][j][1];
-          raw.g[j].w[0] = w[4][j][0]; raw.g[j].w[1] = w[4][j][1];
-        }
-        const float hc[VEC] = {hv[0], hv[1], hv[2], hv[3]};
-        process(raw, tile, hc);
-        slot = slot + 1 == kDmaSlots ? 0 : slot + 1;
-      }
-    } else if constexpr (PF) {
+    if constexpr (PF) {
       if (nT > 0) load(bufA, nT - 1);
       for (int tile = nT - 1; tile >= 0; tile -= 2) {
         if (tile - 1 >= 0) load(bufB, tile - 1);
@@ -625,13 +508,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
 // math runs at the same rate).
 constexpr int kFwdQ = 4, kFwdTC = RB_TILE / kFwdQ;
 constexpr int kBwdQ = 8, kBwdTC = RB_TILE / kBwdQ;
-#ifndef RB_GATE_BWD_PAIR
-#define RB_GATE_BWD_PAIR 1
-#endif
-constexpr bool kBwdPair = RB_GATE_BWD_PAIR != 0;
-#ifndef RB_GATE_BWD_DMA
-#define RB_GATE_BWD_DMA 0
-#endif
+constexpr bool kBwdPair = true;   // packed batches: a long and a short sequence per wave
 
 // alignment/stride check for VEC-wide access: activation pointers (T) need
 // sizeof(T)*V-byte alignment, the fp32 per-channel vectors 4*V
@@ -662,7 +539,7 @@ int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   return launch_status("rb_gate_scan_fwd");
 }
 
-template <typename T, int V, int Q = kBwdQ, int TC = kBwdTC, bool PF = false, bool DMA = false>
+template <typename T, int V, int Q = kBwdQ, int TC = kBwdTC, bool PF = false>
 int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
@@ -674,16 +551,8 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   const int pair = offs != nullptr && kBwdPair;
   const int64_t Bw = pair ? (B + 1) / 2 : B;
   const int64_t blocks = (Bw * ncw + 3) / 4;
-  if constexpr (DMA) {
-    static bool done = false;   // benign race: idempotent
-    if (!done) {
-      (void)hipFuncSetAttribute((const void*)k_gate_scan_bwd<T, V, Q, TC, PF, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kDmaLds);
-      done = true;
-    }
-  }
-  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF, DMA>), dim3((unsigned)blocks),
-                     dim3(256), DMA ? kDmaLds : 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
+  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF>), dim3((unsigned)blocks),
+                     dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
                      dh0_part, B, (int)L, (int)H, ncw, offs, pair, dy_last);
   return launch_status("rb_gate_scan_bwd");
@@ -728,15 +597,9 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   // prefetched in storage format — one wave walks 128 tiles, so it needs two
   // tiles of loads in flight (tools/kbench.hip: 0.36 -> 0.59 of 8 TB/s)
   if constexpr (sizeof(T) == 2) {
-    // dense rows of whole tiles, dy everywhere, 16-B aligned rows of whole
-    // 64-channel wave spans: the LDS-DMA ring (-DRB_GATE_BWD_DMA=1; measured
-    // slower than the register prefetch, 0.564 vs 0.592 of 8 TB/s at configs[4])
-    bool dma = RB_GATE_BWD_DMA && offs == nullptr && dy_last == nullptr && L % RB_TILE == 0 &&
-               H % 64 == 0 && vec_ok<T, 8>(H, strides, act, f32);
-    if (dma)
-      return gate_bwd_v<T, VW, 4, 4, false, true>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries,
-                                                  dy, drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part,
-                                                  dh0_part, B, L, H, offs, st, dy_last);
+    // (an LDS-DMA ring of three tiles per wave instead of the register
+    // prefetch measured slower: 0.564 vs 0.592 of 8 TB/s at configs[4],
+    // profiles/r03_kbench_c5_gate_bwd_dma.txt; kept in git history)
     if (vec_ok<T, VW>(H, strides, act, f32))
       return gate_bwd_v<T, VW, 4, 4, true>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy,
                                            drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part, dh0_part,

@@ -71,12 +71,7 @@ __device__ __forceinline__ void split2h(f32x2 x, f16x2& h0, f16x2& h1) {
 }
 
 __device__ __forceinline__ f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) {
-#ifdef HN_NO_MFMA
-  c[0] += (float)a[0] * (float)b[1];
-  return c;
-#else
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-#endif
 }
 
 // max(|a|, |b|, |c|) in one instruction (no NaN canonicalisation: a NaN input
@@ -164,18 +159,9 @@ __global__ void __launch_bounds__(256) k_split_weights_h(const SplitJobsH jobs) 
 }
 
 // ---------------------------------------------------------------------------
-#ifndef HN_NSA
-#define HN_NSA 3
-#endif
-#ifndef HN_WAVES
-#define HN_WAVES 8
-#endif
-#ifndef HN_MAXC
-#define HN_MAXC 1024
-#endif
-constexpr int N_WAVES = HN_WAVES;
+constexpr int N_WAVES = 8;
 constexpr int N_BM = 32 * N_WAVES, N_BN = 128, N_BK = 32;
-constexpr int N_NSA = HN_NSA, N_NSB = 2;
+constexpr int N_NSA = 3, N_NSB = 2;
 constexpr int N_THREADS = 64 * N_WAVES;
 constexpr int N_LA = N_NSA - 1;                       // A steps in flight
 constexpr int N_NB = N_BN / 32;                       // column blocks per wave (4)
@@ -185,7 +171,7 @@ constexpr int N_A_STAGE = N_BM * N_BK * 4;            // 32 KB
 constexpr int N_B_STAGE = N_BFRAG * 1024;             // 16 KB
 constexpr int N_RING = N_NSA * N_A_STAGE + N_NSB * N_B_STAGE;  // 128 KB
 // + the column exponents and the bias of all C columns (C <= 1024)
-constexpr int N_MAXC = HN_MAXC;
+constexpr int N_MAXC = 1024;
 constexpr int N_MAXFLAG = 32;  // flagged tiles listed per wave (beyond: redo all)
 constexpr int N_LDS = N_RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
 
@@ -201,7 +187,7 @@ struct NtCfg {
   static constexpr int BFRAG = NB * 4;                  // B fragments per k-step
   static constexpr int BDMA = BFRAG / N_WAVES;          // B DMAs per wave per k-step
   static constexpr int B_STAGE = BFRAG * 1024;
-  static constexpr int NSA = NB == 4 ? HN_NSA : 2;
+  static constexpr int NSA = NB == 4 ? N_NSA : 2;
   static constexpr int RING = NSA * N_A_STAGE + N_NSB * B_STAGE;
   static constexpr int LDS = RING + N_MAXC * 8 + N_WAVES * N_MAXFLAG * 4;
 };
@@ -224,28 +210,6 @@ template <int N>
 __device__ __forceinline__ void hwait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
-
-// Diagnostic build only (-DHN_STAMPS, tools/gemmbench_h.hip): per-wave cycle
-// sums of the k-step's segments (wait, barrier, substep 0, DMA issue +
-// deferred stores, substep 1, tile bookkeeping), read their shares, not the
-// build's run time (the stamps' lgkmcnt(0) forbid overlaps).
-#ifdef HN_STAMPS
-constexpr int HN_NSEG = 6;
-__device__ unsigned long long hn_stamps[2048 * 8 * HN_NSEG];
-#define HN_STAMP(k)                                                                  \
-  do {                                                                               \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    unsigned long long t_;                                                           \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");       \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    if ((k) >= 0) st_acc[(k) < 0 ? 0 : (k)] += t_ - st_prev;                           \
-    st_prev = t_;                                                                    \
-  } while (0)
-#else
-#define HN_STAMP(k) \
-  do {              \
-  } while (0)
-#endif
 
 // quad_perm DPP moves (lane k of each quad reads lane k ^ 1 / k ^ 2)
 __device__ __forceinline__ float dpp_xor1(float x) {
@@ -306,13 +270,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   constexpr int N_BN = CF::BN, N_NB = NB, N_BDMA = CF::BDMA, N_NSA = CF::NSA, N_LA = N_NSA - 1;
   constexpr int N_B_STAGE = CF::B_STAGE, N_RING = CF::RING;
   // deferred epilogue for NB = 4 (NB = 8 and DACT: stored at the tile's end)
-#ifdef HN_DACT_DEFER
-  // A/B build: DACT's blocks deferred a k-step each (256 VGPRs, 12 spilled:
-  // 1,068 vs 295 us at 204,632 rows, profiles/r03_ffn_probe.txt)
-  constexpr bool DEFER = NB == 4;
-#else
   constexpr bool DEFER = NB == 4 && !DACT;   // DACT: stored at the tile's end
-#endif
   static_assert(!(NB == 8) || WIDE, "256-column tiles store through the wide epilogue");
   static_assert(!ACT || WIDE, "the activation output rides the wide epilogue");
   static_assert(!DACT || (WIDE && !ACT && !BIAS), "DACT: wide epilogue, no bias");
@@ -381,27 +339,15 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       a_off[q] = (int)(r * lda * 4) + lc * 16;
     }
   };
-#ifdef HN_A_NT
-  // A/B: the A stream with the nontemporal hint when every A row is read
-  // once (a single column tile)
-  const bool a_nt = nct == 1;
-#else
-  constexpr bool a_nt = false;
-#endif
+  // (default cache policy: the nontemporal hint where each A row is read
+  // once measured 1% slower)
   auto issueA = [&]() {
     char* st = smem + a_slot * N_A_STAGE + wave * 4096;
     const char* b = a_base + a_kt * (N_BK * 4);
-    if (a_nt) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024),
-                                         16, 0, 2);
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024),
-                                         16, 0, 0);
-    }
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(b + a_off[q]), (lds_ptr_t)(st + q * 1024),
+                                       16, 0, 0);
     a_slot = a_slot + 1 == N_NSA ? 0 : a_slot + 1;
     if (++a_kt == KT) {
       a_kt = 0;
@@ -498,11 +444,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         f32x4* o = (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane);
         const int64_t row = pend_r0 + 8 * g + 4 * (lane >> 5) + (lane & 3);
         if (pend_full || row < M)
-#ifdef HN_PLAIN_STORE
-          *o = f32x4{v[0], v[1], v[2], v[3]};
-#else
           __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, o);
-#endif
         if constexpr (ACT) {
           float m[4];
           drop.get4(e_base + row * C + pend_c0 + n * 32 + (lane & 28), m);
@@ -616,10 +558,6 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   int i = 0, kt = 0, c_slot_a = 0, c_slot_b = 0;
   int cur_mt, cur_ct;
   tile_of(0, cur_mt, cur_ct);
-#ifdef HN_STAMPS
-  unsigned long long st_acc[HN_NSEG] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-#endif
-  HN_STAMP(-1);
   for (int u = 0; u < U; ++u) {
     // operands of step u landed (own DMAs): the ops younger than B(u) are
     // A(u-1+N_LA) (4, issued by step u-1 if it exists) and the 16 deferred
@@ -646,31 +584,13 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         if (stored_prev) hwait_vm<NST>(); else hwait_vm<0>();
       }
     }
-    HN_STAMP(0);
-#ifndef HN_NO_BARRIER
     __builtin_amdgcn_s_barrier();
-#endif
-    HN_STAMP(1);
-    // DMA issue position: right after the barrier (default: their slots
-    // were last read in step u-1, which every wave has finished; 2-4% faster
-    // than after substep 0, HN_LATE_DMA), or for the waves 4-7 only
-    // (HN_LATE_DMA + HN_STAGGER_DMA: the two waves sharing a SIMD issue at
-    // different times; measured null).  The same issue order (B before A,
-    // stores after), so the counted waits above are unchanged.
-#if !defined(HN_LATE_DMA)
-    constexpr bool early_all = true;
-#else
-    constexpr bool early_all = false;
-#endif
-#if defined(HN_STAGGER_DMA)
-    const bool early = early_all || (wave & 4) != 0;
-#else
-    const bool early = early_all;
-#endif
-    if (early) {
-      if (u + 1 < U) issueB();
-      if (u + N_LA < U) issueA();
-    }
+    // the next steps' DMAs right after the barrier: their slots were last
+    // read in step u-1, which every wave has finished (2-4% faster than after
+    // substep 0; staggering the issue of the two waves of a SIMD: null).  B
+    // before A, the stores after: the counted waits above rely on that order
+    if (u + 1 < U) issueB();
+    if (u + N_LA < U) issueA();
 
     const uint32_t sa = smem_base + c_slot_a * N_A_STAGE;
     const uint32_t sb = smem_base + N_NSA * N_A_STAGE + c_slot_b * N_B_STAGE + lane * 16;
@@ -700,10 +620,6 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         flag_tile = flag_tile || __builtin_amdgcn_ballot_w64(mx > thr) != 0;
       }
       f16x8 a0, a1;
-#ifdef HN_NO_SPLIT
-      a0 = __builtin_bit_cast(f16x8, xa);
-      a1 = __builtin_bit_cast(f16x8, xb);
-#else
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f32x2 v = (q < 2 ? f32x2{xa[2 * q], xa[2 * q + 1]}
@@ -713,7 +629,6 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         a0[2 * q] = h0[0]; a0[2 * q + 1] = h0[1];
         a1[2 * q] = h1[0]; a1[2 * q + 1] = h1[1];
       }
-#endif
       // per column block: the small partial products first; block n + 2's
       // fragments are read behind block n's MFMAs
 #pragma unroll
@@ -726,38 +641,18 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
         acc[n] = mfma_h(a0, bq[n][1], acc[n]);
         acc[n] = mfma_h(a0, bq[n][0], acc[n]);
         if (n + 2 < N_NB) {
-#ifdef HN_HALF_B
-          // ablation (wrong results): the upper half of the column blocks
-          // reuse the lower half's fragments (half the B LDS reads)
-          if (n + 2 >= N_NB / 2 && N_NB >= 4) {
-            bq[n + 2][0] = bq[n + 2 - N_NB / 2][0];
-            bq[n + 2][1] = bq[n + 2 - N_NB / 2][1];
-            continue;
-          }
-#endif
           bq[n + 2][0] = rb(n + 2, 0);
           bq[n + 2][1] = rb(n + 2, 1);
         }
       }
     };
     substep(0);
-    HN_STAMP(2);
-    if (!early) {
-#ifndef HN_NO_BDMA
-      if (u + 1 < U) issueB();
-#endif
-#ifndef HN_NO_ADMA
-      if (u + N_LA < U) issueA();
-#endif
-    }
     stored_prev = false;
     if (DEFER && pend_on && pend_q < N_NB) {
       // a partial tile's guarded stores may issue fewer than 16: not counted
       stored_prev = store_quarter();
     }
-    HN_STAMP(3);
     substep(1);
-    HN_STAMP(4);
     c_slot_a = c_slot_a + 1 == N_NSA ? 0 : c_slot_a + 1;
     c_slot_b ^= 1;
 
@@ -853,12 +748,7 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     } else {
       ++kt;
     }
-    HN_STAMP(5);
   }
-#ifdef HN_STAMPS
-  if (lane == 0 && blockIdx.x < 2048)
-    for (int k = 0; k < HN_NSEG; ++k) hn_stamps[((int)blockIdx.x * 8 + wave) * HN_NSEG + k] = st_acc[k];
-#endif
   while (pend_on && pend_q < N_NB) store_quarter();
 
   // cold tail: the wave's rows of every flagged tile again, with each row's
@@ -1077,12 +967,8 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     for (int q = 0; q < 8; ++q) {
       int64_t row = row0 + q;
       row = row < r_end ? row : r_end - 1;  // rows past the chunk: zeroed on convert
-#ifdef HN_TN_NONTEMPORAL
-      r[q] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(src + row * ld));
-#else
       // plain loads: the other tiles of this split re-read these rows (L2)
       r[q] = *reinterpret_cast<const f32x4*>(src + row * ld);
-#endif
     }
   };
   auto convert = [&](f32x4 (&r)[8], int t, int buf) {
@@ -1111,43 +997,6 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     }
   };
 
-#ifdef HN_TN_16
-  // v_mfma_f32_16x16x32_f16 (one 32-row m-step per product): 4 x 4 blocks of
-  // 16 x 16 per wave
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  auto mma = [&](int buf) {
-    const uint32_t iy = smem_base + buf * CF::STAGE;
-    const uint32_t ix = iy + 2 * CF::YPLANE;
-    f16x8 a[4][2], b[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t oa = tn_off(64 * wm + 16 * i + (lane & 15), lane >> 4);
-      const uint32_t ob = tn_off(64 * wk + 16 * i + (lane & 15), lane >> 4);
-      a[i][0] = hds_read16<f16x8>(iy + oa);
-      a[i][1] = hds_read16<f16x8>(iy + CF::YPLANE + oa);
-      b[i][0] = hds_read16<f16x8>(ix + ob);
-      b[i][1] = hds_read16<f16x8>(ix + CF::XPLANE + ob);
-    }
-    // the reads are inline asm: tie every fragment to the wait
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(a[2][0]),
-                   "+v"(a[2][1]), "+v"(a[3][0]), "+v"(a[3][1]), "+v"(b[0][0]), "+v"(b[0][1]),
-                   "+v"(b[1][0]), "+v"(b[1][1]), "+v"(b[2][0]), "+v"(b[2][1]), "+v"(b[3][0]),
-                   "+v"(b[3][1]));
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
-      }
-  };
-#else
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1186,7 +1035,6 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     }
   };
 
-#endif
   if (T > 0) load(0, raw0);
   if (T > 1) load(1, raw1);
   for (int t = 0; t < T; t += 2) {
@@ -1206,19 +1054,6 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
   // chunks zeros)
   const int sh = ey + ex - 2 * kTT;
   float* out = parts + (int64_t)s * N * K;
-#ifdef HN_TN_16
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = k0 + 64 * wk + 16 * j + (lane & 15);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = n0 + 64 * wm + 16 * i + 4 * (lane >> 4) + e;
-        out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
-      }
-    }
-#else
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1230,223 +1065,9 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
         out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
       }
     }
-#endif
 }
 
 
-
-// k_gemm_tn_pc: the same product and partials as k_gemm_tn_h on the 512-
-// thread tiles (256 x 128 or 128 x 256), with the work divided by role:
-// waves 0-3 only multiply (each a 64-wide slice of the tile's longer side
-// against all of the shorter: 8 blocks of 32 x 32, 128 accumulators), waves
-// 4-7 only load, scale, split and write the next m-step's column-major
-// images.  The two roles share each SIMD (waves w and w + 4), so the
-// conversion's VALU and LDS writes run beside the MFMAs instead of between
-// them; one barrier per 32-row m-step separates the two LDS stages.
-template <int NBN, int NBK>
-__global__ void __launch_bounds__(512, 1)
-k_gemm_tn_pc(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X, int64_t ldx,
-             int64_t M, int N, int K, const float* __restrict__ ymax,
-             const float* __restrict__ xmax, float* __restrict__ parts, int S, int64_t mk,
-             int nt_k) {
-  static_assert(NBN * NBK == 2, "512-thread tiles only");
-  using CF = TnCfg<NBN, NBK>;
-  constexpr int YC = CF::YC, XC = CF::XC;
-  constexpr bool SPLIT_N = YC >= XC;          // MFMA waves split the longer side
-  constexpr int BN = SPLIT_N ? 2 : YC / 32;   // n blocks per MFMA wave
-  constexpr int BK = SPLIT_N ? XC / 32 : 2;   // k blocks per MFMA wave
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int G = gridDim.x;
-  const int idx = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
-  const int nt = (N / YC) * nt_k;
-  const int tile = idx % nt, s = idx / nt;
-  const int n0 = (tile / nt_k) * YC, k0 = (tile % nt_k) * XC;
-  const int64_t r_begin = (int64_t)s * mk;
-  const int64_t r_end = r_begin + mk < M ? r_begin + mk : M;
-  const int64_t nrows = r_end > r_begin ? r_end - r_begin : 0;
-  const int T = (int)((nrows + 31) / 32);
-
-  // chunk scales from the 32-row group maxima
-  float my = 0.0f, mx = 0.0f;
-  for (int64_t g = r_begin / 32 + tid; g * 32 < r_end; g += 512) {
-    my = fmaxf(my, ymax[g]);
-    mx = fmaxf(mx, xmax[g]);
-  }
-  float* red = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    my = fmaxf(my, __shfl_xor(my, o));
-    mx = fmaxf(mx, __shfl_xor(mx, o));
-  }
-  if (lane == 0) { red[wave] = my; red[8 + wave] = mx; }
-  __syncthreads();
-  my = 0.0f;
-  mx = 0.0f;
-#pragma unroll
-  for (int w = 0; w < 8; ++w) {
-    my = fmaxf(my, red[w]);
-    mx = fmaxf(mx, red[8 + w]);
-  }
-  const int ey = my > 0.0f ? __builtin_amdgcn_frexp_expf(my) : 0;
-  const int ex = mx > 0.0f ? __builtin_amdgcn_frexp_expf(mx) : 0;
-  __syncthreads();
-  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-
-  if (wave >= 4) {
-    // ---- converters: YC + XC roles of 4 columns x 8 rows over 256 threads
-    // (role r = ct, then ct + 256 where that exists)
-    const int ct = tid - 256;
-    auto role = [&](int r, const float*& src, int64_t& ld, float& sc, uint32_t& img_off,
-                    uint32_t& plane, int& cc, int& rg) {
-      const int op = r < YC ? 0 : 1;
-      const int lt = op == 0 ? r : r - YC;
-      const int ncg = (op == 0 ? YC : XC) / 4;
-      cc = lt % ncg;
-      rg = lt / ncg;
-      src = op == 0 ? Y + n0 + 4 * cc : X + k0 + 4 * cc;
-      ld = op == 0 ? ldy : ldx;
-      sc = __builtin_amdgcn_ldexpf(1.0f, kTT - (op == 0 ? ey : ex));
-      img_off = op == 0 ? 0u : (uint32_t)(2 * CF::YPLANE);
-      plane = op == 0 ? (uint32_t)CF::YPLANE : (uint32_t)CF::XPLANE;
-    };
-    constexpr int NROLE = (YC + XC + 255) / 256;   // 2
-    const bool two = ct + 256 < YC + XC;           // wave-uniform (waves 4, 5)
-    const float* src[NROLE];
-    int64_t ld[NROLE];
-    float sc[NROLE];
-    uint32_t img_off[NROLE], plane[NROLE];
-    int cc[NROLE], rg[NROLE];
-    role(ct, src[0], ld[0], sc[0], img_off[0], plane[0], cc[0], rg[0]);
-    role(two ? ct + 256 : ct, src[1], ld[1], sc[1], img_off[1], plane[1], cc[1], rg[1]);
-    // two register stages, named (a runtime index would put them in scratch)
-    f32x4 raw0[NROLE][8], raw1[NROLE][8];
-    auto load = [&](int t, f32x4 (&r)[NROLE][8]) {
-#pragma unroll
-      for (int k = 0; k < NROLE; ++k) {
-        if (k == 1 && !two) break;
-        const int64_t row0 = r_begin + (int64_t)t * 32 + rg[k] * 8;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          int64_t row = row0 + q;
-          row = row < r_end ? row : r_end - 1;
-          r[k][q] = *reinterpret_cast<const f32x4*>(src[k] + row * ld[k]);
-        }
-      }
-    };
-    auto convert = [&](int t, f32x4 (&r)[NROLE][8]) {
-      const uint32_t stage = smem_base + (t & 1) * CF::STAGE;
-#pragma unroll
-      for (int k = 0; k < NROLE; ++k) {
-        if (k == 1 && !two) break;
-        const int64_t row0 = r_begin + (int64_t)t * 32 + rg[k] * 8;
-        if (row0 + 8 > r_end) {
-#pragma unroll
-          for (int q = 0; q < 8; ++q)
-            if (row0 + q >= r_end) r[k][q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-        }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          f16x8 h0, h1;
-#pragma unroll
-          for (int q = 0; q < 8; q += 2) {
-            f16x2 p0, p1;
-            split2h(f32x2{r[k][q][c], r[k][q + 1][c]} * sc[k], p0, p1);
-            h0[q] = p0[0]; h0[q + 1] = p0[1];
-            h1[q] = p1[0]; h1[q + 1] = p1[1];
-          }
-          const uint32_t off = stage + img_off[k] + tn_off(4 * cc[k] + c, rg[k]);
-          hds_write16(off, h0);
-          hds_write16(off + plane[k], h1);
-        }
-      }
-    };
-    // step t's operands live in raw0 (t even) / raw1 (t odd), loaded two
-    // steps ahead
-    if (T > 0) load(0, raw0);
-    if (T > 1) load(1, raw1);
-    if (T > 0) {
-      convert(0, raw0);
-      if (T > 2) load(2, raw0);
-    }
-    __syncthreads();
-    for (int t = 0; t < T; t += 2) {
-      if (t + 1 < T) {
-        convert(t + 1, raw1);
-        if (t + 3 < T) load(t + 3, raw1);
-      }
-      __syncthreads();
-      if (t + 1 < T) {
-        if (t + 2 < T) {
-          convert(t + 2, raw0);
-          if (t + 4 < T) load(t + 4, raw0);
-        }
-        __syncthreads();
-      }
-    }
-    return;
-  }
-
-  // ---- MFMA waves: a 64-wide slice of the longer side each
-  f32x16 acc[BN][BK];
-#pragma unroll
-  for (int a = 0; a < BN; ++a)
-#pragma unroll
-    for (int b = 0; b < BK; ++b)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
-  const int h = lane >> 5;
-  const int nb0 = SPLIT_N ? 64 * wave : 0;   // the wave's first n / k of the tile
-  const int kb0 = SPLIT_N ? 0 : 64 * wave;
-  __syncthreads();
-  for (int t = 0; t < T; ++t) {
-    const uint32_t iy = smem_base + (t & 1) * CF::STAGE;
-    const uint32_t ix = iy + 2 * CF::YPLANE;
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      f16x8 a[BN][2], b[BK][2];
-#pragma unroll
-      for (int i = 0; i < BN; ++i) {
-        const uint32_t oa = tn_off(nb0 + 32 * i + (lane & 31), 2 * st + h);
-        a[i][0] = *reinterpret_cast<const f16x8*>(smem + (iy - smem_base) + oa);
-        a[i][1] = *reinterpret_cast<const f16x8*>(smem + (iy - smem_base) + CF::YPLANE + oa);
-      }
-#pragma unroll
-      for (int j = 0; j < BK; ++j) {
-        const uint32_t ob = tn_off(kb0 + 32 * j + (lane & 31), 2 * st + h);
-        b[j][0] = *reinterpret_cast<const f16x8*>(smem + (ix - smem_base) + ob);
-        b[j][1] = *reinterpret_cast<const f16x8*>(smem + (ix - smem_base) + CF::XPLANE + ob);
-      }
-#pragma unroll
-      for (int i = 0; i < BN; ++i)
-#pragma unroll
-        for (int j = 0; j < BK; ++j) {
-          acc[i][j] = mfma_h(a[i][1], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_h(a[i][0], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_h(a[i][0], b[j][0], acc[i][j]);
-        }
-    }
-    __syncthreads();
-  }
-
-  // un-scale and store the partial tile (every split writes its slot, empty
-  // chunks zeros)
-  const int sh = ey + ex - 2 * kTT;
-  float* out = parts + (int64_t)s * N * K;
-#pragma unroll
-  for (int i = 0; i < BN; ++i)
-#pragma unroll
-    for (int j = 0; j < BK; ++j) {
-      const int col = k0 + kb0 + 32 * j + (lane & 31);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = n0 + nb0 + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
-        out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
-      }
-    }
-}
 
 template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>
 void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, const int* ew, int C,
@@ -1490,16 +1111,8 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st) {
   (void)accumulate;  // rejected by rb_gemm_nt_h
-#ifdef HN_NARROW_STORE
-  const bool wide = false;
-#else
   const bool wide = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && ldo % 4 == 0;
-#endif
-#ifdef HN_NB4_ONLY
-  const bool nb8 = false;
-#else
   const bool nb8 = wide && C % 256 == 0;
-#endif
   // The persistent grid runs whole rounds of G tiles; the rows past the last
   // whole round would run on a fraction of the chip (800 row tiles on 256
   // CUs: a fourth round on 32 of them, +18% time for +4% rows), so they run
@@ -1513,23 +1126,12 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
   const int nct0 = C % 128 ? 0 : C / (nb8 ? 256 : 128);
   if (R > 1024 && nct0 == 0) return fail("rb_gemm_nt_h: C % 128 != 0 needs R <= 1024");
   const int64_t rows_round = nct0 ? (int64_t)(G0 / nct0) * N_BM : 0;
-#ifdef HN_NO_TAIL_SPLIT
-  const int64_t M_main = nct0 ? M : 0;
-#else
   int64_t M_main = R > 1024 ? M
                  : (nct0 && G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round
                                                               : (nct0 ? M : 0);
-#ifdef HN_TAIL_ROUNDS
-  // experiment: one more whole round into the 256 x 64-tile launch for
-  // single-column-tile shapes
-  if (nct0 == 1 && R <= 1024 && M_main >= (HN_TAIL_ROUNDS) * rows_round)
-    M_main -= (HN_TAIL_ROUNDS - 1) * rows_round;
-#endif
-#endif
   const f16x8* wf = (const f16x8*)Wf;
   const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
   if (M_main < M) {
-#ifndef HN_TAIL_SMALL
     // a partial round of 256 x 64 tiles: 4x (2x) the 256 x 256 (256 x 128)
     // tiles of the main launch, each a quarter (half) of their time
     // below one round: the few-rows kernel only where it measured faster
@@ -1549,7 +1151,6 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
       const int rc = launch_status("rb_gemm_nt_h");
       if (rc || M_main == 0) return rc;
     } else
-#endif
     {
       const int rc = launch_gemm_nt_hs(A + M_main * lda, lda, M - M_main, R, Wf, C, bias,
                                        out + M_main * ldo, ldo,
@@ -1586,20 +1187,18 @@ bool nt_h_act_ok(int64_t M, int R, int C, const float* out, const float* act, in
   return wide && C % 256 == 0 && C <= N_MAXC && R <= 1024 && !few;
 }
 
-// ACT's main launch: 256 x 256 tiles stored at the tile's end (8; 264 us at
+// ACT's main launch: 256 x 256 tiles stored at the tile's end (264 us at
 // 204,632 rows against 140 + 135-142 us for the GEMM and the activation
-// kernel), or, as an A/B build, 256 x 128 tiles with the deferred epilogue
-// (4: 995 us, profiles/r03_ffn_probe2.txt)
-#ifndef HN_ACT_NB
-#define HN_ACT_NB 8
-#endif
+// kernel; 256 x 128 tiles with the deferred epilogue took 995 us,
+// profiles/r03_ffn_probe2.txt)
+constexpr int ACT_NB = 8;
 int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                          const float* bias, float* out, int64_t ldo, float* rmax, float* act,
                          DropSpec drop, hipStream_t st) {
   if (!nt_h_act_ok(M, R, C, out, act, ldo))
     return fail("rb_gemm_nt_h_act: shape or alignment without a wide-epilogue launch");
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
-  const int nct0 = C / (32 * HN_ACT_NB);
+  const int nct0 = C / (32 * ACT_NB);
   const int64_t rows_round = (int64_t)(G0 / nct0) * N_BM;
   const int64_t M_main = (G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round : M;
   const f16x8* wf = (const f16x8*)Wf;
@@ -1621,8 +1220,8 @@ int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const vo
   const int m_tiles = (int)((M_main + N_BM - 1) / N_BM);
   const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * nct0;
   const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)G0);
-  if (bias) run_nt_h<true, true, HN_ACT_NB, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
-  else run_nt_h<false, true, HN_ACT_NB, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
+  if (bias) run_nt_h<true, true, ACT_NB, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
+  else run_nt_h<false, true, ACT_NB, true>(A, lda, M_main, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, grid, st, act, drop, 0);
   return launch_status("rb_gemm_nt_h_act");
 }
 
@@ -1635,9 +1234,7 @@ int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const vo
 // 512.
 // DACT's main launch: 256 x 128 tiles stored at the tile's end (the 256 x 256
 // tile's 128 accumulators leave no registers for the epilogue's operands)
-#ifndef HN_DACT_NB
-#define HN_DACT_NB 4
-#endif
+constexpr int DACT_NB = 4;
 int64_t nt_h_dact_parts() { return 2 * (int64_t)(num_cus() / 8 * 8 * (8 / N_WAVES)); }
 
 int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
@@ -1646,7 +1243,7 @@ int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const v
   if (!nt_h_act_ok(M, R, C, out, pre, ldo) || C > N_DACT_MAXC)
     return fail("rb_gemm_nt_h_dact: shape or alignment without a wide-epilogue launch");
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
-  const int nct0 = C / (32 * HN_DACT_NB);
+  const int nct0 = C / (32 * DACT_NB);
   const int64_t rows_round = (int64_t)(G0 / nct0) * N_BM;
   const int64_t M_main = (G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round : M;
   const f16x8* wf = (const f16x8*)Wf;
@@ -1668,7 +1265,7 @@ int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const v
     if (rc) return rc;
   }
   if (M_main > 0) {
-    run_nt_h<false, true, HN_DACT_NB, false, true>(A, lda, M_main, R, wf, ew, C, nullptr, out, ldo, rmax,
+    run_nt_h<false, true, DACT_NB, false, true>(A, lda, M_main, R, wf, ew, C, nullptr, out, ldo, rmax,
                                           m_tiles, grid, st, nullptr, drop, 0, pre, dpart);
     const int rc = launch_status("rb_gemm_nt_h_dact");
     if (rc) return rc;
@@ -1684,12 +1281,7 @@ int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const v
 // (1), else 128 x 128 (0).  The big tiles are 512-thread workgroups, one per
 // CU, so the same split count S (~2 x CUs / (N/128 x K/128)) fills the chip.
 inline int tn_tile_shape(int N, int K) {
-#ifdef HN_TN_SMALL
-  (void)N; (void)K;
-  return 0;
-#else
   return N % 256 == 0 ? 2 : (K % 256 == 0 ? 1 : 0);
-#endif
 }
 
 int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
@@ -1708,19 +1300,6 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
     }
     const int nt_k = K / CF::XC;
     const int nt = (N / CF::YC) * nt_k;
-#ifdef HN_TN_PC
-    if constexpr (NBN * NBK == 2) {
-      static bool done_pc = false;
-      if (!done_pc) {
-        (void)hipFuncSetAttribute((const void*)k_gemm_tn_pc<NBN, NBK>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS);
-        done_pc = true;
-      }
-      k_gemm_tn_pc<NBN, NBK><<<(unsigned)(nt * S), 512, CF::LDS, st>>>(
-          Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
-      return;
-    }
-#endif
     k_gemm_tn_h<NBN, NBK><<<(unsigned)(nt * S), CF::THREADS, CF::LDS, st>>>(
         Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
   };

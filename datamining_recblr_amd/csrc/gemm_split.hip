@@ -160,13 +160,8 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
 // reads its A fragments as fp32 and splits them in registers.
 // The column tiles of one row tile are neighbouring workgroups of one XCD
 // (same blockIdx % 8) working in step, so their A re-reads hit that L2.
-#ifdef GS_SMALL
-constexpr int G_BM = 128, G_BN = 128, G_BK = 32;
-constexpr int G_NSA = 2, G_NSB = 2, G_WAVES = 4, G_WG_PER_CU = 2;
-#else
 constexpr int G_BM = 256, G_BN = 128, G_BK = 32;
 constexpr int G_NSA = 3, G_NSB = 2, G_WAVES = 8, G_WG_PER_CU = 1;
-#endif
 constexpr int G_THREADS = 64 * G_WAVES;
 constexpr int G_LA = G_NSA - 1;                            // A steps in flight
 constexpr int G_BDMA = (G_BN / 32) * 2 * 3 / G_WAVES;      // B DMAs per wave per step
@@ -341,11 +336,7 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
       float v0 = odd ? recv : blk[e];
       float v1 = odd ? blk[e + 1] : recv;
       const int64_t r = rbase + (e & 3) + 8 * (e >> 2) + (odd ? 1 : 0);
-#ifdef GS_NO_STORE
-      if (v0 == 1234.5f) {
-#else
       if (full || r < M) {
-#endif
         f32x2* o = reinterpret_cast<f32x2*>(out + r * ldo + col);
         if (BIAS) { v0 += b0; v1 += b1; }
         if constexpr (ACC) {
@@ -397,15 +388,8 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
           b[cb][p] = ds_read16<bf16x8>(sb + (((wn * 2 + cb) * 2 + s) * 3 + p) * 1024);
       asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[1][0]), "+v"(x[1][1]));
       bf16x8 a[2][3];
-#ifdef GS_NO_SPLIT
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) a[m][p] = __builtin_bit_cast(bf16x8, p == 0 ? x[m][0] : x[m][1]);
-#else
       split8(x[0][0], x[0][1], a[0]);
       split8(x[1][0], x[1][1], a[1]);
-#endif
       asm volatile("s_waitcnt lgkmcnt(0)"
                    : "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[0][2]), "+v"(b[1][0]), "+v"(b[1][1]),
                      "+v"(b[1][2]));
@@ -418,19 +402,13 @@ __global__ void __launch_bounds__(G_THREADS, G_WG_PER_CU) k_gemm_nt(const float*
         for (int m = 0; m < 2; ++m)
 #pragma unroll
           for (int n = 0; n < 2; ++n) {
-#ifdef GS_NO_MFMA
-            acc[m][n][q] += (float)a[m][PA[q]][n] * (float)b[n][PB[q]][q];
-#else
             acc[m][n] = mfma(a[m][PA[q]], b[n][PB[q]], acc[m][n]);
-#endif
           }
     };
     if (pend_mt >= 0 && pend_q < 4) load_old();
     substep(0);
-#ifndef GS_NO_DMA
     if (u + 1 < U) issueB(u + 1);
     if (u + G_LA < U) issueA(u + G_LA);
-#endif
     stored_prev = false;
     if (pend_mt >= 0 && pend_q < 4) {
       // a partial tile's guarded stores may issue fewer than 8: not counted
@@ -476,8 +454,8 @@ template <bool BIAS, bool ACC>
 void set_lds_attr() {
   static bool done = false;  // benign race: idempotent
   if (!done) {
-    hipFuncSetAttribute((const void*)k_gemm_nt<BIAS, ACC>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt<BIAS, ACC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G_LDS);
     done = true;
   }
 }

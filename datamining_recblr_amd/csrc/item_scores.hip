@@ -249,9 +249,6 @@ __global__ __launch_bounds__(256) void k_target_dot(const float* __restrict__ E,
   ts[b] = acc;
 }
 
-#ifdef RB_ITEM_PROF
-__device__ uint64_t g_item_prof[65536 * 4];
-#endif
 
 // Workgroup placement.  The grid is 1-D over RB fixed-row blocks x S splits
 // of the streamed operand (S padded to a multiple of 8).  Workgroups are
@@ -297,40 +294,20 @@ __device__ __forceinline__ void stream_tiles(const float* strm, int64_t n_strm, 
     if constexpr (kRowData == 1) rowdata_dma(lb, tb, lse_g, tgt_g, t * kTile, n_strm);
     if constexpr (kRowData == 2) rowexp_dma(lb, lse_g, t * kTile, n_strm);
   };
-#ifdef RB_ITEM_PROF
-  uint64_t c0 = clock64(), cb = 0, cw = 0, cx;
-#define RB_PROF_MARK(acc) do { cx = clock64(); acc += cx - c0; c0 = cx; } while (0)
-#else
-#define RB_PROF_MARK(acc) do {} while (0)
-#endif
   issue(t0, buf0, lbuf0, tbuf0);
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-#ifdef RB_ITEM_PROF
-  const uint64_t cpro = clock64() - c0;
-  c0 = clock64();
-#endif
   for (int64_t t = t0; t < t1; t += 2) {
     if (t + 1 < t1) issue(t + 1, buf1, lbuf1, tbuf1);
     body(t, buf0, lbuf0, tbuf0);
-    RB_PROF_MARK(cb);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    RB_PROF_MARK(cw);
     if (t + 1 >= t1) break;
     if (t + 2 < t1) issue(t + 2, buf0, lbuf0, tbuf0);
     body(t + 1, buf1, lbuf1, tbuf1);
-    RB_PROF_MARK(cb);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    RB_PROF_MARK(cw);
   }
-#ifdef RB_ITEM_PROF
-  if ((threadIdx.x & 63) == 0) {
-    uint64_t* o = g_item_prof + ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * 4;
-    o[0] = cpro; o[1] = cb; o[2] = cw; o[3] = (uint64_t)(t1 - t0);
-  }
-#endif
 }
 
 // ---- CE forward: per (row, vocab split) log-sum-exp partials --------------------

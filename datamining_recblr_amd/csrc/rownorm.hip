@@ -25,16 +25,8 @@ namespace {
 // Store policy of the LayerNorm outputs: the forward's (y, s) nontemporal
 // (its consumers, the in-projection GEMM and through it the conv, read
 // faster: conv forward 0.65 -> 0.69), the backward's (ds, da) default (nt
-// cost the backward kernel 0.68 -> 0.61); tools/ab_bench.sh,
-// profiles/r02_ab_ln_store_policy.log.  RB_LN_NT / RB_LN_PLAIN: all nt /
-// all default, for A/B.
-#if defined(RB_LN_NT)
-constexpr bool kLnFwdNT = true, kLnBwdNT = true;
-#elif defined(RB_LN_PLAIN)
-constexpr bool kLnFwdNT = false, kLnBwdNT = false;
-#else
+// cost the backward kernel 0.68 -> 0.61); profiles/r02_ab_ln_store_policy.log.
 constexpr bool kLnFwdNT = true, kLnBwdNT = false;
-#endif
 template <bool NT, int V>
 __device__ __forceinline__ void st_ln(float* p, const float (&o)[V]) {
   if constexpr (NT) stv(p, o); else stc(p, o);
@@ -52,11 +44,8 @@ __device__ __forceinline__ float row_sum(float v) {
 // 4x the blocks (more rows in flight: add_ln_fwd 0.67 -> 0.69, silu fwd
 // 0.67 -> 0.70 of HBM; the same for the backward kernels lost 1-2% to
 // the larger partial sums; tools/ab_bench.sh, profiles/r02_ab_row_blocks.log)
-#ifndef RB_ROW_BLOCKS
-#define RB_ROW_BLOCKS 1024
-#endif
-constexpr int kRowBlocks = RB_ROW_BLOCKS;
-constexpr int kRowBlocksFwd = 4 * RB_ROW_BLOCKS;
+constexpr int kRowBlocks = 1024;
+constexpr int kRowBlocksFwd = 4 * kRowBlocks;
 
 template <int NV, int LPR>
 __global__ void __launch_bounds__(256)
@@ -329,11 +318,7 @@ k_silu_dropout_bwd(const float* __restrict__ a, const float* __restrict__ bias, 
         o[v] = (g[v] * m[v]) * fdsilu(x[v] + bv[k][v]);
         acc[k][v] += o[v];
       }
-#ifdef RB_SILU_BWD_PLAIN
-      stc(da + e, o);
-#else
       stv(da + e, o);
-#endif
     }
   }
   if (dbias_part == nullptr) return;   // grid-uniform

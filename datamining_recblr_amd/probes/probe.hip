@@ -1,5 +1,7 @@
-// probe.hip — measurement aid for bench.py (not on the model's path): the
-// gate-scan backward's memory access pattern with trivial arithmetic.
+// probe.hip — measurement aids for bench.py, built into their own library
+// (lib/libdmrecblr_probe.so, probes/recblr_probe.h), not the product's: the
+// gate-scan backward's memory access pattern with trivial arithmetic, and the
+// projection GEMMs' row streams without the product.
 //
 // k_probe_gate_bwd_pattern reads r, i (rg), xc, z, dy and writes dr, di
 // (drg), dxc, dz exactly as k_gate_scan_bwd<float, 4, 8, 2> does — the same
@@ -9,7 +11,7 @@
 // computes each output as one product.  Its rate is the ceiling the memory
 // system grants that pattern on the box and moment it runs, which bench.py
 // reports beside the kernel's own rate (roofline.pattern).
-#include "common.h"
+#include "../csrc/common.h"
 
 namespace rb {
 namespace {

@@ -83,3 +83,27 @@ def test_f16_item_ce_argument_errors():
     assert rc == _lib.RB_EINVAL and b"d must be" in lib.rb_last_error_string()
     rc = lib.rb_item_ce_probs_h(16, 16, 16, 16, 16, 16, 16, 4, 8, 128, 0, 16, 7, None)
     assert rc == _lib.RB_EINVAL and b"ld < V" in lib.rb_last_error_string()
+
+
+def test_probe_library_is_separate_and_exports_its_header():
+    """bench.py's measurement aids live in their own library
+    (probes/recblr_probe.h, lib/libdmrecblr_probe.so): the product library
+    exports none of them, the probe library exports exactly its header's."""
+    import os
+    hdr = os.path.join(os.path.dirname(_lib.__file__), "probes", "recblr_probe.h")
+    text = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    names = re.findall(r"\b(rb_[a-z0-9_]+)\s*\(", text)
+    assert set(names) == set(_lib.PROBE_SIGNATURES) | {"rb_probe_last_error_string"}
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert not hasattr(raw, n), n
+    probe = _lib.load_probe()
+    for n in names:
+        assert hasattr(probe, n), n
+    # argument errors are reported without touching the GPU
+    try:
+        _lib.call_probe("rb_probe_gemm_pattern", None, 1, 4, None, 4, None)
+    except _lib.RecBLRNativeError as e:
+        assert "null pointer" in str(e)
+    else:
+        raise AssertionError("null pointers accepted")

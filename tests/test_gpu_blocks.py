@@ -582,7 +582,7 @@ def test_gate_bwd_pattern_probe_covers_every_element(cuda):
     dxc = torch.full((ntok + 5, H), float("nan"), device=cuda)
     dxz = torch.full((ntok + 5, 2 * H), float("nan"), device=cuda)
     z, dz = xz[:, H:], dxz[:, H:]
-    _lib.call("rb_probe_gate_bwd_pattern", rg.data_ptr(), 2 * H, xc.data_ptr(), H, z.data_ptr(),
+    _lib.call_probe("rb_probe_gate_bwd_pattern", rg.data_ptr(), 2 * H, xc.data_ptr(), H, z.data_ptr(),
               2 * H, dy.data_ptr(), drg.data_ptr(), 2 * H, dxc.data_ptr(), H, dz.data_ptr(), 2 * H,
               lens.numel(), 37, H, offs.to(cuda).data_ptr(), _stream(xc))
     torch.cuda.synchronize()
@@ -605,7 +605,7 @@ def test_gemm_pattern_probe_covers_every_output(cuda, M, R, C):
     g = torch.Generator().manual_seed(M + R)
     a = torch.randn(M, R, generator=g).to(cuda)
     out = torch.full((M + 3, C), float("nan"), device=cuda)
-    _lib.call("rb_probe_gemm_pattern", a.data_ptr(), M, R, out.data_ptr(), C, _stream(a))
+    _lib.call_probe("rb_probe_gemm_pattern", a.data_ptr(), M, R, out.data_ptr(), C, _stream(a))
     torch.cuda.synchronize()
     ref = a.double().sum(1, keepdim=True) + (torch.arange(C, device=cuda) % 4).double()[None]
     assert torch.allclose(out[:M].double(), ref, atol=1e-3, rtol=1e-5)

@@ -10,6 +10,6 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     -- python3 bench.py --no-cpu-baseline --no-full-tail --no-c5 --no-ddp-ab > gpurun_out/r04_v0_prof.log 2>&1
 rc=$?
 cp gpurun_out/prof/bench_kernel_stats.csv gpurun_out/r04_v0_kernel_stats.csv 2>/dev/null
-cp gpurun_out/prof/bench_kernel_trace.csv gpurun_out/r04_v0_kernel_trace.csv 2>/dev/null
+python tools/step_sequence.py gpurun_out/prof/bench_kernel_trace.csv 10 > gpurun_out/r04_v0_step_sequence.txt 2>&1
 rm -rf gpurun_out/prof
 exit $rc
