@@ -675,9 +675,9 @@ def main():
     torch.manual_seed(2020)  # the reference run's seed (LOG51:6); same on every rank
     model = RecBLR(make_cfg(args), SyntheticDataset(args.n_items)).to(dev).train()
     step_mod = wrap_ddp(model, env)
-    # the optimizer update: torch's fused Adam, or RECBLR_ADAM=native:
-    # rb_adam_step over every parameter in one launch (datamining_recblr_amd.
-    # optim.Adam; default once measured on the GPU)
+    # the optimizer update: rb_adam_step over every parameter in one launch
+    # (datamining_recblr_amd.optim.Adam; 6.112 vs 6.179 ms per step against
+    # torch's fused Adam, profiles/r04_v0_bench.log), or RECBLR_ADAM=torch
     from datamining_recblr_amd.optim import Adam as NativeAdam
 
     def make_opt(kind):
@@ -685,7 +685,7 @@ def main():
             return NativeAdam(model.parameters(), lr=1e-3)
         return torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
 
-    adam_kind = os.environ.get("RECBLR_ADAM", "torch")
+    adam_kind = os.environ.get("RECBLR_ADAM", "native")
     opt = make_opt(adam_kind)
     batches = [synthetic_interaction(args.batch, args.seq_len, args.n_items, dev,
                                      seed=1000 * env.rank + i) for i in range(4)]
@@ -799,8 +799,8 @@ def main():
         optimizer = {"ms_per_step": round(sum(a.elapsed_time(b) for a, b in opt_events)
                                           / len(opt_events), 4),
                      "impl": type(opt).__module__ + "." + type(opt).__name__,
-                     "note": "Adam over all parameters (torch.optim.Adam(fused=True); "
-                             "RECBLR_ADAM=native: rb_adam_step, one launch); inside every timed "
+                     "note": "Adam over all parameters (rb_adam_step, one launch; "
+                             "RECBLR_ADAM=torch: torch.optim.Adam(fused=True)); inside every timed "
                              "step, timed on its own in the breakdown pass"}
     ms = 1000.0 * elapsed / args.steps
     value = env.world_size * args.batch * args.steps / elapsed

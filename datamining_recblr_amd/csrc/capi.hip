@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 33; }
+int rb_version(void) { return 34; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -591,6 +591,22 @@ int rb_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int6
     return fail("rb_colsum: bad shape or strides");
   if (M * ((C + 63) / 64) > 0x7fffffffLL) return fail("rb_colsum: grid too large");
   return launch_colsum(in, M, P, C, rs, ms, out, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs,
+                      int64_t chunk_rows, float* part, uint32_t* counters, int64_t n_counters,
+                      float* out, void* stream) {
+  if (!in || !out || !part || !counters) return fail("rb_colsum_chunked: null pointer");
+  if (M <= 0 || P <= 0 || C <= 0 || rs < C || chunk_rows <= 0 || chunk_rows > 256 ||
+      P % chunk_rows)
+    return fail("rb_colsum_chunked: bad shape, stride or chunk size");
+  const int64_t cblocks = (C + 63) / 64;
+  if (n_counters < M * cblocks) return fail("rb_colsum_chunked: too few counters");
+  if (M * cblocks * (P / chunk_rows) > 0x7fffffffLL || M * P * rs >= ((int64_t)1 << 40))
+    return fail("rb_colsum_chunked: grid too large");
+  return launch_colsum_chunked(in, M, P, C, rs, (int)chunk_rows, part,
+                               reinterpret_cast<unsigned*>(counters), out,
+                               reinterpret_cast<hipStream_t>(stream));
 }
 
 int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R) { return C * R * 6; }

@@ -423,6 +423,8 @@ int launch_pad_prefix_bwd(const float* conv_b, const float* gw, const float* gb,
                           float* dlam, float* ws, int accumulate, hipStream_t st);
 int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
                   float* out, hipStream_t st);
+int launch_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int CH,
+                          float* part, unsigned* cnt, float* out, hipStream_t st);
 int launch_scan_fwd(const float* gates, const float* tokens, float* states, int64_t rows,
                     int64_t T, hipStream_t st);
 int launch_scan_bwd(const float* gates, const float* states, const float* grad, float* d_gates,

@@ -253,19 +253,20 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int lane) {
 // w_1 bias gradient's partials).  Rows of a tile flagged for the cold
 // recompute tail are summed there instead, from their recomputed values.
 constexpr int N_DACT_MAXC = 512;   // LDS column sums: 8 waves x C floats
+// The NT GEMM over the tiles of one launch phase: workgroup `bid` of `G`
+// takes tiles bid, bid + G, ...  (k_gemm_nt_h: one phase; k_gemm_nt_h2: the
+// whole rounds of 256 x 128 / 256 x 256 tiles, then the rows past them as
+// 256 x 64 tiles, in one launch).
 template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>
-__global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restrict__ A, int64_t lda,
-                                                          int64_t M, int R,
-                                                          const f16x8* __restrict__ Wf,
-                                                          const int* __restrict__ ew, int C,
-                                                          const float* __restrict__ bias,
-                                                          float* __restrict__ out, int64_t ldo,
-                                                          float* __restrict__ rmax, int m_tiles,
-                                                          float* __restrict__ act, DropSpec drop,
-                                                          int64_t e_base,
-                                                          const float* __restrict__ pre,
-                                                          float* __restrict__ dpart) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G,
+                                          const float* __restrict__ A, int64_t lda, int64_t M,
+                                          int R, const f16x8* __restrict__ Wf,
+                                          const int* __restrict__ ew, int C,
+                                          const float* __restrict__ bias, float* __restrict__ out,
+                                          int64_t ldo, float* __restrict__ rmax, int m_tiles,
+                                          float* __restrict__ act, DropSpec drop, int64_t e_base,
+                                          const float* __restrict__ pre,
+                                          float* __restrict__ dpart) {
   using CF = NtCfg<NB>;
   constexpr int N_BN = CF::BN, N_NB = NB, N_BDMA = CF::BDMA, N_NSA = CF::NSA, N_LA = N_NSA - 1;
   constexpr int N_B_STAGE = CF::B_STAGE, N_RING = CF::RING;
@@ -284,12 +285,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
   const int KT = R / N_BK;
   const int KB16 = R / 16;
   const int n_tiles = ((m_tiles + 7) >> 3) * 8 * nct;
-  const int G = gridDim.x;
-  const int my_tiles = (int)blockIdx.x < n_tiles ? (n_tiles - 1 - (int)blockIdx.x) / G + 1 : 0;
+  const int my_tiles = bid < n_tiles ? (n_tiles - 1 - bid) / G + 1 : 0;
   const int U = my_tiles * KT;  // k-steps of this workgroup
   if (U == 0) {
     if (DACT)
-      for (int c = tid; c < C; c += N_THREADS) dpart[(int64_t)blockIdx.x * C + c] = 0.0f;
+      for (int c = tid; c < C; c += N_THREADS) dpart[(int64_t)bid * C + c] = 0.0f;
     return;
   }
 
@@ -306,11 +306,11 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
     for (int c = lane; c < C; c += 64) s_col[c] = 0.0f;
   __syncthreads();
 
-  // tile T = blockIdx.x + i*G: the column tiles of one row tile are
+  // tile T = bid + i*G: the column tiles of one row tile are
   // neighbouring workgroups of one XCD (same blockIdx % 8), so their A
   // re-reads hit that XCD's L2.  (Divisions: once per tile and stream.)
   auto tile_of = [&](int i, int& mt, int& ct) {
-    const int T = blockIdx.x + i * G;
+    const int T = bid + i * G;
     const int g = T >> 3;
     ct = g % nct;
     mt = (g / nct) * 8 + (T & 7);
@@ -847,11 +847,67 @@ __global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restr
       float t = s_all[c];
 #pragma unroll
       for (int w = 1; w < N_WAVES; ++w) t += s_all[w * N_DACT_MAXC + c];
-      dpart[(int64_t)blockIdx.x * C + c] = t;
+      dpart[(int64_t)bid * C + c] = t;
     }
   }
 }
 
+template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>
+__global__ void __launch_bounds__(N_THREADS, 1) k_gemm_nt_h(const float* __restrict__ A, int64_t lda,
+                                                          int64_t M, int R,
+                                                          const f16x8* __restrict__ Wf,
+                                                          const int* __restrict__ ew, int C,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ out, int64_t ldo,
+                                                          float* __restrict__ rmax, int m_tiles,
+                                                          float* __restrict__ act, DropSpec drop,
+                                                          int64_t e_base,
+                                                          const float* __restrict__ pre,
+                                                          float* __restrict__ dpart) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  nt_h_body<BIAS, WIDE, NB, ACT, DACT>(smem, (int)blockIdx.x, (int)gridDim.x, A, lda, M, R, Wf, ew,
+                                       C, bias, out, ldo, rmax, m_tiles, act, drop, e_base, pre,
+                                       dpart);
+}
+
+// One phase's operands (the rows [r0, r0 + M) of a call).
+struct NtPhase {
+  const float* A;
+  int64_t M;
+  float* out;
+  float* rmax;
+  float* act;
+  const float* pre;
+  float* dpart;
+  int64_t e_base;
+  int m_tiles;
+  int grid;
+};
+
+// Both phases of a call in one launch: the whole rounds on NB-column tiles,
+// then the rows past them on 256 x 64 tiles (2-4x as many tiles, so the
+// partial round fills the chip).  A workgroup starts its tail tiles as soon
+// as its own main tiles are done; the LDS is reused after a barrier (every
+// DMA of the main phase has landed: each step waits for its own operands).
+template <bool BIAS, int NB, bool ACT = false, bool DACT = false>
+__global__ void __launch_bounds__(N_THREADS, 1)
+k_gemm_nt_h2(int64_t lda, int R, const f16x8* __restrict__ Wf, const int* __restrict__ ew, int C,
+             const float* __restrict__ bias, int64_t ldo, DropSpec drop, NtPhase main_ph,
+             NtPhase tail_ph) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int bid = (int)blockIdx.x;
+  if (bid < main_ph.grid)
+    nt_h_body<BIAS, true, NB, ACT, DACT>(smem, bid, main_ph.grid, main_ph.A, lda, main_ph.M, R, Wf,
+                                         ew, C, bias, main_ph.out, ldo, main_ph.rmax,
+                                         main_ph.m_tiles, main_ph.act, drop, main_ph.e_base,
+                                         main_ph.pre, main_ph.dpart);
+  __syncthreads();
+  if (bid < tail_ph.grid)
+    nt_h_body<BIAS, true, 2, ACT, DACT>(smem, bid, tail_ph.grid, tail_ph.A, lda, tail_ph.M, R, Wf,
+                                        ew, C, bias, tail_ph.out, ldo, tail_ph.rmax,
+                                        tail_ph.m_tiles, tail_ph.act, drop, tail_ph.e_base,
+                                        tail_ph.pre, tail_ph.dpart);
+}
 
 // ---------------------------------------------------------------------------
 // k_gemm_tn_h (weight gradient, split over rows):
@@ -1086,6 +1142,43 @@ void run_nt_h(const float* A, int64_t lda, int64_t M, int R, const f16x8* wf, co
       A, lda, M, R, wf, ew, C, bias, out, ldo, rmax, m_tiles, act, drop, e_base, pre, dpart);
 }
 
+
+// One phase of a call: the rows [r0, r0 + M) on tiles nbcols columns wide.
+NtPhase nt_phase(const float* A, int64_t lda, int64_t r0, int64_t M, float* out, int64_t ldo,
+                 float* rmax, int C, int nbcols, int G0, float* act = nullptr,
+                 const float* pre = nullptr, float* dpart = nullptr) {
+  NtPhase p{};
+  p.A = A + r0 * lda;
+  p.M = M;
+  p.out = out + r0 * ldo;
+  p.rmax = rmax ? rmax + r0 / 32 : nullptr;
+  p.act = act ? act + r0 * ldo : nullptr;
+  p.pre = pre ? pre + r0 * ldo : nullptr;
+  p.dpart = dpart;
+  p.e_base = r0 * C;
+  p.m_tiles = (int)((M + N_BM - 1) / N_BM);
+  const int64_t nt = (int64_t)((p.m_tiles + 7) / 8) * 8 * (C / nbcols);
+  p.grid = M > 0 ? (int)std::min<int64_t>(nt, (int64_t)G0) : 0;
+  return p;
+}
+
+template <bool BIAS, int NB, bool ACT = false, bool DACT = false>
+void run_nt_h2(int64_t lda, int R, const f16x8* wf, const int* ew, int C, const float* bias,
+               int64_t ldo, DropSpec drop, const NtPhase& mp, const NtPhase& tp, hipStream_t st) {
+  constexpr int base = NtCfg<NB>::LDS > NtCfg<2>::LDS ? NtCfg<NB>::LDS : NtCfg<2>::LDS;
+  constexpr int lds = base + (DACT ? N_WAVES * N_DACT_MAXC * 4 : 0);
+  static_assert(lds <= 160 * 1024, "LDS");
+  static bool done = false;  // benign race: idempotent
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt_h2<BIAS, NB, ACT, DACT>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    done = true;
+  }
+  const unsigned grid = (unsigned)std::max(mp.grid, tp.grid);
+  k_gemm_nt_h2<BIAS, NB, ACT, DACT><<<grid, N_THREADS, lds, st>>>(lda, R, wf, ew, C, bias, ldo,
+                                                                  drop, mp, tp);
+}
+
 }  // namespace
 
 int launch_split_weights_h(const rb_split_job* jobs, int n, hipStream_t st) {
@@ -1138,6 +1231,20 @@ int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* 
     // (a few thousand rows with K = 512, or C = 128; tools/gemmbench_h.hip,
     // profiles/r03_gemmbench_small_m.log) — at 8,192 rows it is 2.7x slower
     const bool few = M_main == 0 && M <= 4096 && (R > 256 || C < 256);
+    if (!few && wide && C % 64 == 0 && M_main > 0) {
+      // both phases in one launch (k_gemm_nt_h2)
+      const int G0w = num_cus() / 8 * 8 * (8 / N_WAVES);
+      const NtPhase mp = nt_phase(A, lda, 0, M_main, out, ldo, rmax, C, nb8 ? 256 : 128, G0w);
+      const NtPhase tp = nt_phase(A, lda, M_main, M - M_main, out, ldo, rmax, C, 64, G0w);
+      if (bias) {
+        if (nb8) run_nt_h2<true, 8>(lda, R, wf, ew, C, bias, ldo, DropSpec{}, mp, tp, st);
+        else run_nt_h2<true, 4>(lda, R, wf, ew, C, bias, ldo, DropSpec{}, mp, tp, st);
+      } else {
+        if (nb8) run_nt_h2<false, 8>(lda, R, wf, ew, C, bias, ldo, DropSpec{}, mp, tp, st);
+        else run_nt_h2<false, 4>(lda, R, wf, ew, C, bias, ldo, DropSpec{}, mp, tp, st);
+      }
+      return launch_status("rb_gemm_nt_h");
+    }
     if (!few && wide && C % 64 == 0) {
       const int64_t Mt = M - M_main;
       const int mt_t = (int)((Mt + N_BM - 1) / N_BM);
@@ -1203,6 +1310,13 @@ int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const vo
   const int64_t M_main = (G0 % nct0 == 0 && rows_round > 0) ? M / rows_round * rows_round : M;
   const f16x8* wf = (const f16x8*)Wf;
   const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * R * 4);
+  if (M_main > 0 && M_main < M) {   // both phases in one launch (k_gemm_nt_h2)
+    const NtPhase mp = nt_phase(A, lda, 0, M_main, out, ldo, rmax, C, 32 * ACT_NB, G0, act);
+    const NtPhase tp = nt_phase(A, lda, M_main, M - M_main, out, ldo, rmax, C, 64, G0, act);
+    if (bias) run_nt_h2<true, ACT_NB, true>(lda, R, wf, ew, C, bias, ldo, drop, mp, tp, st);
+    else run_nt_h2<false, ACT_NB, true>(lda, R, wf, ew, C, bias, ldo, drop, mp, tp, st);
+    return launch_status("rb_gemm_nt_h_act");
+  }
   if (M_main < M) {   // the rows past the last whole round: 256 x 64 tiles
     const int64_t Mt = M - M_main;
     const int mt_t = (int)((Mt + N_BM - 1) / N_BM);
@@ -1256,7 +1370,15 @@ int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const v
   const int64_t nt_t = (int64_t)((mt_t + 7) / 8) * 8 * (C / 64);
   const unsigned grid_t = Mt > 0 ? (unsigned)std::min<int64_t>(nt_t, (int64_t)G0) : 0u;
   if ((int64_t)grid + grid_t > n_parts) return fail("rb_gemm_nt_h_dact: dpart has too few rows");
-  if (Mt > 0) {   // the rows past the last whole round: 256 x 64 tiles
+  if (Mt > 0 && M_main > 0) {   // both phases in one launch (k_gemm_nt_h2)
+    const NtPhase mp = nt_phase(A, lda, 0, M_main, out, ldo, rmax, C, 32 * DACT_NB, G0, nullptr,
+                                pre, dpart);
+    const NtPhase tp = nt_phase(A, lda, M_main, Mt, out, ldo, rmax, C, 64, G0, nullptr, pre,
+                                dpart + (int64_t)grid * C);
+    run_nt_h2<false, DACT_NB, false, true>(lda, R, wf, ew, C, nullptr, ldo, drop, mp, tp, st);
+    const int rc = launch_status("rb_gemm_nt_h_dact");
+    if (rc) return rc;
+  } else if (Mt > 0) {   // the rows past the last whole round: 256 x 64 tiles
     run_nt_h<false, true, 2, false, true>(A + M_main * lda, lda, Mt, R, wf, ew, C, nullptr,
                                           out + M_main * ldo, ldo, rmax ? rmax + M_main / 32 : nullptr,
                                           mt_t, grid_t, st, nullptr, drop, M_main * C,
@@ -1264,7 +1386,7 @@ int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const v
     const int rc = launch_status("rb_gemm_nt_h_dact");
     if (rc) return rc;
   }
-  if (M_main > 0) {
+  if (M_main > 0 && Mt == 0) {
     run_nt_h<false, true, DACT_NB, false, true>(A, lda, M_main, R, wf, ew, C, nullptr, out, ldo, rmax,
                                           m_tiles, grid, st, nullptr, drop, 0, pre, dpart);
     const int rc = launch_status("rb_gemm_nt_h_dact");

@@ -933,6 +933,12 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
 #pragma unroll
     for (int sh = 32; sh >= 1; sh >>= 1) mb = fmaxf(mb, __shfl_xor(mb, sh));
     if (lane == 0 && b0 < B) atomicMax(reinterpret_cast<int*>(bmax) + b0 / kTile, __float_as_int(mb));
+    // out2's padding columns [V, ld2) of the wave's rows: zeros (the first
+    // item split's workgroups; no separate fill launch)
+    if (pl.split == 0 && ld2 > V) {
+      for (int r = 0; r < kTile && b0 + r < B; ++r)
+        for (int64_t v = V + lane; v < ld2; v += 64) out2[(b0 + r) * ld2 + v] = 0.0f;
+    }
   }
 }
 

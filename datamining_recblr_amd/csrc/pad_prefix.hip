@@ -1,6 +1,6 @@
 // pad_prefix.hip — the recurrent state the reference's power-of-two left
-// padding leaves behind (RecBLR.py:176-179), forward (2 small launches) and
-// backward (4).
+// padding leaves behind (RecBLR.py:176-179), forward (1 small launch) and
+// backward (2).
 //
 // Pad positions carry zeros into the causal conv, so every pad step sees the
 // per-channel constants xc_p = silu(conv.bias), (r_p, i_p) = W_g xc_p + b_g,
@@ -36,13 +36,12 @@ __device__ __forceinline__ float expm1_ratio_ds(float P, float s) {
   return (-P * expf(-P * s) * d + expm1f(-P * s) * expf(-s)) / (d * d);
 }
 
-// per-channel constants from the gate pre-activations rg
-__device__ __forceinline__ PadConsts consts(int c, int H, float xc, const float* rg,
-                                            const float* lam) {
+// per-channel constants from the gate pre-activations (r, i) of channel c
+__device__ __forceinline__ PadConsts consts(int c, float r, float i, float xc, const float* lam) {
   PadConsts k;
   k.xc = xc;
-  k.sg_r = sigm(rg[c]);
-  k.sg_i = sigm(rg[H + c]);
+  k.sg_r = sigm(r);
+  k.sg_i = sigm(i);
   k.sp = softplus_f(lam[c]);
   const float s = k.sp * k.sg_r;
   k.clamped = !(s > 1e-20f);
@@ -54,86 +53,95 @@ __device__ __forceinline__ PadConsts consts(int c, int H, float xc, const float*
   return k;
 }
 
-// rg = W_g silu(conv_b) + b_g: one wave per output row, lanes along the row
-// (coalesced), fixed-order butterfly; many workgroups so the 2H row reads
-// are in flight together (a single workgroup is load-latency bound).
-__global__ __launch_bounds__(256) void k_pad_gates(const float* __restrict__ conv_b,
-                                                   const float* __restrict__ gw,
-                                                   const float* __restrict__ gb, int H,
-                                                   float* __restrict__ rg) {
-  const int lane = threadIdx.x & 63;
-  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (o >= 2 * H) return;
+// the gate pre-activation of row o: W_g[o] . silu(conv_b) + b_g[o], lanes
+// along the row (coalesced), fixed-order butterfly; lane 0's sum (the
+// butterfly's association differs per lane)
+__device__ __forceinline__ float pad_gate(const float* __restrict__ conv_b,
+                                          const float* __restrict__ gw,
+                                          const float* __restrict__ gb, int H, int o, int lane) {
   const float* w = gw + (int64_t)o * H;
   float acc = 0.0f;
   for (int k = lane; k < H; k += 64) acc = fmaf(w[k], silu_f(conv_b[k]), acc);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-  if (lane == 0) rg[o] = acc + gb[o];
+  return __shfl(acc, 0) + gb[o];
 }
 
+// forward: one wave per channel c — its two gate pre-activations (rows c and
+// H + c of W_g; many workgroups, so the 2H row reads are in flight together:
+// a single workgroup is load-latency bound), the constants, then h0 of every
+// row (lanes over rows)
 __global__ __launch_bounds__(256) void k_pad_prefix_fwd(const float* __restrict__ conv_b,
-                                                        const float* __restrict__ rg,
+                                                        const float* __restrict__ gw,
+                                                        const float* __restrict__ gb,
                                                         const float* __restrict__ lam,
                                                         const int64_t* __restrict__ pad,
                                                         int64_t pad_len, int64_t n_rows, int H,
                                                         float* __restrict__ h0) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= H) return;
-  const float xc = silu_f(conv_b[c]);
-  const PadConsts k = consts(c, H, xc, rg, lam);
-  for (int64_t r = blockIdx.y; r < n_rows; r += gridDim.y) {
-    const float P = (float)(pad ? pad[r] : pad_len);
-    h0[r * H + c] = k.b * expm1_ratio(P, k.s);
+  const float r = pad_gate(conv_b, gw, gb, H, c, lane);
+  const float i = pad_gate(conv_b, gw, gb, H, H + c, lane);
+  const PadConsts k = consts(c, r, i, silu_f(conv_b[c]), lam);
+  for (int64_t row = lane; row < n_rows; row += 64) {
+    const float P = (float)(pad ? pad[row] : pad_len);
+    h0[row * H + c] = k.b * expm1_ratio(P, k.s);
   }
 }
 
-// per-channel part of the backward: drg [2H], dlam, dgate_b, and the part of
-// d xc_p that flows through b_p (dxb)
+// backward, per channel (one wave each): its gate pre-activations again, the
+// per-row gradient sums in row order (lane 0), drg [2H] / dxb (the part of d
+// xc_p that flows through b_p) for k_pad_prefix_bwd3, dlam, dgate_b, and the
+// channel's two rows of dW_g = drg (x) xc_p (lanes along the row: coalesced)
 __global__ __launch_bounds__(256) void k_pad_prefix_bwd1(
-    const float* __restrict__ conv_b, const float* __restrict__ rg, const float* __restrict__ lam,
-    const int64_t* __restrict__ pad, int64_t pad_len, int64_t n_rows, int H,
-    const float* __restrict__ dh0, float* __restrict__ drg, float* __restrict__ dxb,
-    float* __restrict__ dgb, float* __restrict__ dlam, int acc) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
+    const float* __restrict__ conv_b, const float* __restrict__ gw, const float* __restrict__ gb,
+    const float* __restrict__ lam, const int64_t* __restrict__ pad, int64_t pad_len,
+    int64_t n_rows, int H, const float* __restrict__ dh0, float* __restrict__ drg,
+    float* __restrict__ dxb, float* __restrict__ dgb, float* __restrict__ dlam,
+    float* __restrict__ dgw, int acc) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= H) return;
   const float xc = silu_f(conv_b[c]);
-  const PadConsts k = consts(c, H, xc, rg, lam);
-  float gb_ = 0.0f, gs = 0.0f;   // dL/db_p, dL/ds, rows in order
-  for (int64_t r = 0; r < n_rows; ++r) {
-    const float P = (float)(pad ? pad[r] : pad_len);
-    const float g = dh0[r * H + c];
-    gb_ = fmaf(g, expm1_ratio(P, k.s), gb_);
-    gs = fmaf(g * k.b, expm1_ratio_ds(P, k.s), gs);
+  const float r = pad_gate(conv_b, gw, gb, H, c, lane);
+  const float i = pad_gate(conv_b, gw, gb, H, H + c, lane);
+  const PadConsts k = consts(c, r, i, xc, lam);
+  float dr = 0.0f, di = 0.0f;
+  if (lane == 0) {
+    float gb_ = 0.0f, gs = 0.0f;   // dL/db_p, dL/ds, rows in order
+    for (int64_t row = 0; row < n_rows; ++row) {
+      const float P = (float)(pad ? pad[row] : pad_len);
+      const float g = dh0[row * H + c];
+      gb_ = fmaf(g, expm1_ratio(P, k.s), gb_);
+      gs = fmaf(g * k.b, expm1_ratio_ds(P, k.s), gs);
+    }
+    if (k.clamped) gs = 0.0f;                        // clamp_min(1e-20) passes no gradient
+    // b = beta xc; beta = q sg_i; q = sqrt(1 - alpha^2 + 1e-8); alpha = exp(-s_raw)
+    const float dbeta = gb_ * k.xc;
+    dxb[c] = gb_ * k.beta;
+    const float dq = dbeta * k.sg_i;
+    const float dsg_i = dbeta * k.q;
+    const float dalpha = dq * (-k.alpha / k.q);
+    const float ds = gs + dalpha * (-k.alpha);
+    const float dl = ds * k.sg_r * dsoftplus_f(lam[c]);   // s = softplus(lam) sg_r
+    dlam[c] = acc ? dlam[c] + dl : dl;
+    dr = ds * k.sp * k.sg_r * (1.0f - k.sg_r);
+    di = dsg_i * k.sg_i * (1.0f - k.sg_i);
+    drg[c] = dr;
+    drg[H + c] = di;
+    dgb[c] = acc ? dgb[c] + dr : dr;
+    dgb[H + c] = acc ? dgb[H + c] + di : di;
   }
-  if (k.clamped) gs = 0.0f;                        // clamp_min(1e-20) passes no gradient
-  // b = beta xc; beta = q sg_i; q = sqrt(1 - alpha^2 + 1e-8); alpha = exp(-s_raw)
-  const float dbeta = gb_ * k.xc;
-  dxb[c] = gb_ * k.beta;
-  const float dq = dbeta * k.sg_i;
-  const float dsg_i = dbeta * k.q;
-  const float dalpha = dq * (-k.alpha / k.q);
-  const float ds = gs + dalpha * (-k.alpha);
-  const float dl = ds * k.sg_r * dsoftplus_f(lam[c]);   // s = softplus(lam) sg_r
-  dlam[c] = acc ? dlam[c] + dl : dl;
-  const float dr = ds * k.sp * k.sg_r * (1.0f - k.sg_r);
-  const float di = dsg_i * k.sg_i * (1.0f - k.sg_i);
-  drg[c] = dr;
-  drg[H + c] = di;
-  dgb[c] = acc ? dgb[c] + dr : dr;
-  dgb[H + c] = acc ? dgb[H + c] + di : di;
-}
-
-// dW_g = drg (x) xc_p, grid-stride over the [2H, H] rows (coalesced)
-__global__ __launch_bounds__(256) void k_pad_prefix_bwd2(const float* __restrict__ conv_b, int H,
-                                                         const float* __restrict__ drg,
-                                                         float* __restrict__ dgw, int acc) {
-  const int64_t n = 2 * (int64_t)H * H;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n;
-       e += (int64_t)gridDim.x * 256) {
-    const int64_t o = e / H, c = e - o * H;
-    const float v = drg[o] * silu_f(conv_b[c]);
-    dgw[e] = acc ? dgw[e] + v : v;
+  dr = __shfl(dr, 0);
+  di = __shfl(di, 0);
+  float* wr = dgw + (int64_t)c * H;
+  float* wi = dgw + (int64_t)(H + c) * H;
+  for (int kk = lane; kk < H; kk += 64) {
+    const float x = silu_f(conv_b[kk]);
+    const float vr = dr * x, vi = di * x;
+    wr[kk] = acc ? wr[kk] + vr : vr;
+    wi[kk] = acc ? wi[kk] + vi : vi;
   }
 }
 
@@ -166,12 +174,9 @@ __global__ __launch_bounds__(1024) void k_pad_prefix_bwd3(const float* __restric
 int launch_pad_prefix_fwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                           int64_t H, float* h0, float* ws, hipStream_t st) {
-  float* rg = ws;
-  hipLaunchKernelGGL(k_pad_gates, dim3((unsigned)((2 * H + 3) / 4)), dim3(256), 0, st, conv_b, gw,
-                     gb, (int)H, rg);
-  const unsigned ry = (unsigned)std::min<int64_t>(n_rows, 1024);
-  hipLaunchKernelGGL(k_pad_prefix_fwd, dim3((unsigned)((H + 255) / 256), ry), dim3(256), 0, st,
-                     conv_b, rg, lam, pad, pad_len, n_rows, (int)H, h0);
+  (void)ws;
+  hipLaunchKernelGGL(k_pad_prefix_fwd, dim3((unsigned)((H + 3) / 4)), dim3(256), 0, st, conv_b, gw,
+                     gb, lam, pad, pad_len, n_rows, (int)H, h0);
   return launch_status("rb_pad_prefix_fwd");
 }
 
@@ -179,16 +184,10 @@ int launch_pad_prefix_bwd(const float* conv_b, const float* gw, const float* gb,
                           const float* lam, const int64_t* pad, int64_t pad_len, int64_t n_rows,
                           int64_t H, const float* dh0, float* dconv_b, float* dgw, float* dgb,
                           float* dlam, float* ws, int accumulate, hipStream_t st) {
-  float* rg = ws;
   float* drg = ws + 2 * H;
   float* dxb = ws + 4 * H;
-  hipLaunchKernelGGL(k_pad_gates, dim3((unsigned)((2 * H + 3) / 4)), dim3(256), 0, st, conv_b, gw,
-                     gb, (int)H, rg);
-  hipLaunchKernelGGL(k_pad_prefix_bwd1, dim3((unsigned)((H + 255) / 256)), dim3(256), 0, st,
-                     conv_b, rg, lam, pad, pad_len, n_rows, (int)H, dh0, drg, dxb, dgb, dlam,
-                     accumulate);
-  const unsigned nb = (unsigned)std::min<int64_t>(1024, (2 * H * H + 255) / 256);
-  hipLaunchKernelGGL(k_pad_prefix_bwd2, dim3(nb), dim3(256), 0, st, conv_b, (int)H, drg, dgw,
+  hipLaunchKernelGGL(k_pad_prefix_bwd1, dim3((unsigned)((H + 3) / 4)), dim3(256), 0, st, conv_b,
+                     gw, gb, lam, pad, pad_len, n_rows, (int)H, dh0, drg, dxb, dgb, dlam, dgw,
                      accumulate);
   hipLaunchKernelGGL(k_pad_prefix_bwd3, dim3((unsigned)((H + 63) / 64)), dim3(1024), 0, st, conv_b,
                      gw, (int)H, drg, dxb, dconv_b, accumulate);

@@ -79,6 +79,89 @@ __global__ __launch_bounds__(64 * RG) void k_colsum4(const float* __restrict__ i
   }
 }
 
+// The two-level sum of rb_colsum_chunked in ONE launch: workgroup (m, column
+// block, chunk) sums the chunk's CH rows in k_colsum<RG>'s order and stores
+// the chunk sum to part[m][chunk]; the last of a column block's nch
+// workgroups to arrive (an agent-scope ticket) sums the chunk sums in the
+// same order, so the result is bitwise that of two k_colsum<RG> launches
+// (chunks, then the chunk sums).  Hand-off: plain stores, every storing wave
+// drains, the workgroup barrier, one agent-scope release before the ticket;
+// the last arriver acquires before reading (cdna_hip_programming.md §6
+// Guideline 16, the counter form) and resets its ticket for the next call
+// (the tickets are zeroed once when the caller allocates them).
+template <int RG>
+__global__ __launch_bounds__(64 * RG) void k_colsum_2l(const float* __restrict__ in, int64_t C,
+                                                       int64_t rs, int64_t cblocks, int nch,
+                                                       int CH, float* __restrict__ part,
+                                                       unsigned* __restrict__ cnt,
+                                                       float* __restrict__ out) {
+  __shared__ float red[RG][64];
+  __shared__ int s_last;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t b = blockIdx.x;
+  const int ch = (int)(b % nch);
+  const int64_t mc = b / nch;
+  const int64_t m = mc / cblocks;
+  const int64_t c = (mc - m * cblocks) * 64 + tx;
+  {
+    const float* base = in + ((m * nch + ch) * (int64_t)CH) * rs + c;
+    float s = 0.0f;
+    if (c < C) {
+      int p = ty;
+      for (; p + 3 * RG < CH; p += 4 * RG) {
+        const float a = base[p * rs], q = base[(p + RG) * rs];
+        const float d = base[(p + 2 * RG) * rs], e = base[(p + 3 * RG) * rs];
+        s = (((s + a) + q) + d) + e;
+      }
+      for (; p < CH; p += RG) s += base[p * rs];
+    }
+    red[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && c < C) {
+      float t = red[0][tx];
+#pragma unroll
+      for (int g = 1; g < RG; ++g) t += red[g][tx];
+      part[(m * nch + ch) * C + c] = t;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the fence's own wait may be dropped
+    const unsigned old = __hip_atomic_fetch_add(&cnt[mc], 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (unsigned)(nch - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(&cnt[mc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;   // workgroup-uniform
+  const float* base = part + m * nch * C + c;
+  float s = 0.0f;
+  if (c < C) {
+    int p = ty;
+    for (; p + 3 * RG < nch; p += 4 * RG) {
+      const float a = base[(int64_t)p * C], q = base[(int64_t)(p + RG) * C];
+      const float d = base[(int64_t)(p + 2 * RG) * C], e = base[(int64_t)(p + 3 * RG) * C];
+      s = (((s + a) + q) + d) + e;
+    }
+    for (; p < nch; p += RG) s += base[(int64_t)p * C];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < C) {
+    float t = red[0][tx];
+#pragma unroll
+    for (int g = 1; g < RG; ++g) t += red[g][tx];
+    out[m * C + c] = t;
+  }
+}
+
 // out[g] = max |x[r][c]| over the rows r of 32-row group g (a partial last
 // group too) and all c < C: the row-group maxima rb_gemm_tn_h takes as operand
 // scales, for tensors no f16 GEMM has read.  One 256-thread workgroup per
@@ -154,6 +237,15 @@ int launch_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, 
     hipLaunchKernelGGL(k_colsum<16>, dim3(grid), dim3(1024), 0, st, in, P, C, rs, ms, cblocks,
                        out);
   return launch_status("rb_colsum");
+}
+
+int launch_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int CH,
+                          float* part, unsigned* cnt, float* out, hipStream_t st) {
+  const int64_t cblocks = (C + 63) / 64;
+  const int nch = (int)(P / CH);
+  hipLaunchKernelGGL(k_colsum_2l<4>, dim3((unsigned)(M * cblocks * nch)), dim3(256), 0, st, in, C,
+                     rs, cblocks, nch, CH, part, cnt, out);
+  return launch_status("rb_colsum_chunked");
 }
 
 }  // namespace rb

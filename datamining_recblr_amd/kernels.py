@@ -95,6 +95,20 @@ def _launch(name: str, nbytes: int, *args, _fn: str | None = None, _flops: bool 
     t.records.append((name, nbytes, e0, e1))
 
 
+_tickets = {}
+
+
+def _colsum_tickets(x: torch.Tensor, n: int) -> torch.Tensor:
+    """rb_colsum_chunked's ticket counters for torch's current stream on x's
+    device: zeroed once here, left zero by every call (calls on one stream
+    are ordered; another stream gets its own)."""
+    key = (x.device, _stream(x))
+    t = _tickets.get(key)
+    if t is None or t.numel() < n:
+        t = _tickets[key] = torch.zeros(max(n, 1024), device=x.device, dtype=torch.int32)
+    return t
+
+
 def colsum(x: torch.Tensor) -> torch.Tensor:
     """Fixed-order sum over dim -2 of a [P, C] or [M, P, C] tensor whose last
     dim is unit-stride (rb_colsum; replaces torch's sum(-2), which needs a
@@ -117,12 +131,13 @@ def colsum(x: torch.Tensor) -> torch.Tensor:
     # fixed-order passes, still deterministic.
     CH = 64
     if M * ((C + 63) // 64) < 64 and P >= 4 * CH and P % CH == 0 and ms == P * rs:
+        # one launch (rb_colsum_chunked): chunk sums, the last arriving
+        # workgroup of each column block sums them — bitwise the two passes
         nch = P // CH
         part = torch.empty((M * nch, C), device=x.device, dtype=torch.float32)
-        _lib.call("rb_colsum", x3.data_ptr(), M * nch, CH, C, rs, CH * rs, part.data_ptr(),
-                  _stream(x))
-        _lib.call("rb_colsum", part.data_ptr(), M, nch, C, C, nch * C, out.data_ptr(),
-                  _stream(x))
+        cnt = _colsum_tickets(x, M * ((C + 63) // 64))
+        _lib.call("rb_colsum_chunked", x3.data_ptr(), M, P, C, rs, CH, part.data_ptr(),
+                  cnt.data_ptr(), cnt.numel(), out.data_ptr(), _stream(x))
         return out[0] if squeeze else out
     _lib.call("rb_colsum", x3.data_ptr(), M, P, C, rs, ms, out.data_ptr(), _stream(x))
     return out[0] if squeeze else out
@@ -839,9 +854,7 @@ def item_ce_probs_h_both(seq: SplitRows, items: SplitRows, target, lse, dloss, i
     _check(dloss, "dloss")
     dev = seq.img.device
     Vp = (V + pad_to - 1) // pad_to * pad_to
-    p = torch.empty((B, Vp), device=dev, dtype=torch.float32)
-    if Vp > V:
-        p[:, V:].zero_()
+    p = torch.empty((B, Vp), device=dev, dtype=torch.float32)   # pad columns zeroed in-kernel
     ldt = (B + 3) // 4 * 4
     pt = torch.empty((V, ldt), device=dev, dtype=torch.float32)[:, :B]
     maxes = torch.zeros((B + 31) // 32 + (V + 31) // 32, device=dev, dtype=torch.float32)

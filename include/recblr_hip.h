@@ -281,6 +281,19 @@ int rb_embedding_bwd_apply(const float* grad, int64_t M, int64_t d, int64_t V,
 int rb_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int64_t ms,
               float* out, void* stream);
 
+/* rb_colsum for few columns and many rows in one launch: the rows of each of
+ * the M matrices (contiguous: matrix m starts at in + m*P*rs) are summed in
+ * chunks of `chunk_rows` (P % chunk_rows == 0, chunk_rows <= 256), each chunk
+ * as rb_colsum(P = chunk_rows) does, then the chunk sums as
+ * rb_colsum(P = P / chunk_rows) does — bitwise the two-launch result.  part:
+ * [M, P / chunk_rows, C] fp32 workspace; counters: M * ceil(C / 64) uint32
+ * tickets, zero on the first call and left zero by every call (the last
+ * workgroup of a column block resets its ticket); calls sharing counters must
+ * be ordered on one stream. */
+int rb_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs,
+                      int64_t chunk_rows, float* part, uint32_t* counters, int64_t n_counters,
+                      float* out, void* stream);
+
 /* ---- item scoring (RecBLR.py:86-122), fp32 MFMA, no [B, V] logits ----
  * seq: [B, d] sequence representations (RecBLR.forward's output), items:
  * [V, d] item table (item_embedding.weight), both contiguous and 16-B

@@ -610,3 +610,28 @@ def test_gemm_pattern_probe_covers_every_output(cuda, M, R, C):
     ref = a.double().sum(1, keepdim=True) + (torch.arange(C, device=cuda) % 4).double()[None]
     assert torch.allclose(out[:M].double(), ref, atol=1e-3, rtol=1e-5)
     assert torch.isnan(out[M:]).all()
+
+
+@pytest.mark.parametrize("shape", [(3, 2048, 256), (2048, 256), (1024, 512), (4096, 128)])
+def test_colsum_chunked_one_launch_equals_two_passes(cuda, shape):
+    """rb_colsum_chunked (chunk sums, then the last arriving workgroup of each
+    column block sums them) is bitwise the two rb_colsum passes it replaced,
+    call after call: the tickets reset themselves and the workspace's lines,
+    reused by the allocator, are re-read after the acquire."""
+    from datamining_recblr_amd import _lib, kernels
+    from datamining_recblr_amd.kernels import _stream
+
+    g = torch.Generator(device=cuda).manual_seed(sum(shape))
+    P, C = shape[-2], shape[-1]
+    M = 1 if len(shape) == 2 else shape[0]
+    nch = P // 64
+    for it in range(60):
+        x = torch.randn(shape, device=cuda, generator=g) * (1 + it % 7)
+        out = kernels.colsum(x)
+        part = torch.empty(M * nch, C, device=cuda)
+        ref = torch.empty(M, C, device=cuda)
+        _lib.call("rb_colsum", x.data_ptr(), M * nch, 64, C, C, 64 * C, part.data_ptr(), _stream(x))
+        _lib.call("rb_colsum", part.data_ptr(), M, nch, C, C, nch * C, ref.data_ptr(), _stream(x))
+        assert torch.equal(out.reshape(M, C), ref), it
+    tickets = kernels._tickets[(x.device, _stream(x))]
+    assert int(tickets.abs().sum()) == 0
