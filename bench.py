@@ -897,6 +897,24 @@ def main():
         ffn_act_ab["note"] = ("RECBLR_FFN_ACT A/B on the headline's batches: w_1 with "
                               "dropout(silu(.)) in its epilogue vs the GEMM and "
                               "rb_silu_dropout_fwd, best of 3 alternated runs each")
+    order_ab = None
+    if not args.no_full_tail:
+        # the gate backward's consumers: the conv backward right behind the
+        # dX GEMM that wrote its second input (default) vs the weight gradient
+        # first (round 3), alternated 3x on the lease
+        from datamining_recblr_amd import recurrence as _rec
+        saved_o = _rec.set_conv_first(True)
+        runs = {"conv_first": [], "wgrad_first": []}
+        for _ in range(3):
+            for name, on in (("conv_first", True), ("wgrad_first", False)):
+                _rec.set_conv_first(on)
+                runs[name].append(timed_variant(True, True)["ms_per_step"])
+        _rec.set_conv_first(saved_o)
+        order_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
+        order_ab["headline"] = "conv_first" if saved_o else "wgrad_first"
+        order_ab["note"] = ("RECBLR_CONV_FIRST A/B on the headline's batches: in the "
+                            "GatedRecurrentLayer backward, the conv backward before the gates "
+                            "weight gradient (its inputs just written) or after it; best of 3")
     adam_ab = None
     if not args.no_full_tail:
         # the optimizer update: rb_adam_step (one launch over every parameter)
@@ -1027,6 +1045,7 @@ def main():
             "fused_grl": fused_ab,
             "ffn_act": ffn_act_ab,
             "adam": adam_ab,
+            "bwd_order": order_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 34
+ABI_VERSION = 35
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -43,10 +43,10 @@ SIGNATURES = {
     "rb_gate_scan_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp,
                                         _i64, _fp, _i64, _i64, _i64, _fp, _fp]),
     "rb_gate_scan_fwd_last": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp,
-                                             _i64, _fp, _fp, _i64, _i64, _i64, _fp, _fp]),
+                                             _i64, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp]),
     "rb_gate_scan_bwd_last": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp,
                                              _fp, _fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp,
-                                             _i64, _i64, _i64, _fp, _fp]),
+                                             _i64, _i64, _i64, _fp, _fp, _fp]),
     "rb_gate_scan_bwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp,
                                         _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64, _i64, _i64,
                                         _fp, _fp]),

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 34; }
+int rb_version(void) { return 35; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -147,7 +147,7 @@ int rb_gate_scan_fwd_last(const float* rg, int64_t rg_rs, const float* xc, int64
                           const float* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* h0, int64_t h0_bs, float* y_last, float* carries,
                           int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets,
-                          void* stream) {
+                          const int64_t* batch_row, void* stream) {
   if (!rg || !xc || !z || !lam || !y_last) return fail("rb_gate_scan_fwd_last: null pointer");
   if (h0_bs != 0 && h0_bs < H)
     return fail("rb_gate_scan_fwd_last: h0 batch stride must be 0 or >= H");
@@ -156,7 +156,7 @@ int rb_gate_scan_fwd_last(const float* rg, int64_t rg_rs, const float* xc, int64
   if (int r = check_dims("rb_gate_scan_fwd_last", B, L, H, max4(rg_rs, xc_rs, z_rs, H))) return r;
   return launch_gate_fwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, h0, h0_bs, nullptr, H,
                          carries, B, L, H, seq_offsets, reinterpret_cast<hipStream_t>(stream),
-                         y_last);
+                         y_last, batch_row);
 }
 
 int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
@@ -186,7 +186,7 @@ int rb_gate_scan_bwd_last(const float* rg, int64_t rg_rs, const float* xc, int64
                           const float* carries, const float* dy_last, float* drg,
                           int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz, int64_t dz_rs,
                           float* part, float* dh0_part, int64_t B, int64_t L, int64_t H,
-                          const int64_t* seq_offsets, void* stream) {
+                          const int64_t* seq_offsets, const int64_t* batch_row, void* stream) {
   if (!rg || !xc || !z || !lam || !carries || !dy_last || !drg || !dxc || !dz || !part ||
       !dh0_part)
     return fail("rb_gate_scan_bwd_last: null pointer");
@@ -197,7 +197,7 @@ int rb_gate_scan_bwd_last(const float* rg, int64_t rg_rs, const float* xc, int64
     return r;
   return launch_gate_bwd(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gate_b, carries, nullptr, drg,
                          drg_rs, dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, seq_offsets,
-                         reinterpret_cast<hipStream_t>(stream), dy_last);
+                         reinterpret_cast<hipStream_t>(stream), dy_last, batch_row);
 }
 
 int rb_scan_fwd_bf16(const rb_bf16* gates, const rb_bf16* tokens, rb_bf16* states, int64_t B,

@@ -293,13 +293,13 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
                     int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
-                    float* y_last = nullptr);
+                    float* y_last = nullptr, const int64_t* order = nullptr);
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
                     int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
-                    const float* dy_last = nullptr);
+                    const float* dy_last = nullptr, const int64_t* order = nullptr);
 int launch_scan_fwd_bf16(const bf16_t* gates, const bf16_t* tokens, bf16_t* states,
                          int64_t rows, int64_t T, hipStream_t st);
 int launch_scan_bwd_bf16(const bf16_t* gates, const bf16_t* states, const bf16_t* grad,

@@ -5,9 +5,16 @@
 //
 // torch sorts the indices and runs a segmented reduction whose sum_and_scatter
 // kernel took ~4.8 ms per training step at B=2048 L=200 d=128.  Here:
-//   1. keys = int32(idx), vals = position; rocPRIM stable radix sort on the
-//      log2(V) key bits (positions stay in order inside every key);
-//   2. seg[v] = lower_bound(sorted keys, v) for v in [0, V];
+//   1. vals = the positions grouped by key, in position order inside every
+//      key (a stable counting sort, three launches, for V <= kPlanMaxKeys:
+//      256 row blocks count their keys in LDS; one thread per key scans
+//      its counts over the blocks, and the last workgroup to finish turns
+//      the key totals into the key segments seg[v], the chunk offsets and
+//      descriptors; each block places its positions, ranks inside a wave
+//      from ballots over the key bits; larger V: rocPRIM's stable radix
+//      sort, a binary search for seg and a scan for the chunks — 15
+//      launches);
+//   2. seg[v] = first slot of key v, v in [0, V];
 //   3. every key's run is cut into chunks of kChunk rows (long runs of very
 //      popular items are spread over many waves); chunk offsets by a scan;
 //   4. one wave per chunk sums its rows in a fixed order (its key and rows
@@ -216,6 +223,176 @@ k_emb_finish(const int* __restrict__ nch, const int* __restrict__ choff,
     dw[(int64_t)v * d + col] = ((red[0][col] + red[1][col]) + red[2][col]) + red[3][col];
 }
 
+// ---- the counting-sort plan (V <= kPlanMaxKeys) -----------------------------------
+constexpr int kPlanBlocks = 256;       // T: row blocks of the counting sort
+constexpr int kPlanMaxKeys = 16384;    // LDS key counters (64 KB)
+
+// cnt[t * V + v] = positions of block t (rows [t*per, (t+1)*per)) with key v
+// (block-major: each block writes its V counts contiguously)
+__global__ void __launch_bounds__(1024) k_emb_hist(const int64_t* __restrict__ idx, int64_t M,
+                                                   int V, int64_t per, int* __restrict__ cnt,
+                                                   unsigned* __restrict__ ticket) {
+  __shared__ int h[kPlanMaxKeys];
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ticket = 0u;   // k_emb_keys' arrival count
+  for (int v = threadIdx.x; v < V; v += blockDim.x) h[v] = 0;
+  __syncthreads();
+  const int64_t beg = (int64_t)blockIdx.x * per, end = min(M, beg + per);
+  for (int64_t i = beg + threadIdx.x; i < end; i += blockDim.x) {
+    const int64_t k = idx[i];
+    if (k >= 0 && k < V) atomicAdd(&h[k], 1);   // integer counts: order-independent
+  }
+  __syncthreads();
+  int* row = cnt + (int64_t)blockIdx.x * V;
+  for (int v = threadIdx.x; v < V; v += blockDim.x) row[v] = h[v];
+}
+
+// exclusive workgroup-wide scan (1024 threads, one value each); *total = sum
+__device__ int block_scan_excl(int x, int* sh, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  if (w == 0) {
+    int s = lane < 16 ? sh[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int y = __shfl_up(s, o);
+      if (lane >= o) s += y;
+    }
+    if (lane < 16) sh[16 + lane] = s;
+  }
+  __syncthreads();
+  const int before = w ? sh[16 + w - 1] : 0;
+  *total = sh[16 + 15];
+  __syncthreads();
+  return before + incl - x;
+}
+
+// The last workgroup (1024 threads): seg, nch, choff (exclusive scans over the keys, in key
+// order) and the chunk descriptors; thread j owns keys [j*kpt, (j+1)*kpt)
+__device__ void emb_offsets(const int* __restrict__ tot, int V, int* __restrict__ seg,
+                            int* __restrict__ nch, int* __restrict__ choff,
+                            int4* __restrict__ desc, int* ts, int* sh) {
+  for (int v = threadIdx.x; v < V; v += 1024) ts[v] = tot[v];
+  __syncthreads();
+  const int kpt = (V + 1023) / 1024;
+  const int v0 = threadIdx.x * kpt, v1 = min(V, v0 + kpt);
+  int sum = 0, chs = 0;
+  for (int v = v0; v < v1; ++v) {
+    const int s = ts[v];
+    sum += s;
+    chs += (s + kChunk - 1) / kChunk;
+  }
+  int all, all_ch;
+  int pos = block_scan_excl(sum, sh, &all);
+  int cpos = block_scan_excl(chs, sh, &all_ch);
+  for (int v = v0; v < v1; ++v) {
+    const int s = ts[v];
+    const int n = (s + kChunk - 1) / kChunk;
+    seg[v] = pos;
+    nch[v] = n;
+    choff[v] = cpos;
+    for (int i = 0; i < n; ++i)
+      desc[cpos + i] = make_int4(v, pos + i * kChunk, min(pos + s, pos + (i + 1) * kChunk), n == 1);
+    pos += s;
+    cpos += n;
+  }
+  if (threadIdx.x == 0) {
+    seg[V] = all;
+    nch[V] = 0;
+    choff[V] = all_ch;
+  }
+}
+
+// One thread per key: cnt[t][v] becomes the exclusive prefix over the
+// blocks (in block order), tot[v] the key's count; the lanes of a wave read
+// and write 64 consecutive keys per block, 16 blocks in flight.  The last
+// workgroup to finish (arrival ticket, zeroed by k_emb_hist) then runs
+// emb_offsets over all keys.
+__global__ void __launch_bounds__(1024) k_emb_keys(int* __restrict__ cnt, int V,
+                                                   int* __restrict__ tot, int* __restrict__ seg,
+                                                   int* __restrict__ nch, int* __restrict__ choff,
+                                                   int4* __restrict__ desc,
+                                                   unsigned* __restrict__ ticket) {
+  __shared__ int ts[kPlanMaxKeys];
+  __shared__ int sh[32];
+  __shared__ int s_last;
+  const int v = blockIdx.x * 1024 + threadIdx.x;
+  if (v < V) {
+    int carry = 0;
+    for (int t0 = 0; t0 < kPlanBlocks; t0 += 16) {
+      int c[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c[q] = cnt[(int64_t)(t0 + q) * V + v];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        cnt[(int64_t)(t0 + q) * V + v] = carry;
+        carry += c[q];
+      }
+    }
+    tot[v] = carry;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;   // workgroup-uniform
+  emb_offsets(tot, V, seg, nch, choff, desc, ts, sh);
+}
+
+// Block t (one wave) places its positions in position order: slot = seg[k]
+// + the key's positions in earlier blocks + its earlier positions in this
+// block; inside a 64-row step the lanes with equal keys are found from
+// ballots over the key bits, and each key's running count stays in LDS
+// across the block's steps.
+__global__ void __launch_bounds__(64) k_emb_place(const int64_t* __restrict__ idx, int64_t M,
+                                                  int V, int bits, int64_t per,
+                                                  const int* __restrict__ seg,
+                                                  const int* __restrict__ cnt,
+                                                  int* __restrict__ vals) {
+  __shared__ int run[kPlanMaxKeys];
+  const int lane = threadIdx.x;
+  for (int v = lane; v < V; v += 64) run[v] = 0;
+  __syncthreads();
+  const int64_t beg = (int64_t)blockIdx.x * per, end = min(M, beg + per);
+  const uint64_t lt = (uint64_t(1) << lane) - 1;
+  for (int64_t r0 = beg; r0 < end; r0 += 64) {
+    const int64_t i = r0 + lane;
+    const int64_t kk = i < end ? idx[i] : -1;
+    const bool ok = kk >= 0 && kk < V;
+    const int k = ok ? (int)kk : 0;
+    uint64_t same = __builtin_amdgcn_ballot_w64(ok);
+    for (int b = 0; b < bits; ++b) {
+      const bool bit = (k >> b) & 1;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(ok && bit);
+      same &= bit ? m : ~m;
+    }
+    if (ok) {
+      const int before = run[k];
+      vals[seg[k] + cnt[(int64_t)blockIdx.x * V + k] + before + __popcll(same & lt)] =
+          (int)i;
+      // the group's lowest lane advances the key's count (groups: distinct keys)
+      if ((same & lt) == 0) run[k] = before + __popcll(same);
+    }
+  }
+}
+
 // rocPRIM picks its block-sort + merge-sort path below 2^20 items (~100 us
 // for the bench's ~205k packed positions: block sort plus 14 merge passes);
 // a merge-sort limit of 0 selects Onesweep, the LSD radix sort (stable: the
@@ -232,7 +409,8 @@ int key_bits(int64_t V) {
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 struct EmbWs {
-  size_t keys_in, keys_out, vals_in, vals_out, seg, nch, choff, desc, partial, sort_tmp, scan_tmp;
+  size_t keys_in, keys_out, vals_in, vals_out, seg, nch, choff, desc, partial, sort_tmp, scan_tmp,
+      cnt, tot, ticket;
   size_t sort_bytes, scan_bytes, total;
 };
 
@@ -258,6 +436,9 @@ EmbWs emb_layout(int64_t M, int64_t V, int64_t d) {
   (void)rocprim::exclusive_scan(nullptr, w.scan_bytes, (const int*)nullptr, (int*)nullptr, 0,
                           (size_t)(V + 1), rocprim::plus<int>());
   w.scan_tmp = take(w.scan_bytes);
+  w.cnt = V <= kPlanMaxKeys ? take((size_t)V * kPlanBlocks * 4) : 0;
+  w.tot = V <= kPlanMaxKeys ? take((size_t)V * 4) : 0;
+  w.ticket = V <= kPlanMaxKeys ? take(4) : 0;
   w.total = off;
   return w;
 }
@@ -310,6 +491,19 @@ int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, v
   int* seg = reinterpret_cast<int*>(ws + w.seg);
   int* nch = reinterpret_cast<int*>(ws + w.nch);
   int* choff = reinterpret_cast<int*>(ws + w.choff);
+  if (V <= kPlanMaxKeys && M < ((int64_t)1 << 31)) {   // the counting sort: three launches
+    int* cnt = reinterpret_cast<int*>(ws + w.cnt);
+    int* tot = reinterpret_cast<int*>(ws + w.tot);
+    unsigned* ticket = reinterpret_cast<unsigned*>(ws + w.ticket);
+    const int64_t per = (M + kPlanBlocks - 1) / kPlanBlocks;
+    hipLaunchKernelGGL(k_emb_hist, dim3(kPlanBlocks), dim3(1024), 0, st, idx, M, (int)V, per, cnt,
+                       ticket);
+    hipLaunchKernelGGL(k_emb_keys, dim3((unsigned)((V + 1023) / 1024)), dim3(1024), 0, st, cnt,
+                       (int)V, tot, seg, nch, choff, reinterpret_cast<int4*>(ws + w.desc), ticket);
+    hipLaunchKernelGGL(k_emb_place, dim3(kPlanBlocks), dim3(64), 0, st, idx, M, (int)V,
+                       key_bits(V), per, seg, cnt, vals_out);
+    return launch_status("rb_embedding_plan");
+  }
   const int64_t pblocks = std::min<int64_t>(4096, (M + 255) / 256);
   hipLaunchKernelGGL(k_emb_prep, dim3((unsigned)pblocks), dim3(256), 0, st, idx, keys_in, vals_in,
                      M);

@@ -42,7 +42,8 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 const float* __restrict__ gbias, const float* __restrict__ h0, int h0_bs,
                 T* __restrict__ y, int y_rs,
                 float* __restrict__ carries, int64_t B, int Lmax, int H, int ncw,
-                const int64_t* __restrict__ offs, T* __restrict__ y_last) {
+                const int64_t* __restrict__ offs, T* __restrict__ y_last,
+                const int64_t* __restrict__ order) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -165,7 +166,7 @@ k_gate_scan_fwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
         out[v] = fsilu(in.z[j][v]) * cin[v];
       }
       if (y_last != nullptr) {   // only each sequence's last position is kept: [B, H]
-        if (cv && t0 + j == L - 1) stv(y_last + b * H + c0, out);
+        if (cv && t0 + j == L - 1) stv(y_last + (order ? order[b] : b) * H + c0, out);
       } else if (cv && t0 + j < L) {
         stv(yb + (t0 + j) * y_rs, out);
       }
@@ -249,7 +250,8 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
                 T* __restrict__ drg, int drg_rs, T* __restrict__ dxc, int dxc_rs,
                 T* __restrict__ dz, int dz_rs, float* __restrict__ part,
                 float* __restrict__ dh0_part, int64_t B, int Lmax, int H, int ncw,
-                const int64_t* __restrict__ offs, int pair, const T* __restrict__ dy_last) {
+                const int64_t* __restrict__ offs, int pair, const T* __restrict__ dy_last,
+                const int64_t* __restrict__ order) {
   constexpr int G = kWave / Q;
   constexpr int TILE = Q * TC;
   static_assert(TILE == RB_TILE, "tile must match the carries checkpoint stride");
@@ -267,12 +269,13 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
   const int cc = cv ? c0 : 0;
   // dense rows (b, t) at b * Lmax + t, or packed variable-length sequences:
   // sequence b at rows offs[b] .. offs[b+1] (wave-uniform)
-  int64_t b = bw, row0 = 0;
+  int64_t b = bw, row0 = 0, bl = bw;   // bl: the batch row of dy_last
   int L = 0;
   const T *rgb = nullptr, *xcb = nullptr, *zb = nullptr, *dyb = nullptr;
   T *drgb = nullptr, *dxcb = nullptr, *dzb = nullptr;
   auto bind = [&](int64_t bs) {
     b = bs;
+    bl = order != nullptr ? order[bs] : bs;
     if (offs != nullptr) {
       row0 = offs[b];
       L = (int)(offs[b + 1] - row0);
@@ -317,7 +320,7 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
       if (dy_last == nullptr) {
         ld_raw(in.g[j], dyb + t * H);
       } else if (t == L - 1) {   // dy is zero except at each sequence's last position
-        ld_raw(in.g[j], dy_last + b * H + cc);
+        ld_raw(in.g[j], dy_last + bl * H + cc);
       } else {
         zero_raw(in.g[j]);
       }
@@ -529,13 +532,13 @@ template <typename T, int V, bool PF = true>
 int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-               const int64_t* offs, hipStream_t st, T* y_last) {
+               const int64_t* offs, hipStream_t st, T* y_last, const int64_t* order = nullptr) {
   const int span = (kWave / kFwdQ) * V;
   const int ncw = (int)((H + span - 1) / span);
   const int64_t blocks = (B * ncw + 3) / 4;
   hipLaunchKernelGGL((k_gate_scan_fwd<T, V, kFwdQ, kFwdTC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
-                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw, offs, y_last);
+                     h0, (int)h0_bs, y, (int)y_rs, carries, B, (int)L, (int)H, ncw, offs, y_last, order);
   return launch_status("rb_gate_scan_fwd");
 }
 
@@ -544,7 +547,7 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
                float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
-               hipStream_t st, const T* dy_last) {
+               hipStream_t st, const T* dy_last, const int64_t* order = nullptr) {
   const int span = (kWave / Q) * V;
   const int ncw = (int)((H + span - 1) / span);
   // packed (variable-length, longest-first) batches: one wave per sequence pair
@@ -554,7 +557,7 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
-                     dh0_part, B, (int)L, (int)H, ncw, offs, pair, dy_last);
+                     dh0_part, B, (int)L, (int)H, ncw, offs, pair, dy_last, order);
   return launch_status("rb_gate_scan_bwd");
 }
 
@@ -564,7 +567,7 @@ template <typename T>
 int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* h0, int64_t h0_bs,
                T* y, int64_t y_rs, float* carries, int64_t B, int64_t L, int64_t H,
-               const int64_t* offs, hipStream_t st, T* y_last) {
+               const int64_t* offs, hipStream_t st, T* y_last, const int64_t* order) {
   constexpr int VW = sizeof(T) == 2 ? 4 : 2;
   const auto strides = {rg_rs, xc_rs, z_rs, y_rs, h0_bs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)y,
@@ -573,12 +576,12 @@ int gate_fwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   // bf16: no register prefetch (measured 3% faster at config 5, tools/kbench.hip)
   if (vec_ok<T, VW>(H, strides, act, f32))
     return gate_fwd_v<T, VW, sizeof(T) == 4>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs,
-                                             y, y_rs, carries, B, L, H, offs, st, y_last);
+                                             y, y_rs, carries, B, L, H, offs, st, y_last, order);
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_fwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                            B, L, H, offs, st, y_last);
+                            B, L, H, offs, st, y_last, order);
   return gate_fwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries, B,
-                          L, H, offs, st, y_last);
+                          L, H, offs, st, y_last, order);
 }
 
 template <typename T>
@@ -586,7 +589,7 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
                float* part, float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
-               hipStream_t st, const T* dy_last) {
+               hipStream_t st, const T* dy_last, const int64_t* order) {
   constexpr int VW = 4;
   const auto strides = {rg_rs, xc_rs, z_rs, drg_rs, dxc_rs, dz_rs};
   const auto act = {(const void*)rg, (const void*)xc, (const void*)z, (const void*)dy,
@@ -603,17 +606,17 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
     if (vec_ok<T, VW>(H, strides, act, f32))
       return gate_bwd_v<T, VW, 4, 4, true>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy,
                                            drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part, dh0_part,
-                                           B, L, H, offs, st, dy_last);
+                                           B, L, H, offs, st, dy_last, order);
   }
   if (vec_ok<T, VW>(H, strides, act, f32)) {
     return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
+                             dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last, order);
   }
   if (vec_ok<T, 2>(H, strides, act, f32))
     return gate_bwd_v<T, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last, order);
   return gate_bwd_v<T, 1>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
+                          dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last, order);
 }
 
 }  // namespace
@@ -622,9 +625,9 @@ int launch_gate_fwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* z, int64_t z_rs, const float* lam, const float* gb,
                     const float* h0, int64_t h0_bs, float* y, int64_t y_rs, float* carries,
                     int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
-                    float* y_last) {
+                    float* y_last, const int64_t* order) {
   return gate_fwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                           B, L, H, offs, st, y_last);
+                           B, L, H, offs, st, y_last, order);
 }
 
 int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
@@ -632,7 +635,7 @@ int launch_gate_fwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int6
                          const float* h0, int64_t h0_bs, bf16_t* y, int64_t y_rs, float* carries,
                          int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st) {
   return gate_fwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, h0, h0_bs, y, y_rs, carries,
-                            B, L, H, offs, st, nullptr);
+                            B, L, H, offs, st, nullptr, nullptr);
 }
 
 int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
@@ -640,9 +643,9 @@ int launch_gate_bwd(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_
                     const float* carries, const float* dy, float* drg, int64_t drg_rs, float* dxc,
                     int64_t dxc_rs, float* dz, int64_t dz_rs, float* part, float* dh0_part,
                     int64_t B, int64_t L, int64_t H, const int64_t* offs, hipStream_t st,
-                    const float* dy_last) {
+                    const float* dy_last, const int64_t* order) {
   return gate_bwd_t<float>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs, dxc,
-                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last);
+                           dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, dy_last, order);
 }
 
 int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int64_t xc_rs,
@@ -652,7 +655,7 @@ int launch_gate_bwd_bf16(const bf16_t* rg, int64_t rg_rs, const bf16_t* xc, int6
                          float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* offs,
                          hipStream_t st) {
   return gate_bwd_t<bf16_t>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
-                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, nullptr);
+                            dxc, dxc_rs, dz, dz_rs, part, dh0_part, B, L, H, offs, st, nullptr, nullptr);
 }
 
 }  // namespace rb

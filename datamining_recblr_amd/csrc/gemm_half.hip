@@ -953,13 +953,22 @@ __device__ __forceinline__ void hds_write16(uint32_t addr, f16x8 v) {
 }
 
 template <int NBN, int NBK>
-__global__ void __launch_bounds__(256 * NBN * NBK, 2 / (NBN * NBK))
-k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X, int64_t ldx,
-            int64_t M, int N, int K, const float* __restrict__ ymax,
-            const float* __restrict__ xmax, float* __restrict__ parts, int S, int64_t mk,
-            int nt_k) {
+__device__ __attribute__((noinline)) void tn_percol(char* smem, const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X,
+                                        int64_t ldx, int64_t M, int N, int K,
+                                        const float* __restrict__ ymax,
+                                        const float* __restrict__ xmax, float* __restrict__ parts,
+                                        int S, int64_t mk, int nt_k);
+
+// The body of k_gemm_tn_h.  PERCOL = false: the chunk scales, then (a column
+// spread past 2^16) tn_percol; PERCOL = true: the tile's chunk again with the
+// column scales the first pass left in stage 0's padding bytes.
+template <int NBN, int NBK, bool PERCOL>
+__device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X,
+                                        int64_t ldx, int64_t M, int N, int K,
+                                        const float* __restrict__ ymax,
+                                        const float* __restrict__ xmax, float* __restrict__ parts,
+                                        int S, int64_t mk, int nt_k) {
   using CF = TnCfg<NBN, NBK>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1012,7 +1021,20 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
   const int rg = loader ? lt / ncg : 0;
   const float* src = op == 0 ? Y + n0 + 4 * cc : X + k0 + 4 * cc;
   const int64_t ld = op == 0 ? ldy : ldx;
-  const float sc = __builtin_amdgcn_ldexpf(1.0f, kTT - (op == 0 ? ey : ex));
+  // the operand scale of each of the thread's 4 columns: the chunk's (the
+  // first pass) or the column's own (the redo pass, below)
+  float scv[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    int e = op == 0 ? ey : ex;
+    if constexpr (PERCOL) {
+      const int col = 4 * cc + c;
+      e = *reinterpret_cast<const int*>(smem + (op == 0 ? col * T_PITCH
+                                                        : 2 * CF::YPLANE + col * T_PITCH) + 64);
+    }
+    scv[c] = __builtin_amdgcn_ldexpf(1.0f, kTT - e);
+  }
+  float cm[4] = {0.0f, 0.0f, 0.0f, 0.0f};   // max |value| of the thread's columns
   const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
 
   f32x4 raw0[8], raw1[8];
@@ -1042,8 +1064,9 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
       f16x8 h0, h1;
 #pragma unroll
       for (int q = 0; q < 8; q += 2) {
+        if constexpr (!PERCOL) cm[c] = max3abs(cm[c], r[q][c], r[q + 1][c]);
         f16x2 p0, p1;
-        split2h(f32x2{r[q][c], r[q + 1][c]} * sc, p0, p1);
+        split2h(f32x2{r[q][c], r[q + 1][c]} * scv[c], p0, p1);
         h0[q] = p0[0]; h0[q + 1] = p0[1];
         h1[q] = p1[0]; h1[q + 1] = p1[1];
       }
@@ -1106,23 +1129,93 @@ k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ 
     }
   }
 
+  // Column spread.  The chunk scale keeps 22 bits for values within 2^17 of
+  // the chunk max; a whole column far below it (dY / X columns spread over
+  // more than 2^16 inside one chunk) would lose bits at its own scale.  Such
+  // a tile's chunk is done again (tn_percol, a cold path) with one scale per
+  // column — exact powers of two that factor out of dW[n, k] = sum_m dY[m, n]
+  // X[m, k] — from the column maxima of the values this pass loaded, left in
+  // the 16 padding bytes of each column's slot of stage 0 (the images use
+  // bytes 0-63 of the 80-B pitch).
+  constexpr int NCOL = CF::YC + CF::XC;
+  constexpr int pass = PERCOL ? 1 : 0;
+  if constexpr (!PERCOL) {
+    __syncthreads();   // every wave's last stage reads are done: the LDS is free
+    float* s_cm = reinterpret_cast<float*>(smem + CF::STAGE);   // [4 row groups][NCOL]
+    int* s_redo = reinterpret_cast<int*>(smem + CF::STAGE) + 4 * NCOL;
+    if (tid == 0) *s_redo = 0;
+    if (loader) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s_cm[rg * NCOL + (op == 0 ? 0 : CF::YC) + 4 * cc + c] = cm[c];
+    }
+    __syncthreads();
+    for (int col = tid; col < NCOL; col += CF::THREADS) {
+      const float m = fmaxf(fmaxf(s_cm[col], s_cm[NCOL + col]),
+                            fmaxf(s_cm[2 * NCOL + col], s_cm[3 * NCOL + col]));
+      const int ec = col < CF::YC ? ey : ex;   // the chunk exponent
+      if (m > 0.0f && m < __builtin_amdgcn_ldexpf(1.0f, ec - 16)) *s_redo = 1;   // all store 1
+      const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
+      const int slot = col < CF::YC ? col * T_PITCH : 2 * CF::YPLANE + (col - CF::YC) * T_PITCH;
+      *reinterpret_cast<int*>(smem + slot + 64) = e;
+    }
+    __syncthreads();
+    if (*s_redo != 0) {   // workgroup-uniform
+      tn_percol<NBN, NBK>(smem, Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
+      return;
+    }
+  }
+
   // un-scale and store the partial tile (every split writes its slot, empty
-  // chunks zeros)
-  const int sh = ey + ex - 2 * kTT;
+  // chunks zeros): the chunk exponents, or (pass 1) each column's
   float* out = parts + (int64_t)s * N * K;
+  if constexpr (pass == 0) {
+    const int sh = ey + ex - 2 * kTT;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = k0 + 64 * wk + 32 * j + (lane & 31);
+      for (int j = 0; j < 2; ++j) {
+        const int col = k0 + 64 * wk + 32 * j + (lane & 31);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int row = n0 + 64 * wm + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+          out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int row = n0 + 64 * wm + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
-        out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
+        const int nl = 64 * wm + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+        const int en = *reinterpret_cast<const int*>(smem + nl * T_PITCH + 64) - 2 * kTT;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int kl = 64 * wk + 32 * j + (lane & 31);
+          const int ek = *reinterpret_cast<const int*>(smem + 2 * CF::YPLANE + kl * T_PITCH + 64);
+          out[(int64_t)(n0 + nl) * K + k0 + kl] = __builtin_amdgcn_ldexpf(acc[i][j][e], en + ek);
+        }
       }
-    }
+  }
 }
 
+template <int NBN, int NBK>
+__device__ __attribute__((noinline)) void tn_percol(char* smem, const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X,
+                                        int64_t ldx, int64_t M, int N, int K,
+                                        const float* __restrict__ ymax,
+                                        const float* __restrict__ xmax, float* __restrict__ parts,
+                                        int S, int64_t mk, int nt_k) {
+  tn_body<NBN, NBK, true>(smem, Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
+}
+
+template <int NBN, int NBK>
+__global__ void __launch_bounds__(256 * NBN * NBK, 2 / (NBN * NBK))
+k_gemm_tn_h(const float* __restrict__ Y, int64_t ldy, const float* __restrict__ X, int64_t ldx,
+            int64_t M, int N, int K, const float* __restrict__ ymax,
+            const float* __restrict__ xmax, float* __restrict__ parts, int S, int64_t mk,
+            int nt_k) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  tn_body<NBN, NBK, false>(smem, Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
+}
 
 
 template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>

@@ -204,7 +204,8 @@ class Packed:
     """Packed variable-length sequences: sequence b occupies rows
     offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
     right-padded batch without the padding; include/recblr_hip.h)."""
-    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv", "pieces", "G", "max_tiles")
+    __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv", "order", "pieces", "G",
+                 "max_tiles")
 
     def __init__(self, offsets: torch.Tensor, L: int, ntok: int,
                  pos: torch.Tensor | None = None):
@@ -222,6 +223,9 @@ class Packed:
         # positions gather_indexes reads (rb_gate_scan_*_last)
         self.last = None
         self.inv = None
+        # optional: each packed sequence's batch row (the inverse of inv); the
+        # last-position scan kernels then write / read y_last in batch order
+        self.order = None
         # optional (grl_pieces): the fused GatedRecurrentLayer kernel's work
         # lists (int32 [3B + G + 1] on the device) and their count G
         self.pieces = None
@@ -338,7 +342,7 @@ def conv_silu_bwd(x, weight, bias, g1, g2, dx, seq: Packed | None = None):
 
 
 def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=None,
-                  seq: Packed | None = None, last_only: bool = False):
+                  seq: Packed | None = None, last_only: bool = False, batch_row=None):
     """Fused alpha/beta gates + BD-LRU scan + silu(z) merge.
 
     rg: [B, L, 2H]; xc, z: [B, L, H] views (or packed [ntok, 2H] / [ntok, H]
@@ -346,7 +350,8 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
     state per row) or None; gate_b: [2H] bias added to rg inside the kernel
     (or None).  Returns (y in xc's layout, carries [B, nT, H] or None when not
     wanted).  last_only (fp32): y is only needed at each sequence's last
-    position — returns y_last [B, H] instead (rb_gate_scan_fwd_last)."""
+    position — returns y_last [B, H] instead (rb_gate_scan_fwd_last); with
+    batch_row (int64 [B] permutation) sequence b's row is batch_row[b]."""
     dt = _act_dtype(xc, "xc")
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z")):
         _check(t, n, dt)
@@ -376,8 +381,8 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
         _launch("rb_gate_scan_fwd", 4 * n * 4 + B * H * 4, rg.data_ptr(), rg_rs, xc.data_ptr(),
                 xc_rs, z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H),
                 0 if h0 is None else h0.data_ptr(), h0_bs, y_last.data_ptr(),
-                0 if carries is None else carries.data_ptr(), B, L, H, offs, _stream(xc),
-                _fn="rb_gate_scan_fwd_last")
+                0 if carries is None else carries.data_ptr(), B, L, H, offs,
+                _batch_row_ptr(batch_row, B, xc.device), _stream(xc), _fn="rb_gate_scan_fwd_last")
         return y_last, carries
     if y is None:
         y = torch.empty(xc.shape[:-1] + (H,), device=xc.device, dtype=dt)
@@ -391,6 +396,15 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
     return y, carries
 
 
+def _batch_row_ptr(batch_row, B, dev):
+    if batch_row is None:
+        return None
+    if (batch_row.dtype != torch.int64 or batch_row.shape != (B,) or not batch_row.is_contiguous()
+            or batch_row.device != dev):
+        raise ValueError(f"batch_row must be a contiguous int64 [{B}] tensor on {dev}")
+    return batch_row.data_ptr()
+
+
 def _gb_ptr(gate_b, H):
     if gate_b is None:
         return None
@@ -401,12 +415,14 @@ def _gb_ptr(gate_b, H):
 
 
 def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=False,
-                  gate_b=None, seq: Packed | None = None, last_only: bool = False):
+                  gate_b=None, seq: Packed | None = None, last_only: bool = False,
+                  batch_row=None):
     """Backward of gate_scan_fwd.  Writes dz (a row-strided view) and returns
     (drg, dxc, dlam [H], dgate_bias [2H], dh0), dh0 [H] (summed over rows) or
     [B, H] when dh0_rows (a per-row h0).  Layouts as in gate_scan_fwd.
     last_only: dy is [B, H], the gradient at each sequence's last position
-    (zero elsewhere; rb_gate_scan_bwd_last)."""
+    (zero elsewhere; rb_gate_scan_bwd_last), row batch_row[b] for sequence b
+    when batch_row is given."""
     H = xc.shape[-1]
     dt = _act_dtype(xc, "xc")
     for t, n in ((rg, "rg"), (xc, "xc"), (z, "z"), (dy, "dy"), (dz, "dz")):
@@ -436,12 +452,14 @@ def gate_scan_bwd(rg, xc, z, lam, carries, dy, dz, drg=None, dxc=None, dh0_rows=
     dh0_part = part[3]
     n = xc.numel()
     nbytes = (8 * n + B * H if last_only else 9 * n) * xc.element_size()
+    tail = ((offs, _batch_row_ptr(batch_row, B, xc.device), _stream(xc)) if last_only
+            else (offs, _stream(xc)))
     _launch("rb_gate_scan_bwd" + _sfx(dt), nbytes, rg.data_ptr(), rg_rs,
             xc.data_ptr(), xc_rs,
             z.data_ptr(), z_rs, lam.contiguous().data_ptr(), _gb_ptr(gate_b, H), carries.data_ptr(),
             dy.data_ptr(),
             drg.data_ptr(), drg_rs, dxc.data_ptr(), dxc_rs, dz.data_ptr(), dz_rs,
-            part.data_ptr(), dh0_part.data_ptr(), B, L, H, offs, _stream(xc),
+            part.data_ptr(), dh0_part.data_ptr(), B, L, H, *tail,
             _fn="rb_gate_scan_bwd_last" if last_only else None)
     if dh0_rows:
         sums = colsum(part[:3])

@@ -156,7 +156,7 @@ class GatedRecurrentLayer(nn.Module):
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad,
                    seq=seq, last_only=last_only, observe=observe)
-        if last_only:
+        if last_only and seq.order is None:
             y = y.index_select(0, seq.inv)   # packed-sequence order -> batch order
         elif rows is not None:
             y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
@@ -365,7 +365,7 @@ class RecBLR(SequentialRecommender):
         # batch row's packed index and last token
         ids, pos, inv, last = pack_plan(item_seq.to(torch.int64), offsets, order, ntok)
         seq = Packed(offsets, L, ntok, pos if _CONV_ROWS else None)
-        seq.last, seq.inv = last, inv
+        seq.last, seq.inv, seq.order = last, inv, order
         if pieces is not None and pad is None:   # per-row pad prefixes: three-launch path
             seq.pieces, seq.G, seq.max_tiles = pieces, G, max_tiles
         if pad is not None:

@@ -50,6 +50,17 @@ _FUSED = os.environ.get("RECBLR_FUSED_GRL", "0") != "0"
 _FUSED_BWD = os.environ.get("RECBLR_FUSED_GRL_BWD", "0") != "0"
 
 
+# order of the backward's conv and gates weight gradient (see BDLRUCore.backward)
+_CONV_FIRST = os.environ.get("RECBLR_CONV_FIRST", "1") != "0"
+
+
+def set_conv_first(on: bool) -> bool:
+    """Set the backward order (bench A/B); returns the previous setting."""
+    global _CONV_FIRST
+    prev, _CONV_FIRST = _CONV_FIRST, bool(on)
+    return prev
+
+
 def fused_ok(has_pieces: bool, H: int, use_conv: bool, kc: int, dtype) -> bool:
     """Whether BDLRUCore's forward runs as one rb_grl_fwd launch (has_pieces:
     the packed batch carries the kernel's work lists)."""
@@ -118,6 +129,9 @@ class BDLRUCore(torch.autograd.Function):
         H = H2 // 2
         x, z = xz[..., :H], xz[..., H:]
         train = any(ctx.needs_input_grad)
+        # last_only on packed sequences: y_last in batch order (seq.order)
+        batch_row = seq.order if (last_only and seq is not None) else None
+        ctx.batch_row = batch_row
         if (observe is None and (h0 is None or h0.dim() == 1)
                 and fused_ok(seq is not None and seq.pieces is not None, H, use_conv, conv_w.shape[-1], xz.dtype)):
             # conv + gates GEMM + gate scan in one launch (rb_grl_fwd).  Its
@@ -127,6 +141,8 @@ class BDLRUCore(torch.autograd.Function):
             y, carries, xc, rg, r_xc = kernels.grl_fwd(
                 xz, conv_w, conv_b, linear_mod._weight_split(gate_w, False), gate_b, lam, h0,
                 seq, want_y=not last_only, want_train=train, tile_carries=ctx.fused_bwd)
+            if batch_row is not None:   # rb_grl_fwd keeps packed order
+                y = y.index_select(0, seq.inv)
             ctx.r_xc = r_xc if ctx.needs_input_grad[3] and linear_mod.rmax_wanted() else None
             if ctx.fused_bwd:   # rb_grl_bwd writes xc and both operands' row maxima
                 ctx.h0 = h0
@@ -147,7 +163,8 @@ class BDLRUCore(torch.autograd.Function):
             if observe is not None:   # module hooks of the fused conv / gates (model.py)
                 observe(x, xc, rg)
             y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train,
-                                               gate_b=gate_b, seq=seq, last_only=last_only)
+                                               gate_b=gate_b, seq=seq, last_only=last_only,
+                                               batch_row=batch_row)
         ctx.use_conv = use_conv
         ctx.last_only = last_only
         ctx.has_h0 = h0 is not None and pad_len is None
@@ -173,15 +190,20 @@ class BDLRUCore(torch.autograd.Function):
         dxz = torch.empty_like(xz)
         drg, dxc, dlam, dgate_b, dh0 = kernels.gate_scan_bwd(
             rg, xc, z, lam, carries, dy, dxz[..., H:], dh0_rows=ctx.h0_rows, gate_b=gate_b,
-            seq=seq, last_only=ctx.last_only)
+            seq=seq, last_only=ctx.last_only, batch_row=ctx.batch_row)
         drg2 = drg.view(rows, H2)
         gflops = 2 * rows * H * H2
         # dL/dxc through the gates GEMM: the conv backward reads it as its second
         # gradient term (g1 + g2 on load, no separate add pass)
         r_drg = rmax_buffer(drg2, H, H2) if ctx.r_xc is not None else None
         dxc_g = _timed("gemm", gflops, mm_nn, drg2, gate_w, rmax=r_drg).view_as(dxc)
-        dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H), ymax=r_drg,
-                         xmax=ctx.r_xc)
+        # the conv backward right behind the GEMM that wrote dxc_g (its inputs
+        # still in the Infinity Cache), the weight gradient after it
+        # (RECBLR_CONV_FIRST=0: the weight gradient first, the round-3 order)
+        dgate_w = None
+        if not _CONV_FIRST:
+            dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H), ymax=r_drg,
+                             xmax=ctx.r_xc)
         dconv_w = dconv_b = None
         if ctx.use_conv:
             dw, dconv_b = kernels.conv_silu_bwd(x, conv_w, conv_b, dxc, dxc_g, dxz[..., :H],
@@ -189,6 +211,9 @@ class BDLRUCore(torch.autograd.Function):
             dconv_w = dw.view_as(conv_w)
         else:
             torch.add(dxc, dxc_g, out=dxz[..., :H])
+        if dgate_w is None:
+            dgate_w = _timed("gemm", gflops, wgrad, drg2, xc.reshape(rows, H), ymax=r_drg,
+                             xmax=ctx.r_xc)
         if ctx.pad_len is not None:   # + the pad-prefix state's share, in place
             kernels.pad_prefix_bwd(conv_b, gate_w, gate_b, lam, ctx.pad_len, dh0.float(),
                                    into=(dconv_b, dgate_w, dgate_b, dlam))
@@ -207,6 +232,8 @@ class BDLRUCore(torch.autograd.Function):
         H = xz.shape[-1] // 2
         rows = xz.shape[0]
         want_rmax = ctx.want_rmax
+        if ctx.batch_row is not None:   # batch order -> packed order
+            dy = dy.index_select(0, ctx.batch_row)
         (dxz, drg, xc, r_drg, r_xc, dlam, dgate_b, dh0, dconv_w, dconv_b) = kernels.grl_bwd(
             xz, conv_w, conv_b, linear_mod._weight_split(gate_w, False),
             linear_mod._weight_split(gate_w, True), gate_b, lam, ctx.h0, seq, tile_carries,
@@ -240,7 +267,8 @@ def bd_lru(xz, conv_w, conv_b, gate_w, gate_b, lam, use_conv=True, pad=None, seq
     unpadded sequence, run_with_unseen.py:222-225).
     seq: kernels.Packed — xz holds only each sequence's first len_b positions
     ([ntok, 2H]); the batch's L (for the pad prefix) is seq.L.
-    last_only: return only each sequence's last position, [B, H] (fp32).
+    last_only: return only each sequence's last position, [B, H] (fp32); in
+    batch order when seq.order is set, else in packed-sequence order.
     observe: optional callable (x, xc, rg) run in the forward (module hooks)."""
     if pad is None:
         P = pow2_pad_len(seq.L if seq is not None else xz.shape[1])

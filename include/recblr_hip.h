@@ -154,18 +154,22 @@ int rb_gate_scan_bwd(const float* rg, int64_t rg_rs, const float* xc,
  * RecBLR.py:84, on the last layer): the forward writes y_last [B, H]
  * contiguous (row b = y at position L-1, or at seq_offsets[b+1]-1 packed)
  * instead of y; the backward takes dy_last [B, H] with dy = 0 at every other
- * position (no [B, L, H] dy is materialised or read).  fp32. */
+ * position (no [B, L, H] dy is materialised or read).  fp32.
+ * batch_row (int64 [B], a permutation of 0..B-1, or NULL): sequence b's row
+ * of y_last / dy_last is batch_row[b] instead of b — packed sequences run
+ * longest first, so the last layer's output lands in batch order without a
+ * gather (and its gradient is read without a scatter). */
 int rb_gate_scan_fwd_last(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                           const float* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* h0, int64_t h0_bs, float* y_last, float* carries,
                           int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets,
-                          void* stream);
+                          const int64_t* batch_row, void* stream);
 int rb_gate_scan_bwd_last(const float* rg, int64_t rg_rs, const float* xc, int64_t xc_rs,
                           const float* z, int64_t z_rs, const float* lam, const float* gate_b,
                           const float* carries, const float* dy_last, float* drg,
                           int64_t drg_rs, float* dxc, int64_t dxc_rs, float* dz, int64_t dz_rs,
                           float* part, float* dh0_part, int64_t B, int64_t L, int64_t H,
-                          const int64_t* seq_offsets, void* stream);
+                          const int64_t* seq_offsets, const int64_t* batch_row, void* stream);
 
 /* The state the power-of-two left padding leaves in the recurrence
  * (RecBLR.py:176-179: F.pad of x by P zero steps before conv + scan), without

@@ -125,6 +125,29 @@ def test_embedding_bwd_skewed_and_deterministic(cuda):
     assert torch.equal(dw, kernels.embedding_bwd(idx, grad, V, padding_idx=0))
 
 
+@pytest.mark.parametrize("M", [1, 63, 257, 16385, 409600])
+def test_embedding_counting_sort_plan_equals_radix_plan(cuda, M):
+    """Tables up to 16384 rows are planned by the four-launch counting sort,
+    larger ones by the rocPRIM radix sort; both order each id's positions
+    ascending, so the segment sums are bitwise equal (the larger table's
+    extra rows stay zero).  Ragged M: fewer rows than row blocks, partial
+    64-row steps."""
+    from datamining_recblr_amd import kernels
+
+    V, d = 10544, 64
+    g = torch.Generator(device="cpu").manual_seed(M)
+    w = 1.0 / torch.arange(1, V + 1, dtype=torch.float64) ** 1.1
+    idx = torch.multinomial(w, M, replacement=True, generator=g).to(cuda)
+    grad = torch.randn(M, d, generator=g).to(cuda)
+    small = kernels.embedding_bwd(idx, grad, V, padding_idx=0)
+    big = kernels.embedding_bwd(idx, grad, 16385, padding_idx=0)
+    assert torch.equal(small, big[:V])
+    assert big[V:].abs().max().item() == 0.0
+    ref = torch.zeros(V, d, dtype=torch.float64, device=cuda).index_add_(0, idx, grad.double())
+    ref[0] = 0
+    close(small, ref.float(), atol=1e-3, rtol=1e-5, what="dW")
+
+
 @pytest.mark.parametrize("mode", ["none", "mask", "philox"])
 def test_silu_dropout(cuda, mode):
     from datamining_recblr_amd import kernels
@@ -433,6 +456,19 @@ def test_gate_scan_last_only_equals_full(cuda):
     r2 = kernels.gate_scan_bwd(rg, xc, z, lam, car, dyl, dz2, gate_b=gb, seq=seq, last_only=True)
     assert torch.equal(dz1, dz2)
     for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+    # batch_row: sequence s's row of y_last / dy_last is perm[s]
+    perm = torch.randperm(B, generator=g).to(cuda)
+    yp, _ = kernels.gate_scan_fwd(rg, xc, z, lam, h0, gate_b=gb, seq=seq, last_only=True,
+                                  batch_row=perm)
+    assert torch.equal(yp.index_select(0, perm), yl)
+    dyp = torch.empty_like(dyl)
+    dyp[perm] = dyl
+    dz3 = torch.empty(ntok, H, device=cuda)
+    r3 = kernels.gate_scan_bwd(rg, xc, z, lam, car, dyp, dz3, gate_b=gb, seq=seq, last_only=True,
+                               batch_row=perm)
+    assert torch.equal(dz1, dz3)
+    for a, b in zip(r1, r3):
         assert torch.equal(a, b)
 
 

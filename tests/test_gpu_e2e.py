@@ -1,5 +1,6 @@
 """End-to-end parity of the configurations the benchmark times, with the
-split-bf16 projection GEMM (csrc/gemm_split.hip, rb_gemm_nt) asserted engaged.
+f16x3 projection GEMMs (csrc/gemm_half.hip: rb_gemm_nt_h forward / input
+gradients, rb_gemm_tn_h weight gradients) asserted engaged.
 
 RecBLR.calculate_loss + backward (RecBLR.py:86-103, 210-227 and the encoder
 :75-84, :140-207) on the GPU against the CPU oracle (oracle/recblr_oracle.py,
@@ -15,7 +16,7 @@ Shapes:
   stand-in): d = 128, L = 50, B = 2048 (train_batch_size), n_items = 10,544.
 Each runs packed (the benchmark's default) and dense, with the split
 threshold as shipped and at 0 (every projection, the gathered last-layer
-tail included, through rb_gemm_nt).  Eval mode: dropout streams differ
+tail included, through the split kernels).  Eval mode: dropout streams differ
 between implementations.
 """
 import pytest
@@ -87,9 +88,9 @@ def test_train_step_matches_oracle_with_split_gemm(cuda, split_gemm_calls, monke
     big = [c for c in split_gemm_calls if c[0] == rows]
     # per layer and direction: in, gates, out (fwd) and their dX GEMMs; layer
     # 0's FFN (the last layer's tail runs on the B gathered rows).  Packed,
-    # the gates forward GEMM runs inside rb_grl_fwd (RECBLR_FUSED_GRL, on by
-    # default) and with RECBLR_FUSED_GRL_BWD=1 the gates dX GEMM inside
-    # rb_grl_bwd.
+    # with RECBLR_FUSED_GRL=1 (opt-in, off by default) the gates forward GEMM
+    # runs inside rb_grl_fwd, and with RECBLR_FUSED_GRL_BWD=1 the gates dX
+    # GEMM inside rb_grl_bwd.
     on = packed and recurrence._FUSED
     on_b = on and recurrence._FUSED_BWD
     assert len(big) >= 12 - 2 * on - 2 * on_b, (rows, split_gemm_calls)

@@ -402,6 +402,36 @@ def test_weight_gradient_columns_spread_over_2_to_the_16(cuda):
     assert e_h < 1e-5 and e_h < 4 * max(e_t, 1e-7), (e_h, e_t)
 
 
+@pytest.mark.parametrize("spread", [24, 40])
+@pytest.mark.parametrize("N,K", [(256, 128), (512, 256), (128, 512)])
+def test_weight_gradient_columns_spread_beyond_2_to_the_16(cuda, spread, N, K):
+    """Column magnitudes of dY and X spread over 2^24 and 2^40 inside every
+    row chunk: the columns far below the chunk max would lose bits under the
+    chunk's one scale, so the kernel detects them (the loaded values' column
+    maxima) and redoes that tile's chunk with one exact power-of-two scale
+    per column.  Per element at its own scale (dW[n, k] / (cy[n] cx[k])), at
+    the level of hipBLASLt's fp32 GEMM; rows with ordinary magnitudes (no
+    spread) take the one-pass path and stay bitwise as before."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(spread + N + K)
+    M, S = 40000, 64
+    cy = torch.exp2(-float(spread) * torch.arange(N) / (N - 1))
+    cx = torch.exp2(-float(spread) * torch.arange(K) / (K - 1))
+    dy = (torch.randn(M, N, generator=g) * cy).to(cuda)
+    x = (torch.randn(M, K, generator=g) * cx).to(cuda)
+    dw = kernels.colsum(kernels.gemm_tn_h(dy, x, _row_group_max(dy), _row_group_max(x), S)
+                        .view(S, -1)).view(N, K)
+    ref = dy.double().t() @ x.double()
+    scale = (cy[:, None] * cx[None, :]).double().to(cuda)
+
+    def scaled(out):
+        return ((out.double() - ref).abs() / scale).max().item() / (ref.abs() / scale).max().item()
+
+    e_h, e_t = scaled(dw), scaled(dy.t() @ x)
+    assert e_h < 1e-5 and e_h < 4 * max(e_t, 1e-7), (e_h, e_t)
+
+
 @pytest.mark.parametrize("M,K,N", [(2048, 512, 128), (2048, 128, 512), (2048, 256, 128),
                                    (77, 64, 32), (5000, 96, 96), (196608 + 8024, 256, 512),
                                    (196608 + 8024, 512, 128), (65536 * 3 + 31, 128, 256)])

@@ -13,3 +13,5 @@ cp gpurun_out/prof/bench_kernel_stats.csv gpurun_out/r04_v1_kernel_stats.csv 2>/
 python tools/step_sequence.py gpurun_out/prof/bench_kernel_trace.csv 10 > gpurun_out/r04_v1_step_sequence.txt 2>&1
 rm -rf gpurun_out/prof
 exit $rc
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 tools/bin/gemm_epi 204632 9 > gpurun_out/r04_gemm_epi.txt 2>&1
