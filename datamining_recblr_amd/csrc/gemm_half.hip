@@ -1019,7 +1019,6 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   const int ncg = (op == 0 ? CF::YC : CF::XC) / 4;   // column groups of the operand
   const int cc = loader ? lt % ncg : 0;
   const int rg = loader ? lt / ncg : 0;
-  const float* src = op == 0 ? Y + n0 + 4 * cc : X + k0 + 4 * cc;
   const int64_t ld = op == 0 ? ldy : ldx;
   // the operand scale of each of the thread's 4 columns: the chunk's (the
   // first pass) or the column's own (the redo pass, below)
@@ -1038,42 +1037,50 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
 
   f32x4 raw0[8], raw1[8];
+  // The operand rows of the chunk through a buffer descriptor (wave-uniform
+  // base: the chunk's first row of this wave's operand; records: the chunk's
+  // bytes): 32-bit lane offsets, and rows past the chunk read as zeros by the
+  // descriptor's range check — which covers the lane offset only, so the row
+  // is in the lane offset, never in the scalar one.  Plain (default-policy)
+  // loads: the other tiles of this split re-read these rows from L2.
+  const float* cbase = (op == 0 ? Y + n0 : X + k0) + r_begin * ld;
+  const uint64_t cb = reinterpret_cast<uint64_t>(cbase);
+  // (readfirstlane returns int: through uint32_t, or the low word's sign
+  // would extend into the high one)
+  const uint64_t cbu =
+      (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)cb) |
+      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(cb >> 32)) << 32);
+  const uint32_t ld4 = __builtin_amdgcn_readfirstlane((uint32_t)(ld * 4));
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>(cbu), 0, (int)(nrows * ld4), 0x00020000);
+  const uint32_t voff = (uint32_t)(rg * 8) * ld4 + (uint32_t)(16 * cc);
   auto load = [&](int t, f32x4 (&r)[8]) {
     if (!loader) return;
-    const int64_t row0 = r_begin + (int64_t)t * 32 + rg * 8;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      int64_t row = row0 + q;
-      row = row < r_end ? row : r_end - 1;  // rows past the chunk: zeroed on convert
-      // plain loads: the other tiles of this split re-read these rows (L2)
-      r[q] = *reinterpret_cast<const f32x4*>(src + row * ld);
-    }
+    for (int q = 0; q < 8; ++q)
+      r[q] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (uint32_t)(t * 32 + q) * ld4, 0, 0));
   };
-  auto convert = [&](f32x4 (&r)[8], int t, int buf) {
-    if (!loader) return;
-    const int64_t row0 = r_begin + (int64_t)t * 32 + rg * 8;
-    if (row0 + 8 > r_end) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        if (row0 + q >= r_end) r[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-    }
+  // one column c of the thread's 8 x 4 block of step t into image `buf`
+  // (rows past the chunk are zeros from the loads: no branch, so the
+  // conversion sits in one basic block with the MFMAs it overlaps)
+  auto convert_col = [&](const f32x4 (&r)[8], int t, int buf, int c) {
+    (void)t;
     const uint32_t img = smem_base + buf * CF::STAGE + (op == 0 ? 0 : 2 * CF::YPLANE);
     const uint32_t plane = op == 0 ? CF::YPLANE : CF::XPLANE;
+    f16x8 h0, h1;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      f16x8 h0, h1;
-#pragma unroll
-      for (int q = 0; q < 8; q += 2) {
-        if constexpr (!PERCOL) cm[c] = max3abs(cm[c], r[q][c], r[q + 1][c]);
-        f16x2 p0, p1;
-        split2h(f32x2{r[q][c], r[q + 1][c]} * scv[c], p0, p1);
-        h0[q] = p0[0]; h0[q + 1] = p0[1];
-        h1[q] = p1[0]; h1[q + 1] = p1[1];
-      }
-      const uint32_t off = tn_off(4 * cc + c, rg);
-      hds_write16(img + off, h0);
-      hds_write16(img + plane + off, h1);
+    for (int q = 0; q < 8; q += 2) {
+      const float v0 = r[q][c], v1 = r[q + 1][c];
+      if constexpr (!PERCOL) cm[c] = max3abs(cm[c], v0, v1);
+      f16x2 p0, p1;
+      split2h(f32x2{v0, v1} * scv[c], p0, p1);
+      h0[q] = p0[0]; h0[q + 1] = p0[1];
+      h1[q] = p1[0]; h1[q + 1] = p1[1];
     }
+    const uint32_t off = tn_off(4 * cc + c, rg);
+    hds_write16(img + off, h0);
+    hds_write16(img + plane + off, h1);
   };
 
   f32x16 acc[2][2];
@@ -1085,47 +1092,75 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
       for (int e = 0; e < 16; ++e) acc[a][b][e] = 0.0f;
 
   const int h = lane >> 5;
-  auto mma = [&](int buf) {
+  // The products of image `buf` (one m-step of 32 rows: two substeps of 16);
+  // with CONV, step t's columns converted into image nbuf in front of each
+  // substep's fragment reads — substep 1's splits and LDS writes issue while
+  // substep 0's MFMAs execute (each substep: two columns, fragment reads,
+  // their wait, 12 MFMAs).
+  auto mma = [&](int buf, auto conv_c, const f32x4 (&r)[8], int t, int nbuf) {
+    constexpr bool CONV = decltype(conv_c)::value;
     const uint32_t iy = smem_base + buf * CF::STAGE;
     const uint32_t ix = iy + 2 * CF::YPLANE;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      f16x8 a[2][2], b[2][2];
+      if constexpr (CONV) {
+        convert_col(r, t, nbuf, 2 * st);
+        convert_col(r, t, nbuf, 2 * st + 1);
+      }
+      // B fragments of both column blocks, then the A fragments one row
+      // block at a time (24 fragment registers live, not 32)
+      f16x8 b[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint32_t ob = tn_off(64 * wk + 32 * j + (lane & 31), 2 * st + h);
+        b[j][0] = hds_read16<f16x8>(ix + ob);
+        b[j][1] = hds_read16<f16x8>(ix + CF::XPLANE + ob);
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const uint32_t oa = tn_off(64 * wm + 32 * i + (lane & 31), 2 * st + h);
-        const uint32_t ob = tn_off(64 * wk + 32 * i + (lane & 31), 2 * st + h);
-        a[i][0] = hds_read16<f16x8>(iy + oa);
-        a[i][1] = hds_read16<f16x8>(iy + CF::YPLANE + oa);
-        b[i][0] = hds_read16<f16x8>(ix + ob);
-        b[i][1] = hds_read16<f16x8>(ix + CF::XPLANE + ob);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[1][0]), "+v"(a[1][1]), "+v"(b[0][0]),
-                     "+v"(b[0][1]), "+v"(b[1][0]), "+v"(b[1][1]));
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
+        f16x8 a0 = hds_read16<f16x8>(iy + oa);
+        f16x8 a1 = hds_read16<f16x8>(iy + CF::YPLANE + oa);
+        if (i == 0)
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(a0), "+v"(a1), "+v"(b[0][0]), "+v"(b[0][1]), "+v"(b[1][0]),
+                         "+v"(b[1][1]));
+        else
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a0), "+v"(a1));
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mfma_h(a[i][1], b[j][0], acc[i][j]);
-          acc[i][j] = mfma_h(a[i][0], b[j][1], acc[i][j]);
-          acc[i][j] = mfma_h(a[i][0], b[j][0], acc[i][j]);
+          acc[i][j] = mfma_h(a1, b[j][0], acc[i][j]);
+          acc[i][j] = mfma_h(a0, b[j][1], acc[i][j]);
+          acc[i][j] = mfma_h(a0, b[j][0], acc[i][j]);
         }
+      }
     }
   };
+  using conv_t = std::true_type;
+  using noconv_t = std::false_type;
 
+  // Pipeline: raw0 / raw1 hold the register copies of steps loaded two steps
+  // ahead; image t & 1 holds step t.  Step t's products run with step t+1's
+  // conversion into the other image (last read by step t-1's products, which
+  // every wave finished before the previous barrier); one barrier per step.
   if (T > 0) load(0, raw0);
   if (T > 1) load(1, raw1);
+  if (T > 0 && loader) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) convert_col(raw0, 0, 0, c);
+  }
+  if (T > 2) load(2, raw0);
+  __syncthreads();
   for (int t = 0; t < T; t += 2) {
-    convert(raw0, t, 0);
-    if (t + 2 < T) load(t + 2, raw0);
+    if (loader && t + 1 < T) mma(0, conv_t{}, raw1, t + 1, 1);
+    else mma(0, noconv_t{}, raw1, 0, 0);
+    if (t + 3 < T) load(t + 3, raw1);
     __syncthreads();
-    mma(0);
     if (t + 1 < T) {
-      convert(raw1, t + 1, 1);
-      if (t + 3 < T) load(t + 3, raw1);
+      if (loader && t + 2 < T) mma(1, conv_t{}, raw0, t + 2, 0);
+      else mma(1, noconv_t{}, raw0, 0, 0);
+      if (t + 4 < T) load(t + 4, raw0);
       __syncthreads();
-      mma(1);
     }
   }
 

@@ -12,4 +12,5 @@ rc=$?
 cp gpurun_out/prof/bench_kernel_stats.csv gpurun_out/${T}_kernel_stats.csv 2>/dev/null
 python tools/step_sequence.py gpurun_out/prof/bench_kernel_trace.csv 10 > gpurun_out/${T}_step_sequence.txt 2>&1
 rm -rf gpurun_out/prof
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 tools/bin/mix_bench 204632 7 > gpurun_out/${T}_mix_bench.txt 2>&1
