@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 35; }
+int rb_version(void) { return 36; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -473,14 +473,16 @@ int rb_item_ce_probs(const float* seq, const float* items, const int64_t* target
                               reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_item_split_h(const float* x, int64_t n, int64_t d, void* image, int* exps, void* stream) {
+int rb_item_split_h(const float* x, int64_t n, int64_t d, void* image, int* exps,
+                    float* group_max, void* stream) {
   if (!x || !image || !exps) return fail("rb_item_split_h: null pointer");
   if (n <= 0) return fail("rb_item_split_h: n must be positive");
   if (d != 16 && d != 32 && d != 64 && d != 128 && d != 256)
     return fail("rb_item_split_h: d must be 16, 32, 64, 128 or 256");
   if (!aligned16(x) || !aligned16(image)) return fail("rb_item_split_h: operands must be 16-B aligned");
   if (n >= (int64_t(1) << 31)) return fail("rb_item_split_h: n too large");
-  return launch_item_split_h(x, n, d, image, exps, reinterpret_cast<hipStream_t>(stream));
+  return launch_item_split_h(x, n, d, image, exps, group_max,
+                             reinterpret_cast<hipStream_t>(stream));
 }
 
 namespace {

@@ -404,7 +404,8 @@ int launch_item_ce_probs(const float* E, const float* W, const int64_t* tgt, con
                          int64_t n_total, float* out, int64_t ld, hipStream_t st);
 int launch_item_scores(const float* E, const float* W, int64_t B, int64_t V, int64_t D,
                        float* out, hipStream_t st);
-int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex, hipStream_t st);
+int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex, float* gmax,
+                        hipStream_t st);
 int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                          const int64_t* tgt, int64_t B, int64_t V, int64_t D, float* lse,
                          float* loss, void* ws, int64_t ws_bytes, hipStream_t st);

@@ -385,8 +385,9 @@ __global__ void __launch_bounds__(64) k_emb_place(const int64_t* __restrict__ id
     }
     if (ok) {
       const int before = run[k];
-      vals[seg[k] + cnt[(int64_t)blockIdx.x * V + k] + before + __popcll(same & lt)] =
-          (int)i;
+      const int64_t slot = (int64_t)seg[k] + cnt[(int64_t)blockIdx.x * V + k] + before +
+                           __popcll(same & lt);
+      if (slot < M) vals[slot] = (int)i;   // always (the slots are a permutation)
       // the group's lowest lane advances the key's count (groups: distinct keys)
       if ((same & lt) == 0) run[k] = before + __popcll(same);
     }

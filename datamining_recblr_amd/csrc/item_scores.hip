@@ -711,6 +711,55 @@ __global__ __launch_bounds__(256) void k_split_rows_h(const float* __restrict__ 
   if (lane == 0) ex[r] = e;
 }
 
+// The same split with the 32-row group maxima of x as a side output (the
+// weight-gradient GEMM's operand scales: rb_group_absmax's values, bit for
+// bit): 32 rows per workgroup, a wave's 8 rows loaded together (d <= 256:
+// one float4 per lane and row), the group's max over the four waves in LDS.
+__global__ __launch_bounds__(256) void k_split_rows_hg(const float* __restrict__ X, int64_t N,
+                                                       int D, _Float16* __restrict__ img,
+                                                       int* __restrict__ ex,
+                                                       float* __restrict__ gmax) {
+  __shared__ float sm[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * 32 + w * 8;
+  const int nq = D / 4;
+  const float4* x = reinterpret_cast<const float4*>(X);
+  float4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    v[j] = (r0 + j < N && lane < nq) ? x[(r0 + j) * nq + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float wm = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float m = fmaxf(fmaxf(fabsf(v[j].x), fabsf(v[j].y)), fmaxf(fabsf(v[j].z), fabsf(v[j].w)));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    wm = fmaxf(wm, m);
+    const int64_t r = r0 + j;
+    if (r < N) {
+      const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
+      if (lane < nq) {
+        const float t[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+        _Float16 a[4], b[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float sv = __builtin_amdgcn_ldexpf(t[i], kTS - e);
+          a[i] = (_Float16)sv;
+          b[i] = (_Float16)(sv - (float)a[i]);
+        }
+        typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+        _Float16* h0 = img + r * 2 * D;
+        *reinterpret_cast<f16x4*>(h0 + 4 * lane) = f16x4{a[0], a[1], a[2], a[3]};
+        *reinterpret_cast<f16x4*>(h0 + D + 4 * lane) = f16x4{b[0], b[1], b[2], b[3]};
+      }
+      if (lane == 0) ex[r] = e;
+    }
+  }
+  if (lane == 0) sm[w] = wm;
+  __syncthreads();
+  if (threadIdx.x == 0) gmax[blockIdx.x] = fmaxf(fmaxf(sm[0], sm[1]), fmaxf(sm[2], sm[3]));
+}
+
 // this lane's register operand: row `row` of an image, k-blocks 16s + 8h ..
 // 16s + 8h + 7 of both planes (the MFMA fragment of step s)
 template <int D>
@@ -1172,8 +1221,13 @@ int launch_item_ce_probs(const float* E, const float* W, const int64_t* tgt, con
   return launch_status("rb_item_ce_probs");
 }
 
-int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex,
+int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex, float* gmax,
                         hipStream_t st) {
+  if (gmax != nullptr) {
+    hipLaunchKernelGGL(k_split_rows_hg, dim3((unsigned)((N + 31) / 32)), dim3(256), 0, st, X, N,
+                       (int)D, (_Float16*)img, ex, gmax);
+    return launch_status("rb_item_split_h");
+  }
   hipLaunchKernelGGL(k_split_rows_h, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, X, N, (int)D,
                      (_Float16*)img, ex);
   return launch_status("rb_item_split_h");

@@ -767,10 +767,10 @@ class SplitRows:
     img [n, 2d] fp16 (per row d halfs x0 | d halfs x1), exps [n] int32.  Row
     slices are views (rows(v0, v1)) for the sliced CE backward."""
 
-    __slots__ = ("img", "exps")
+    __slots__ = ("img", "exps", "gmax")
 
-    def __init__(self, img, exps):
-        self.img, self.exps = img, exps
+    def __init__(self, img, exps, gmax=None):
+        self.img, self.exps, self.gmax = img, exps, gmax
 
     @property
     def shape(self):
@@ -780,8 +780,9 @@ class SplitRows:
         return SplitRows(self.img[v0:v1], self.exps[v0:v1])
 
 
-def item_split_h(x) -> SplitRows:
-    """x [n, d] fp32 -> SplitRows (x = 2^(e-14) (x0 + x1) per row, 22 bits)."""
+def item_split_h(x, group_max: bool = False) -> SplitRows:
+    """x [n, d] fp32 -> SplitRows (x = 2^(e-14) (x0 + x1) per row, 22 bits);
+    group_max: also .gmax [ceil(n/32)], group_absmax(x) from the same pass."""
     _check(x, "split operand")
     if x.dim() != 2 or x.shape[1] not in ITEM_DIMS:
         raise ValueError(f"[n, d] with d in {ITEM_DIMS} required, got {tuple(x.shape)}")
@@ -789,9 +790,11 @@ def item_split_h(x) -> SplitRows:
     n, d = x.shape
     img = torch.empty((n, 2 * d), device=x.device, dtype=torch.float16)
     exps = torch.empty((n,), device=x.device, dtype=torch.int32)
+    gmax = (torch.empty(((n + 31) // 32,), device=x.device, dtype=torch.float32) if group_max
+            else None)
     _launch("rb_item_split_h", 8 * n * d + 4 * n, x.data_ptr(), n, d, img.data_ptr(),
-            exps.data_ptr(), _stream(x))
-    return SplitRows(img, exps)
+            exps.data_ptr(), None if gmax is None else gmax.data_ptr(), _stream(x))
+    return SplitRows(img, exps, gmax)
 
 
 def _split_operands(seq, items, target):

@@ -156,8 +156,9 @@ class GatedRecurrentLayer(nn.Module):
         y = bd_lru(xz, self.conv1d.weight, self.conv1d.bias, self.gates.weight,
                    self.gates.bias, self.Lambda, use_conv=not self.disable_conv1d, pad=pad,
                    seq=seq, last_only=last_only, observe=observe)
-        if last_only and seq.order is None:
-            y = y.index_select(0, seq.inv)   # packed-sequence order -> batch order
+        if last_only:
+            if seq.order is None:   # packed-sequence order -> batch order
+                y = y.index_select(0, seq.inv)
         elif rows is not None:
             y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
         return self.output(y)

@@ -104,12 +104,13 @@ def _bwd_f16(seq, table, target, lse, dloss, want_seq, want_items, split):
     if want_items:
         Vp = p.shape[1]
         S1 = max(8, min(_tn_splits8(seq.device, (Vp // 256) * (d // 128)), B // 256 // 8 * 8))
-        parts = _timed("gemm", fl, kernels.gemm_tn_h, p, seq, bmax, kernels.group_absmax(seq), S1)
+        smax = s_seq.gmax if s_seq.gmax is not None else kernels.group_absmax(seq)
+        parts = _timed("gemm", fl, kernels.gemm_tn_h, p, seq, bmax, smax, S1)
         dtable = kernels.colsum(parts.view(S1, -1)).view(Vp, d)[:V]
     if want_seq:
         S2 = _tn_splits8(seq.device, (B // 256) * (d // 128), div=2)
-        parts = _timed("gemm", fl, kernels.gemm_tn_h, pt, table, gmax,
-                       kernels.group_absmax(table), S2)
+        tmax = s_tab.gmax if s_tab.gmax is not None else kernels.group_absmax(table)
+        parts = _timed("gemm", fl, kernels.gemm_tn_h, pt, table, gmax, tmax, S2)
         dseq = kernels.colsum(parts.view(S2, -1)).view(B, d)
     return dseq, dtable
 
@@ -145,7 +146,10 @@ class _ItemCE(torch.autograd.Function):
     def forward(ctx, seq, table, target):
         seq, table = seq.contiguous(), table.contiguous()
         if CE_PIPE == "f16":
-            s_seq, s_tab = kernels.item_split_h(seq), kernels.item_split_h(table)
+            # the split also gives the 32-row group maxima the f16 backward's
+            # weight-gradient GEMMs scale these operands by
+            s_seq = kernels.item_split_h(seq, group_max=True)
+            s_tab = kernels.item_split_h(table, group_max=True)
             loss, lse = kernels.item_ce_fwd_h(s_seq, s_tab, target)
             ctx.split = (s_seq, s_tab)
         else:

@@ -342,8 +342,11 @@ int rb_item_ce_probs(const float* seq, const float* items, const int64_t* target
  * split into x0 = f16(x'), x1 = f16(x' - x0); a score is x0.y0 + x0.y1 + x1.y0
  * in fp32 on v_mfma_f32_32x32x16_f16, un-scaled exactly.
  * rb_item_split_h: x [n, d] fp32 (16-B aligned) -> image [n, 2d] fp16
- * (row: d halfs x0 | d halfs x1, 16-B aligned) and exps [n] int32. */
-int rb_item_split_h(const float* x, int64_t n, int64_t d, void* image, int* exps, void* stream);
+ * (row: d halfs x0 | d halfs x1, 16-B aligned) and exps [n] int32;
+ * group_max (float [ceil(n/32)], or NULL): max |x| over each 32-row group —
+ * rb_group_absmax's output, for the weight-gradient GEMM on the same x. */
+int rb_item_split_h(const float* x, int64_t n, int64_t d, void* image, int* exps,
+                    float* group_max, void* stream);
 
 /* rb_item_ce_fwd on split images (workspace: rb_item_ce_workspace). */
 int rb_item_ce_fwd_h(const void* seq_img, const int* seq_exp, const void* item_img,

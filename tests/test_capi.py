@@ -71,11 +71,11 @@ def test_row_conv_and_batched_split_argument_errors():
 def test_f16_item_ce_argument_errors():
     """ABI 24 entry points (the CE on split images) validate before any HIP call."""
     lib = _lib.load()
-    rc = lib.rb_item_split_h(None, 4, 128, 16, 16, None)
+    rc = lib.rb_item_split_h(None, 4, 128, 16, 16, None, None)
     assert rc == _lib.RB_EINVAL and b"null" in lib.rb_last_error_string()
-    rc = lib.rb_item_split_h(16, 4, 48, 16, 16, None)
+    rc = lib.rb_item_split_h(16, 4, 48, 16, 16, None, None)
     assert rc == _lib.RB_EINVAL and b"d must be" in lib.rb_last_error_string()
-    rc = lib.rb_item_split_h(8, 4, 128, 16, 16, None)     # 8 is not 16-B aligned
+    rc = lib.rb_item_split_h(8, 4, 128, 16, 16, None, None)     # 8 is not 16-B aligned
     assert rc == _lib.RB_EINVAL and b"aligned" in lib.rb_last_error_string()
     rc = lib.rb_item_ce_fwd_h(16, None, 16, 16, 16, 4, 8, 128, 16, 16, 16, 1 << 20, None)
     assert rc == _lib.RB_EINVAL and b"exponent" in lib.rb_last_error_string()

@@ -235,7 +235,8 @@ def _split_ref(x):
             torch.from_numpy(e).to(dev))
 
 
-@pytest.mark.parametrize("n,d", [(1, 16), (37, 32), (300, 64), (1000, 128), (5, 256)])
+@pytest.mark.parametrize("n,d", [(1, 16), (37, 32), (300, 64), (1000, 128), (5, 256),
+                                 (10544, 128), (64, 256)])
 def test_item_split_h_planes(cuda, n, d):
     from datamining_recblr_amd import kernels
 
@@ -253,6 +254,11 @@ def test_item_split_h_planes(cuda, n, d):
                        (sp.exps - 14)[:, None].double())
     rel = ((back - x.double()).abs().amax(1) / x.double().abs().amax(1).clamp_min(1e-300))
     assert (rel <= 2.0 ** -21).all()
+    # with the 32-row group maxima (rb_item_split_h's group_max): the same
+    # planes and exponents, and rb_group_absmax's values bit for bit
+    sg = kernels.item_split_h(x, group_max=True)
+    assert torch.equal(sg.img, sp.img) and torch.equal(sg.exps, sp.exps)
+    assert torch.equal(sg.gmax, kernels.group_absmax(x))
 
 
 @pytest.mark.parametrize("B,V,d", [(1, 1, 16), (33, 64, 64), (300, 10544, 128), (37, 515, 256),
