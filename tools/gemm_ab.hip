@@ -114,21 +114,28 @@ int main(int argc, char** argv) {
   // weight gradients dW = dY^T X (split partials, no column sum)
   struct TShape { const char* name; int N, K, S; };
   const TShape tshapes[] = {{"gates.dW", 512, 256, 64}, {"in.dW", 512, 128, 128},
-                            {"w2.dW", 128, 512, 128}, {"out.dW", 128, 256, 256}};
+                            {"w2.dW", 128, 512, 128}, {"out.dW", 128, 256, 256},
+                            // the CE backward's products (B = 2048 rows of P, V = 10544
+                            // rows of P^T): M below, N, K, S
+                            {"ce.ditems", 10752, 128, 8}, {"ce.dseq", 2048, 128, 32}};
+  const int64_t tM[] = {M, M, M, M, 2048, 10544};
   float *Y, *ymax, *xmax, *parts;
   CK(hipMalloc(&Y, M * 512 * 4));
   CK(hipMalloc(&ymax, (M / 32 + 1) * 4));
   CK(hipMalloc(&xmax, (M / 32 + 1) * 4));
-  CK(hipMalloc(&parts, (size_t)256 * 128 * 256 * 4));
+  CK(hipMalloc(&parts, (size_t)16 << 20 << 2));
   fill<<<4096, 256>>>(Y, M * 512, 3, 1.0f);
   double ttot = 0;
-  for (const TShape& s : tshapes) {
-    gmax32<<<(unsigned)((M + 31) / 32), 256>>>(Y, M, s.N, ymax);
-    gmax32<<<(unsigned)((M + 31) / 32), 256>>>(A, M, s.K, xmax);
+  for (int si = 0; si < 6; ++si) {
+    const TShape& s = tshapes[si];
+    const int64_t Mt = tM[si];
+    if ((int64_t)Mt * s.N > M * 512 || (int64_t)s.S * s.N * s.K > (16 << 20)) return 2;
+    gmax32<<<(unsigned)((Mt + 31) / 32), 256>>>(Y, Mt, s.N, ymax);
+    gmax32<<<(unsigned)((Mt + 31) / 32), 256>>>(A, Mt, s.K, xmax);
     std::vector<float> ts;
     for (int rep = 0; rep < reps; ++rep) {
       CK(hipEventRecord(e0, 0));
-      if (launch_gemm_tn_h(Y, s.N, A, s.K, M, s.N, s.K, ymax, xmax, parts, s.S, 0)) return 1;
+      if (launch_gemm_tn_h(Y, s.N, A, s.K, Mt, s.N, s.K, ymax, xmax, parts, s.S, 0)) return 1;
       CK(hipEventRecord(e1, 0));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -142,7 +149,7 @@ int main(int argc, char** argv) {
     std::sort(ts.begin(), ts.end());
     const double us = ts[ts.size() / 2];
     ttot += us;
-    const double bytes = (double)M * (s.N + s.K) * 4;
+    const double bytes = (double)Mt * (s.N + s.K) * 4;
     printf("%-10s N=%3d K=%3d S=%3d  %7.1f us  %5.2f TB/s  min %7.1f  fnv %016llx\n", s.name, s.N,
            s.K, s.S, us, bytes / us / 1e6, ts[0], (unsigned long long)f);
   }
