@@ -255,3 +255,34 @@ def test_interaction_to_keeps_host_lengths():
     assert not hasattr(moved["item_id"], HOST_LENGTHS)
     # a CPU -> CPU move attaches nothing (the tensor is already on the host)
     assert not hasattr(inter.to("cpu")["item_length"], HOST_LENGTHS)
+
+
+@pytest.mark.parametrize("cus", [80, 104, 228, 256, 304])
+def test_ce_weight_gradient_splits_are_multiples_of_8(monkeypatch, cus):
+    """The CE backward's row splits for rb_gemm_tn_h (multiples of 8, >= 8)
+    on any CU count and batch: B = 768 / 1792 on 256 CUs and B = 2048 on a
+    304-CU part gave 84 / 36 / 36 before the rounding."""
+    from datamining_recblr_amd import linear, scoring
+
+    monkeypatch.setitem(linear._ncus, "fake", cus)
+    for B in (256, 512, 768, 1792, 2048, 4096):
+        for V in (500, 10544, 65536):
+            nt1 = ((V + 255) // 256) * 1
+            s1 = max(8, min(scoring._tn_splits8("fake", nt1), B // 256 // 8 * 8))
+            s2 = scoring._tn_splits8("fake", (B // 256) * 1, div=2)
+            assert s1 % 8 == 0 and s1 >= 8, (B, V, s1)
+            assert s2 % 8 == 0 and s2 >= 8, (B, V, s2)
+
+
+def test_ce_f16_grads_fall_back_past_the_weight_gradient_width():
+    """The f16 CE backward runs the item gradient as rb_gemm_tn_h with
+    N = V rounded up to 256 <= 65536; larger vocabularies take the sliced
+    path instead of failing in the kernel."""
+    from datamining_recblr_amd import linear, scoring
+
+    if scoring.CE_GRADS != "f16" or linear.gemm_format() != "f16x3":
+        pytest.skip("f16 CE gradients not selected in this environment")
+    seq = torch.empty(256, 128)
+    assert scoring._f16_grads_ok(seq, torch.empty(65536, 128))
+    assert not scoring._f16_grads_ok(seq, torch.empty(65537, 128))
+    assert not scoring._f16_grads_ok(torch.empty(300, 128), torch.empty(1000, 128))
