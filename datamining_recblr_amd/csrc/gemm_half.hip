@@ -725,7 +725,10 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
       const bool in = lane < 32 && myinfo >= 0;
       const uint32_t m_start = (uint32_t)__builtin_amdgcn_ballot_w64(in && (myinfo & 255) == 0);
       const uint32_t m_last = (uint32_t)__builtin_amdgcn_ballot_w64(in && ((myinfo >> 8) & 1));
-      const uint32_t m_ckpt = (uint32_t)__builtin_amdgcn_ballot_w64(in && (myinfo & 15) == 15);
+      // every 16th row except a sequence's last: the carry entering its next
+      // 16 steps (slots of the sequence's own tiles only, as rb_gate_scan_fwd)
+      const uint32_t m_ckpt = (uint32_t)__builtin_amdgcn_ballot_w64(
+          in && (myinfo & 15) == 15 && !((myinfo >> 8) & 1));
       const uint32_t l_start = m_start >> hsh;      // this lane's rows: bit o
       // does the tile's first row continue a sequence of the previous tile?
       const int tinfo = gs.rinfo[(int64_t)cur_mt * N_BM];

@@ -46,6 +46,16 @@ def _inputs(seq, H, dev, seed, tiny_rows=()):
     return (xz.to(dev), xc.to(dev), gw.to(dev), gb.to(dev), lam.to(dev), h0.to(dev))
 
 
+def _carries_close(seq, c, c_r):
+    """The carry slots of each sequence's own 16-step tiles (the rest of the
+    [B, nT, H] buffer is never written nor read)."""
+    lens = (seq.offsets[1:] - seq.offsets[:-1]).cpu()
+    nt = (lens + 15) // 16
+    valid = torch.arange(c.shape[1])[None, :] < nt[:, None]
+    a, b = c.cpu()[valid], c_r.cpu()[valid]
+    return _rel(a, b)
+
+
 def _rel(a, b):
     return ((a.double() - b.double()).abs().max() / b.double().abs().max().clamp_min(1e-30)).item()
 
@@ -101,7 +111,7 @@ def test_gate_gemm_equals_two_launch_path(cuda, kind, H, with_h0):
     assert kernels.gate_gemm_errors() == 0
     assert torch.equal(rg, rg_r)
     assert _rel(y, y_r) < 2e-6, _rel(y, y_r)
-    assert _rel(c, c_r) < 2e-6, _rel(c, c_r)
+    assert _carries_close(seq, c, c_r) < 2e-6, _carries_close(seq, c, c_r)
 
 
 @pytest.mark.parametrize("kind", ["bench", "mixed"])
@@ -119,7 +129,7 @@ def test_gate_gemm_last_rows_in_batch_order(cuda, kind):
     _, yl, c = _fused(seq, xz, xc, gw, gb, lam, h0, True, seq.order)
     torch.cuda.synchronize()
     assert kernels.gate_gemm_errors() == 0
-    assert _rel(yl, yl_r) < 2e-6 and _rel(c, c_r) < 2e-6
+    assert _rel(yl, yl_r) < 2e-6 and _carries_close(seq, c, c_r) < 2e-6
 
 
 def test_gate_gemm_flagged_rows(cuda):
@@ -139,7 +149,7 @@ def test_gate_gemm_flagged_rows(cuda):
     torch.cuda.synchronize()
     assert kernels.gate_gemm_errors() == 0
     assert torch.equal(rg, rg_r)
-    assert _rel(y, y_r) < 2e-6 and _rel(c, c_r) < 2e-6
+    assert _rel(y, y_r) < 2e-6 and _carries_close(seq, c, c_r) < 2e-6
 
 
 def test_gate_gemm_repeated_calls_and_rmax(cuda):
@@ -163,5 +173,6 @@ def test_gate_gemm_repeated_calls_and_rmax(cuda):
         torch.cuda.synchronize()
         assert torch.equal(rm, rm_r)
     assert kernels.gate_gemm_errors() == 0
-    for o in outs[1:]:
-        assert all(torch.equal(a, b) for a, b in zip(o, outs[0]))
+    for o in outs[1:]:   # deterministic: rg, y and the carry slots bit for bit
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+        assert _carries_close(seq, o[2], outs[0][2]) == 0.0
