@@ -302,21 +302,12 @@ def kernel_report(summ, steps, ntok_step=None, H=None, layers=None):
         path = {"ms_per_step": round(cms / steps, 4),
                 "achieved_gbs": round(cb / (cms * 1e-3) / 1e9, 1),
                 "frac": round(cb / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        # with the gates GEMM's BD-LRU epilogue (rb_gate_gemm_fwd_h, the
-        # default on packed batches) the gate kernel's forward (K2, 5N) runs
-        # inside that GEMM, timed with the GEMMs: the model then counts 15N
-        k2_fwd = any(n in summ for n in ("rb_gate_scan_fwd", "rb_grl_fwd"))
-        per_layer = 20.0 if k2_fwd else 15.0
         if ntok_step and H and layers:
-            mb = per_layer * ntok_step * H * 4 * layers
+            mb = 20.0 * ntok_step * H * 4 * layers
             path["model_bytes_per_step"] = int(mb)
             path["model_frac"] = round(mb / (cms / steps * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             path["model"] = ("SURVEY §8(d): 20 * ntok * H * 4 B per layer (fwd 7N + bwd 13N), "
-                             "ntok = packed tokens per step, against the path kernels' time"
-                             if k2_fwd else
-                             "SURVEY §8(d) less K2's forward (5N, in the gates GEMM's epilogue, "
-                             "rb_gate_gemm_fwd_h): 15 * ntok * H * 4 B per layer (K1 2N, K2^T 9N, "
-                             "K1^T 4N) against the conv and gate-backward kernels' time")
+                             "ntok = packed tokens per step, against the path kernels' time")
         rep["scan_conv_gate_path"] = path
     if tot_ms:
         rep["fused_path_total"] = {
@@ -924,23 +915,6 @@ def main():
         order_ab["note"] = ("RECBLR_CONV_FIRST A/B on the headline's batches: in the "
                             "GatedRecurrentLayer backward, the conv backward before the gates "
                             "weight gradient (its inputs just written) or after it; best of 3")
-    gate_ab = None
-    if not args.no_full_tail:
-        # the gates projection with the BD-LRU in its epilogue (rb_gate_gemm_fwd_h)
-        # against the gates GEMM + rb_gate_scan_fwd, alternated 3x on the lease
-        from datamining_recblr_amd import recurrence as _rec
-        saved_g = _rec.set_gate_gemm(True)
-        runs = {"gate_gemm": [], "two_launches": []}
-        for _ in range(3):
-            for name, on in (("gate_gemm", True), ("two_launches", False)):
-                _rec.set_gate_gemm(on)
-                runs[name].append(timed_variant(True, True)["ms_per_step"])
-        _rec.set_gate_gemm(saved_g)
-        gate_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
-        gate_ab["headline"] = "gate_gemm" if saved_g else "two_launches"
-        gate_ab["note"] = ("RECBLR_GATE_GEMM A/B on the headline's batches: the gates GEMM with "
-                           "the BD-LRU gates, scan and silu(z) merge in its epilogue vs the GEMM "
-                           "and rb_gate_scan_fwd; best of 3 alternated runs")
     adam_ab = None
     if not args.no_full_tail:
         # the optimizer update: rb_adam_step (one launch over every parameter)
@@ -1072,7 +1046,6 @@ def main():
             "ffn_act": ffn_act_ab,
             "adam": adam_ab,
             "bwd_order": order_ab,
-            "gate_gemm": gate_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

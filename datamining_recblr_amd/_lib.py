@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 37
+ABI_VERSION = 38
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -105,8 +105,7 @@ SIGNATURES = {
     "rb_gemm_split_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
     "rb_gemm_split_weight": (ctypes.c_int, [_fp, _i64, _i64, _i64, ctypes.c_int, _fp, _fp]),
     "rb_gemm_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
-    "rb_pack_plan": (ctypes.c_int, [_fp, _i64, _fp, _fp, _i64, _i64, _fp, _fp, _fp, _fp, _fp,
-                                    _fp]),
+    "rb_pack_plan": (ctypes.c_int, [_fp, _i64, _fp, _fp, _i64, _i64, _fp, _fp, _fp, _fp, _fp]),
     "rb_gemm_nt": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
                                   _fp]),
     "rb_gemm_h_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
@@ -115,9 +114,6 @@ SIGNATURES = {
                                     _fp, _fp]),
     "rb_gemm_nt_h_act": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, _fp,
                                         _fp, _u64, _f32, _fp]),
-    "rb_gate_gemm_fwd_h": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _fp, _i64, _fp, _fp, _fp,
-                                          _fp, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp, _fp,
-                                          _fp, _i64, ctypes.c_uint32, _fp, _fp]),
     "rb_adam_step": (ctypes.c_int, [_fp, _i64, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_double, _fp]),

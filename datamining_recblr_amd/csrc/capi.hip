@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 37; }
+int rb_version(void) { return 38; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -626,15 +626,13 @@ int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int 
 
 int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_offsets,
                  const int64_t* order, int64_t B, int64_t L, int64_t* ids, int64_t* row_pos,
-                 int64_t* inv, int64_t* last, int32_t* rinfo, void* stream) {
+                 int64_t* inv, int64_t* last, void* stream) {
   if (!item_seq || !seq_offsets || !order || !ids || !row_pos || !inv || !last)
     return fail("rb_pack_plan: null pointer");
   if (B < 1 || L < 1 || seq_rs < L) return fail("rb_pack_plan: bad shape or row stride");
   if ((B + 3) / 4 > 0x7fffffffLL) return fail("rb_pack_plan: grid too large");
-  if (rinfo && (L > 256 || B > (1 << 22)))
-    return fail("rb_pack_plan: rinfo needs L <= 256 and B <= 2^22");
   return launch_pack_plan(item_seq, seq_rs, seq_offsets, order, B, ids, row_pos, inv, last,
-                          rinfo, reinterpret_cast<hipStream_t>(stream));
+                          reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {
@@ -694,30 +692,6 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
   if ((M + 31) / 32 > 0x7fffffffLL) return fail("rb_gemm_nt_h: grid too large");
   return launch_gemm_nt_h(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate, rmax,
                           reinterpret_cast<hipStream_t>(stream));
-}
-
-int rb_gate_gemm_fwd_h(const float* xc, int64_t lda, int64_t M, int64_t H, const void* Wf,
-                       const float* z, int64_t z_rs, const float* gate_b, const float* lam,
-                       const float* h0, float* rg, int64_t ldo, float* y, int64_t y_rs,
-                       float* y_last, const int64_t* order, float* carries, int64_t nTc,
-                       const int32_t* rinfo, float* rmax, void* tails, int64_t tails_bytes,
-                       uint32_t epoch, int32_t* err, void* stream) {
-  if (!xc || !Wf || !z || !gate_b || !lam || !rg || !rinfo || !tails || !err)
-    return fail("rb_gate_gemm_fwd_h: null pointer");
-  if (!y == !y_last) return fail("rb_gate_gemm_fwd_h: exactly one of y and y_last");
-  if (M <= 0 || H <= 0 || H % 128 || H > 512)
-    return fail("rb_gate_gemm_fwd_h: H must be 128, 256, 384 or 512 and M > 0");
-  if (lda < H || lda % 4 || ldo < 2 * H || ldo % 4 || z_rs < H || (y && y_rs < H))
-    return fail("rb_gate_gemm_fwd_h: bad row strides");
-  if (!aligned16(xc) || !aligned16(Wf) || !aligned16(rg))
-    return fail("rb_gate_gemm_fwd_h: xc, Wf and rg must be 16-byte aligned");
-  if (carries && nTc < 1) return fail("rb_gate_gemm_fwd_h: carries need nTc >= 1");
-  if (epoch == 0) return fail("rb_gate_gemm_fwd_h: epoch 0 is the buffer's initial state");
-  if (tails_bytes < (M + 255) / 256 * H * 8) return fail("rb_gate_gemm_fwd_h: tails too small");
-  if ((M + 255) / 256 > 0x7fffffffLL / 8) return fail("rb_gate_gemm_fwd_h: grid too large");
-  return launch_gate_gemm_h(xc, lda, M, (int)H, Wf, z, z_rs, gate_b, lam, h0, rg, ldo, y, y_rs,
-                            y_last, order, carries, (int)nTc, rinfo, rmax, tails, epoch, err,
-                            reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,

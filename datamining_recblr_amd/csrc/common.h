@@ -282,7 +282,7 @@ DropSpec make_drop(const uint8_t* mask, uint64_t seed, float p);
 // host launch helpers (defined in the .hip files)
 int launch_pack_plan(const int64_t* seq, int64_t seq_rs, const int64_t* offs,
                      const int64_t* order, int64_t B, int64_t* ids, int64_t* pos, int64_t* inv,
-                     int64_t* last, int* rinfo, hipStream_t st);
+                     int64_t* last, hipStream_t st);
 int launch_split_weights(const rb_split_job* jobs, int n, hipStream_t st);
 int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st);
@@ -353,12 +353,6 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st);
-int launch_gate_gemm_h(const float* xc, int64_t lda, int64_t M, int H, const void* Wf,
-                       const float* z, int64_t z_rs, const float* gbias, const float* lam,
-                       const float* h0, float* rg, int64_t ldo, float* y, int64_t y_rs,
-                       float* y_last, const int64_t* order, float* carries, int nTc,
-                       const int* rinfo, float* rmax, void* tails, uint32_t epoch, int* err,
-                       hipStream_t st);
 int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                          const float* bias, float* out, int64_t ldo, float* rmax, float* act,
                          DropSpec drop, hipStream_t st);

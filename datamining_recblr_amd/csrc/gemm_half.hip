@@ -253,64 +253,11 @@ __device__ __forceinline__ void quad_transpose(float (&v)[4], int lane) {
 // w_1 bias gradient's partials).  Rows of a tile flagged for the cold
 // recompute tail are summed there instead, from their recomputed values.
 constexpr int N_DACT_MAXC = 512;   // LDS column sums: 8 waves x C floats
-
-// GATE (the gates projection of the BD-LRU, RecBLR.py:196-206, with the
-// gates, the recurrence and the silu(z) merge in its tile-end epilogue — the
-// "fused gate projection": rg [M, 2H] = xc W_g^T is still written (the
-// backward reads r and i), but the gate-scan kernel's reads of rg, xc and z
-// and its launch are gone).  A tile is 256 packed rows x NB/2 channel blocks
-// of 32 channels: the r columns of those channels in blocks 0 .. NB/2-1 and
-// their i columns (C offset H) in blocks NB/2 .. NB-1, so a lane's r and i
-// accumulators are the same (row, channel) pairs.  Rows are packed
-// sequences back to back (rinfo[row] = s << 9 | last << 8 | position, L <=
-// 256).  The epilogue:
-//   1. stores rg (raw, without the bias: the backward adds it as the gate
-//      kernels do) and forms alpha / b' = beta * xc in the accumulators (xc
-//      read back at the tile's channels; a sequence's first row folds in h0);
-//   2. scans the tile: per lane its four 4-row groups, the partner lane's
-//      (lane ^ 32 holds the interleaved groups), the 8 waves' 32-row
-//      composites through LDS;
-//   3. chains row tiles: a tile publishes the state after its last row to
-//      tails[tile, channel] as (epoch, value) — one 64-bit relaxed atomic
-//      store at agent scope per channel, so no fence is needed — and the next
-//      row tile, if its first row continues a sequence, spins on that word
-//      until the epoch matches (bounded: err is set after ~50 ms).  With L
-//      <= 256 a tile's last-row state never depends on its predecessor (the
-//      sequence holding it started inside the tile), so it is published
-//      before any wait and no chain forms;
-//   4. runs the rows from their exact incoming states: y = silu(z) h (every
-//      row, or each sequence's last row into y_last in batch order) and the
-//      16-step carry checkpoints rb_gate_scan_bwd reads.
-struct GateSpec {
-  const float* z;            // z = xz[:, H:] (row stride z_rs)
-  int64_t z_rs;
-  const float* gbias;        // [2H]
-  const float* lam;          // Lambda [H]
-  const float* h0;           // [H] or null (zero)
-  float* y;                  // [M, H] (row stride y_rs) or null
-  int64_t y_rs;
-  float* y_last;             // [S, H] or null: each sequence's last row
-  const int64_t* order;      // y_last row of sequence s (null: s)
-  float* carries;            // [S, nTc, H] or null
-  int nTc;
-  const int* rinfo;          // [M] (this phase's rows)
-  unsigned long long* tails; // [row tiles of the call, H]
-  int* err;
-  unsigned epoch;
-  int H;
-  int mt_base;               // the call's row-tile index of this phase's first tile
-};
-constexpr int G_SPIN_LIMIT = 1 << 20;
-constexpr int G_COMP_LDS = N_WAVES * 128 * 8;   // the waves' composites (NB/2 <= 4 blocks)
-constexpr int G_SPEC_LDS = 256;                  // the GateSpec, staged (see nt_h_body)
-constexpr int G_COMP_OFF = NtCfg<8>::LDS > NtCfg<4>::LDS ? NtCfg<8>::LDS : NtCfg<4>::LDS;
-static_assert(NtCfg<2>::LDS <= G_COMP_OFF, "LDS layout");
-
 // The NT GEMM over the tiles of one launch phase: workgroup `bid` of `G`
 // takes tiles bid, bid + G, ...  (k_gemm_nt_h: one phase; k_gemm_nt_h2: the
 // whole rounds of 256 x 128 / 256 x 256 tiles, then the rows past them as
 // 256 x 64 tiles, in one launch).
-template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false, bool GATE = false>
+template <bool BIAS, bool WIDE, int NB, bool ACT = false, bool DACT = false>
 __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G,
                                           const float* __restrict__ A, int64_t lda, int64_t M,
                                           int R, const f16x8* __restrict__ Wf,
@@ -319,28 +266,15 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
                                           int64_t ldo, float* __restrict__ rmax, int m_tiles,
                                           float* __restrict__ act, DropSpec drop, int64_t e_base,
                                           const float* __restrict__ pre,
-                                          float* __restrict__ dpart,
-                                          const GateSpec& gs_arg = GateSpec{}) {
+                                          float* __restrict__ dpart) {
   using CF = NtCfg<NB>;
   constexpr int N_BN = CF::BN, N_NB = NB, N_BDMA = CF::BDMA, N_NSA = CF::NSA, N_LA = N_NSA - 1;
   constexpr int N_B_STAGE = CF::B_STAGE, N_RING = CF::RING;
   // deferred epilogue for NB = 4 (NB = 8 and DACT: stored at the tile's end)
-  constexpr bool DEFER = NB == 4 && !DACT && !GATE;   // DACT, GATE: stored at the tile's end
+  constexpr bool DEFER = NB == 4 && !DACT;   // DACT: stored at the tile's end
   static_assert(!(NB == 8) || WIDE, "256-column tiles store through the wide epilogue");
   static_assert(!ACT || WIDE, "the activation output rides the wide epilogue");
   static_assert(!DACT || (WIDE && !ACT && !BIAS), "DACT: wide epilogue, no bias");
-  static_assert(!GATE || (WIDE && !ACT && !DACT && !BIAS && (NB == 8 || NB == 4 || NB == 2)),
-                "GATE: 256-row tiles, wide rg stores, the bias in the gates");
-  constexpr int NCH = NB / 2;   // GATE: channel blocks per tile
-  const int gH = GATE ? gs_arg.H : 0;
-  // first output column of the tile's column block n (GATE: r blocks, then
-  // the same channels' i blocks at C offset H)
-  auto col0 = [&](int ct, int n) -> int {
-    if constexpr (GATE)
-      return n < NCH ? (ct * NCH + n) * 32 : gH + (ct * NCH + n - NCH) * 32;
-    else
-      return ct * N_BN + n * 32;
-  };
   const int64_t act_delta = ACT ? (reinterpret_cast<char*>(act) - reinterpret_cast<char*>(out)) : 0;
   const int64_t pre_delta =
       DACT ? (reinterpret_cast<const char*>(pre) - reinterpret_cast<const char*>(out)) : 0;
@@ -365,14 +299,6 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
   for (int c = tid; c < C; c += N_THREADS) {
     s_ew[c] = ew[c];
     if (BIAS) s_bias[c] = bias[c];
-  }
-  // GATE: the spec staged in LDS and read back by each tile's epilogue, so
-  // its ~30 scalars are not held in registers across the main loop
-  if constexpr (GATE) {
-    static_assert(sizeof(GateSpec) <= G_SPEC_LDS && sizeof(GateSpec) % 4 == 0, "GateSpec");
-    if (tid < (int)(sizeof(GateSpec) / 4))
-      reinterpret_cast<int*>(smem + G_COMP_OFF + G_COMP_LDS)[tid] =
-          reinterpret_cast<const int*>(&gs_arg)[tid];
   }
   // DACT: per-wave column sums of dA1 (wave-private: no atomics)
   float* s_col = reinterpret_cast<float*>(smem + CF::LDS) + wave * N_DACT_MAXC;
@@ -431,12 +357,12 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
   // ---- B stream (the k-step's 16 weight fragments, 1 KB each, shared by
   // the 8 waves; issued one step ahead): fragment f = (n * 2 + s) * 2 + p,
   // wave w DMAs fragments N_BDMA*w ...
-  int b_i = 0, b_kt = 0, b_slot = 0, b_ct = 0;
+  int b_i = 0, b_kt = 0, b_slot = 0;
   const f16x8* b_base = nullptr;
   auto b_tile = [&]() {
-    int mt;
-    tile_of(b_i, mt, b_ct);
-    b_base = GATE ? Wf + lane : Wf + (int64_t)b_ct * N_NB * KB16 * 2 * 64 + lane;
+    int mt, ct;
+    tile_of(b_i, mt, ct);
+    b_base = Wf + (int64_t)ct * N_NB * KB16 * 2 * 64 + lane;
   };
   auto issueB = [&]() {
     char* st = smem + N_NSA * N_A_STAGE + b_slot * N_B_STAGE;
@@ -444,8 +370,7 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
     for (int q = 0; q < N_BDMA; ++q) {
       const int f = wave * N_BDMA + q;
       const int n = f >> 2, s = (f >> 1) & 1, p = f & 1;
-      const int nb = GATE ? col0(b_ct, n) >> 5 : n;   // the image's 32-column block
-      const f16x8* src = b_base + ((nb * KB16 + b_kt * 2 + s) * 2 + p) * 64;
+      const f16x8* src = b_base + ((n * KB16 + b_kt * 2 + s) * 2 + p) * 64;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + f * 1024), 16, 0, 0);
     }
     b_slot ^= 1;
@@ -482,9 +407,6 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
         a_rd[s][c] = row * 128 + (((4 * s + 2 * (lane >> 5) + c) ^ sw) << 4);
   }
   const int ccol = lane & 31;
-  int cur_mt, cur_ct;   // the tile of the current k-steps
-  // byte offset of column block n inside an output row of the tile
-  auto blk_off = [&](int n) -> int { return GATE ? col0(cur_ct, n) * 4 : n * 128; };
   // C-layout row of accumulator register j: 8*(j>>2) + 4*(lane>>5) + (j&3)
   auto crow = [&](int j) { return 8 * (j >> 2) + 4 * (lane >> 5) + (j & 3); };
 
@@ -519,7 +441,7 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = BIAS ? blk[4 * g + r] + pbias[n] : blk[4 * g + r];
         quad_transpose(v, lane);
-        f32x4* o = (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + blk_off(n) + st_lane);
+        f32x4* o = (f32x4*)(pend_base + (int64_t)(8 * g) * ldo * 4 + n * 128 + st_lane);
         const int64_t row = pend_r0 + 8 * g + 4 * (lane >> 5) + (lane & 3);
         if (pend_full || row < M)
           __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]}, o);
@@ -631,288 +553,10 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
       }
     }
   };
-  // GATE, a flagged tile (a row value beyond its online scale's headroom):
-  // the wave's 32 rows recomputed now, each at its exact row max (as the
-  // cold tail below does for the other variants), into acc un-scaled
-  auto gate_exact = [&](const int (&ecol)[N_NB]) {
-    if constexpr (GATE) {
-      hwait_vm<0>();
-      int64_t row = pend_r0 + (lane & 31);
-      if (row >= M) row = M - 1;
-      const float* arow = A + row * lda + 8 * (lane >> 5);
-      float m = 0.0f;
-      for (int kb = 0; kb < KB16; ++kb) {
-        const f32x4 p = *reinterpret_cast<const f32x4*>(arow + kb * 16);
-        const f32x4 q = *reinterpret_cast<const f32x4*>(arow + kb * 16 + 4);
-        m = fmaxf(m, max8abs(p, q));
-      }
-      m = fmaxf(m, __shfl_xor(m, 32));
-      const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
-      const float sc = __builtin_amdgcn_ldexpf(1.0f, kTW - e);
-      int erow[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) erow[j] = __shfl(e, crow(j)) - 2 * kTW;
-#pragma unroll
-      for (int n = 0; n < N_NB; ++n) {
-        f32x16 c;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) c[j] = 0.0f;
-        const int nb = col0(cur_ct, n) >> 5;
-        for (int kb = 0; kb < KB16; ++kb) {
-          const f32x4 p = *reinterpret_cast<const f32x4*>(arow + kb * 16);
-          const f32x4 q = *reinterpret_cast<const f32x4*>(arow + kb * 16 + 4);
-          f16x8 a0, a1;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const f32x2 v = (t < 2 ? f32x2{p[2 * t], p[2 * t + 1]} : f32x2{q[2 * t - 4], q[2 * t - 3]}) * sc;
-            f16x2 h0, h1;
-            split2h(v, h0, h1);
-            a0[2 * t] = h0[0]; a0[2 * t + 1] = h0[1];
-            a1[2 * t] = h1[0]; a1[2 * t + 1] = h1[1];
-          }
-          const f16x8* bp = Wf + ((int64_t)(nb * KB16 + kb) * 2) * 64 + lane;
-          const f16x8 b0 = bp[0], b1 = bp[64];
-          c = mfma_h(a1, b0, c);
-          c = mfma_h(a0, b1, c);
-          c = mfma_h(a0, b0, c);
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) acc[n][j] = __builtin_amdgcn_ldexpf(c[j], erow[j] + ecol[n]);
-      }
-    }
-  };
-
-  // GATE: the tile-end epilogue (see GateSpec) on the un-scaled rg in acc.
-  // One channel block per iteration of a rolled loop (a barrier each; the
-  // next block's r / i accumulators are shifted into blocks 0 / NCH at the
-  // end, so the body indexes registers statically): one block's scan state,
-  // not four, is live beside the accumulators.  A lane's rows are r0 + 4 (lane
-  // >> 5) + o, o = 8 g + t (g, t < 4; register j = 4 g + t); the rows' flags
-  // are bits of wave-uniform masks (ballots of rinfo), and the sparse outputs
-  // (carries, y_last) are written by a loop over those masks' bits after the
-  // rows have run.
-  auto gate_epilogue = [&]() {
-    if constexpr (GATE) {
-      GateSpec gs;
-      {
-        int w[sizeof(GateSpec) / 4];
-        const int* src = reinterpret_cast<const int*>(smem + G_COMP_OFF + G_COMP_LDS);
-#pragma unroll
-        for (int k = 0; k < (int)(sizeof(GateSpec) / 4); ++k)
-          w[k] = __builtin_amdgcn_readfirstlane(src[k]);
-        __builtin_memcpy(&gs, w, sizeof(GateSpec));
-      }
-      // Everything here derives from values re-materialised at this point
-      // (opaque to the compiler: the lane id, the spec's address, the
-      // strides), so nothing of the epilogue is hoisted out of the tile loop
-      // into registers held across the main loop's k-steps
-      int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-      asm volatile("" : "+v"(lane));
-      const int ccol = lane & 31;
-      int H = __builtin_amdgcn_readfirstlane(gs.H), ldx = __builtin_amdgcn_readfirstlane((int)lda);
-      int zrs = __builtin_amdgcn_readfirstlane((int)gs.z_rs);
-      int yrs = __builtin_amdgcn_readfirstlane((int)gs.y_rs);
-      asm volatile("" : "+s"(H), "+s"(ldx), "+s"(zrs), "+s"(yrs));
-      const int64_t r0 = pend_r0;                   // the wave's first row
-      const int mt_g = gs.mt_base + cur_mt;         // the call's row tile
-      const bool lastw = wave == N_WAVES - 1;
-      const int hsh = 4 * (lane >> 5);              // the lane half's row shift
-      const int64_t lim64 = M - r0 - hsh;           // a lane's rows o < lim are < M
-      const int lim = lim64 > 32 ? 32 : (int)lim64;
-      // row flags of the wave's 32 rows (bit k: row r0 + k), from lanes 0..31
-      int myinfo = -1;
-      if (lane < 32 && r0 + lane < M) myinfo = gs.rinfo[r0 + lane];
-      const bool in = lane < 32 && myinfo >= 0;
-      const uint32_t m_start = (uint32_t)__builtin_amdgcn_ballot_w64(in && (myinfo & 255) == 0);
-      const uint32_t m_last = (uint32_t)__builtin_amdgcn_ballot_w64(in && ((myinfo >> 8) & 1));
-      // every 16th row except a sequence's last: the carry entering its next
-      // 16 steps (slots of the sequence's own tiles only, as rb_gate_scan_fwd)
-      const uint32_t m_ckpt = (uint32_t)__builtin_amdgcn_ballot_w64(
-          in && (myinfo & 15) == 15 && !((myinfo >> 8) & 1));
-      const uint32_t l_start = m_start >> hsh;      // this lane's rows: bit o
-      // does the tile's first row continue a sequence of the previous tile?
-      const int tinfo = gs.rinfo[(int64_t)cur_mt * N_BM];
-      const bool need = mt_g > 0 && (tinfo & 255) != 0;
-      unsigned long long* tl = gs.tails + (int64_t)mt_g * H;
-      const unsigned long long ep = (unsigned long long)gs.epoch << 32;
-      float* s_comp = reinterpret_cast<float*>(smem + G_COMP_OFF);
-      const float* xw = A + r0 * lda;               // wave-uniform bases
-      const float* zw = gs.z + r0 * gs.z_rs;
-      float* yw = gs.y != nullptr ? gs.y + r0 * gs.y_rs : nullptr;
-      // rg first (raw, no bias): its stores drain behind the math below
-#pragma unroll
-      for (int n = 0; n < N_NB; ++n) store_block(acc[n], n);
-#pragma unroll 1
-      for (int q = 0; q < NCH; ++q) {
-        const int ch = (cur_ct * NCH + q) * 32 + ccol;
-        const float nsp = -softplus_f(gs.lam[ch]);
-        const float br = gs.gbias[ch], bi = gs.gbias[H + ch];
-        const float h0v = gs.h0 != nullptr ? gs.h0[ch] : 0.0f;
-        // acc[0] <- alpha (0 at a sequence start, 1 past M), acc[NCH] <- b'
-        // (+ alpha h0 at a sequence start, 0 past M): h_t = a_t h_{t-1} + b_t
-        {
-          const int xo = hsh * ldx + ch;
-          float xv[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int o = 8 * (j >> 2) + (j & 3);
-            xv[j] = o < lim ? xw[xo + o * ldx] : 0.0f;
-          }
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int o = 8 * (j >> 2) + (j & 3);
-            const float a = fexp(nsp * fsigm(acc[0][j] + br));
-            const float beta = fsqrt(1.0f - a * a + 1e-8f) * fsigm(acc[NCH][j] + bi);
-            const float bp = beta * xv[j];
-            const bool start = (l_start >> o) & 1;
-            const bool ok = o < lim;
-            acc[0][j] = ok ? (start ? 0.0f : a) : 1.0f;
-            acc[NCH][j] = ok ? (start ? h0v * a + bp : bp) : 0.0f;
-          }
-        }
-        // the lane's 4-row groups; the wave's 8 groups in row order (group
-        // 2g + h: lane half h, j-block g): each own group's incoming state as
-        // an affine map (cA, cX) of the state entering the wave
-        float cA[4], cX[4];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float Ag = 1.0f, Xg = 0.0f;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            Xg = Xg * acc[0][4 * g + t] + acc[NCH][4 * g + t];
-            Ag = Ag * acc[0][4 * g + t];
-          }
-          cA[g] = Ag;
-          cX[g] = Xg;
-        }
-        float Pw = 1.0f, Qw = 0.0f;
-        {
-          const int half = lane >> 5;
-          float pA[4], pX[4];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            pA[g] = __shfl_xor(cA[g], 32);
-            pX[g] = __shfl_xor(cX[g], 32);
-          }
-#pragma unroll
-          for (int gi = 0; gi < 8; ++gi) {
-            const int g = gi >> 1;
-            const bool own = (gi & 1) == half;
-            const float Ag = own ? cA[g] : pA[g];
-            const float Xg = own ? cX[g] : pX[g];
-            if (own) {
-              cA[g] = Pw;
-              cX[g] = Qw;
-            }
-            Qw = Qw * Ag + Xg;
-            Pw = Pw * Ag;
-          }
-        }
-        float* sc = s_comp + q * (N_WAVES * 64);
-        if (lane < 32) *reinterpret_cast<f32x2*>(sc + (wave * 32 + ccol) * 2) = f32x2{Pw, Qw};
-        __syncthreads();
-        // the state entering this wave as an affine map (Pt, Qt) of the tile's
-        float Pt = 1.0f, Qt = 0.0f;
-        for (int w = 0; w < wave; ++w) {
-          const f32x2 c = *reinterpret_cast<const f32x2*>(sc + (w * 32 + ccol) * 2);
-          Qt = Qt * c[0] + c[1];
-          Pt = Pt * c[0];
-        }
-        // the tile's last-row state (last wave): published now unless it
-        // depends on the tile's incoming state (no sequence starts in the tile)
-        const float Pe = Pt * Pw, Qe = Qt * Pw + Qw;
-        if (lastw && lane < 32 && Pe == 0.0f)
-          __hip_atomic_store(tl + ch, ep | __float_as_uint(Qe), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        // the previous row tile's last-row state, if this wave depends on it
-        float hin = 0.0f;
-        if (need && (Pt != 0.0f || (lastw && Pe != 0.0f))) {
-          const unsigned long long* src = tl - H + ch;
-          unsigned long long v = 0;
-          for (int it = 0;; ++it) {
-            v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((unsigned)(v >> 32) == gs.epoch) break;
-            if (it >= G_SPIN_LIMIT) {   // never expected: report, do not hang
-              *gs.err = 1;
-              v = 0;
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-          hin = __uint_as_float((unsigned)v);
-        }
-        if (lastw && lane < 32 && Pe != 0.0f)
-          __hip_atomic_store(tl + ch, ep | __float_as_uint(hin * Pe + Qe), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        // every row from its exact incoming state; h kept in acc[NCH]
-        const float hw = hin * Pt + Qt;
-        if (yw != nullptr) {
-          const int zo = hsh * zrs + ch, yo = hsh * yrs + ch;
-          float zv[16];
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int o = 8 * (j >> 2) + (j & 3);
-            zv[j] = o < lim ? zw[zo + o * zrs] : 0.0f;
-          }
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float h = hw * cA[g] + cX[g];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const int j = 4 * g + t, o = 8 * g + t;
-              h = h * acc[0][j] + acc[NCH][j];
-              acc[NCH][j] = h;
-              if (o < lim) yw[yo + o * yrs] = fsilu(zv[j]) * h;
-            }
-          }
-        } else {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float h = hw * cA[g] + cX[g];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              const int j = 4 * g + t;
-              h = h * acc[0][j] + acc[NCH][j];
-              acc[NCH][j] = h;
-            }
-          }
-        }
-        // the sparse rows: each sequence's first row (carry 0 = h0), every
-        // 16th row (the carry entering the next 16 steps), the last row (y_last)
-        uint32_t msp = (gs.carries != nullptr ? (m_start | m_ckpt) : 0u) |
-                       (gs.y_last != nullptr ? m_last : 0u);
-        while (msp != 0u) {
-          const int k = __builtin_ctz(msp);
-          msp &= msp - 1u;
-          const int jk = 4 * (k >> 3) + (k & 3);   // its register; lane half (k >> 2) & 1
-          const float hk = acc[NCH][jk];
-          if (((k >> 2) & 1) == (lane >> 5)) {
-            const int info = gs.rinfo[r0 + k];
-            const int sq = info >> 9, pos = info & 255;
-            if (gs.carries != nullptr) {
-              if ((m_start >> k) & 1) gs.carries[(int64_t)sq * gs.nTc * H + ch] = h0v;
-              if (((m_ckpt >> k) & 1) && (pos >> 4) + 1 < gs.nTc)
-                gs.carries[((int64_t)sq * gs.nTc + (pos >> 4) + 1) * H + ch] = hk;
-            }
-            if (gs.y_last != nullptr && ((m_last >> k) & 1)) {
-              const int64_t orow = gs.order != nullptr ? gs.order[sq] : sq;
-              gs.y_last[orow * H + ch] = fsilu(zw[k * zrs + ch]) * hk;
-            }
-          }
-        }
-        // the next channel block's r / i into blocks 0 / NCH
-#pragma unroll
-        for (int n = 0; n + 1 < NCH; ++n) {
-          acc[n] = acc[n + 1];
-          acc[NCH + n] = acc[NCH + n + 1];
-        }
-      }
-    }
-  };
-
   bool stored_prev = false;
 
   int i = 0, kt = 0, c_slot_a = 0, c_slot_b = 0;
+  int cur_mt, cur_ct;
   tile_of(0, cur_mt, cur_ct);
   for (int u = 0; u < U; ++u) {
     // operands of step u landed (own DMAs): the ops younger than B(u) are
@@ -1021,7 +665,7 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
       }
       int ecol[N_NB];
 #pragma unroll
-      for (int n = 0; n < N_NB; ++n) ecol[n] = hds_read_i32(s_ew_addr + (col0(cur_ct, n) + ccol) * 4);
+      for (int n = 0; n < N_NB; ++n) ecol[n] = hds_read_i32(s_ew_addr + (cur_ct * N_BN + n * 32 + ccol) * 4);
       if (BIAS) {
 #pragma unroll
         for (int n = 0; n < N_NB; ++n)
@@ -1047,31 +691,23 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
         const int64_t r0 = (int64_t)cur_mt * N_BM + wave * 32;
         const bool full = r0 + 32 <= M;
         if (cur_mt < m_tiles) {
-          pend_base = reinterpret_cast<const char*>(out + r0 * ldo + (GATE ? 0 : cur_ct * N_BN));
+          pend_base = reinterpret_cast<const char*>(out + r0 * ldo + cur_ct * N_BN);
           pend_r0 = r0;
           pend_c0 = cur_ct * N_BN;
           pend_full = full;
-          if (GATE && flag_tile) {
-            gate_exact(ecol);   // the wave's rows again at their exact scales
-          } else {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-              const int erj = __shfl(er, crow(j)) - kTA - kTW;
+          for (int j = 0; j < 16; ++j) {
+            const int erj = __shfl(er, crow(j)) - kTA - kTW;
 #pragma unroll
-              for (int n = 0; n < N_NB; ++n) acc[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
-            }
+            for (int n = 0; n < N_NB; ++n) acc[n][j] = __builtin_amdgcn_ldexpf(acc[n][j], erj + ecol[n]);
           }
           if constexpr (DACT) {
             dact_epilogue(flag_tile);
-            stored_prev = full;
-          } else if constexpr (GATE) {
-            gate_epilogue();
-            stored_prev = false;   // a data-dependent number of stores: wait for all
           } else {
 #pragma unroll
             for (int n = 0; n < N_NB; ++n) store_block(acc[n], n);
-            stored_prev = full;
           }
+          stored_prev = full;
         }
 #pragma unroll
         for (int n = 0; n < N_NB; ++n)
@@ -1090,10 +726,8 @@ __device__ __forceinline__ void nt_h_body(char* smem, const int bid, const int G
       tmax = 0.0f;
       const bool tile_flagged = flag_tile;
       if (flag_tile) {
-        if (!GATE) {   // GATE: recomputed above (its successor tile waits for it)
-          if (nflag < N_MAXFLAG) s_flag[nflag] = i;
-          ++nflag;
-        }
+        if (nflag < N_MAXFLAG) s_flag[nflag] = i;
+        ++nflag;
         flag_tile = false;
       }
       if constexpr (DEFER) {
@@ -1273,31 +907,6 @@ k_gemm_nt_h2(int64_t lda, int R, const f16x8* __restrict__ Wf, const int* __rest
                                         ew, C, bias, tail_ph.out, ldo, tail_ph.rmax,
                                         tail_ph.m_tiles, tail_ph.act, drop, tail_ph.e_base,
                                         tail_ph.pre, tail_ph.dpart);
-}
-
-constexpr int G_MAIN_NB = 4;   // main-phase tiles: 256 rows x 64 channels (r and i)
-// The gates projection with the BD-LRU in its epilogue (GATE, see GateSpec):
-// the call's whole rounds of 256 x 256 tiles (128 channels), then the rows
-// past them on 256 x 64 tiles (32 channels), in one launch.  Every tile of
-// both phases is resident (one workgroup per CU, at most one per CU in the
-// grid) and a tile only waits for an earlier row tile, which its workgroup
-// (processing its tiles in order) has started or finished.
-__global__ void __launch_bounds__(N_THREADS, 1)
-k_gate_gemm_h2(int64_t lda, int R, const f16x8* __restrict__ Wf, const int* __restrict__ ew, int C,
-               int64_t ldo, NtPhase main_ph, NtPhase tail_ph, GateSpec g_main, GateSpec g_tail) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int bid = (int)blockIdx.x;
-  if (bid < main_ph.grid)
-    nt_h_body<false, true, G_MAIN_NB, false, false, true>(smem, bid, main_ph.grid, main_ph.A, lda,
-                                                  main_ph.M, R, Wf, ew, C, nullptr, main_ph.out,
-                                                  ldo, main_ph.rmax, main_ph.m_tiles, nullptr,
-                                                  DropSpec{}, 0, nullptr, nullptr, g_main);
-  __syncthreads();
-  if (bid < tail_ph.grid)
-    nt_h_body<false, true, 2, false, false, true>(smem, bid, tail_ph.grid, tail_ph.A, lda,
-                                                  tail_ph.M, R, Wf, ew, C, nullptr, tail_ph.out,
-                                                  ldo, tail_ph.rmax, tail_ph.m_tiles, nullptr,
-                                                  DropSpec{}, 0, nullptr, nullptr, g_tail);
 }
 
 // ---------------------------------------------------------------------------
@@ -1950,50 +1559,6 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
     default: run(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}); break;
   }
   return launch_status("rb_gemm_tn_h");
-}
-
-// The gates projection of packed sequences with the BD-LRU in its epilogue
-// (k_gate_gemm_h2).  The same row split as launch_gemm_nt_h for C = 2H, so rg
-// is bitwise the rb_gemm_nt_h result; the two phases are chained by the
-// row-tile tails (tails: >= row tiles x H words; epoch: this call's, != 0 and
-// != any value the buffer holds from earlier calls).
-int launch_gate_gemm_h(const float* xc, int64_t lda, int64_t M, int H, const void* Wf,
-                       const float* z, int64_t z_rs, const float* gbias, const float* lam,
-                       const float* h0, float* rg, int64_t ldo, float* y, int64_t y_rs,
-                       float* y_last, const int64_t* order, float* carries, int nTc,
-                       const int* rinfo, float* rmax, void* tails, uint32_t epoch, int* err,
-                       hipStream_t st) {
-  const int C = 2 * H;
-  const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
-  const int nct0 = C / (32 * G_MAIN_NB);
-  const int64_t rows_round = (G0 % nct0 == 0) ? (int64_t)(G0 / nct0) * N_BM : 0;
-  const int64_t M_main = rows_round > 0 ? M / rows_round * rows_round : 0;
-  const f16x8* wf = (const f16x8*)Wf;
-  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * H * 4);
-  const NtPhase mp = nt_phase(xc, lda, 0, M_main, rg, ldo, rmax, C, 32 * G_MAIN_NB, G0);
-  const NtPhase tp = nt_phase(xc, lda, M_main, M - M_main, rg, ldo, rmax, C, 64, G0);
-  GateSpec gm{};
-  gm.z = z; gm.z_rs = z_rs; gm.gbias = gbias; gm.lam = lam; gm.h0 = h0;
-  gm.y = y; gm.y_rs = y_rs; gm.y_last = y_last; gm.order = order;
-  gm.carries = carries; gm.nTc = nTc; gm.rinfo = rinfo;
-  gm.tails = reinterpret_cast<unsigned long long*>(tails); gm.err = err; gm.epoch = epoch;
-  gm.H = H; gm.mt_base = 0;
-  GateSpec gt = gm;
-  gt.z = z + M_main * z_rs;
-  gt.y = y ? y + M_main * y_rs : nullptr;
-  gt.rinfo = rinfo + M_main;
-  gt.mt_base = (int)(M_main / N_BM);
-  constexpr int lds = G_COMP_OFF + G_COMP_LDS + G_SPEC_LDS;
-  static_assert(lds <= 160 * 1024, "LDS");
-  static bool done = false;  // benign race: idempotent
-  if (!done) {
-    (void)hipFuncSetAttribute((const void*)k_gate_gemm_h2,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    done = true;
-  }
-  const unsigned grid = (unsigned)std::max(mp.grid, tp.grid);
-  k_gate_gemm_h2<<<grid, N_THREADS, lds, st>>>(lda, H, wf, ew, C, ldo, mp, tp, gm, gt);
-  return launch_status("rb_gate_gemm_fwd_h");
 }
 
 }  // namespace rb

@@ -8,8 +8,6 @@
 //   ids[r]  = item_seq[order[s], t]   (the packed item ids the embedding reads)
 //   pos[r]  = t                       (row r's position inside its sequence)
 //   inv[order[s]]  = s,  last[order[s]] = offs[s+1] - 1
-//   rinfo[r] = s << 9 | (t == len - 1) << 8 | (t & 255)   (optional: the row
-//              info of the gates GEMM's BD-LRU epilogue, gemm_half.hip GATE)
 // for r = offs[s] + t — what a dozen torch index/arange/scatter launches did.
 #include "common.h"
 
@@ -19,8 +17,7 @@ namespace {
 __global__ void __launch_bounds__(256)
 k_pack_plan(const int64_t* __restrict__ seq, int64_t seq_rs, const int64_t* __restrict__ offs,
             const int64_t* __restrict__ order, int64_t B, int64_t* __restrict__ ids,
-            int64_t* __restrict__ pos, int64_t* __restrict__ inv, int64_t* __restrict__ last,
-            int* __restrict__ rinfo) {
+            int64_t* __restrict__ pos, int64_t* __restrict__ inv, int64_t* __restrict__ last) {
   const int64_t s = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (s >= B) return;   // wave-uniform
   const int lane = threadIdx.x & 63;
@@ -31,8 +28,6 @@ k_pack_plan(const int64_t* __restrict__ seq, int64_t seq_rs, const int64_t* __re
   for (int64_t t = lane; t < len; t += 64) {
     ids[r0 + t] = src[t];
     pos[r0 + t] = t;
-    if (rinfo != nullptr)
-      rinfo[r0 + t] = (int)(s << 9) | (t == len - 1 ? 256 : 0) | (int)(t & 255);
   }
   if (lane == 0) {
     inv[b] = s;
@@ -44,10 +39,10 @@ k_pack_plan(const int64_t* __restrict__ seq, int64_t seq_rs, const int64_t* __re
 
 int launch_pack_plan(const int64_t* seq, int64_t seq_rs, const int64_t* offs,
                      const int64_t* order, int64_t B, int64_t* ids, int64_t* pos, int64_t* inv,
-                     int64_t* last, int* rinfo, hipStream_t st) {
+                     int64_t* last, hipStream_t st) {
   const int64_t blocks = (B + 3) / 4;
   hipLaunchKernelGGL(k_pack_plan, dim3((unsigned)blocks), dim3(256), 0, st, seq, seq_rs, offs,
-                     order, B, ids, pos, inv, last, rinfo);
+                     order, B, ids, pos, inv, last);
   return launch_status("rb_pack_plan");
 }
 

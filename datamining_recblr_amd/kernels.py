@@ -205,7 +205,7 @@ class Packed:
     offsets[b] .. offsets[b+1] of a 2-D [ntok, C] activation (RecBole's
     right-padded batch without the padding; include/recblr_hip.h)."""
     __slots__ = ("offsets", "B", "L", "ntok", "pos", "last", "inv", "order", "pieces", "G",
-                 "max_tiles", "rinfo")
+                 "max_tiles")
 
     def __init__(self, offsets: torch.Tensor, L: int, ntok: int,
                  pos: torch.Tensor | None = None):
@@ -231,10 +231,6 @@ class Packed:
         self.pieces = None
         self.G = 0
         self.max_tiles = 0          # 64-row tiles of the longest work list
-        # optional (rb_pack_plan's rinfo, L <= 256): each packed row's
-        # sequence, last-row flag and position — the gates GEMM's BD-LRU
-        # epilogue (gate_gemm_fwd)
-        self.rinfo = None
 
 
 def _layout(t: torch.Tensor, name: str, C: int, seq: "Packed | None"):
@@ -398,89 +394,6 @@ def gate_scan_fwd(rg, xc, z, lam, h0=None, y=None, want_carries=True, gate_b=Non
             h0_bs, y.data_ptr(), y_rs, 0 if carries is None else carries.data_ptr(), B, L, H,
             offs, _stream(xc))
     return y, carries
-
-
-class _GateTails:
-    """Per-device state of rb_gate_gemm_fwd_h: the row-tile tail buffer
-    (grown as needed, zero-initialised: epoch 0 never matches), the call
-    counter that tags each call's tails, and the wait-timeout flag."""
-
-    def __init__(self, dev):
-        self.tails = torch.zeros(0, device=dev, dtype=torch.int64)
-        self.err = torch.zeros(1, device=dev, dtype=torch.int32)
-        self.epoch = 0
-
-    def next(self, words: int):
-        if self.tails.numel() < words:
-            # a new buffer starts at zero: the epochs start over
-            self.tails = torch.zeros(max(words, 2 * self.tails.numel()), device=self.err.device,
-                                     dtype=torch.int64)
-            self.epoch = 0
-        self.epoch = self.epoch + 1 if self.epoch < 0xFFFFFFFF else 1
-        return self.tails, self.epoch
-
-
-_gate_tails = {}
-
-
-def gate_gemm_errors(dev=None) -> int:
-    """Number of (device, stream) states whose gates-GEMM epilogue reported
-    a tile that waited out its predecessor (rb_gate_gemm_fwd_h's err; syncs)."""
-    n = 0
-    for (d, _), st in _gate_tails.items():
-        if dev is None or d == torch.device(dev):
-            n += int(st.err.item() != 0)
-    return n
-
-
-def gate_gemm_fwd(xc, wg_img, z, gate_b, lam, h0, seq: Packed, last_only: bool = False,
-                  batch_row=None, want_carries=True, rmax=None):
-    """rb_gate_gemm_fwd_h: the gates projection rg = xc W_g^T (raw, f16x3 —
-    bitwise gemm_nt_h) with the BD-LRU gates, scan and silu(z) merge in its
-    epilogue (RecBLR.py:196-206) on packed sequences (seq.rinfo set).
-    xc [ntok, H], z [ntok, H] views; wg_img: W_g's f16 image
-    (linear._weight_split(gate_w, False)); h0 [H] or None.  Returns (rg
-    [ntok, 2H], y [ntok, H] or y_last [B, H] (batch order with batch_row),
-    carries [B, nT, H] or None) — gate_scan_fwd's y and carries."""
-    _check(xc, "xc")
-    _check(z, "z")
-    _check(lam, "Lambda")
-    H = xc.shape[-1]
-    if seq is None or seq.rinfo is None:
-        raise ValueError("gate_gemm_fwd needs packed sequences with rinfo (pack_plan)")
-    M = seq.ntok
-    lda = _layout(xc, "xc", H, seq)[2]
-    z_rs = _layout(z, "z", H, seq)[2]
-    if lam.shape != (H,):
-        raise ValueError(f"Lambda must be [{H}]")
-    if h0 is not None:
-        _check(h0, "h0")
-        if h0.shape != (H,):
-            raise ValueError(f"h0 must be [{H}]")
-        h0 = h0.contiguous()
-    dev = xc.device
-    rg = torch.empty((M, 2 * H), device=dev, dtype=torch.float32)
-    carries = (torch.empty((seq.B, num_tiles(seq.L), H), device=dev, dtype=torch.float32)
-               if want_carries else None)
-    if last_only:
-        y, y_last = None, torch.empty((seq.B, H), device=dev, dtype=torch.float32)
-    else:
-        y, y_last = torch.empty((M, H), device=dev, dtype=torch.float32), None
-    key = (dev, _stream(xc))   # calls on one stream are ordered
-    st = _gate_tails.get(key)
-    if st is None:
-        st = _gate_tails[key] = _GateTails(dev)
-    words = (M + 255) // 256 * H
-    tails, epoch = st.next(words)
-    # a projection GEMM: timed by its caller as one (linear._timed), like rb_gemm_nt_h
-    _lib.call("rb_gate_gemm_fwd_h", xc.data_ptr(), lda, M, H, wg_img.data_ptr(),
-            z.data_ptr(), z_rs, _gb_ptr(gate_b, H), lam.contiguous().data_ptr(),
-            None if h0 is None else h0.data_ptr(), rg.data_ptr(), 2 * H,
-            None if y is None else y.data_ptr(), H, None if y_last is None else y_last.data_ptr(),
-            _batch_row_ptr(batch_row, seq.B, dev), None if carries is None else carries.data_ptr(),
-            num_tiles(seq.L), seq.rinfo.data_ptr(), None if rmax is None else rmax.data_ptr(),
-            tails.data_ptr(), tails.numel() * 8, epoch, st.err.data_ptr(), _stream(xc))
-    return rg, (y if y is not None else y_last), carries
 
 
 def _batch_row_ptr(batch_row, B, dev):
@@ -1086,12 +999,10 @@ def gemm_split_weight(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
     return wf
 
 
-def pack_plan(item_seq: torch.Tensor, offsets: torch.Tensor, order: torch.Tensor, ntok: int,
-              want_rinfo: bool = False):
-    """rb_pack_plan: (ids [ntok], row_pos [ntok], inv [B], last [B], rinfo
-    [ntok] int32 or None) of the packed layout (sequence s = batch row
-    order[s] at rows offsets[s] .. offsets[s+1]); item_seq [B, L] int64 on the
-    device.  rinfo (want_rinfo, L <= 256): s << 9 | last << 8 | position."""
+def pack_plan(item_seq: torch.Tensor, offsets: torch.Tensor, order: torch.Tensor, ntok: int):
+    """rb_pack_plan: (ids [ntok], row_pos [ntok], inv [B], last [B]) of the
+    packed layout (sequence s = batch row order[s] at rows offsets[s] ..
+    offsets[s+1]); item_seq [B, L] int64 on the device."""
     for t, n in ((item_seq, "item_seq"), (offsets, "offsets"), (order, "order")):
         _check(t, n, torch.int64)
     if item_seq.dim() != 2 or item_seq.stride(1) != 1:
@@ -1104,11 +1015,10 @@ def pack_plan(item_seq: torch.Tensor, offsets: torch.Tensor, order: torch.Tensor
     pos = torch.empty(ntok, device=dev, dtype=torch.int64)
     inv = torch.empty(B, device=dev, dtype=torch.int64)
     last = torch.empty(B, device=dev, dtype=torch.int64)
-    rinfo = torch.empty(ntok, device=dev, dtype=torch.int32) if want_rinfo else None
     _lib.call("rb_pack_plan", item_seq.data_ptr(), item_seq.stride(0), offsets.data_ptr(),
               order.data_ptr(), B, L, ids.data_ptr(), pos.data_ptr(), inv.data_ptr(),
-              last.data_ptr(), None if rinfo is None else rinfo.data_ptr(), _stream(item_seq))
-    return ids, pos, inv, last, rinfo
+              last.data_ptr(), _stream(item_seq))
+    return ids, pos, inv, last
 
 
 class _SplitJob(ctypes.Structure):

@@ -33,7 +33,7 @@ from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_n
 from .kernels import Packed, grl_max_tiles, grl_pieces, pack_plan
 from .linear import HipLinearForward, fire_hooks, has_hooks, linear
 from .recbole_compat import BPRLoss, SequentialRecommender, install_interaction_hook
-from .recurrence import bd_lru, fused_ok, gate_gemm_wanted, pow2_pad_len, row_pad_lens
+from .recurrence import bd_lru, fused_ok, pow2_pad_len, row_pad_lens
 
 
 from .scoring import full_sort_scores, item_cross_entropy, target_ranks
@@ -364,10 +364,9 @@ class RecBLR(SequentialRecommender):
         # one launch (rb_pack_plan): the packed item ids, each token's position
         # in its sequence (lets the conv forward tile the packed rows), each
         # batch row's packed index and last token
-        ids, pos, inv, last, rinfo = pack_plan(item_seq.to(torch.int64), offsets, order, ntok,
-                                               want_rinfo=gate_gemm_wanted(L, H))
+        ids, pos, inv, last = pack_plan(item_seq.to(torch.int64), offsets, order, ntok)
         seq = Packed(offsets, L, ntok, pos if _CONV_ROWS else None)
-        seq.last, seq.inv, seq.order, seq.rinfo = last, inv, order, rinfo
+        seq.last, seq.inv, seq.order = last, inv, order
         if pieces is not None and pad is None:   # per-row pad prefixes: three-launch path
             seq.pieces, seq.G, seq.max_tiles = pieces, G, max_tiles
         if pad is not None:

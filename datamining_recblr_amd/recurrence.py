@@ -50,34 +50,6 @@ _FUSED = os.environ.get("RECBLR_FUSED_GRL", "0") != "0"
 _FUSED_BWD = os.environ.get("RECBLR_FUSED_GRL_BWD", "0") != "0"
 
 
-# RECBLR_GATE_GEMM=0: the gates projection and the gate scan as two launches
-# (rb_gemm_nt_h, rb_gate_scan_fwd) instead of the gates GEMM with the BD-LRU
-# in its epilogue (rb_gate_gemm_fwd_h: packed fp32 sequences, L <= 256,
-# H % 128 == 0; DESIGN.md §4 "The gates projection with the BD-LRU epilogue")
-_GATE_GEMM = os.environ.get("RECBLR_GATE_GEMM", "1") != "0"
-
-
-def set_gate_gemm(on: bool) -> bool:
-    """Set the gates-GEMM epilogue path (bench A/B); returns the previous setting."""
-    global _GATE_GEMM
-    prev, _GATE_GEMM = _GATE_GEMM, bool(on)
-    return prev
-
-
-def gate_gemm_wanted(L: int, H: int) -> bool:
-    """Whether a packed batch of max length L should carry the row info the
-    gates-GEMM epilogue reads (RecBLR._forward_packed asks before packing)."""
-    return _GATE_GEMM and L <= 256 and H % 128 == 0 and H <= 512
-
-
-def _gate_gemm_ok(seq, xc, h0, gate_w) -> bool:
-    return (_GATE_GEMM and seq is not None and seq.rinfo is not None and seq.L <= 256
-            and (h0 is None or h0.dim() == 1) and xc.dtype == torch.float32
-            and linear_mod.gemm_format() == "f16x3"
-            and linear_mod._split_ok(xc.reshape(-1, xc.shape[-1]), 2 * xc.shape[-1], xc.shape[-1])
-            and xc.shape[-1] % 128 == 0 and gate_w.dtype == torch.float32)
-
-
 # order of the backward's conv and gates weight gradient (see BDLRUCore.backward)
 _CONV_FIRST = os.environ.get("RECBLR_CONV_FIRST", "1") != "0"
 
@@ -186,22 +158,13 @@ class BDLRUCore(torch.autograd.Function):
             # gates GEMM without its bias: the gate kernels add gate_b on the fly
             xc2 = xc.reshape(rows, H)
             r_xc = rmax_buffer(xc2, H2, H) if ctx.needs_input_grad[3] else None
+            rg = _timed("gemm", gflops, mm_nt, xc2, gate_w, rmax=r_xc).view(*xz.shape[:-1], H2)
             ctx.r_xc = r_xc
-            if observe is None and _gate_gemm_ok(seq, xc2, h0, gate_w):
-                # the gates projection with the BD-LRU in its epilogue: rg is
-                # written for the backward, y (or y_last) and the carries
-                # come from the GEMM's tiles (no gate-scan launch)
-                rg, y, carries = _timed(
-                    "gemm", gflops, kernels.gate_gemm_fwd, xc2,
-                    linear_mod._weight_split(gate_w, False), z, gate_b, lam, h0, seq,
-                    last_only=last_only, batch_row=batch_row, want_carries=train, rmax=r_xc)
-            else:
-                rg = _timed("gemm", gflops, mm_nt, xc2, gate_w, rmax=r_xc).view(*xz.shape[:-1], H2)
-                if observe is not None:   # module hooks of the fused conv / gates (model.py)
-                    observe(x, xc, rg)
-                y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train,
-                                                   gate_b=gate_b, seq=seq, last_only=last_only,
-                                                   batch_row=batch_row)
+            if observe is not None:   # module hooks of the fused conv / gates (model.py)
+                observe(x, xc, rg)
+            y, carries = kernels.gate_scan_fwd(rg, xc, z, lam, h0, want_carries=train,
+                                               gate_b=gate_b, seq=seq, last_only=last_only,
+                                               batch_row=batch_row)
         ctx.use_conv = use_conv
         ctx.last_only = last_only
         ctx.has_h0 = h0 is not None and pad_len is None

@@ -465,12 +465,10 @@ int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int 
  * sequence s is batch row order[s], rows seq_offsets[s] .. seq_offsets[s+1])
  * -> ids[r] = item_seq[order[s], t] and row_pos[r] = t for r =
  * seq_offsets[s] + t (ntok = seq_offsets[B] entries each), inv[order[s]] = s,
- * last[order[s]] = seq_offsets[s+1] - 1.  All device int64.  rinfo (int32
- * [ntok], optional, needs L <= 256): rinfo[r] = s << 9 | (t == len_s - 1) << 8
- * | t, the row info rb_gate_gemm_fwd_h reads. */
+ * last[order[s]] = seq_offsets[s+1] - 1.  All device int64. */
 int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_offsets,
                  const int64_t* order, int64_t B, int64_t L, int64_t* ids, int64_t* row_pos,
-                 int64_t* inv, int64_t* last, int32_t* rinfo, void* stream);
+                 int64_t* inv, int64_t* last, void* stream);
 
 /* One Adam step (torch.optim.Adam semantics, L2 weight decay, no amsgrad)
  * over up to RB_MAX_ADAM_JOBS fp32 tensors in one launch — the optimizer of
@@ -551,28 +549,6 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
 int rb_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
                      const float* bias, float* out, int64_t ldo, float* rmax, float* act,
                      uint64_t seed, float p, void* stream);
-
-/* The gates projection with the BD-LRU in its epilogue (RecBLR.py:196-206:
- * gates(x), the alpha / beta gates, parallel_scan and silu(z) * h, on packed
- * sequences of length <= 256): rg [M, 2H] = xc W_g^T (raw, no bias; bitwise
- * rb_gemm_nt_h with Wf = W_g's image), and from the same tiles
- * y = silu(z) * BD-LRU(xc) — what rb_gate_scan_fwd computes from rg, xc, z —
- * into y [M, H] (row stride y_rs) or, with y NULL, each sequence's last row
- * into y_last[order ? order[s] : s] [S, H]; carries [S, nTc, H] (optional)
- * the 16-step checkpoints rb_gate_scan_bwd reads; h0 [H] or NULL; rmax as
- * rb_gemm_nt_h's.  rinfo: rb_pack_plan's.  Row tiles hand their last-row
- * state to the next through tails (>= ceil(M / 256) * H * 8 bytes, kept
- * between calls) tagged with `epoch`: != 0 and different from the previous
- * call's on the same buffer (e.g. a counter).  err (int32, device): set to 1
- * if a tile waited ~50 ms for its predecessor (never expected; the results
- * are then wrong).  H in {128, 256, 384, 512}; xc, Wf, rg 16-B aligned; row
- * strides multiples of 4. */
-int rb_gate_gemm_fwd_h(const float* xc, int64_t lda, int64_t M, int64_t H, const void* Wf,
-                       const float* z, int64_t z_rs, const float* gate_b, const float* lam,
-                       const float* h0, float* rg, int64_t ldo, float* y, int64_t y_rs,
-                       float* y_last, const int64_t* order, float* carries, int64_t nTc,
-                       const int32_t* rinfo, float* rmax, void* tails, int64_t tails_bytes,
-                       uint32_t epoch, int32_t* err, void* stream);
 
 /* The backward of rb_gemm_nt_h_act's activation fused into the FeedForward's
  * input-gradient GEMM dU = dA2 W_2 (RecBLR.py:219-222 backward): dU is not

@@ -39,7 +39,7 @@ def split_gemm_calls(monkeypatch):
     to check actually ran the kernel."""
     from datamining_recblr_amd import kernels
 
-    calls = _Calls()
+    calls = []
     for name in ("gemm_nt", "gemm_nt_h", "gemm_nt_h_act", "gemm_nt_h_dact"):
         orig = getattr(kernels, name)
 
@@ -48,23 +48,7 @@ def split_gemm_calls(monkeypatch):
             return _orig(a, wf, C, *args, **kw)
 
         monkeypatch.setattr(kernels, name, counted)
-    # the gates projection with the BD-LRU epilogue (rb_gate_gemm_fwd_h) runs
-    # the same split GEMM: recorded as (M, H, 2H), and listed in calls.gate
-    gate = calls.gate = []
-    orig_g = kernels.gate_gemm_fwd
-
-    def counted_g(xc, wf, *args, **kw):
-        calls.append((xc.shape[0], xc.shape[1], 2 * xc.shape[1]))
-        gate.append((xc.shape[0], xc.shape[1]))
-        return orig_g(xc, wf, *args, **kw)
-
-    monkeypatch.setattr(kernels, "gate_gemm_fwd", counted_g)
     return calls
-
-
-class _Calls(list):
-    """A list of (M, R, C) with the gates-GEMM epilogue calls in .gate."""
-    gate = ()
 
 
 @pytest.fixture

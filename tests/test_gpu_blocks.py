@@ -511,8 +511,7 @@ def test_pack_plan_matches_torch(cuda):
     offs = torch.zeros(B + 1, dtype=torch.int64)
     torch.cumsum(lens[order], 0, out=offs[1:])
     ntok = int(offs[-1])
-    ids, pos, inv, last, rinfo = kernels.pack_plan(item_seq.to(cuda), offs.to(cuda),
-                                                   order.to(cuda), ntok, want_rinfo=True)
+    ids, pos, inv, last = kernels.pack_plan(item_seq.to(cuda), offs.to(cuda), order.to(cuda), ntok)
     seq_of = torch.repeat_interleave(torch.arange(B), lens[order])
     pos_r = torch.arange(ntok) - offs[seq_of]
     ids_r = item_seq.reshape(-1)[order[seq_of] * L + pos_r]
@@ -520,9 +519,6 @@ def test_pack_plan_matches_torch(cuda):
     inv_r[order] = torch.arange(B)
     assert torch.equal(ids.cpu(), ids_r) and torch.equal(pos.cpu(), pos_r)
     assert torch.equal(inv.cpu(), inv_r) and torch.equal(last.cpu(), offs[inv_r + 1] - 1)
-    is_last = (pos_r == (offs[seq_of + 1] - offs[seq_of] - 1)).to(torch.int64)
-    rinfo_r = (seq_of << 9) | (is_last << 8) | pos_r
-    assert torch.equal(rinfo.cpu().to(torch.int64), rinfo_r)
 
 
 @pytest.mark.parametrize("pads", [56, [0, 3, 14, 56]])
