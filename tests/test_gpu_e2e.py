@@ -140,3 +140,23 @@ def test_bpr_c3_matches_oracle(cuda, split_gemm_calls):
     """BPR loss (RecBLR.py:89-95) at the C3 shape, packed."""
     _run(cuda, 2048, 50, packed=True, gather=True, seed=5, loss_type="BPR")
     assert len(split_gemm_calls) >= 12
+
+
+@pytest.mark.parametrize("bwd", [False, True], ids=["fused_fwd", "fused_fwd_bwd"])
+@pytest.mark.parametrize("B,L", [(192, 200), (2048, 50)], ids=["C2", "C3"])
+def test_fused_grl_kernels_match_oracle(cuda, monkeypatch, B, L, bwd):
+    """The opt-in one-launch GatedRecurrentLayer kernels (rb_grl_fwd, and
+    rb_grl_bwd with bwd; RECBLR_FUSED_GRL / RECBLR_FUSED_GRL_BWD) in the whole
+    training step against the CPU oracle — loss and every parameter gradient
+    at the suite's 1e-4 bar — with both kernels asserted engaged on both
+    layers (tests/test_gpu_fused.py compares them with the three-launch path)."""
+    from datamining_recblr_amd import kernels, recurrence
+
+    monkeypatch.setattr(recurrence, "_FUSED", True)
+    monkeypatch.setattr(recurrence, "_FUSED_BWD", bwd)
+    fwd_calls, bwd_calls = [], []
+    orig, orig_b = kernels.grl_fwd, kernels.grl_bwd
+    monkeypatch.setattr(kernels, "grl_fwd", lambda *a, **k: fwd_calls.append(1) or orig(*a, **k))
+    monkeypatch.setattr(kernels, "grl_bwd", lambda *a, **k: bwd_calls.append(1) or orig_b(*a, **k))
+    _run(cuda, B, L, packed=True, gather=True, seed=B + 3 * L)
+    assert len(fwd_calls) == 2 and len(bwd_calls) == 2 * bwd, (fwd_calls, bwd_calls)
