@@ -915,6 +915,25 @@ def main():
         order_ab["note"] = ("RECBLR_CONV_FIRST A/B on the headline's batches: in the "
                             "GatedRecurrentLayer backward, the conv backward before the gates "
                             "weight gradient (its inputs just written) or after it; best of 3")
+    ce_ab = None
+    if not args.no_full_tail:
+        # the CE backward's products: inside kernels that recompute the logits
+        # (rb_item_ce_bwd_h, P never stored) vs P in both layouts + two
+        # weight-gradient GEMMs (RECBLR_CE_GRADS=f16), alternated 3x
+        from datamining_recblr_amd import scoring as _sc
+        saved_c = _sc.set_ce_grads("fused")
+        runs = {"fused": [], "f16_probs_tn": []}
+        for _ in range(3):
+            for name, mode in (("fused", "fused"), ("f16_probs_tn", "f16")):
+                _sc.set_ce_grads(mode)
+                runs[name].append(timed_variant(True, True)["ms_per_step"])
+        _sc.set_ce_grads(saved_c)
+        ce_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
+        ce_ab["headline"] = "fused" if saved_c == "fused" else "f16_probs_tn"
+        ce_ab["note"] = ("RECBLR_CE_GRADS A/B on the headline's batches: dseq = P W and "
+                         "ditems = P^T seq inside the logits-recomputing kernels "
+                         "(rb_item_ce_bwd_h) vs P written in both layouts and two "
+                         "rb_gemm_tn_h products; best of 3 alternated runs")
     adam_ab = None
     if not args.no_full_tail:
         # the optimizer update: rb_adam_step (one launch over every parameter)
@@ -1046,6 +1065,7 @@ def main():
             "ffn_act": ffn_act_ab,
             "adam": adam_ab,
             "bwd_order": order_ab,
+            "ce_grads": ce_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 38
+ABI_VERSION = 39
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -72,6 +72,8 @@ SIGNATURES = {
     "rb_colsum_chunked": (ctypes.c_int, [_fp, _i64, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp,
                                          _fp]),
     "rb_item_ce_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
+    "rb_item_ce_bwd_h": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp,
+                                        _fp, _fp, _i64, _fp]),
     "rb_item_ce_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp, _i64, _fp]),
     "rb_item_ce_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
                                       _i64, _fp]),

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 38; }
+int rb_version(void) { return 39; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -545,6 +545,18 @@ int rb_item_ce_probs_h_both(const void* seq_img, const int* seq_exp, const void*
   return launch_item_ce_probs_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
                                 item_offset, probs_t, ldt, item_group_max, probs, ld,
                                 row_group_max, reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_item_ce_bwd_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                     const int* item_exp, const int64_t* target, const float* lse,
+                     const float* dloss, int64_t B, int64_t V, int64_t d, float* dseq,
+                     float* ditems, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (int rc = check_items_h(seq_img, seq_exp, item_img, item_exp, B, V, d)) return rc;
+  if (!target || !lse || !dloss || !workspace) return fail("rb_item_ce_bwd_h: null pointer");
+  if (d != 32 && d != 64 && d != 128) return fail("rb_item_ce_bwd_h: d must be 32, 64 or 128");
+  return launch_item_ce_bwd_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
+                              dseq, ditems, workspace, workspace_bytes,
+                              reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out, void* stream) {

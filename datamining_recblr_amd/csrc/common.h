@@ -409,6 +409,10 @@ int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex
 int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                          const int64_t* tgt, int64_t B, int64_t V, int64_t D, float* lse,
                          float* loss, void* ws, int64_t ws_bytes, hipStream_t st);
+int launch_item_ce_bwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
+                         const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
+                         int64_t V, int64_t D, float* dE, float* dW, void* ws, int64_t ws_bytes,
+                         hipStream_t st);
 int launch_item_ce_probs_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                            const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
                            int64_t V, int64_t D, int64_t v_off, float* out, int64_t ld,

@@ -677,7 +677,8 @@ def embedding_plan(idx, num_rows, d, stream=None):
 # MFMA roofline).
 FLOP_KERNELS = frozenset({"rb_item_ce_fwd", "rb_item_ce_bwd", "rb_item_ce_probs", "rb_item_rank",
                           "rb_item_scores", "rb_item_ce_fwd_h", "rb_item_ce_probs_h",
-                          "rb_item_ce_probs_h_t", "rb_item_ce_probs_h_both"})
+                          "rb_item_ce_probs_h_t", "rb_item_ce_probs_h_both",
+                          "rb_item_ce_bwd_h"})
 
 
 def f16_split_kernel(name: str) -> bool:
@@ -862,6 +863,32 @@ def item_ce_probs_h_t(seq: SplitRows, items: SplitRows, target, lse, dloss, item
             lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
             int(item_offset), pt.data_ptr(), ldt, gmax.data_ptr(), _stream(seq.img), _flops=True)
     return pt, gmax
+
+
+def item_ce_bwd_h(seq: SplitRows, items: SplitRows, target, lse, dloss, want_seq=True,
+                  want_items=True):
+    """(dseq [B, d], ditems [V, d]) of the CE on split images with P never
+    stored (rb_item_ce_bwd_h: each product from a kernel that recomputes the
+    logits and multiplies P from its accumulators, f16x3); d in {32, 64, 128}."""
+    B, V, d, target = _split_operands(seq, items, target)
+    if d not in (32, 64, 128):
+        raise ValueError("item_ce_bwd_h: d must be 32, 64 or 128")
+    _check(lse, "lse")
+    _check(dloss, "dloss")
+    dev = seq.img.device
+    lib = _lib.load()
+    ws_bytes = int(lib.rb_item_ce_workspace(B, V, d))
+    ws = torch.empty((ws_bytes,), device=dev, dtype=torch.uint8)
+    dseq = torch.empty((B, d), device=dev, dtype=torch.float32) if want_seq else None
+    ditems = torch.empty((V, d), device=dev, dtype=torch.float32) if want_items else None
+    flops = 4 * B * V * d * (int(want_seq) + int(want_items))   # logits + product, each
+    _launch("rb_item_ce_bwd_h", flops, seq.img.data_ptr(), seq.exps.data_ptr(),
+            items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
+            lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
+            None if dseq is None else dseq.data_ptr(),
+            None if ditems is None else ditems.data_ptr(), ws.data_ptr(), ws_bytes,
+            _stream(seq.img), _flops=True)
+    return dseq, ditems
 
 
 def item_ce_probs_h_both(seq: SplitRows, items: SplitRows, target, lse, dloss, item_offset=0,

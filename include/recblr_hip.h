@@ -385,6 +385,18 @@ int rb_item_ce_probs_h_both(const void* seq_img, const int* seq_exp, const void*
                             int64_t ldt, float* row_group_max, float* item_group_max,
                             void* stream);
 
+/* The CE backward (RecBLR.py:100-102: nn.CrossEntropyLoss over the item
+ * table, its input gradients) on split images with P never stored: dseq [B,
+ * d] = P W and ditems [V, d] = P^T seq (either NULL to skip), P = (softmax -
+ * onehot) * dloss / B, each from a kernel that recomputes the logits exactly
+ * as rb_item_ce_fwd_h (bit-identical) and feeds P from its accumulators into
+ * a second f16x3 product, fixed-order split partials summed in the
+ * workspace (rb_item_ce_workspace).  d in {32, 64, 128}. */
+int rb_item_ce_bwd_h(const void* seq_img, const int* seq_exp, const void* item_img,
+                     const int* item_exp, const int64_t* target, const float* lse,
+                     const float* dloss, int64_t B, int64_t V, int64_t d, float* dseq,
+                     float* ditems, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* out [ceil(n/32)] = max |x| over each 32-row group of x [n, c] (row stride
  * ld): rb_gemm_tn_h's operand scales for a tensor no f16 GEMM has read. */
 int rb_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out, void* stream);

@@ -274,14 +274,15 @@ def test_ce_weight_gradient_splits_are_multiples_of_8(monkeypatch, cus):
             assert s2 % 8 == 0 and s2 >= 8, (B, V, s2)
 
 
-def test_ce_f16_grads_fall_back_past_the_weight_gradient_width():
-    """The f16 CE backward runs the item gradient as rb_gemm_tn_h with
-    N = V rounded up to 256 <= 65536; larger vocabularies take the sliced
-    path instead of failing in the kernel."""
+def test_ce_f16_grads_fall_back_past_the_weight_gradient_width(monkeypatch):
+    """The f16 CE backward (RECBLR_CE_GRADS=f16) runs the item gradient as
+    rb_gemm_tn_h with N = V rounded up to 256 <= 65536; larger vocabularies
+    take the sliced path instead of failing in the kernel."""
     from datamining_recblr_amd import linear, scoring
 
-    if scoring.CE_GRADS != "f16" or linear.gemm_format() != "f16x3":
-        pytest.skip("f16 CE gradients not selected in this environment")
+    if linear.gemm_format() != "f16x3":
+        pytest.skip("f16x3 GEMMs not selected in this environment")
+    monkeypatch.setattr(scoring, "CE_GRADS", "f16")
     seq = torch.empty(256, 128)
     assert scoring._f16_grads_ok(seq, torch.empty(65536, 128))
     assert not scoring._f16_grads_ok(seq, torch.empty(65537, 128))
