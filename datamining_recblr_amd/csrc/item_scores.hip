@@ -1018,6 +1018,9 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
 // split into two f16 planes like every other operand; the partial sums are
 // un-scaled once by 2^(emax + e_g - 2 kTS) (exact).  emax = the streamed
 // operand's largest row exponent (each workgroup reduces the exponent array).
+// (A ds_read_b64_tr_b16 form of the gather, two reads per fragment instead of
+// eight, returned wrong operands on this XOR-swizzled tile image:
+// profiles/r04_ce_pytest_items_tr16.log.)
 // At d = 128 a wave holds its fixed operand's fragments (64 registers) and
 // the second product's four accumulators (64) beside the first's: one wave
 // per SIMD (the accumulator chains keep the MFMA pipe fed); d <= 64 two.

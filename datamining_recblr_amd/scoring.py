@@ -43,14 +43,14 @@ PROBS_SLICE_BYTES = 1 << 30
 # Logits pipe of the CE forward and of the sliced backward's P: "f16" (two-part
 # split operands on the f16 MFMA, fp32-level accuracy; default) or "f32".
 CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
-# The backward's two products dseq = P W, ditems = P^T seq: "fused" (default:
-# rb_item_ce_bwd_h, each product inside a kernel that recomputes the logits,
-# P never stored; d in {32, 64, 128}), "f16" (P written in both layouts, both
-# products on the f16x3 weight-gradient kernel, _bwd_f16) or "torch"
-# (hipBLASLt fp32 on P, sliced).  An earlier f16 variant ran ditems as the NT
+# The backward's two products dseq = P W, ditems = P^T seq: "f16" (default:
+# P written in both layouts, both products on the f16x3 weight-gradient
+# kernel, _bwd_f16), "fused" (rb_item_ce_bwd_h, each product inside a kernel
+# that recomputes the logits, P never stored; d in {32, 64, 128}: equal step
+# time, profiles/r04_ce_bench_*.log) or "torch" (hipBLASLt fp32 on P, sliced).  An earlier f16 variant ran ditems as the NT
 # kernel on P^T: 2.2x slower (42 row tiles with K = 2048 and online row
 # scales that P^T's rows outgrow; profiles/r03_ce_grads_probe.log).
-CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "fused")
+CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "f16")
 
 
 def set_ce_grads(mode: str) -> str:

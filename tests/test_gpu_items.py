@@ -320,8 +320,7 @@ def test_item_ce_f16_probs_slices_and_invalid_target(cuda):
 
 
 def test_item_ce_f16_engaged_in_training_loss(cuda):
-    """The model's CE (calculate_loss) runs the f16 kernels by default: the
-    forward and the P-free backward (rb_item_ce_bwd_h)."""
+    """The model's CE (calculate_loss) runs the f16 kernels by default."""
     from datamining_recblr_amd import kernels
     from datamining_recblr_amd.distributed import synthetic_interaction
     from datamining_recblr_amd.model import RecBLR
@@ -335,7 +334,7 @@ def test_item_ce_f16_engaged_in_training_loss(cuda):
     with kernels.kernel_timing() as t:
         model.calculate_loss(inter).backward()
     names = {r[0] for r in t.records}
-    assert {"rb_item_split_h", "rb_item_ce_fwd_h", "rb_item_ce_bwd_h"} <= names, names
+    assert {"rb_item_split_h", "rb_item_ce_fwd_h", "rb_item_ce_probs_h"} <= names, names
 
 
 def test_item_ce_f16_probs_transposed(cuda):
@@ -421,14 +420,14 @@ def test_item_ce_f16_grads_vs_fp64(cuda, monkeypatch, B, V, slice_bytes, on):
 
 @pytest.mark.parametrize("B,V,d", [(2048, 10544, 128), (512, 1000, 128), (300, 515, 64),
                                    (37, 33, 32), (1, 1, 64), (130, 97, 128)])
-def test_item_ce_fused_h_grads_vs_fp64(cuda, B, V, d):
-    """RECBLR_CE_GRADS=fused (default): both products inside kernels that
-    recompute the logits (rb_item_ce_bwd_h, P never stored) — no P buffer,
-    no weight-gradient GEMM, no library GEMM — against torch fp64 at the
-    suite's normwise 2e-5, partial tiles of both axes included."""
+def test_item_ce_fused_h_grads_vs_fp64(cuda, monkeypatch, B, V, d):
+    """RECBLR_CE_GRADS=fused: both products inside kernels that recompute
+    the logits (rb_item_ce_bwd_h, P never stored) — no P buffer, no
+    weight-gradient GEMM, no library GEMM — against torch fp64 at the suite's
+    normwise 2e-5, partial tiles of both axes included."""
     from datamining_recblr_amd import kernels, scoring
 
-    assert scoring.CE_GRADS == "fused"
+    monkeypatch.setattr(scoring, "CE_GRADS", "fused")
     seq, W, tgt = _data(B, V, d, cuda, seed=17, scale=0.5)
     s1 = seq.clone().requires_grad_()
     w1 = W.clone().requires_grad_()
