@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 39; }
+int rb_version(void) { return 40; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -775,6 +775,52 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
   if ((N / 128) * (K / 128) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_h: grid too large");
   return launch_gemm_tn_h(dY, ldy, X, ldx, M, (int)N, (int)K, ymax, xmax, parts, (int)splits,
                           reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_bf16_weight_image(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
+                              void* img, void* stream) {
+  if (!W || !img) return fail("rb_gemm_bf16_weight_image: null pointer");
+  if (C <= 0 || R <= 0 || C % 32 || R % 16 || C > 65536 || R > 65536)
+    return fail("rb_gemm_bf16_weight_image: C % 32 == 0 and R % 16 == 0 required (<= 65536)");
+  if (ldw < (transpose ? C : R)) return fail("rb_gemm_bf16_weight_image: bad row stride");
+  if (!aligned16(img)) return fail("rb_gemm_bf16_weight_image: img must be 16-byte aligned");
+  return launch_bf16_weight_image(W, ldw, (int)C, (int)R, transpose ? 1 : 0, img,
+                                  reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int64_t R, const void* img, int64_t C,
+                    const float* bias, void* out, int64_t ldo, void* stream) {
+  if (!A || !img || !out) return fail("rb_gemm_nt_bf16: null pointer");
+  if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt_bf16: empty shape");
+  if (R % 64 || C % 256 || R > 16384 || C > 65536)
+    return fail("rb_gemm_nt_bf16: R % 64 == 0 (<= 16384) and C % 256 == 0 required");
+  if (lda < R || lda % 8 || lda > (1 << 20) || ldo < C || ldo % 4)
+    return fail("rb_gemm_nt_bf16: bad row strides (lda % 8 == 0, ldo % 4 == 0)");
+  if (!aligned16(A) || !aligned16(img) || (reinterpret_cast<uintptr_t>(out) & 7) ||
+      (bias && !aligned16(bias)))
+    return fail("rb_gemm_nt_bf16: A, img and bias must be 16-byte aligned, out 8-byte aligned");
+  if ((M + 255) / 256 > 0x7fffffffLL / (C / 256) / 2) return fail("rb_gemm_nt_bf16: too many tiles");
+  return launch_gemm_nt_bf16(A, lda, M, (int)R, img, (int)C, bias, out, ldo,
+                             reinterpret_cast<hipStream_t>(stream));
+}
+
+int rb_gemm_tn_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t M, int64_t N,
+                    int64_t K, float* parts, int64_t splits, void* stream) {
+  if (!dY || !X || !parts) return fail("rb_gemm_tn_bf16: null pointer");
+  if (M <= 0 || N <= 0 || K <= 0) return fail("rb_gemm_tn_bf16: empty shape");
+  if (N % 256 || K % 256 || N > 65536 || K > 65536)
+    return fail("rb_gemm_tn_bf16: N and K must be multiples of 256 (<= 65536)");
+  if (splits < 8 || splits % 8 || splits > 65536)
+    return fail("rb_gemm_tn_bf16: splits must be a positive multiple of 8");
+  if (ldy < N || ldx < K || ldy % 8 || ldx % 8) return fail("rb_gemm_tn_bf16: bad row strides");
+  if (!aligned16(dY) || !aligned16(X) || !aligned16(parts))
+    return fail("rb_gemm_tn_bf16: dY, X and parts must be 16-byte aligned");
+  const int64_t chunk = ((M + splits - 1) / splits + 63) / 64 * 64;
+  if (chunk * (ldy > ldx ? ldy : ldx) * 2 >= 0x7fffffffLL)
+    return fail("rb_gemm_tn_bf16: a row chunk exceeds 2 GiB (use more splits)");
+  if ((N / 256) * (K / 256) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_bf16: grid too large");
+  return launch_gemm_tn_bf16(dY, ldy, X, ldx, M, (int)N, (int)K, parts, (int)splits,
+                             reinterpret_cast<hipStream_t>(stream));
 }
 
 int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,

@@ -1,0 +1,473 @@
+// gemm_bf16.hip — the projections of bf16 activations (BASELINE configs[4]:
+// L = 2,048, d = 256, H = 512, 2M rows per step) on the bf16 MFMA pipe: one
+// v_mfma_f32_32x32x16_bf16 per fragment pair, fp32 accumulation.
+//
+// rb_gemm_nt_bf16: out[M, C] = A[M, R] . Bm[C, R]^T (+ bias[C]), bf16 out
+//   nn.Linear's forward (Bm = W) and input gradient (Bm = W^T) on bf16
+//   activations (RecBLR.py:162,165,167 and their autograd).  Bm is the fp32
+//   weight rounded to bf16 once per call, in MFMA fragment order
+//   (rb_gemm_bf16_weight_image: fragment (column block cb, k16 block kb) =
+//   64 lanes x 16 B, lane l: column 32 cb + l % 32, k 16 kb + 8 (l / 32) ..
+//   + 7), so a k-step's weight slice is a run of contiguous 1 KB DMAs from L2.
+//   The bias is added in fp32 before the one rounding to bf16.
+// rb_gemm_tn_bf16: part[s][N, K] = dY[chunk_s]^T . X[chunk_s], fp32
+//   The weight gradients of the same Linears over row chunks; the fixed-order
+//   column sum (rb_colsum) adds the partials.
+//
+// Both: one 512-thread workgroup per CU (128 KB of LDS: 2 stages of A and B),
+// 256 x 256 output tiles, waves 4 x 2 owning 64 x 128 each (2 x 4 blocks of
+// 32 x 32), every operand global -> LDS by LDS-DMA, the next k-step issued
+// right after the barrier that frees its slot.
+#include "common.h"
+
+#include <type_traits>
+
+namespace rb {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(3))) fp16x4_t* lds_h4_ptr;
+
+__device__ __forceinline__ f32x16 mfma_bf(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ T bds_read16(uint32_t addr) {
+  T r;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+template <int OFF, typename T>
+__device__ __forceinline__ T bds_read16o(uint32_t addr) {
+  T r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "n"(OFF));
+  return r;
+}
+
+template <int N>
+__device__ __forceinline__ void bwait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// workgroup barrier that no LDS access is moved across
+__device__ __forceinline__ void bbarrier() { asm volatile("s_barrier" ::: "memory"); }
+
+// 4 x 4 transpose inside each lane quad (lane k of a quad holds column k,
+// v[r] = row r on entry; row k, v[c] = column c on exit)
+__device__ __forceinline__ float bdpp(float x, int ctl) {
+  return __builtin_bit_cast(float, ctl == 0xB1
+      ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false)
+      : __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void quad_t(float (&v)[4], int lane) {
+  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const float y = bdpp(b1 ? v[r] : v[r + 2], 0x4E);
+    if (b1) v[r] = y; else v[r + 2] = y;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r += 2) {
+    const float y = bdpp(b0 ? v[r] : v[r + 1], 0xB1);
+    if (b0) v[r] = y; else v[r + 1] = y;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight image: Bm[c][k] = W[c * ldw + k] (transpose = 0) or W[k * ldw + c]
+// (transpose = 1: Bm = W^T), rounded to bf16, fragment order
+__global__ void __launch_bounds__(256) k_bf16_weight_image(const float* __restrict__ W, int64_t ldw,
+                                                           int C, int R, int transpose,
+                                                           bf16x8* __restrict__ img) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int KB = R / 16;
+  if (t >= (int64_t)(C / 32) * KB * 64) return;
+  const int lane = (int)(t & 63);
+  const int64_t fi = t >> 6;
+  const int cb = (int)(fi / KB), kb = (int)(fi % KB);
+  const int c = cb * 32 + (lane & 31), k0 = kb * 16 + 8 * (lane >> 5);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    o[j] = (__bf16)(transpose ? W[(int64_t)(k0 + j) * ldw + c] : W[(int64_t)c * ldw + k0 + j]);
+  img[t] = o;
+}
+
+// ---------------------------------------------------------------------------
+constexpr int BF_BM = 256, BF_BN = 256, BF_BK = 64;
+constexpr int BF_WAVES = 8, BF_THREADS = 64 * BF_WAVES;
+constexpr int BF_A_STAGE = BF_BM * BF_BK * 2;                   // 32 KB: 256 rows x 128 B
+constexpr int BF_B_STAGE = (BF_BN / 32) * (BF_BK / 16) * 1024;  // 32 KB: 8 x 4 fragments
+constexpr int BF_LDS = 2 * (BF_A_STAGE + BF_B_STAGE);           // 128 KB
+
+// Persistent over tiles T = blockIdx.x + i * gridDim.x; the column tiles of
+// one row tile are neighbouring workgroups of one XCD (same blockIdx % 8), so
+// their A re-reads hit that XCD's L2.  A tile's results are rounded at its
+// end and stored two blocks per k-step during the next tile (behind its
+// MFMAs), so the k-step waits never drain a whole tile's stores.
+template <bool BIAS>
+__global__ void __launch_bounds__(BF_THREADS, 1)
+k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
+             const bf16x8* __restrict__ Wf, int C, const float* __restrict__ bias,
+             __bf16* __restrict__ out, int64_t ldo, int m_tiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nct = C / BF_BN, KT = R / BF_BK, KB16 = R / 16;
+  const int n_tiles = ((m_tiles + 7) >> 3) * 8 * nct;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int my_tiles = bid < n_tiles ? (n_tiles - 1 - bid) / G + 1 : 0;
+  const int U = my_tiles * KT;
+  if (U == 0) return;
+  auto tile_of = [&](int i, int& mt, int& ct) {
+    const int T = bid + i * G;
+    const int g = T >> 3;
+    ct = g % nct;
+    mt = (g / nct) * 8 + (T & 7);
+  };
+
+  // ---- DMA of one k-step into stage `slot`.  A image: 128-B rows, 16-B
+  // chunk c of row r at chunk c ^ ((r >> 1) & 7) (conflict-free fragment
+  // reads); wave w moves rows 32w .. 32w + 31 (4 x 8 rows).  B image:
+  // fragment (cb, s) at (4 cb + s) KB; wave w moves column block w.
+  int d_i = 0, d_kt = 0, d_mt, d_ct;
+  const char* d_base = nullptr;   // the wave's first row of the tile (uniform)
+  uint32_t d_off[4];              // + 32-bit lane offsets (rows past M repeat row M - 1)
+  auto d_tile = [&]() {
+    tile_of(d_i, d_mt, d_ct);
+    // base row clamped to M - 1 (padding tiles past m_tiles start there), so
+    // every lane offset is a non-negative row distance of at most 31
+    const int64_t r0 = (int64_t)d_mt * BF_BM + wave * 32;
+    const int64_t rb0 = r0 < M ? r0 : M - 1;
+    d_base = reinterpret_cast<const char*>(A + rb0 * lda);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int rr = q * 8 + (lane >> 3);
+      const int64_t r = (r0 + rr < M ? r0 + rr : M - 1) - rb0;
+      d_off[q] = (uint32_t)(r * lda * 2) + (((lane & 7) ^ ((rr >> 1) & 7)) << 4);
+    }
+  };
+  d_tile();
+  auto issue = [&](int slot) {
+    char* sa = smem + slot * BF_A_STAGE + wave * 4096;
+    const char* b = d_base + d_kt * (BF_BK * 2);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(b + d_off[q]), (lds_ptr_t)(sa + q * 1024), 16, 0, 0);
+    char* sb = smem + 2 * BF_A_STAGE + slot * BF_B_STAGE + wave * 4096;
+    const bf16x8* ws = Wf + ((int64_t)(d_ct * 8 + wave) * KB16 + d_kt * 4) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(ws + q * 64), (lds_ptr_t)(sb + q * 1024), 16, 0, 0);
+    if (++d_kt == KT) {
+      d_kt = 0;
+      if (++d_i < my_tiles) d_tile();
+    }
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][n][e] = 0.0f;
+
+  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  // A fragment (rows 64 wm + 32 rb + lane % 32, k 16 s + 8 (lane / 32) ..):
+  // logical chunk 2s + lane / 32 of its row
+  // ((2s + h) ^ sw) << 4 = ((h ^ sw) << 4) ^ (s << 5): one register per rb
+  uint32_t a_off[2];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int row = wm * 64 + rb * 32 + (lane & 31);
+    a_off[rb] = row * 128 + (((lane >> 5) ^ ((row >> 1) & 7)) << 4);
+  }
+
+  // pending results of the previous tile: bf16, after the quad transpose a
+  // lane holds 4 consecutive columns of one row per 4-row group
+  u32x2 pend[2][4][4];
+  int pend_mt = -1, pend_ct = 0, pend_q = 4;
+  bool pend_full = true;
+  auto store_blk = [&](int rb, int cb, const u32x2 (&blk)[4]) {
+    const int col = pend_ct * BF_BN + wn * 128 + cb * 32 + (lane & 28);
+    const int64_t rbase = (int64_t)pend_mt * BF_BM + wm * 64 + rb * 32 + 4 * (lane >> 5) + (lane & 3);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int64_t row = rbase + 8 * g;
+      if (pend_full || row < M)
+        __builtin_nontemporal_store(blk[g], reinterpret_cast<u32x2*>(out + row * ldo + col));
+    }
+  };
+  // static register indexing: two blocks per call
+  auto store_pair = [&]() {
+    const int q = pend_q++;
+    if (q == 0) { store_blk(0, 0, pend[0][0]); store_blk(0, 1, pend[0][1]); }
+    else if (q == 1) { store_blk(0, 2, pend[0][2]); store_blk(0, 3, pend[0][3]); }
+    else if (q == 2) { store_blk(1, 0, pend[1][0]); store_blk(1, 1, pend[1][1]); }
+    else { store_blk(1, 2, pend[1][2]); store_blk(1, 3, pend[1][3]); }
+    return pend_full;   // 8 stores issued (partial tiles: maybe fewer)
+  };
+
+  issue(0);
+  int i = 0, kt = 0;
+  bool stored_prev = false;
+  for (int u = 0; u < U; ++u) {
+    // own DMAs of step u landed (younger: the 8 stores of step u - 1)
+    if (stored_prev) bwait_vm<8>(); else bwait_vm<0>();
+    bbarrier();
+    if (u + 1 < U) issue((u + 1) & 1);
+    const uint32_t sa = smem_base + (u & 1) * BF_A_STAGE;
+    const uint32_t sb = smem_base + 2 * BF_A_STAGE + (u & 1) * BF_B_STAGE + wn * 16384 + lane * 16;
+    stored_prev = false;
+    auto substep = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+      bf16x8 a0 = bds_read16<bf16x8>(sa + (a_off[0] ^ (s << 5)));
+      bf16x8 a1 = bds_read16<bf16x8>(sa + (a_off[1] ^ (s << 5)));
+      bf16x8 b[4];
+      b[0] = bds_read16o<(0 + s) * 1024, bf16x8>(sb);
+      b[1] = bds_read16o<(4 + s) * 1024, bf16x8>(sb);
+      b[2] = bds_read16o<(8 + s) * 1024, bf16x8>(sb);
+      b[3] = bds_read16o<(12 + s) * 1024, bf16x8>(sb);
+      asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a0), "+v"(a1), "+v"(b[0]));
+      acc[0][0] = mfma_bf(a0, b[0], acc[0][0]);
+      acc[1][0] = mfma_bf(a1, b[0], acc[1][0]);
+      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b[1]));
+      acc[0][1] = mfma_bf(a0, b[1], acc[0][1]);
+      acc[1][1] = mfma_bf(a1, b[1], acc[1][1]);
+      asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(b[2]));
+      acc[0][2] = mfma_bf(a0, b[2], acc[0][2]);
+      acc[1][2] = mfma_bf(a1, b[2], acc[1][2]);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[3]));
+      acc[0][3] = mfma_bf(a0, b[3], acc[0][3]);
+      acc[1][3] = mfma_bf(a1, b[3], acc[1][3]);
+    };
+    substep(std::integral_constant<int, 0>{});
+    if (pend_mt >= 0 && pend_q < 4) stored_prev = store_pair();
+    substep(std::integral_constant<int, 1>{});
+    substep(std::integral_constant<int, 2>{});
+    substep(std::integral_constant<int, 3>{});
+
+    if (kt == KT - 1) {
+      int mt, ct;
+      tile_of(i, mt, ct);
+      while (pend_mt >= 0 && pend_q < 4) store_pair();   // tiles shorter than 4 k-steps
+      float bv[4][4];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int col = ct * BF_BN + wn * 128 + cb * 32 + (lane & 28);
+        const f32x4 b4 = BIAS ? *reinterpret_cast<const f32x4*>(bias + col) : f32x4{0, 0, 0, 0};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) bv[cb][c] = b4[c];
+      }
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][4 * g + r];
+            quad_t(v, lane);
+            const f32x4 x = {v[0] + bv[cb][0], v[1] + bv[cb][1], v[2] + bv[cb][2], v[3] + bv[cb][3]};
+            pend[rb][cb][g] = __builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4));
+          }
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[rb][cb][e] = 0.0f;
+        }
+      pend_mt = mt < m_tiles ? mt : -1;
+      pend_ct = ct;
+      pend_q = 0;
+      pend_full = (int64_t)mt * BF_BM + BF_BM <= M;
+      kt = 0;
+      ++i;
+    } else {
+      ++kt;
+    }
+  }
+  while (pend_mt >= 0 && pend_q < 4) store_pair();
+}
+
+// ---------------------------------------------------------------------------
+// TN: the output tile (256 rows n of dY's columns x 256 columns k of X's) of
+// one row chunk.  Each k-step stages 64 rows of both operands as 512-B rows
+// (16-B chunk c of row r at chunk c ^ 4 (r & 3)), read into MFMA fragments by
+// ds_read_b64_tr_b16: per 16-lane group a 4-row x 16-column block, lane
+// 4q + p addressing row q, columns 4p .. 4p + 3, lane i receiving column i
+// (row q in element q), so two reads give a lane its column's 8 rows
+// 8 (lane / 32) .. + 7 of the 16-row block — the same rows for both operands.
+// Rows past the chunk read as zeros (buffer descriptor range check).
+constexpr int TB_BN = 256, TB_BK = 256, TB_ROWS = 64;
+constexpr int TB_STAGE = TB_ROWS * 512;              // 32 KB per operand
+constexpr int TB_LDS = 2 * 2 * TB_STAGE;             // 128 KB
+
+__device__ __forceinline__ bf16x8 tr_frag(uint32_t stage, int kb, int c0, int lane) {
+  const int q = (lane >> 2) & 3;
+  const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+  const uint32_t cpart = ((((col >> 3) ^ (q << 2))) << 4) + (col & 7) * 2;
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * kb + 8 * (lane >> 5) + 4 * i + q;
+    const fp16x4_t v =
+        __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4_ptr)(uintptr_t)(stage + row * 512 + cpart));
+    const bf16x4 w = __builtin_bit_cast(bf16x4, v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r[4 * i + e] = w[e];
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(BF_THREADS, 1)
+k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict__ X, int64_t ldx,
+             int64_t M, int N, int K, int64_t chunk, float* __restrict__ parts, int S) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nkt = K / TB_BK, ntile = (N / TB_BN) * nkt;
+  // the tiles of one chunk: neighbouring workgroups of one XCD
+  const int bid = blockIdx.x, li = bid >> 3;
+  const int tile = li % ntile, s = (li / ntile) * 8 + (bid & 7);
+  if (s >= S) return;
+  const int n0 = (tile / nkt) * TB_BN, k0 = (tile % nkt) * TB_BK;
+  const int64_t r_begin = (int64_t)s * chunk;
+  const int64_t left = M - r_begin;
+  const int rows = left <= 0 ? 0 : (int)(left < chunk ? left : chunk);
+  const int T = (rows + TB_ROWS - 1) / TB_ROWS;
+
+  auto rsrc_of = [&](const __bf16* base, int64_t ld) {
+    const uint64_t p = reinterpret_cast<uint64_t>(base + (rows ? r_begin * ld : 0));
+    const uint64_t pu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pu), 0,
+                                             (int)((int64_t)rows * ld * 2), 0x00020000);
+  };
+  const auto ry = rsrc_of(Y + n0, ldy);
+  const auto rx = rsrc_of(X + k0, ldx);
+  const uint32_t ldy2 = (uint32_t)(ldy * 2), ldx2 = (uint32_t)(ldx * 2);
+  // DMA: instruction j = 4 wave + q moves rows 2j, 2j + 1 of the step
+  auto issue = [&](int t, int slot) {
+    char* st = smem + slot * 2 * TB_STAGE;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = wave * 4 + q;
+      const int row = 2 * j + (lane >> 5);
+      const int lc = (lane & 31) ^ ((row & 3) << 2);
+      const uint32_t r = (uint32_t)(t * TB_ROWS + row);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_ptr_t)(st + j * 1024), 16, r * ldy2 + lc * 16, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(st + TB_STAGE + j * 1024), 16,
+                                           r * ldx2 + lc * 16, 0, 0, 0);
+    }
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][n][e] = 0.0f;
+
+  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
+  if (T > 0) issue(0, 0);
+  for (int t = 0; t < T; ++t) {
+    bwait_vm<0>();
+    bbarrier();
+    if (t + 1 < T) issue(t + 1, (t + 1) & 1);
+    const uint32_t sy = smem_base + (t & 1) * 2 * TB_STAGE, sx = sy + TB_STAGE;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      bf16x8 a[2], b[4];
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) a[rb] = tr_frag(sy, kb, wr * 64 + rb * 32, lane);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) b[cb] = tr_frag(sx, kb, wc * 128 + cb * 32, lane);
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb) acc[rb][cb] = mfma_bf(a[rb], b[cb], acc[rb][cb]);
+    }
+  }
+
+  // partial tile: lane quads transposed, 16-B stores
+  float* P = parts + (int64_t)s * N * K;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][4 * g + r];
+        quad_t(v, lane);
+        const int n = n0 + wr * 64 + rb * 32 + 8 * g + 4 * (lane >> 5) + (lane & 3);
+        const int k = k0 + wc * 128 + cb * 32 + (lane & 28);
+        __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]},
+                                    reinterpret_cast<f32x4*>(P + (int64_t)n * K + k));
+      }
+}
+
+template <typename F>
+void set_lds(F* f, int bytes) {
+  (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
+
+}  // namespace
+
+int launch_bf16_weight_image(const float* W, int64_t ldw, int C, int R, int transpose, void* img,
+                             hipStream_t st) {
+  const int64_t total = (int64_t)(C / 32) * (R / 16) * 64;
+  k_bf16_weight_image<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(W, ldw, C, R, transpose,
+                                                                       (bf16x8*)img);
+  return launch_status("rb_gemm_bf16_weight_image");
+}
+
+int launch_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int R, const void* img, int C,
+                        const float* bias, void* out, int64_t ldo, hipStream_t st) {
+  static bool attr = false;   // benign race: idempotent
+  if (!attr) {
+    set_lds(k_gemm_nt_bf<true>, BF_LDS);
+    set_lds(k_gemm_nt_bf<false>, BF_LDS);
+    attr = true;
+  }
+  const int m_tiles = (int)((M + BF_BM - 1) / BF_BM);
+  const int64_t n_tiles = (int64_t)((m_tiles + 7) / 8) * 8 * (C / BF_BN);
+  const unsigned grid = (unsigned)std::min<int64_t>(n_tiles, (int64_t)num_cus() / 8 * 8);
+  const __bf16* a = (const __bf16*)A;
+  const bf16x8* w = (const bf16x8*)img;
+  __bf16* o = (__bf16*)out;
+  if (bias)
+    k_gemm_nt_bf<true><<<grid, BF_THREADS, BF_LDS, st>>>(a, lda, M, R, w, C, bias, o, ldo, m_tiles);
+  else
+    k_gemm_nt_bf<false><<<grid, BF_THREADS, BF_LDS, st>>>(a, lda, M, R, w, C, bias, o, ldo, m_tiles);
+  return launch_status("rb_gemm_nt_bf16");
+}
+
+int launch_gemm_tn_bf16(const void* Y, int64_t ldy, const void* X, int64_t ldx, int64_t M, int N,
+                        int K, float* parts, int S, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    set_lds(k_gemm_tn_bf, TB_LDS);
+    attr = true;
+  }
+  const int64_t per = (M + S - 1) / S;
+  const int64_t chunk = (per + TB_ROWS - 1) / TB_ROWS * TB_ROWS;
+  const int ntile = (N / TB_BN) * (K / TB_BK);
+  k_gemm_tn_bf<<<(unsigned)(ntile * S), BF_THREADS, TB_LDS, st>>>(
+      (const __bf16*)Y, ldy, (const __bf16*)X, ldx, M, N, K, chunk, parts, S);
+  return launch_status("rb_gemm_tn_bf16");
+}
+
+}  // namespace rb

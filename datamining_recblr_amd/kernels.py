@@ -1248,6 +1248,56 @@ def gemm_tn_h(dy: torch.Tensor, x: torch.Tensor, ymax: torch.Tensor, xmax: torch
     return parts
 
 
+def bf16_weight_image(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """The bf16 fragment image of Bm = w [C, R] (transpose=False) or w^T
+    (transpose=True; w [R, C]) for gemm_nt_bf16 (rb_gemm_bf16_weight_image)."""
+    _check(w, "w")
+    if w.dim() != 2 or w.stride(1) != 1:
+        raise ValueError("w must be a 2-D tensor with unit inner stride")
+    C, R = (w.shape[1], w.shape[0]) if transpose else (w.shape[0], w.shape[1])
+    img = torch.empty(C * R, device=w.device, dtype=torch.bfloat16)
+    _lib.call("rb_gemm_bf16_weight_image", w.data_ptr(), w.stride(0), C, R, int(transpose),
+              img.data_ptr(), _stream(w))
+    return img
+
+
+def gemm_nt_bf16(a: torch.Tensor, img: torch.Tensor, C: int,
+                 bias: torch.Tensor | None = None) -> torch.Tensor:
+    """out[M, C] (bf16) = a[M, R] (bf16) @ Bm^T (+ bias, fp32, added before the
+    rounding) on the bf16 MFMA pipe (rb_gemm_nt_bf16); img from
+    bf16_weight_image."""
+    _check(a, "a", torch.bfloat16)
+    _check(img, "img", torch.bfloat16)
+    if a.dim() != 2 or a.stride(1) != 1:
+        raise ValueError("a must be a 2-D tensor with unit inner stride")
+    M, R = a.shape
+    if img.numel() != C * R:
+        raise ValueError("img does not match a [M, R] operand with C outputs")
+    if bias is not None:
+        _check(bias, "bias")
+    out = torch.empty((M, C), device=a.device, dtype=torch.bfloat16)
+    _lib.call("rb_gemm_nt_bf16", a.data_ptr(), a.stride(0), M, R, img.data_ptr(), C,
+              0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0), _stream(a))
+    return out
+
+
+def gemm_tn_bf16(dy: torch.Tensor, x: torch.Tensor, splits: int) -> torch.Tensor:
+    """Row-chunk partials of dW = dy^T x on bf16 operands (rb_gemm_tn_bf16):
+    fp32 [splits, N, K]."""
+    _check(dy, "dy", torch.bfloat16)
+    _check(x, "x", torch.bfloat16)
+    if dy.dim() != 2 or x.dim() != 2 or dy.stride(1) != 1 or x.stride(1) != 1:
+        raise ValueError("dy and x must be 2-D with unit inner stride")
+    M, N = dy.shape
+    K = x.shape[1]
+    if x.shape[0] != M:
+        raise ValueError("dy and x must have the same rows")
+    parts = torch.empty((splits, N, K), device=dy.device, dtype=torch.float32)
+    _lib.call("rb_gemm_tn_bf16", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K,
+              parts.data_ptr(), splits, _stream(dy))
+    return parts
+
+
 def gemm_tn_hs(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
                accumulate: bool = False) -> torch.Tensor:
     """dW = dy^T x [N, K] for few rows on the f16 pipe (rb_gemm_tn_hs: exact

@@ -88,6 +88,7 @@ if register_optimizer_step_post_hook is not None:
 
 def invalidate_split_cache() -> None:
     _split_cache.clear()
+    _bf16_cache.clear()
 
 
 def _stamp(w: torch.Tensor):
@@ -168,11 +169,50 @@ def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
     return None
 
 
+# bf16 activations (BASELINE configs[4]): the projections on our bf16 MFMA
+# kernels (csrc/gemm_bf16.hip); RECBLR_BF16_GEMM=0: torch (hipBLASLt).  The
+# weight's bf16 fragment images (W for the forward, W^T for the input
+# gradient) are cached per weight version like the split images.
+_bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "1") != "0"
+_bf16_cache: dict = {}
+
+
+def set_bf16_gemm(on: bool) -> bool:
+    """Switch the bf16 projection kernels (A/B in bench.py); returns the
+    previous setting."""
+    global _bf16_gemm
+    prev, _bf16_gemm = _bf16_gemm, bool(on)
+    return prev
+
+
+def _bf16_image(w: torch.Tensor, transpose: bool) -> torch.Tensor:
+    key = (id(w), transpose)
+    e = _bf16_cache.get(key)
+    if (_cache_on and e is not None and e[0]() is w and e[1] == w.data_ptr()
+            and e[2] == _stamp(w)):
+        return e[3]
+    img = kernels.bf16_weight_image(w, transpose)
+    if _cache_on:
+        for k in [k for k, v in _bf16_cache.items() if v[0]() is None]:
+            del _bf16_cache[k]
+        _bf16_cache[key] = (weakref.ref(w), w.data_ptr(), _stamp(w), img)
+    return img
+
+
+def _bf16_ok(a: torch.Tensor, w: torch.Tensor, C: int, R: int) -> bool:
+    return (_bf16_gemm and a.dtype == torch.bfloat16 and w.dtype == torch.float32 and a.is_cuda
+            and a.dim() == 2 and a.stride(1) == 1 and a.stride(0) % 8 == 0
+            and a.data_ptr() % 16 == 0 and w.stride(1) == 1 and R % 64 == 0 and C % 256 == 0)
+
+
 def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
           rmax: torch.Tensor | None = None) -> torch.Tensor:
     """a [M, K] @ w[N, K]^T (+ bias): F.linear's forward GEMM.  bf16
     activations (config 5) use the weight rounded to bf16 (bf16 MFMA, fp32
     accumulation, bf16 output).  rmax: from rmax_buffer(a, N, K)."""
+    if a.dtype != w.dtype and _bf16_ok(a, w, w.shape[0], w.shape[1]):
+        b = None if bias is None else bias.contiguous()
+        return kernels.gemm_nt_bf16(a, _bf16_image(w, False), w.shape[0], bias=b)
     if a.dtype != w.dtype:
         wb = w.to(a.dtype)
         return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
@@ -237,6 +277,8 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
           rmax: torch.Tensor | None = None) -> torch.Tensor:
     """dy [M, N] @ w [N, K] (the input gradient of F.linear); with `out`,
     accumulated into it in place (out += dy @ w)."""
+    if dy.dtype != w.dtype and out is None and _bf16_ok(dy, w, w.shape[1], w.shape[0]):
+        return kernels.gemm_nt_bf16(dy, _bf16_image(w, True), w.shape[1])
     if dy.dtype != w.dtype:
         wb = w.to(dy.dtype)
         return out.addmm_(dy, wb) if out is not None else dy @ wb
@@ -262,6 +304,8 @@ MIN_ROWS_FOR_SPLIT = 16384
 # another lease) — the step then runs no library GEMM (RECBLR_TN_FEW=0:
 # hipBLASLt)
 TN_FEW_MIN_ROWS = 2048
+# bf16 operands (configs[4]): the bf16 weight-gradient kernel from this many rows
+TN_BF16_MIN_ROWS = 4096
 _tn_few = os.environ.get("RECBLR_TN_FEW", "1") != "0"
 
 
@@ -295,6 +339,15 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
         if M < MIN_ROWS_FOR_SPLIT:   # at least one 32-row group per split
             S = max(8, min(S, M // 32 // 8 * 8))
         parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
+        return kernels.colsum(parts.view(S, -1)).view(N, K)
+    if (_bf16_gemm and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+            and M >= TN_BF16_MIN_ROWS and N % 256 == 0 and K % 256 == 0
+            and dy2.stride(1) == 1 and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0
+            and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0):
+        # one 256 x 256 tile per chunk and CU: splits x tiles ~ one round
+        nt = (N // 256) * (K // 256)
+        S = max(8, min(_tn_splits(dy2.device, nt) // 2 // 8 * 8, M // 64 // 8 * 8))
+        parts = kernels.gemm_tn_bf16(dy2, x2, S)
         return kernels.colsum(parts.view(S, -1)).view(N, K)
     if (_small_tn and _half and _split_on and _tn_on and M < MIN_ROWS_FOR_SPLIT and N % 32 == 0
             and K % 32 == 0 and dy2.dtype == torch.float32 and x2.dtype == torch.float32

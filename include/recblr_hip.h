@@ -589,6 +589,34 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
                  int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
                  void* stream);
 
+/* ---- bf16 activations (BASELINE configs[4]: L = 2048, d = 256) ----------
+ * The same Linears (RecBLR.py:162,165,167 and their autograd) when the
+ * activations are bf16: bf16 operands on v_mfma_f32_32x32x16_bf16, fp32
+ * accumulation (csrc/gemm_bf16.hip).  Replace torch.addmm / mm / bmm on
+ * bf16 tensors (hipBLASLt).
+ *
+ * The weight image: Bm [C, R] = W (transpose = 0; W row stride ldw) or W^T
+ * (transpose = 1), rounded to bf16 (nearest even) in MFMA fragment order;
+ * img holds C * R bf16 (2 C R bytes, 16-byte aligned); C % 32 == 0,
+ * R % 16 == 0. */
+int rb_gemm_bf16_weight_image(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
+                              void* img, void* stream);
+
+/* out[M, C] (bf16, row stride ldo) = A[M, R] (bf16, row stride lda) . Bm^T
+ * (+ bias[C], fp32, added before the one rounding to bf16).  R % 64 == 0,
+ * C % 256 == 0, lda % 8 == 0, ldo % 4 == 0; A, img, bias 16-byte aligned,
+ * out 8-byte aligned. */
+int rb_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int64_t R, const void* img, int64_t C,
+                    const float* bias, void* out, int64_t ldo, void* stream);
+
+/* Weight gradient on bf16 operands: parts[s][n, k] (fp32, every slot
+ * written) = sum over the rows m of chunk s of dY[m, n] X[m, k] (bf16;
+ * chunks of a multiple of 64 rows); sum the partials in order (rb_colsum).
+ * N % 256 == 0, K % 256 == 0, splits % 8 == 0, row strides multiples of 8,
+ * pointers 16-byte aligned. */
+int rb_gemm_tn_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t M, int64_t N,
+                    int64_t K, float* parts, int64_t splits, void* stream);
+
 /* dW (+)= dY^T X for few rows M (F.linear's weight gradient on the gathered
  * last-layer tail, RecBLR.py:167,213,214 at B rows; any M up to 2^24, fastest
  * below ~16k): dW [N, K] row-major fp32, written (accumulate = 0) or added to

@@ -1,0 +1,156 @@
+"""bf16-operand projection GEMMs (csrc/gemm_bf16.hip: rb_gemm_nt_bf16,
+rb_gemm_tn_bf16, rb_gemm_bf16_weight_image) — the configs[4] Linears
+(RecBLR.py:162,165,167 and their autograd) on bf16 activations.
+
+Reference: the same bf16 operands in fp64 on the host.  The NT output is one
+rounding of an fp32 sum to bf16, so each element must sit within a bf16
+half-ulp (2^-9 relative, tested at 2^-8) plus the fp32 accumulation bound
+(K 2^-24 sum |a w|, tested at 1e-5 of that sum); the weight-gradient partials
+are fp32 sums of exact bf16 products (tested at 1e-5 of sum |dy x|)."""
+import pytest
+import torch
+
+from datamining_recblr_amd import kernels, linear
+
+BF = torch.bfloat16
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+def _nt_ref(a, wb, bias):
+    ref = a.double().cpu() @ wb.double().cpu().t()
+    mag = a.double().abs().cpu() @ wb.double().abs().cpu().t()
+    if bias is not None:
+        ref = ref + bias.double().cpu()
+        mag = mag + bias.double().abs().cpu()
+    return ref, mag
+
+
+@pytest.mark.parametrize("M,R,C,with_bias", [
+    (4096 + 37, 256, 1024, True),     # in-proj shape, partial last row tile
+    (2048, 512, 1024, True),          # gates
+    (1000, 512, 256, False),          # out-proj, fewer rows than one round
+    (300, 64, 512, False),            # one k-step per tile (stores flushed per tile)
+    (8 * 256 * 3 + 5, 1024, 512, False),   # dX shapes: K = 1024
+])
+def test_gemm_nt_bf16_vs_fp64(cuda, M, R, C, with_bias):
+    g = torch.Generator(device=cuda).manual_seed(M + R + C)
+    a = torch.randn(M, R, device=cuda, generator=g).to(BF)
+    w = torch.randn(C, R, device=cuda, generator=g) * R ** -0.5
+    bias = torch.randn(C, device=cuda, generator=g) if with_bias else None
+    out = kernels.gemm_nt_bf16(a, kernels.bf16_weight_image(w), C, bias=bias)
+    assert out.dtype == BF and out.shape == (M, C)
+    ref, mag = _nt_ref(a, w.to(BF), bias)
+    err = (out.double().cpu() - ref).abs()
+    bound = 2.0 ** -8 * ref.abs() + 1e-5 * mag + 1e-30
+    assert bool((err <= bound).all()), f"max excess {(err - bound).max().item():.3e}"
+
+
+def test_gemm_nt_bf16_transposed_image(cuda):
+    """The input-gradient form dX = dY W: Bm = W^T from the transposed image."""
+    g = torch.Generator(device=cuda).manual_seed(3)
+    M, N, K = 4096, 1024, 256            # dY [M, N], W [N, K] -> dX [M, K]
+    dy = torch.randn(M, N, device=cuda, generator=g).to(BF)
+    w = torch.randn(N, K, device=cuda, generator=g) * N ** -0.5
+    out = kernels.gemm_nt_bf16(dy, kernels.bf16_weight_image(w, transpose=True), K)
+    ref, mag = _nt_ref(dy, w.to(BF).t(), None)
+    err = (out.double().cpu() - ref).abs()
+    assert bool((err <= 2.0 ** -8 * ref.abs() + 1e-5 * mag).all())
+
+
+def test_bf16_weight_image_layout(cuda):
+    """Fragment (cb, kb), lane l: column 32 cb + l % 32, k 16 kb + 8 (l / 32) + j."""
+    C, R = 64, 48
+    w = torch.arange(C * R, device=cuda, dtype=torch.float32).view(C, R) / 64.0
+    img = kernels.bf16_weight_image(w).view(C // 32, R // 16, 64, 8).cpu()
+    wb = w.to(BF).cpu()
+    for cb in range(C // 32):
+        for kb in range(R // 16):
+            for lane in (0, 5, 31, 32, 63):
+                c, k0 = 32 * cb + lane % 32, 16 * kb + 8 * (lane // 32)
+                assert torch.equal(img[cb, kb, lane], wb[c, k0:k0 + 8])
+    imt = kernels.bf16_weight_image(w, transpose=True).view(R // 32, C // 16, 64, 8).cpu()
+    assert torch.equal(imt[1, 2, 33], wb[32:40, 32 + 1])
+
+
+@pytest.mark.parametrize("M,N,K,S", [
+    (4096, 1024, 256, 64),
+    (100000, 256, 512, 16),      # chunks of 6,272 rows, the last one short
+    (300, 512, 256, 16),         # most chunks empty: their slots written as zeros
+    (4096 + 33, 1024, 512, 8),
+])
+def test_gemm_tn_bf16_vs_fp64(cuda, M, N, K, S):
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    dy = torch.randn(M, N, device=cuda, generator=g).to(BF)
+    x = torch.randn(M, K, device=cuda, generator=g).to(BF)
+    parts = torch.full((S, N, K), float("nan"), device=cuda)
+    parts = kernels.gemm_tn_bf16(dy, x, S)
+    assert bool(torch.isfinite(parts).all())
+    dw = parts.sum(0).double().cpu()
+    ref = dy.double().cpu().t() @ x.double().cpu()
+    mag = dy.double().abs().cpu().t() @ x.double().abs().cpu()
+    assert bool(((dw - ref).abs() <= 1e-5 * mag).all())
+    # each slot is its own chunk's product
+    chunk = ((M + S - 1) // S + 63) // 64 * 64
+    s = 1 if M > chunk else 0
+    r0, r1 = s * chunk, min(M, (s + 1) * chunk)
+    ref1 = dy[r0:r1].double().cpu().t() @ x[r0:r1].double().cpu()
+    mag1 = dy[r0:r1].double().abs().cpu().t() @ x[r0:r1].double().abs().cpu()
+    assert bool(((parts[s].double().cpu() - ref1).abs() <= 1e-5 * mag1 + 1e-30).all())
+
+
+def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
+    """configs[4]'s GatedRecurrentLayer (d = 256, L = 2048) runs all three
+    projections' forward, input-gradient and weight-gradient GEMMs on the bf16
+    kernels, and agrees with the hipBLASLt path to bf16 accuracy."""
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    calls = {"nt": 0, "tn": 0}
+    nt0, tn0 = kernels.gemm_nt_bf16, kernels.gemm_tn_bf16
+
+    def nt(*a, **k):
+        calls["nt"] += 1
+        return nt0(*a, **k)
+
+    def tn(*a, **k):
+        calls["tn"] += 1
+        return tn0(*a, **k)
+
+    monkeypatch.setattr(kernels, "gemm_nt_bf16", nt)
+    monkeypatch.setattr(kernels, "gemm_tn_bf16", tn)
+    torch.manual_seed(5)
+    layer = GatedRecurrentLayer(d_model=256).to(cuda)
+    g = torch.Generator(device=cuda).manual_seed(9)
+    x = torch.randn(2, 2048, 256, device=cuda, generator=g).to(BF)
+    gy = torch.randn(2, 2048, 256, device=cuda, generator=g).to(BF)
+
+    def run(on):
+        prev = linear.set_bf16_gemm(on)
+        try:
+            layer.zero_grad(set_to_none=True)
+            xx = x.clone().requires_grad_()
+            y = layer(xx)
+            y.backward(gy)
+            return y.detach().float(), xx.grad.float(), {n: p.grad.clone() for n, p in
+                                                         layer.named_parameters()}
+        finally:
+            linear.set_bf16_gemm(prev)
+
+    y1, dx1, g1 = run(True)
+    assert calls == {"nt": 6, "tn": 3}, calls
+    y0, dx0, g0 = run(False)
+    assert calls == {"nt": 6, "tn": 3}
+
+    def rel(a, b):
+        return ((a - b).abs().max() / b.abs().max()).item()
+
+    assert rel(y1, y0) < 2e-2
+    assert rel(dx1, dx0) < 2e-2
+    for n in g0:
+        assert rel(g1[n], g0[n]) < 2e-2, n

@@ -8,16 +8,23 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef __fp16 fp16x4_t __attribute__((__vector_size__(8)));
 typedef __attribute__((address_space(3))) fp16x4_t* lds_h4_ptr;
 
-template <int D>
-__device__ __forceinline__ f16x8 tile_gather_h(const _Float16* tile, int ch0, int kb, int lane) {
+// EV: the even swizzle (2 r mod NS) item_scores.hip's fused CE kernels use;
+// otherwise r mod NS, the other streamed tiles' swizzle
+template <int D, bool EV>
+__device__ __forceinline__ int swz(int r) {
   constexpr int NS = D / 4;
+  return EV ? (2 * r) & (NS - 1) : r % NS;
+}
+
+template <int D, bool EV>
+__device__ __forceinline__ f16x8 tile_gather_h(const _Float16* tile, int ch0, int kb, int lane) {
   const int h = lane >> 5, q = (lane >> 2) & 3;
   const int c = ch0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
   f16x8 r;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = 16 * kb + 8 * i + 4 * h + q;
-    const _Float16* a = tile + row * 2 * D + (((c >> 3) ^ (row % NS)) << 3) + (c & 7);
+    const _Float16* a = tile + row * 2 * D + (((c >> 3) ^ swz<D, EV>(row)) << 3) + (c & 7);
     const fp16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4_ptr)(a));
 #pragma unroll
     for (int e = 0; e < 4; ++e) r[4 * i + e] = __builtin_bit_cast(_Float16, v[e]);
@@ -25,15 +32,14 @@ __device__ __forceinline__ f16x8 tile_gather_h(const _Float16* tile, int ch0, in
   return r;
 }
 
-template <int D>
+template <int D, bool EV>
 __global__ void k(int* bad, int enc) {
-  constexpr int NS = D / 4;
   __shared__ __attribute__((aligned(16))) _Float16 t[32 * 2 * D];
-  // image: logical half-column lc of row r stored at physical slot (lc>>3) ^ (r % NS);
+  // image: logical half-column lc of row r stored at physical slot (lc>>3) ^ swz(r);
   // enc 0: the element holds its row, enc 1: its logical column (exact in f16)
   for (int i = threadIdx.x; i < 32 * 2 * D; i += 64) {
     const int r = i / (2 * D), pc = i % (2 * D);
-    const int lc = ((((pc >> 3) ^ (r % NS))) << 3) + (pc & 7);   // XOR is an involution
+    const int lc = ((((pc >> 3) ^ swz<D, EV>(r))) << 3) + (pc & 7);   // XOR is an involution
     t[i] = (_Float16)(float)(enc == 0 ? r : lc);
   }
   __syncthreads();
@@ -43,7 +49,7 @@ __global__ void k(int* bad, int enc) {
     for (int p = 0; p < 2; ++p)
       for (int n = 0; n < D / 32; ++n) {
         const int ch0 = p * D + 32 * n;
-        const f16x8 g = tile_gather_h<D>(t, ch0, kb, lane);
+        const f16x8 g = tile_gather_h<D, EV>(t, ch0, kb, lane);
         for (int kk = 0; kk < 8; ++kk) {
           const int row = 16 * kb + 8 * (kk >> 2) + 4 * h + (kk & 3);
           const int want = enc == 0 ? row : ch0 + (lane & 31);
@@ -57,15 +63,21 @@ int main() {
   int* d;
   (void)hipMalloc(&d, 16);
   int h;
-  for (int enc = 0; enc < 2; ++enc) {
-    (void)hipMemset(d, 0, 4);
-    k<32><<<1, 64>>>(d, enc);
-    (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
-    printf("D=32 enc %d mismatches %d\n", enc, h);
-    (void)hipMemset(d, 0, 4);
-    k<128><<<1, 64>>>(d, enc);
-    (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
-    printf("D=128 enc %d mismatches %d\n", enc, h);
-  }
+  for (int ev = 0; ev < 2; ++ev)
+    for (int enc = 0; enc < 2; ++enc) {
+      const char* sw = ev ? "2r mod NS" : "r mod NS";
+      (void)hipMemset(d, 0, 4);
+      if (ev) k<32, true><<<1, 64>>>(d, enc); else k<32, false><<<1, 64>>>(d, enc);
+      (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+      printf("swizzle %-9s D=32  enc %d mismatches %d\n", sw, enc, h);
+      (void)hipMemset(d, 0, 4);
+      if (ev) k<64, true><<<1, 64>>>(d, enc); else k<64, false><<<1, 64>>>(d, enc);
+      (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+      printf("swizzle %-9s D=64  enc %d mismatches %d\n", sw, enc, h);
+      (void)hipMemset(d, 0, 4);
+      if (ev) k<128, true><<<1, 64>>>(d, enc); else k<128, false><<<1, 64>>>(d, enc);
+      (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
+      printf("swizzle %-9s D=128 enc %d mismatches %d\n", sw, enc, h);
+    }
   return 0;
 }
