@@ -354,7 +354,8 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
     projections) forward + backward on synthetic input; sequences/s over all
     ranks (weak scaling, max-over-ranks time).  The HBM fraction is that of
     the bf16 conv + gate-scan kernels (algorithmic bytes 20*N*2 per step,
-    N = B*L*H)."""
+    N = B*L*H).  The projections run on rb_gemm_nt_bf16 / rb_gemm_tn_bf16
+    (RECBLR_BF16_GEMM=0: torch's bf16 GEMMs); projection_gemms_ab times both."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     B, L, d = args.c5_batch, 2048, 256
@@ -381,6 +382,27 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
         barrier(env)
         el = max_over_ranks(time.perf_counter() - t0, env, dev)
     summ = t.summary()
+    # the projections on our bf16 kernels (rb_gemm_nt_bf16 / rb_gemm_tn_bf16)
+    # vs torch's bf16 GEMMs (hipBLASLt), alternated, best of 2 per variant
+    from datamining_recblr_amd import linear as _lin
+    saved_g = _lin.set_bf16_gemm(True)
+    runs = {"own_bf16_kernels": [], "torch_hipblaslt": []}
+    for _ in range(2):
+        for name, on in (("own_bf16_kernels", True), ("torch_hipblaslt", False)):
+            _lin.set_bf16_gemm(on)
+            one()
+            torch.cuda.synchronize()
+            barrier(env)
+            t1 = time.perf_counter()
+            for _ in range(steps):
+                one()
+            torch.cuda.synchronize()
+            barrier(env)
+            runs[name].append(round(1000.0 * max_over_ranks(time.perf_counter() - t1, env, dev)
+                                    / steps, 3))
+    _lin.set_bf16_gemm(saved_g)
+    gemm_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
+    gemm_ab["headline"] = "own_bf16_kernels" if saved_g else "torch_hipblaslt"
     path = [summ[n] for n in ("rb_conv_silu_fwd_bf16", "rb_conv_silu_bwd_bf16",
                               "rb_gate_scan_fwd_bf16", "rb_gate_scan_bwd_bf16") if n in summ]
     pb, pms = sum(p["bytes"] for p in path), sum(p["ms"] for p in path)
@@ -395,6 +417,7 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
             "dtype": "bf16 storage, fp32 recurrence math", "steps": steps,
             "value": round(env.world_size * B * steps / el, 1), "unit": "sequences/sec",
             "ms_per_step": round(1000.0 * el / steps, 3),
+            "projection_gemms_ab": gemm_ab,
             "scan_conv_gate_path": {"ms_per_step": round(pms / steps, 3),
                                     "achieved_gbs": round(gbs, 1) if gbs else None,
                                     "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
