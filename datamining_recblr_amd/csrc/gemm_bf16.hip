@@ -104,7 +104,8 @@ constexpr int BF_BM = 256, BF_BN = 256, BF_BK = 64;
 constexpr int BF_WAVES = 8, BF_THREADS = 64 * BF_WAVES;
 constexpr int BF_A_STAGE = BF_BM * BF_BK * 2;                   // 32 KB: 256 rows x 128 B
 constexpr int BF_B_STAGE = (BF_BN / 32) * (BF_BK / 16) * 1024;  // 32 KB: 8 x 4 fragments
-constexpr int BF_LDS = 2 * (BF_A_STAGE + BF_B_STAGE);           // 128 KB
+constexpr int BF_NSA = 3;                                       // A stages: 2 k-steps ahead
+constexpr int BF_LDS = BF_NSA * BF_A_STAGE + 2 * BF_B_STAGE;    // 160 KB
 
 // Persistent over tiles T = blockIdx.x + i * gridDim.x; the column tiles of
 // one row tile are neighbouring workgroups of one XCD (same blockIdx % 8), so
@@ -138,7 +139,7 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   // chunk c of row r at chunk c ^ ((r >> 1) & 7) (conflict-free fragment
   // reads); wave w moves rows 32w .. 32w + 31 (4 x 8 rows).  B image:
   // fragment (cb, s) at (4 cb + s) KB; wave w moves column block w.
-  int d_i = 0, d_kt = 0, d_mt, d_ct;
+  int d_i = 0, d_kt = 0, d_mt, d_ct, a_slot = 0;
   const char* d_base = nullptr;   // the wave's first row of the tile (uniform)
   uint32_t d_off[4];              // + 32-bit lane offsets (rows past M repeat row M - 1)
   auto d_tile = [&]() {
@@ -156,20 +157,31 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
     }
   };
   d_tile();
-  auto issue = [&](int slot) {
-    char* sa = smem + slot * BF_A_STAGE + wave * 4096;
+  // A (HBM) runs two k-steps ahead through 3 stages, B (L2) one ahead
+  // through 2: per wave and k-step 4 DMAs each
+  auto issueA = [&]() {
+    char* sa = smem + a_slot * BF_A_STAGE + wave * 4096;
     const char* b = d_base + d_kt * (BF_BK * 2);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       __builtin_amdgcn_global_load_lds((const void*)(b + d_off[q]), (lds_ptr_t)(sa + q * 1024), 16, 0, 0);
-    char* sb = smem + 2 * BF_A_STAGE + slot * BF_B_STAGE + wave * 4096;
-    const bf16x8* ws = Wf + ((int64_t)(d_ct * 8 + wave) * KB16 + d_kt * 4) * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((const void*)(ws + q * 64), (lds_ptr_t)(sb + q * 1024), 16, 0, 0);
+    a_slot = a_slot == BF_NSA - 1 ? 0 : a_slot + 1;
     if (++d_kt == KT) {
       d_kt = 0;
       if (++d_i < my_tiles) d_tile();
+    }
+  };
+  int b_i = 0, b_kt = 0, b_mt, b_ct;
+  tile_of(0, b_mt, b_ct);
+  auto issueB = [&](int slot) {
+    char* sb = smem + BF_NSA * BF_A_STAGE + slot * BF_B_STAGE + wave * 4096;
+    const bf16x8* ws = Wf + ((int64_t)(b_ct * 8 + wave) * KB16 + b_kt * 4) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      __builtin_amdgcn_global_load_lds((const void*)(ws + q * 64), (lds_ptr_t)(sb + q * 1024), 16, 0, 0);
+    if (++b_kt == KT) {
+      b_kt = 0;
+      if (++b_i < my_tiles) tile_of(b_i, b_mt, b_ct);
     }
   };
 
@@ -217,16 +229,27 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
     return pend_full;   // 8 stores issued (partial tiles: maybe fewer)
   };
 
-  issue(0);
-  int i = 0, kt = 0;
+  // issue order: A(0), B(0), A(1); then in step u: B(u + 1), A(u + 2)
+  issueA();
+  issueB(0);
+  if (U > 1) issueA();
+  int i = 0, kt = 0, sa_slot = 0;
   bool stored_prev = false;
   for (int u = 0; u < U; ++u) {
-    // own DMAs of step u landed (younger: the 8 stores of step u - 1)
-    if (stored_prev) bwait_vm<8>(); else bwait_vm<0>();
+    // own DMAs A(u), B(u) landed; younger than B(u): A(u + 1) (4, when it
+    // exists) and the 8 stores of step u - 1
+    if (u + 1 < U) {
+      if (stored_prev) bwait_vm<12>(); else bwait_vm<4>();
+    } else {
+      if (stored_prev) bwait_vm<8>(); else bwait_vm<0>();
+    }
     bbarrier();
-    if (u + 1 < U) issue((u + 1) & 1);
-    const uint32_t sa = smem_base + (u & 1) * BF_A_STAGE;
-    const uint32_t sb = smem_base + 2 * BF_A_STAGE + (u & 1) * BF_B_STAGE + wn * 16384 + lane * 16;
+    if (u + 1 < U) issueB((u + 1) & 1);
+    if (u + 2 < U) issueA();
+    const uint32_t sa = smem_base + sa_slot * BF_A_STAGE;
+    sa_slot = sa_slot == BF_NSA - 1 ? 0 : sa_slot + 1;
+    const uint32_t sb =
+        smem_base + BF_NSA * BF_A_STAGE + (u & 1) * BF_B_STAGE + wn * 16384 + lane * 16;
     stored_prev = false;
     auto substep = [&](auto S_) {
       constexpr int s = decltype(S_)::value;
@@ -306,9 +329,9 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
 // (row q in element q), so two reads give a lane its column's 8 rows
 // 8 (lane / 32) .. + 7 of the 16-row block — the same rows for both operands.
 // Rows past the chunk read as zeros (buffer descriptor range check).
-constexpr int TB_BN = 256, TB_BK = 256, TB_ROWS = 64;
-constexpr int TB_STAGE = TB_ROWS * 512;              // 32 KB per operand
-constexpr int TB_LDS = 2 * 2 * TB_STAGE;             // 128 KB
+constexpr int TB_BN = 256, TB_BK = 256, TB_ROWS = 32, TB_NS = 4;
+constexpr int TB_STAGE = TB_ROWS * 512;              // 16 KB per operand
+constexpr int TB_LDS = TB_NS * 2 * TB_STAGE;         // 128 KB: 3 k-steps in flight
 
 __device__ __forceinline__ bf16x8 tr_frag(uint32_t stage, int kb, int c0, int lane) {
   const int q = (lane >> 2) & 3;
@@ -356,12 +379,13 @@ k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict
   const auto ry = rsrc_of(Y + n0, ldy);
   const auto rx = rsrc_of(X + k0, ldx);
   const uint32_t ldy2 = (uint32_t)(ldy * 2), ldx2 = (uint32_t)(ldx * 2);
-  // DMA: instruction j = 4 wave + q moves rows 2j, 2j + 1 of the step
-  auto issue = [&](int t, int slot) {
-    char* st = smem + slot * 2 * TB_STAGE;
+  // DMA: instruction j = 2 wave + q moves rows 2j, 2j + 1 of the step
+  // (per wave and k-step 2 + 2 DMAs)
+  auto issue = [&](int t) {
+    char* st = smem + (t % TB_NS) * 2 * TB_STAGE;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = wave * 4 + q;
+    for (int q = 0; q < 2; ++q) {
+      const int j = wave * 2 + q;
       const int row = 2 * j + (lane >> 5);
       const int lc = (lane & 31) ^ ((row & 3) << 2);
       const uint32_t r = (uint32_t)(t * TB_ROWS + row);
@@ -380,14 +404,17 @@ k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict
       for (int e = 0; e < 16; ++e) acc[m][n][e] = 0.0f;
 
   const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  if (T > 0) issue(0, 0);
+  for (int t = 0; t < TB_NS - 1 && t < T; ++t) issue(t);
   for (int t = 0; t < T; ++t) {
-    bwait_vm<0>();
+    // own DMAs of step t landed; younger: those of steps t + 1, t + 2
+    if (t + 2 < T) bwait_vm<8>();
+    else if (t + 1 < T) bwait_vm<4>();
+    else bwait_vm<0>();
     bbarrier();
-    if (t + 1 < T) issue(t + 1, (t + 1) & 1);
-    const uint32_t sy = smem_base + (t & 1) * 2 * TB_STAGE, sx = sy + TB_STAGE;
+    if (t + TB_NS - 1 < T) issue(t + TB_NS - 1);
+    const uint32_t sy = smem_base + (t % TB_NS) * 2 * TB_STAGE, sx = sy + TB_STAGE;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < TB_ROWS / 16; ++kb) {
       bf16x8 a[2], b[4];
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb) a[rb] = tr_frag(sy, kb, wr * 64 + rb * 32, lane);

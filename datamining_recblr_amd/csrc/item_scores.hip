@@ -71,17 +71,7 @@ struct Stream {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-// The slot XOR of row r: r mod NS, or (EV, the tiles the CE backward's
-// transposed gathers read) the even value 2r mod NS, which keeps the two
-// 16-B slots of every aligned 32-B pair adjacent and in order (and the 16
-// rows of a 16-lane read group on distinct slots for NS >= 32).
-template <int D, bool EV>
-__device__ __forceinline__ int swz(int r) {
-  constexpr int NS = D / 4;
-  return EV ? (2 * r) & (NS - 1) : r % NS;
-}
-
-template <int D, bool EV = false>
+template <int D>
 __device__ __forceinline__ void tile_dma(float* buf, const float* M, int64_t r0, int64_t n) {
   using S = Stream<D>;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -91,7 +81,7 @@ __device__ __forceinline__ void tile_dma(float* buf, const float* M, int64_t r0,
     if (S::NI % kWaves == 0 || i < S::NI) {
       const int p = i * 64 + lane;
       const int row = p / S::NS, slot = p % S::NS;
-      const float* g = M + min(r0 + row, n - 1) * D + (slot ^ swz<D, EV>(row)) * 4;
+      const float* g = M + min(r0 + row, n - 1) * D + (slot ^ (row % S::NS)) * 4;
       __builtin_amdgcn_global_load_lds(g, (lds_ptr_t)(buf + i * 256), 16, 0, 0);
     }
   }
@@ -283,7 +273,7 @@ __device__ __forceinline__ bool place(int64_t RB, int64_t S, Place& p) {
 // per-row lse / target values ride along, with 2 the per-row int32 scale
 // exponents of a split image (passed as lse_g, landing in lds_lse), with 3
 // all three (the exponents from ex_g into a fifth body argument).
-template <int D, int kRowData, class Body, bool EV = false>
+template <int D, int kRowData, class Body>
 __device__ __forceinline__ void stream_tiles(const float* strm, int64_t n_strm, int64_t per,
                                              int64_t split, const float* lse_g,
                                              const int64_t* tgt_g, Body&& body,
@@ -304,7 +294,7 @@ __device__ __forceinline__ void stream_tiles(const float* strm, int64_t n_strm, 
   const int64_t t0 = split * per, t1 = min(t0 + per, nt);
   if (t0 >= t1) return;
   auto issue = [&](int64_t t, float* b, float* lb, int64_t* tb, float* xb) {
-    tile_dma<D, EV>(b, strm, t * kTile, n_strm);
+    tile_dma<D>(b, strm, t * kTile, n_strm);
     if constexpr (kRowData == 1 || kRowData == 3) rowdata_dma(lb, tb, lse_g, tgt_g, t * kTile, n_strm);
     if constexpr (kRowData == 2) rowexp_dma(lb, lse_g, t * kTile, n_strm);
     if constexpr (kRowData == 3) rowexp_dma(xb, ex_g, t * kTile, n_strm);
@@ -797,12 +787,12 @@ __device__ __forceinline__ void ld_frag_h(f16x8 (&p0)[D / 16], f16x8 (&p1)[D / 1
 // the tile supplies A — rows of X are items — else B).  Per k16 step the
 // three products item1.seq0, item0.seq1, item0.seq0, in that order in both
 // orientations.  The tile reads run one step ahead of the MFMAs.
-template <int D, bool kTileIsA, bool EV = false>
+template <int D, bool kTileIsA>
 __device__ __forceinline__ f32x16 lds_dot_h(const float* tile, int j, int h, const f16x8 (&r0)[D / 16],
                                             const f16x8 (&r1)[D / 16]) {
   constexpr int KS = D / 16;
   const float* row = tile + j * D;
-  int sw = swz<D, EV>(j);
+  int sw = j % Stream<D>::NS;
   asm volatile("" : "+v"(sw));
   auto rd = [&](int slot) {
     return __builtin_bit_cast(f16x8, *reinterpret_cast<const float4*>(row + ((slot ^ sw) << 2)));
@@ -1021,13 +1011,16 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
 // accumulator tile holds them in its 16 registers (rows crow(r, h)), so
 // registers 8kb .. 8kb + 7 of a lane are its 8 K values of K-block kb and
 // the other operand's fragment gathers the same rows (crow(8kb + k, h), k <
-// 8) of the tile's image (two transposing LDS reads, tile_gather_h).  The
+// 8) of the tile's image (ds_read_u16 per element, tile_gather_h).  The
 // tile's rows carry their own power-of-two scales (image = x 2^(kTS - e)),
 // which do not factor out of a sum over rows: they are folded into P,
 //   P' = P 2^(e_row - emax) 2^(kTS - e_g)   (|P'| < 2^kTS, e_g: frexp of |dloss / B|),
 // split into two f16 planes like every other operand; the partial sums are
 // un-scaled once by 2^(emax + e_g - 2 kTS) (exact).  emax = the streamed
 // operand's largest row exponent (each workgroup reduces the exponent array).
+// (A ds_read_b64_tr_b16 form of the gather, two reads per fragment instead of
+// eight, returned wrong operands on this XOR-swizzled tile image:
+// profiles/r04_ce_pytest_items_tr16.log.)
 // At d = 128 a wave holds its fixed operand's fragments (64 registers) and
 // the second product's four accumulators (64) beside the first's: one wave
 // per SIMD (the accumulator chains keep the MFMA pipe fed); d <= 64 two.
@@ -1047,31 +1040,16 @@ __device__ __forceinline__ int block_max_exp(const int* e, int64_t n) {
   return m;
 }
 
-// The other operand's fragment of K-block kb: the 8 halfs of image column
-// ch0 + (lane & 31) (plane p: ch0 = p D + 32 n) at rows crow(8 kb + k, h), k <
-// 8, of an even-swizzled LDS image tile (swz<D, true>).  Those rows are two
-// runs of 4 (16 kb + 4h + 0..3 and 16 kb + 8 + 4h + 0..3), so two
-// ds_read_b64_tr_b16 gather them: per 16-lane group a 4-row x 16-column
-// block, lane 4q + p addressing row q, columns 4p .. 4p + 3, lane i
-// receiving column i (profiles/r04_tr16_probe.txt).  The 16 columns are an
-// aligned 32-B pair of slots, adjacent and in order under the even swizzle
-// (the plain r mod NS swizzle swaps them on odd rows and the read then
-// returns wrong operands: profiles/r04_ce_pytest_items_tr16.log).  Every
-// lane executes both (EXEC all ones).
-typedef __fp16 fp16x4_t __attribute__((__vector_size__(8)));
-typedef __attribute__((address_space(3))) fp16x4_t* lds_h4_ptr;
+// the 8 halfs of image column `ch` (plane p: ch = p D + col) at rows
+// crow(8 kb + k, h), k < 8, of a swizzled LDS image tile
 template <int D>
-__device__ __forceinline__ f16x8 tile_gather_h(const _Float16* tile, int ch0, int kb, int lane) {
-  const int h = lane >> 5, q = (lane >> 2) & 3;
-  const int c = ch0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+__device__ __forceinline__ f16x8 tile_gather_h(const _Float16* tile, int ch, int kb, int h) {
+  constexpr int NS = Stream<D>::NS;
   f16x8 r;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * kb + 8 * i + 4 * h + q;
-    const _Float16* a = tile + row * 2 * D + (((c >> 3) ^ swz<D, true>(row)) << 3) + (c & 7);
-    const fp16x4_t v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4_ptr)(a));
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[4 * i + e] = __builtin_bit_cast(_Float16, v[e]);
+  for (int k = 0; k < 8; ++k) {
+    const int row = 16 * kb + 8 * (k >> 2) + 4 * h + (k & 3);
+    r[k] = tile[row * 2 * D + ((((ch >> 3) ^ (row % NS))) << 3) + (ch & 7)];
   }
   return r;
 }
@@ -1094,13 +1072,13 @@ __device__ __forceinline__ void split_p(const float (&pv)[16], f16x8 (&p0)[2], f
 // products first as everywhere on the f16 pipe
 template <int D>
 __device__ __forceinline__ void gemm2_h(f32x16 (&acc)[D / 32], const f16x8 (&p0)[2],
-                                        const f16x8 (&p1)[2], const _Float16* tile, int lane) {
+                                        const f16x8 (&p1)[2], const _Float16* tile, int j, int h) {
 #pragma unroll
   for (int n = 0; n < D / 32; ++n)
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-      const f16x8 t0 = tile_gather_h<D>(tile, n * 32, kb, lane);
-      const f16x8 t1 = tile_gather_h<D>(tile, D + n * 32, kb, lane);
+      const f16x8 t0 = tile_gather_h<D>(tile, n * 32 + j, kb, h);
+      const f16x8 t1 = tile_gather_h<D>(tile, D + n * 32 + j, kb, h);
       acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(p1[kb], t0, acc[n], 0, 0, 0);
       acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(p0[kb], t1, acc[n], 0, 0, 0);
       acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(p0[kb], t0, acc[n], 0, 0, 0);
@@ -1118,7 +1096,7 @@ __device__ __forceinline__ f32x16 lds_dot_h_seqA(const float* tile, int j, int h
                                                  const f16x8 (&r0)[D / 16], const f16x8 (&r1)[D / 16]) {
   constexpr int KS = D / 16;
   const float* row = tile + j * D;
-  int sw = swz<D, true>(j);
+  int sw = j % Stream<D>::NS;
   asm volatile("" : "+v"(sw));
   auto rd = [&](int slot) {
     return __builtin_bit_cast(f16x8, *reinterpret_cast<const float4*>(row + ((slot ^ sw) << 2)));
@@ -1170,9 +1148,11 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void k_ce_bwd_seq_h(const _Fl
   f32x16 acc[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) acc[n] = f32x16{};
-  auto body = [&](int64_t t, const float* tile, const float* ebuf, const int64_t*) {
+  stream_tiles<D, 2>(reinterpret_cast<const float*>(Wi), V, per, pl.split,
+                     reinterpret_cast<const float*>(We), nullptr,
+                     [&](int64_t t, const float* tile, const float* ebuf, const int64_t*) {
     const int64_t v0 = t * kTile;
-    const f32x16 x = lds_dot_h<D, true, true>(tile, j, h, e0, e1);   // X^T[v][b], k_ce_fwd_h's
+    const f32x16 x = lds_dot_h<D, true>(tile, j, h, e0, e1);   // X^T[v][b], k_ce_fwd_h's
     const int4* ev = reinterpret_cast<const int4*>(ebuf);
     const int hi = rel32(V, v0), tt = rel32(tb, v0);
     float pv[16];
@@ -1190,10 +1170,8 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void k_ce_bwd_seq_h(const _Fl
     }
     f16x8 p0[2], p1[2];
     split_p(pv, p0, p1);
-    gemm2_h<D>(acc, p0, p1, reinterpret_cast<const _Float16*>(tile), lane);
-  };
-  stream_tiles<D, 2, decltype(body)&, true>(reinterpret_cast<const float*>(Wi), V, per, pl.split,
-                                           reinterpret_cast<const float*>(We), nullptr, body);
+    gemm2_h<D>(acc, p0, p1, reinterpret_cast<const _Float16*>(tile), j, h);
+  });
   if (b0 >= B) return;
   float* out = de_part + pl.split * B * D;
   const int sh = emax + eg - 2 * kTS;
@@ -1233,8 +1211,9 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void k_ce_bwd_item_h(const _F
   f32x16 acc[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) acc[n] = f32x16{};
-  auto body = [&](int64_t t, const float* tile, const float* lt, const int64_t* tt,
-                  const float* xb) {
+  stream_tiles<D, 3>(reinterpret_cast<const float*>(Ei), B, per, pl.split, lse, tgt,
+                     [&](int64_t t, const float* tile, const float* lt, const int64_t* tt,
+                         const float* xb) {
     const int64_t bt0 = t * kTile;
     const f32x16 x = lds_dot_h_seqA<D>(tile, j, h, w0, w1);   // X[b][v]
     const int* eb = reinterpret_cast<const int*>(xb);
@@ -1250,10 +1229,8 @@ __global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void k_ce_bwd_item_h(const _F
     }
     f16x8 p0[2], p1[2];
     split_p(pv, p0, p1);
-    gemm2_h<D>(acc, p0, p1, reinterpret_cast<const _Float16*>(tile), lane);
-  };
-  stream_tiles<D, 3, decltype(body)&, true>(reinterpret_cast<const float*>(Ei), B, per, pl.split,
-                                           lse, tgt, body, reinterpret_cast<const float*>(Ee));
+    gemm2_h<D>(acc, p0, p1, reinterpret_cast<const _Float16*>(tile), j, h);
+  }, reinterpret_cast<const float*>(Ee));
   if (v0 >= V) return;
   float* out = dw_part + pl.split * V * D;
   const int sh = emax + eg - 2 * kTS;

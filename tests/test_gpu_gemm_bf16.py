@@ -66,7 +66,7 @@ def test_gemm_nt_bf16_transposed_image(cuda):
 
 def test_bf16_weight_image_layout(cuda):
     """Fragment (cb, kb), lane l: column 32 cb + l % 32, k 16 kb + 8 (l / 32) + j."""
-    C, R = 64, 48
+    C, R = 64, 96
     w = torch.arange(C * R, device=cuda, dtype=torch.float32).view(C, R) / 64.0
     img = kernels.bf16_weight_image(w).view(C // 32, R // 16, 64, 8).cpu()
     wb = w.to(BF).cpu()
@@ -76,7 +76,9 @@ def test_bf16_weight_image_layout(cuda):
                 c, k0 = 32 * cb + lane % 32, 16 * kb + 8 * (lane // 32)
                 assert torch.equal(img[cb, kb, lane], wb[c, k0:k0 + 8])
     imt = kernels.bf16_weight_image(w, transpose=True).view(R // 32, C // 16, 64, 8).cpu()
-    assert torch.equal(imt[1, 2, 33], wb[32:40, 32 + 1])
+    # Bm = w^T: fragment (cb=1, kb=2), lane 33: column 32 + 1 of Bm = w's
+    # column 33, k = 32 + 8 .. + 7 = w's rows 40 .. 47
+    assert torch.equal(imt[1, 2, 33], wb[40:48, 33])
 
 
 @pytest.mark.parametrize("M,N,K,S", [

@@ -59,6 +59,16 @@ __global__ void k(int* bad, int enc) {
   atomicAdd(bad, nbad);
 }
 
+// rows each lane receives (D = 32, r mod NS swizzle, kb = 0), for the record
+__global__ void dump(float* o) {
+  constexpr int D = 32;
+  __shared__ __attribute__((aligned(16))) _Float16 t[32 * 2 * D];
+  for (int i = threadIdx.x; i < 32 * 2 * D; i += 64) t[i] = (_Float16)(float)(i / (2 * D));
+  __syncthreads();
+  const f16x8 g = tile_gather_h<D, false>(t, 0, 0, threadIdx.x);
+  for (int k = 0; k < 8; ++k) o[threadIdx.x * 8 + k] = (float)g[k];
+}
+
 int main() {
   int* d;
   (void)hipMalloc(&d, 16);
@@ -79,5 +89,16 @@ int main() {
       (void)hipMemcpy(&h, d, 4, hipMemcpyDeviceToHost);
       printf("swizzle %-9s D=128 enc %d mismatches %d\n", sw, enc, h);
     }
+  float* o;
+  (void)hipMalloc(&o, 64 * 8 * 4);
+  dump<<<1, 64>>>(o);
+  float ho[64 * 8];
+  (void)hipMemcpy(ho, o, sizeof ho, hipMemcpyDeviceToHost);
+  printf("rows received (D=32, kb=0; expected 8i + 4h + e for element 4i + e):\n");
+  for (int l = 0; l < 64; ++l) {
+    printf("lane %2d:", l);
+    for (int k = 0; k < 8; ++k) printf(" %2d", (int)ho[l * 8 + k]);
+    printf("\n");
+  }
   return 0;
 }
