@@ -354,8 +354,9 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
     projections) forward + backward on synthetic input; sequences/s over all
     ranks (weak scaling, max-over-ranks time).  The HBM fraction is that of
     the bf16 conv + gate-scan kernels (algorithmic bytes 20*N*2 per step,
-    N = B*L*H).  The projections run on rb_gemm_nt_bf16 / rb_gemm_tn_bf16
-    (RECBLR_BF16_GEMM=0: torch's bf16 GEMMs); projection_gemms_ab times both."""
+    N = B*L*H).  The projections run on torch's bf16 GEMMs (hipBLASLt) unless
+    RECBLR_BF16_GEMM=1 (rb_gemm_nt_bf16 / rb_gemm_tn_bf16, measured slower);
+    projection_gemms_ab times both."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     B, L, d = args.c5_batch, 2048, 256
@@ -385,7 +386,7 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
     # the projections on our bf16 kernels (rb_gemm_nt_bf16 / rb_gemm_tn_bf16)
     # vs torch's bf16 GEMMs (hipBLASLt), alternated, best of 2 per variant
     from datamining_recblr_amd import linear as _lin
-    saved_g = _lin.set_bf16_gemm(True)
+    saved_g = _lin.set_bf16_gemm(_lin._bf16_gemm)
     runs = {"own_bf16_kernels": [], "torch_hipblaslt": []}
     for _ in range(2):
         for name, on in (("own_bf16_kernels", True), ("torch_hipblaslt", False)):

@@ -329,9 +329,11 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
 // (row q in element q), so two reads give a lane its column's 8 rows
 // 8 (lane / 32) .. + 7 of the 16-row block — the same rows for both operands.
 // Rows past the chunk read as zeros (buffer descriptor range check).
-constexpr int TB_BN = 256, TB_BK = 256, TB_ROWS = 32, TB_NS = 4;
-constexpr int TB_STAGE = TB_ROWS * 512;              // 16 KB per operand
-constexpr int TB_LDS = TB_NS * 2 * TB_STAGE;         // 128 KB: 3 k-steps in flight
+// (32-row k-steps with 3 in flight measured slower: 1.91 vs 1.59 ms per call
+// at configs[4], profiles/r04_bf2_c5_kernel_stats.csv)
+constexpr int TB_BN = 256, TB_BK = 256, TB_ROWS = 64, TB_NS = 2;
+constexpr int TB_STAGE = TB_ROWS * 512;              // 32 KB per operand
+constexpr int TB_LDS = TB_NS * 2 * TB_STAGE;         // 128 KB: 1 k-step in flight
 
 __device__ __forceinline__ bf16x8 tr_frag(uint32_t stage, int kb, int c0, int lane) {
   const int q = (lane >> 2) & 3;
@@ -379,13 +381,13 @@ k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict
   const auto ry = rsrc_of(Y + n0, ldy);
   const auto rx = rsrc_of(X + k0, ldx);
   const uint32_t ldy2 = (uint32_t)(ldy * 2), ldx2 = (uint32_t)(ldx * 2);
-  // DMA: instruction j = 2 wave + q moves rows 2j, 2j + 1 of the step
-  // (per wave and k-step 2 + 2 DMAs)
+  // DMA: instruction j = 4 wave + q moves rows 2j, 2j + 1 of the step
+  // (per wave and k-step 4 + 4 DMAs)
   auto issue = [&](int t) {
     char* st = smem + (t % TB_NS) * 2 * TB_STAGE;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int j = wave * 2 + q;
+    for (int q = 0; q < 4; ++q) {
+      const int j = wave * 4 + q;
       const int row = 2 * j + (lane >> 5);
       const int lc = (lane & 31) ^ ((row & 3) << 2);
       const uint32_t r = (uint32_t)(t * TB_ROWS + row);
@@ -406,10 +408,8 @@ k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict
   const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
   for (int t = 0; t < TB_NS - 1 && t < T; ++t) issue(t);
   for (int t = 0; t < T; ++t) {
-    // own DMAs of step t landed; younger: those of steps t + 1, t + 2
-    if (t + 2 < T) bwait_vm<8>();
-    else if (t + 1 < T) bwait_vm<4>();
-    else bwait_vm<0>();
+    // own DMAs of step t landed (nothing younger is in flight)
+    bwait_vm<0>();
     bbarrier();
     if (t + TB_NS - 1 < T) issue(t + TB_NS - 1);
     const uint32_t sy = smem_base + (t % TB_NS) * 2 * TB_STAGE, sx = sy + TB_STAGE;
@@ -490,7 +490,7 @@ int launch_gemm_tn_bf16(const void* Y, int64_t ldy, const void* X, int64_t ldx, 
     attr = true;
   }
   const int64_t per = (M + S - 1) / S;
-  const int64_t chunk = (per + TB_ROWS - 1) / TB_ROWS * TB_ROWS;
+  const int64_t chunk = (per + 63) / 64 * 64;   // the C-ABI's chunking (64-row multiples)
   const int ntile = (N / TB_BN) * (K / TB_BK);
   k_gemm_tn_bf<<<(unsigned)(ntile * S), BF_THREADS, TB_LDS, st>>>(
       (const __bf16*)Y, ldy, (const __bf16*)X, ldx, M, N, K, chunk, parts, S);

@@ -107,9 +107,10 @@ def test_gemm_tn_bf16_vs_fp64(cuda, M, N, K, S):
 
 
 def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
-    """configs[4]'s GatedRecurrentLayer (d = 256, L = 2048) runs all three
-    projections' forward, input-gradient and weight-gradient GEMMs on the bf16
-    kernels, and agrees with the hipBLASLt path to bf16 accuracy."""
+    """configs[4]'s GatedRecurrentLayer (d = 256, L = 2048) with
+    RECBLR_BF16_GEMM on runs all three projections' forward, input-gradient and
+    weight-gradient GEMMs on the bf16 kernels, and agrees with the hipBLASLt
+    path (the default) to bf16 accuracy."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     calls = {"nt": 0, "tn": 0}

@@ -20,4 +20,3 @@ rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_mfma
 cp gpurun_out/${T}_pmc_traffic.json profiles/${T}_pmc_traffic.json
 cp gpurun_out/${T}_pmc_mfma.json profiles/${T}_pmc_mfma.json
 timeout -k 10 900 python bench.py > gpurun_out/${T}_bench.log 2>&1
-timeout -k 10 60 tools/bin/tr16_gather_probe > gpurun_out/r04_tr16_gather_probe.txt 2>&1 || true
