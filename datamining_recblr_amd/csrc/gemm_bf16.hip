@@ -109,9 +109,9 @@ constexpr int BF_LDS = BF_NSA * BF_A_STAGE + 2 * BF_B_STAGE;    // 160 KB
 
 // Persistent over tiles T = blockIdx.x + i * gridDim.x; the column tiles of
 // one row tile are neighbouring workgroups of one XCD (same blockIdx % 8), so
-// their A re-reads hit that XCD's L2.  A tile's results are rounded at its
-// end and stored two blocks per k-step during the next tile (behind its
-// MFMAs), so the k-step waits never drain a whole tile's stores.
+// their A re-reads hit that XCD's L2.  A tile's results are rounded and
+// stored at its end; the next k-step's wait counts them (they drain during
+// that k-step, behind its MFMAs).
 template <bool BIAS>
 __global__ void __launch_bounds__(BF_THREADS, 1)
 k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
@@ -204,32 +204,8 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
     a_off[rb] = row * 128 + (((lane >> 5) ^ ((row >> 1) & 7)) << 4);
   }
 
-  // pending results of the previous tile: bf16, after the quad transpose a
-  // lane holds 4 consecutive columns of one row per 4-row group
-  u32x2 pend[2][4][4];
-  int pend_mt = -1, pend_ct = 0, pend_q = 4;
-  bool pend_full = true;
-  auto store_blk = [&](int rb, int cb, const u32x2 (&blk)[4]) {
-    const int col = pend_ct * BF_BN + wn * 128 + cb * 32 + (lane & 28);
-    const int64_t rbase = (int64_t)pend_mt * BF_BM + wm * 64 + rb * 32 + 4 * (lane >> 5) + (lane & 3);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int64_t row = rbase + 8 * g;
-      if (pend_full || row < M)
-        __builtin_nontemporal_store(blk[g], reinterpret_cast<u32x2*>(out + row * ldo + col));
-    }
-  };
-  // static register indexing: two blocks per call
-  auto store_pair = [&]() {
-    const int q = pend_q++;
-    if (q == 0) { store_blk(0, 0, pend[0][0]); store_blk(0, 1, pend[0][1]); }
-    else if (q == 1) { store_blk(0, 2, pend[0][2]); store_blk(0, 3, pend[0][3]); }
-    else if (q == 2) { store_blk(1, 0, pend[1][0]); store_blk(1, 1, pend[1][1]); }
-    else { store_blk(1, 2, pend[1][2]); store_blk(1, 3, pend[1][3]); }
-    return pend_full;   // 8 stores issued (partial tiles: maybe fewer)
-  };
-
-  // issue order: A(0), B(0), A(1); then in step u: B(u + 1), A(u + 2)
+  // issue order: A(0), B(0), A(1); then in step u: B(u + 1), A(u + 2); a
+  // tile's 32 result stores (per wave) follow its last step's MFMAs
   issueA();
   issueB(0);
   if (U > 1) issueA();
@@ -237,11 +213,11 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   bool stored_prev = false;
   for (int u = 0; u < U; ++u) {
     // own DMAs A(u), B(u) landed; younger than B(u): A(u + 1) (4, when it
-    // exists) and the 8 stores of step u - 1
+    // exists) and the 32 stores at the end of step u - 1 (a whole tile's)
     if (u + 1 < U) {
-      if (stored_prev) bwait_vm<12>(); else bwait_vm<4>();
+      if (stored_prev) bwait_vm<36>(); else bwait_vm<4>();
     } else {
-      if (stored_prev) bwait_vm<8>(); else bwait_vm<0>();
+      if (stored_prev) bwait_vm<32>(); else bwait_vm<0>();
     }
     bbarrier();
     if (u + 1 < U) issueB((u + 1) & 1);
@@ -251,73 +227,89 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
     const uint32_t sb =
         smem_base + BF_NSA * BF_A_STAGE + (u & 1) * BF_B_STAGE + wn * 16384 + lane * 16;
     stored_prev = false;
-    auto substep = [&](auto S_) {
-      constexpr int s = decltype(S_)::value;
-      bf16x8 a0 = bds_read16<bf16x8>(sa + (a_off[0] ^ (s << 5)));
-      bf16x8 a1 = bds_read16<bf16x8>(sa + (a_off[1] ^ (s << 5)));
-      bf16x8 b[4];
-      b[0] = bds_read16o<(0 + s) * 1024, bf16x8>(sb);
-      b[1] = bds_read16o<(4 + s) * 1024, bf16x8>(sb);
-      b[2] = bds_read16o<(8 + s) * 1024, bf16x8>(sb);
-      b[3] = bds_read16o<(12 + s) * 1024, bf16x8>(sb);
-      asm volatile("s_waitcnt lgkmcnt(3)" : "+v"(a0), "+v"(a1), "+v"(b[0]));
-      acc[0][0] = mfma_bf(a0, b[0], acc[0][0]);
-      acc[1][0] = mfma_bf(a1, b[0], acc[1][0]);
-      asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(b[1]));
-      acc[0][1] = mfma_bf(a0, b[1], acc[0][1]);
-      acc[1][1] = mfma_bf(a1, b[1], acc[1][1]);
-      asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(b[2]));
-      acc[0][2] = mfma_bf(a0, b[2], acc[0][2]);
-      acc[1][2] = mfma_bf(a1, b[2], acc[1][2]);
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(b[3]));
-      acc[0][3] = mfma_bf(a0, b[3], acc[0][3]);
-      acc[1][3] = mfma_bf(a1, b[3], acc[1][3]);
+    // fragments double-buffered: substep s + 1's six reads are in flight
+    // during substep s's eight MFMAs
+    bf16x8 fa[2][2], fb[2][4];
+    auto load = [&](auto S_, auto P_) {
+      constexpr int s = decltype(S_)::value, p = decltype(P_)::value;
+      fa[p][0] = bds_read16<bf16x8>(sa + (a_off[0] ^ (s << 5)));
+      fa[p][1] = bds_read16<bf16x8>(sa + (a_off[1] ^ (s << 5)));
+      fb[p][0] = bds_read16o<(0 + s) * 1024, bf16x8>(sb);
+      fb[p][1] = bds_read16o<(4 + s) * 1024, bf16x8>(sb);
+      fb[p][2] = bds_read16o<(8 + s) * 1024, bf16x8>(sb);
+      fb[p][3] = bds_read16o<(12 + s) * 1024, bf16x8>(sb);
     };
-    substep(std::integral_constant<int, 0>{});
-    if (pend_mt >= 0 && pend_q < 4) stored_prev = store_pair();
-    substep(std::integral_constant<int, 1>{});
-    substep(std::integral_constant<int, 2>{});
-    substep(std::integral_constant<int, 3>{});
-
-    if (kt == KT - 1) {
-      int mt, ct;
-      tile_of(i, mt, ct);
-      while (pend_mt >= 0 && pend_q < 4) store_pair();   // tiles shorter than 4 k-steps
-      float bv[4][4];
+    auto mma = [&](auto P_) {
+      constexpr int p = decltype(P_)::value;
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const int col = ct * BF_BN + wn * 128 + cb * 32 + (lane & 28);
-        const f32x4 b4 = BIAS ? *reinterpret_cast<const f32x4*>(bias + col) : f32x4{0, 0, 0, 0};
+        acc[0][cb] = mfma_bf(fa[p][0], fb[p][cb], acc[0][cb]);
+        acc[1][cb] = mfma_bf(fa[p][1], fb[p][cb], acc[1][cb]);
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    load(I0{}, I0{});
+    load(I1{}, I1{});
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fb[0][0]),
+                 "+v"(fb[0][1]), "+v"(fb[0][2]), "+v"(fb[0][3]));
+    mma(I0{});
+    load(I2{}, I0{});
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[1][0]),
+                 "+v"(fb[1][1]), "+v"(fb[1][2]), "+v"(fb[1][3]));
+    mma(I1{});
+    load(I3{}, I1{});
+    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fb[0][0]),
+                 "+v"(fb[0][1]), "+v"(fb[0][2]), "+v"(fb[0][3]));
+    mma(I0{});
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[1][0]),
+                 "+v"(fb[1][1]), "+v"(fb[1][2]), "+v"(fb[1][3]));
+    mma(I1{});
+
+    if (kt == KT - 1) {
+      // the tile's results: + bias in fp32, one rounding to bf16, quad
+      // transposes (a lane: 4 consecutive columns of one row), 8-B stores
+      int mt, ct;
+      tile_of(i, mt, ct);
+      const bool full = (int64_t)mt * BF_BM + BF_BM <= M;
+      if (mt < m_tiles) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) bv[cb][c] = b4[c];
+        for (int cb = 0; cb < 4; ++cb) {
+          const int col = ct * BF_BN + wn * 128 + cb * 32 + (lane & 28);
+          const f32x4 b4 = BIAS ? *reinterpret_cast<const f32x4*>(bias + col) : f32x4{0, 0, 0, 0};
+#pragma unroll
+          for (int rb = 0; rb < 2; ++rb) {
+            const int64_t rbase = (int64_t)mt * BF_BM + wm * 64 + rb * 32 + 4 * (lane >> 5) + (lane & 3);
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              float v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][4 * g + r];
+              quad_t(v, lane);
+              const f32x4 x = {v[0] + b4[0], v[1] + b4[1], v[2] + b4[2], v[3] + b4[3]};
+              const int64_t row = rbase + 8 * g;
+              if (full || row < M)
+                __builtin_nontemporal_store(__builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4)),
+                                            reinterpret_cast<u32x2*>(out + row * ldo + col));
+            }
+          }
+        }
+        stored_prev = full;   // 32 stores issued (partial tiles: fewer, not counted)
       }
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][4 * g + r];
-            quad_t(v, lane);
-            const f32x4 x = {v[0] + bv[cb][0], v[1] + bv[cb][1], v[2] + bv[cb][2], v[3] + bv[cb][3]};
-            pend[rb][cb][g] = __builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4));
-          }
+        for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
           for (int e = 0; e < 16; ++e) acc[rb][cb][e] = 0.0f;
-        }
-      pend_mt = mt < m_tiles ? mt : -1;
-      pend_ct = ct;
-      pend_q = 0;
-      pend_full = (int64_t)mt * BF_BM + BF_BM <= M;
       kt = 0;
       ++i;
     } else {
       ++kt;
     }
   }
-  while (pend_mt >= 0 && pend_q < 4) store_pair();
 }
 
 // ---------------------------------------------------------------------------
