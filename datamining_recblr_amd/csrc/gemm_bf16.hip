@@ -291,8 +291,8 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
               const f32x4 x = {v[0] + b4[0], v[1] + b4[1], v[2] + b4[2], v[3] + b4[3]};
               const int64_t row = rbase + 8 * g;
               if (full || row < M)
-                __builtin_nontemporal_store(__builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4)),
-                                            reinterpret_cast<u32x2*>(out + row * ldo + col));
+                *reinterpret_cast<u32x2*>(out + row * ldo + col) =
+                    __builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4));
             }
           }
         }

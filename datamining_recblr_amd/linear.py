@@ -170,9 +170,10 @@ def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
 
 
 # bf16 activations (BASELINE configs[4]): RECBLR_BF16_GEMM=1 runs the
-# projections on our bf16 MFMA kernels (csrc/gemm_bf16.hip), tested, but
-# 15-40% slower per shape than torch's bf16 GEMMs (hipBLASLt), which stay the
-# default (configs[4] step 26.0 vs 22.2 ms; profiles/r04_bf3_shapes.txt).  The
+# projections on our bf16 MFMA kernels (csrc/gemm_bf16.hip), tested; the
+# weight gradient at parity, the NT kernel 5-23% slower per shape than torch's
+# bf16 GEMMs (hipBLASLt), which stay the default (configs[4] step 23.9 vs
+# 22.1 ms; profiles/r04_bf5_shapes.txt).  The
 # weight's bf16 fragment images (W for the forward, W^T for the input
 # gradient) are cached per weight version like the split images.
 _bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "0") == "1"

@@ -2,7 +2,7 @@
 # per-shape timings, configs[4] step A/B
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-T=r04_bf4
+T=${T:-r04_bf4}
 timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread \
     tests/test_gpu_gemm_bf16.py > gpurun_out/${T}_pytest.log 2>&1 || exit $?
 timeout -k 10 300 python -u tools/bf16_gemm_probe.py > gpurun_out/${T}_shapes.txt 2>&1 || exit $?
