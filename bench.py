@@ -217,8 +217,8 @@ def pmc_mfma(args):
     summary (profiles/*_pmc_mfma.json, tools/pmc_mfma.py:
     SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE x SIMDs)), per kernel family:
     the f16 split kernels (k_gemm_nt_h / k_gemm_tn_h: 3 f16 MFMA products per
-    fp32 product), the bf16 six-product kernel (k_gemm_nt) and hipBLASLt's fp32
-    kernels (>= 20 GFLOP per launch).  Busy is the fraction of the MFMA pipe's
+    fp32 product), bf16 kernels (configs[4]) and hipBLASLt's fp32 kernels
+    (>= 20 GFLOP per launch).  Busy is the fraction of the MFMA pipe's
     cycles, whatever the dtype."""
     if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
         return None
@@ -226,14 +226,14 @@ def pmc_mfma(args):
     if not files:
         return None
     data = json.load(open(files[-1]))
-    fam = {"f16x3": [], "bf16x6": [], "hipblaslt_f32": []}
+    fam = {"f16x3": [], "bf16": [], "hipblaslt_f32": []}
     for name, k in data.get("kernels", {}).items():
         if not k.get("mfma_util"):
             continue
         if "k_gemm_nt_h" in name or "k_gemm_tn_h" in name:
             fam["f16x3"].append(k["mfma_util"])
         elif k.get("mfma_flops_bf16_per_dispatch", 0) >= 2e10:
-            fam["bf16x6"].append(k["mfma_util"])
+            fam["bf16"].append(k["mfma_util"])
         elif k.get("mfma_flops_f32_per_dispatch", 0) >= 2e10:
             fam["hipblaslt_f32"].append(k["mfma_util"])
     out = {f: {"min": min(u), "max": max(u)} for f, u in fam.items() if u}
@@ -888,7 +888,7 @@ def main():
         devlen["recbole_interaction_path"] = recbole_path
     fused_ab = None
     if not args.no_full_tail:
-        # the fused GatedRecurrentLayer kernels (csrc/grl_fused.hip, opt-in):
+        # the fused GatedRecurrentLayer kernels (experimental/grl_fused.hip, opt-in):
         # A/B against the headline's three-launch path on the same batches
         from datamining_recblr_amd import recurrence
         saved_f = (recurrence._FUSED, recurrence._FUSED_BWD)
@@ -939,25 +939,6 @@ def main():
         order_ab["note"] = ("RECBLR_CONV_FIRST A/B on the headline's batches: in the "
                             "GatedRecurrentLayer backward, the conv backward before the gates "
                             "weight gradient (its inputs just written) or after it; best of 3")
-    ce_ab = None
-    if not args.no_full_tail:
-        # the CE backward's products: inside kernels that recompute the logits
-        # (rb_item_ce_bwd_h, P never stored) vs P in both layouts + two
-        # weight-gradient GEMMs (RECBLR_CE_GRADS=f16), alternated 3x
-        from datamining_recblr_amd import scoring as _sc
-        saved_c = _sc.set_ce_grads("fused")
-        runs = {"fused": [], "f16_probs_tn": []}
-        for _ in range(3):
-            for name, mode in (("fused", "fused"), ("f16_probs_tn", "f16")):
-                _sc.set_ce_grads(mode)
-                runs[name].append(timed_variant(True, True)["ms_per_step"])
-        _sc.set_ce_grads(saved_c)
-        ce_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
-        ce_ab["headline"] = "fused" if saved_c == "fused" else "f16_probs_tn"
-        ce_ab["note"] = ("RECBLR_CE_GRADS A/B on the headline's batches: dseq = P W and "
-                         "ditems = P^T seq inside the logits-recomputing kernels "
-                         "(rb_item_ce_bwd_h) vs P written in both layouts and two "
-                         "rb_gemm_tn_h products; best of 3 alternated runs")
     adam_ab = None
     if not args.no_full_tail:
         # the optimizer update: rb_adam_step (one launch over every parameter)
@@ -1015,10 +996,7 @@ def main():
                     "flops_per_step": int(g["bytes"] / args.steps),
                     "library": {"f16x3": "f16 two-part split MFMA kernels (csrc/gemm_half.hip): "
                                          "rb_gemm_nt_h forward/input-gradient, rb_gemm_tn_h "
-                                         "weight gradients; torch/hipBLASLt below 4096 rows",
-                                "bf16x6": "split-bf16 MFMA kernel (csrc/gemm_split.hip) for the "
-                                          "[B*L] forward/input-gradient GEMMs, hipBLASLt split-K "
-                                          "weight gradients",
+                                         "weight gradients",
                                 "torch": "hipBLASLt/rocBLAS via torch"}[fmt],
                     "tuned_table": tuned_gemms_active(),
                     "mfma_busy": pmc_mfma(args),
@@ -1089,7 +1067,6 @@ def main():
             "ffn_act": ffn_act_ab,
             "adam": adam_ab,
             "bwd_order": order_ab,
-            "ce_grads": ce_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

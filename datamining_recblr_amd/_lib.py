@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 40
+ABI_VERSION = 41
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -72,8 +72,6 @@ SIGNATURES = {
     "rb_colsum_chunked": (ctypes.c_int, [_fp, _i64, _i64, _i64, _i64, _i64, _fp, _fp, _i64, _fp,
                                          _fp]),
     "rb_item_ce_workspace": (ctypes.c_int64, [_i64, _i64, _i64]),
-    "rb_item_ce_bwd_h": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp,
-                                        _fp, _fp, _i64, _fp]),
     "rb_item_ce_fwd": (ctypes.c_int, [_fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp, _i64, _fp]),
     "rb_item_ce_bwd": (ctypes.c_int, [_fp, _fp, _fp, _fp, _fp, _i64, _i64, _i64, _fp, _fp, _fp,
                                       _i64, _fp]),
@@ -104,12 +102,7 @@ SIGNATURES = {
     "rb_gate_scan_bwd_bf16": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp,
                                              _fp, _i64, _fp, _i64, _fp, _i64, _fp, _fp, _i64,
                                              _i64, _i64, _fp, _fp]),
-    "rb_gemm_split_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
-    "rb_gemm_split_weight": (ctypes.c_int, [_fp, _i64, _i64, _i64, ctypes.c_int, _fp, _fp]),
-    "rb_gemm_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
     "rb_pack_plan": (ctypes.c_int, [_fp, _i64, _fp, _fp, _i64, _i64, _fp, _fp, _fp, _fp, _fp]),
-    "rb_gemm_nt": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
-                                  _fp]),
     "rb_gemm_h_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
     "rb_gemm_h_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
     "rb_gemm_nt_h": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
@@ -128,6 +121,18 @@ SIGNATURES = {
     "rb_gemm_tn_h": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _i64,
                                     _fp]),
     "rb_gemm_tn_hs": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, ctypes.c_int, _fp]),
+}
+
+
+class RecBLRNativeError(RuntimeError):
+    """The HIP extension is missing, failed to load, or a kernel call failed."""
+
+
+# the experimental library (experimental/recblr_exp.h: opt-in kernels that
+# measured slower than the default path; never loaded unless requested)
+EXP_SIGNATURES = {
+    "rb_exp_version": (ctypes.c_int, []),
+    "rb_exp_last_error_string": (ctypes.c_char_p, []),
     "rb_grl_fwd": (ctypes.c_int, [_fp, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _fp, _fp, _i64, _i64,
                                   _i64, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _i64, _fp, _fp,
                                   _i64, _fp]),
@@ -135,11 +140,6 @@ SIGNATURES = {
                                   _i64, _i64, _i64, _fp, _i64, _fp, _fp, _fp, _i64, _fp, _fp,
                                   _fp, _fp, _fp, _fp, _fp]),
 }
-
-
-class RecBLRNativeError(RuntimeError):
-    """The HIP extension is missing, failed to load, or a kernel call failed."""
-
 
 # the probe library (probes/recblr_probe.h: bench.py's measurement aids)
 PROBE_SIGNATURES = {
@@ -152,6 +152,7 @@ PROBE_SIGNATURES = {
 _lock = threading.Lock()
 _lib = None
 _probe = None
+_exp = None
 
 
 def load(path: str | None = None) -> ctypes.CDLL:
@@ -183,6 +184,14 @@ def load(path: str | None = None) -> ctypes.CDLL:
 
 
 _fns = {}
+_failure_hooks = []
+
+
+def on_failure(hook) -> None:
+    """Register hook() to run whenever a C-ABI call returns an error (device
+    state cached by the Python side, e.g. the column sums' ticket counters,
+    is dropped rather than trusted after a failure)."""
+    _failure_hooks.append(hook)
 
 
 def call(name: str, *args) -> None:
@@ -192,6 +201,8 @@ def call(name: str, *args) -> None:
         fn = _fns[name] = getattr(load(), name)
     rc = fn(*args)
     if rc != 0:
+        for hook in _failure_hooks:
+            hook()
         lib = load()
         msg = lib.rb_last_error_string()
         msg = msg.decode() if msg else ""
@@ -227,3 +238,39 @@ def call_probe(name: str, *args) -> None:
     if rc != 0:
         msg = lib.rb_probe_last_error_string()
         raise RecBLRNativeError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def load_exp() -> ctypes.CDLL:
+    """The experimental library (lib/libdmrecblr_exp.so, experimental/
+    recblr_exp.h): the opt-in fused GatedRecurrentLayer kernels.  Loaded only
+    when one of them is requested; the default path never loads it."""
+    global _exp
+    with _lock:
+        if _exp is not None:
+            return _exp
+        p = os.path.join(os.path.dirname(LIB_PATH), "libdmrecblr_exp.so")
+        if not os.path.exists(p):
+            raise RecBLRNativeError(f"experimental library not built: {p} is missing. Run "
+                                    "`python -m datamining_recblr_amd.build`.")
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in EXP_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.rb_exp_version() != ABI_VERSION:
+            raise RecBLRNativeError(f"experimental library ABI {lib.rb_exp_version()} vs "
+                                    f"{ABI_VERSION}; rebuild")
+        _exp = lib
+        return lib
+
+
+def call_exp(name: str, *args) -> None:
+    """Invoke an experimental-library entry point and raise on a non-zero status."""
+    lib = load_exp()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        for hook in _failure_hooks:
+            hook()
+        msg = lib.rb_exp_last_error_string()
+        kind = "invalid argument" if rc == RB_EINVAL else f"hipError {rc}"
+        raise RecBLRNativeError(f"{name} failed ({kind}): {msg.decode() if msg else ''}")

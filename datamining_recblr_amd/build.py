@@ -23,6 +23,11 @@ OUT = os.path.join(_HERE, "lib", "libdmrecblr.so")
 PROBE_SOURCES = sorted(glob.glob(os.path.join(_HERE, "probes", "*.hip")))
 PROBE_HEADERS = HEADERS + sorted(glob.glob(os.path.join(_HERE, "probes", "*.h")))
 PROBE_OUT = os.path.join(_HERE, "lib", "libdmrecblr_probe.so")
+# opt-in experimental kernels (experimental/recblr_exp.h): their own library,
+# hidden visibility, loaded only when requested (RECBLR_FUSED_GRL*)
+EXP_SOURCES = sorted(glob.glob(os.path.join(_HERE, "experimental", "*.hip")))
+EXP_HEADERS = HEADERS + sorted(glob.glob(os.path.join(_HERE, "experimental", "*.h")))
+EXP_OUT = os.path.join(_HERE, "lib", "libdmrecblr_exp.so")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 
 # -ffp-contract=off: the reference scan is compiled with enable_fp_fusion=False
@@ -59,12 +64,14 @@ def _compile(out, sources, extra, verbose, jobs):
 
 
 def build(force: bool = False, verbose: bool = False, jobs: int = 4) -> str:
-    """Build the product library (and the probe library beside it); returns
-    the product library's path."""
+    """Build the product library (and the probe and experimental libraries
+    beside it); returns the product library's path."""
     if force or _stale(OUT, SOURCES + HEADERS):
         _compile(OUT, SOURCES, [], verbose, jobs)
     if PROBE_SOURCES and (force or _stale(PROBE_OUT, PROBE_SOURCES + PROBE_HEADERS)):
         _compile(PROBE_OUT, PROBE_SOURCES, ["-fvisibility=hidden"], verbose, jobs)
+    if EXP_SOURCES and (force or _stale(EXP_OUT, EXP_SOURCES + EXP_HEADERS)):
+        _compile(EXP_OUT, EXP_SOURCES, ["-fvisibility=hidden"], verbose, jobs)
     return OUT
 
 

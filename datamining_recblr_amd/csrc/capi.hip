@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 40; }
+int rb_version(void) { return 41; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -547,18 +547,6 @@ int rb_item_ce_probs_h_both(const void* seq_img, const int* seq_exp, const void*
                                 row_group_max, reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_item_ce_bwd_h(const void* seq_img, const int* seq_exp, const void* item_img,
-                     const int* item_exp, const int64_t* target, const float* lse,
-                     const float* dloss, int64_t B, int64_t V, int64_t d, float* dseq,
-                     float* ditems, void* workspace, int64_t workspace_bytes, void* stream) {
-  if (int rc = check_items_h(seq_img, seq_exp, item_img, item_exp, B, V, d)) return rc;
-  if (!target || !lse || !dloss || !workspace) return fail("rb_item_ce_bwd_h: null pointer");
-  if (d != 32 && d != 64 && d != 128) return fail("rb_item_ce_bwd_h: d must be 32, 64 or 128");
-  return launch_item_ce_bwd_h(seq_img, seq_exp, item_img, item_exp, target, lse, dloss, B, V, d,
-                              dseq, ditems, workspace, workspace_bytes,
-                              reinterpret_cast<hipStream_t>(stream));
-}
-
 int rb_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out, void* stream) {
   if (!x || !out) return fail("rb_group_absmax: null pointer");
   if (n <= 0 || c <= 0 || ld < c) return fail("rb_group_absmax: bad shape");
@@ -623,19 +611,6 @@ int rb_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int64_t 
                                reinterpret_cast<hipStream_t>(stream));
 }
 
-int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R) { return C * R * 6; }
-
-int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
-                         void* Wf, void* stream) {
-  if (!W || !Wf) return fail("rb_gemm_split_weight: null pointer");
-  if (C <= 0 || R <= 0 || C % 32 || R % 16 || C > (1 << 20) || R > (1 << 20))
-    return fail("rb_gemm_split_weight: C must be a multiple of 32 and R of 16");
-  if (ldw < (transpose ? C : R)) return fail("rb_gemm_split_weight: bad row stride");
-  if (!aligned16(Wf)) return fail("rb_gemm_split_weight: Wf must be 16-byte aligned");
-  return launch_split_weight(W, ldw, (int)C, (int)R, transpose, Wf,
-                             reinterpret_cast<hipStream_t>(stream));
-}
-
 int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_offsets,
                  const int64_t* order, int64_t B, int64_t L, int64_t* ids, int64_t* row_pos,
                  int64_t* inv, int64_t* last, void* stream) {
@@ -645,33 +620,6 @@ int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_off
   if ((B + 3) / 4 > 0x7fffffffLL) return fail("rb_pack_plan: grid too large");
   return launch_pack_plan(item_seq, seq_rs, seq_offsets, order, B, ids, row_pos, inv, last,
                           reinterpret_cast<hipStream_t>(stream));
-}
-
-int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {
-  if (!jobs || n < 1 || n > RB_MAX_SPLIT_JOBS)
-    return fail("rb_gemm_split_weights: need 1..RB_MAX_SPLIT_JOBS jobs");
-  for (int64_t j = 0; j < n; ++j) {
-    const rb_split_job& b = jobs[j];
-    if (!b.W || !b.Wf) return fail("rb_gemm_split_weights: null pointer");
-    if (b.C <= 0 || b.R <= 0 || b.C % 32 || b.R % 16 || b.C > (1 << 20) || b.R > (1 << 20))
-      return fail("rb_gemm_split_weights: C must be a multiple of 32 and R of 16");
-    if (b.ldw < (b.transpose ? b.C : b.R)) return fail("rb_gemm_split_weights: bad row stride");
-    if (!aligned16(b.Wf)) return fail("rb_gemm_split_weights: Wf must be 16-byte aligned");
-  }
-  return launch_split_weights(jobs, (int)n, reinterpret_cast<hipStream_t>(stream));
-}
-
-int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
-               const float* bias, float* out, int64_t ldo, int accumulate, void* stream) {
-  if (!A || !Wf || !out) return fail("rb_gemm_nt: null pointer");
-  if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt: empty shape");
-  if (R % 32 || C % 128 || R > (1 << 16) || C > (1 << 16))
-    return fail("rb_gemm_nt: R must be a multiple of 32 and C of 128");
-  if (lda < R || lda % 4 || ldo < C) return fail("rb_gemm_nt: bad row strides");
-  if (!aligned16(A) || !aligned16(Wf)) return fail("rb_gemm_nt: A and Wf must be 16-byte aligned");
-  if ((M + 127) / 128 * (C / 128) > 0x7fffffffLL) return fail("rb_gemm_nt: grid too large");
-  return launch_gemm_nt(A, lda, M, (int)R, Wf, (int)C, bias, out, ldo, accumulate,
-                        reinterpret_cast<hipStream_t>(stream));
 }
 
 int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R) { return C * R * 4 + ((C * 4 + 15) / 16) * 16; }
@@ -773,6 +721,11 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
   if (ldy < N || ldx < K || ldy % 4 || ldx % 4) return fail("rb_gemm_tn_h: bad row strides");
   if (!aligned16(dY) || !aligned16(X)) return fail("rb_gemm_tn_h: dY and X must be 16-byte aligned");
   if ((N / 128) * (K / 128) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_h: grid too large");
+  // the kernel reads a row chunk through a buffer descriptor: 32-bit record
+  // count and lane offsets over the chunk's bytes (launch_gemm_tn_h's chunk)
+  const int64_t mk = ((M + splits - 1) / splits + 31) / 32 * 32;
+  if (mk * (ldy > ldx ? ldy : ldx) * 4 >= 0x7fffffffLL)
+    return fail("rb_gemm_tn_h: a row chunk spans 2 GiB or more (use more splits)");
   return launch_gemm_tn_h(dY, ldy, X, ldx, M, (int)N, (int)K, ymax, xmax, parts, (int)splits,
                           reinterpret_cast<hipStream_t>(stream));
 }
@@ -823,60 +776,7 @@ int rb_gemm_tn_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx, int
                              reinterpret_cast<hipStream_t>(stream));
 }
 
-int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
-               const float* conv_b, const void* wg_img, const float* gate_b, const float* lam,
-               const float* h0, const int32_t* pieces, int64_t B, int64_t G, int64_t ntok,
-               int64_t H, float* y, int64_t y_rs, float* y_last, float* xc, float* rg,
-               float* carries, int64_t n_tiles, float* xc_rmax, float* tile_carries,
-               int64_t max_tiles, void* stream) {
-  if (!xz || !conv_w || !conv_b || !wg_img || !gate_b || !lam || !pieces)
-    return fail("rb_grl_fwd: null pointer");
-  if (tile_carries && (max_tiles <= 0 || G * max_tiles * H >= (1LL << 40)))
-    return fail("rb_grl_fwd: tile_carries need max_tiles");
-  if (H != 256) return fail("rb_grl_fwd: the fused kernel is built for H = 256");
-  if (kc < 2 || kc > 4) return fail("rb_grl_fwd: conv kernel size must be 2, 3 or 4");
-  if (B <= 0 || G <= 0 || ntok <= 0 || ntok >= (1LL << 31) || G > (1 << 20))
-    return fail("rb_grl_fwd: bad sizes");
-  if (!y == !y_last) return fail("rb_grl_fwd: exactly one of y / y_last");
-  if (xz_rs < 2 * H || xz_rs % 4 || !aligned16(xz)) return fail("rb_grl_fwd: xz layout");
-  if (y && (y_rs < H || y_rs % 4 || !aligned16(y))) return fail("rb_grl_fwd: y layout");
-  if (ntok * (y && y_rs > xz_rs ? y_rs : xz_rs) >= (1LL << 31))   // 32-bit element offsets
-    return fail("rb_grl_fwd: ntok * row stride must be < 2^31");
-  if (carries && n_tiles <= 0) return fail("rb_grl_fwd: carries need n_tiles");
-  if ((xc && !aligned16(xc)) || !aligned16(wg_img)) return fail("rb_grl_fwd: alignment");
-  return launch_grl_fwd(xz, xz_rs, conv_w, (int)kc, conv_b, wg_img, gate_b, lam, h0,
-                        reinterpret_cast<const int*>(pieces), B, G, ntok, y, y_rs, y_last, xc,
-                        rg, carries, n_tiles, xc_rmax, tile_carries, max_tiles,
-                        reinterpret_cast<hipStream_t>(stream));
-}
 
-int rb_grl_bwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
-               const float* conv_b, const void* wg_img, const void* wgt_img, const float* gate_b,
-               const float* lam, const float* h0, const int32_t* pieces, int64_t B, int64_t G,
-               int64_t ntok, int64_t H, const float* tile_carries, int64_t max_tiles,
-               const float* dy, const float* dy_last, float* dxz, int64_t dxz_rs, float* drg,
-               float* xc, float* drg_rmax, float* xc_rmax, float* part, float* cpart,
-               void* stream) {
-  if (!xz || !conv_w || !conv_b || !wg_img || !wgt_img || !gate_b || !lam || !pieces ||
-      !tile_carries || !dxz || !drg || !xc || !part || !cpart)
-    return fail("rb_grl_bwd: null pointer");
-  if (H != 256) return fail("rb_grl_bwd: the fused kernel is built for H = 256");
-  if (kc < 2 || kc > 4) return fail("rb_grl_bwd: conv kernel size must be 2, 3 or 4");
-  if (B <= 0 || G <= 0 || ntok <= 0 || G > (1 << 20) || max_tiles <= 0)
-    return fail("rb_grl_bwd: bad sizes");
-  if (!dy == !dy_last) return fail("rb_grl_bwd: exactly one of dy / dy_last");
-  if (xz_rs < 2 * H || xz_rs % 4 || !aligned16(xz)) return fail("rb_grl_bwd: xz layout");
-  if (dxz_rs < 2 * H || dxz_rs % 4 || !aligned16(dxz)) return fail("rb_grl_bwd: dxz layout");
-  // 32-bit element offsets inside the kernel
-  if (ntok * (xz_rs > dxz_rs ? xz_rs : dxz_rs) >= (1LL << 31))
-    return fail("rb_grl_bwd: ntok * row stride must be < 2^31");
-  if (!aligned16(xc) || !aligned16(wg_img) || !aligned16(wgt_img))
-    return fail("rb_grl_bwd: alignment");
-  return launch_grl_bwd(xz, xz_rs, conv_w, (int)kc, conv_b, wg_img, wgt_img, gate_b, lam, h0,
-                        reinterpret_cast<const int*>(pieces), B, G, ntok, tile_carries,
-                        max_tiles, dy, dy_last, dxz, dxz_rs, drg, xc, drg_rmax, xc_rmax, part,
-                        cpart, reinterpret_cast<hipStream_t>(stream));
-}
 
 int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
                   int64_t K, float* dw, int accumulate, void* stream) {

@@ -41,17 +41,9 @@ __device__ __forceinline__ float dsilu_f(float x) {
 // 1 - alpha^2 with alpha -> 0.999, depends on alpha's absolute error (~ulp(1))
 // exactly as it does with expf.
 constexpr float kLog2e = 1.4426950408889634f;
-#ifdef RB_ABL_CHEAP_MATH
-// timing ablation only (tools/kbench.hip; wrong results): the transcendentals
-// as one full-rate op each
-__device__ __forceinline__ float fexp(float x) { return x * kLog2e; }
-__device__ __forceinline__ float frcp(float x) { return 1.5f - x; }
-__device__ __forceinline__ float fsqrt(float x) { return 0.5f * x; }
-#else
 __device__ __forceinline__ float fexp(float x) { return __builtin_amdgcn_exp2f(x * kLog2e); }
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fsqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
-#endif
 __device__ __forceinline__ float fsigm(float x) { return frcp(1.0f + fexp(-x)); }
 __device__ __forceinline__ float fsilu(float x) { return x * fsigm(x); }
 __device__ __forceinline__ float fdsilu(float x) {
@@ -283,7 +275,6 @@ DropSpec make_drop(const uint8_t* mask, uint64_t seed, float p);
 int launch_pack_plan(const int64_t* seq, int64_t seq_rs, const int64_t* offs,
                      const int64_t* order, int64_t B, int64_t* ids, int64_t* pos, int64_t* inv,
                      int64_t* last, hipStream_t st);
-int launch_split_weights(const rb_split_job* jobs, int n, hipStream_t st);
 int launch_conv_fwd(const float* x, int64_t x_rs, const float* w, const float* bias, float* xc,
                     int64_t xc_rs, int64_t B, int64_t L, int64_t H, int64_t K, const int64_t* offs, hipStream_t st);
 int launch_conv_bwd(const float* x, int64_t x_rs, const float* w, const float* bias,
@@ -342,10 +333,6 @@ int launch_silu_dropout_bwd(const float* a, const float* bias, const DropSpec& d
                             const float* du, float* da, float* dbias_part, int64_t nparts,
                             int64_t rows, int64_t cols, hipStream_t st);
 int launch_dropout_mask(const DropSpec& drop, uint8_t* out, int64_t n, hipStream_t st);
-int launch_split_weight(const float* W, int64_t ldw, int C, int R, int transpose, void* Wf,
-                        hipStream_t st);
-int launch_gemm_nt(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
-                   const float* bias, float* out, int64_t ldo, int accumulate, hipStream_t st);
 int launch_split_weights_h(const rb_split_job* jobs, int n, hipStream_t st);
 int launch_bf16_weight_image(const float* W, int64_t ldw, int C, int R, int transpose, void* img,
                              hipStream_t st);
@@ -370,19 +357,6 @@ int launch_adam(const rb_adam_job* jobs, int n, double lr, double beta1, double 
                 double weight_decay, double bc1, double bc2, hipStream_t st);
 int launch_gemm_nt_hs(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                       const float* bias, float* out, int64_t ldo, float* rmax, hipStream_t st);
-int grl_fwd_lds_bytes();
-int launch_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int KC,
-                   const float* conv_b, const void* wf, const float* gate_b, const float* lam,
-                   const float* h0, const int* pieces, int64_t B, int64_t G, int64_t ntok,
-                   float* y, int64_t y_rs, float* y_last, float* xc_out, float* rg_out,
-                   float* carries, int64_t nTc, float* xc_rmax, float* tile_carries,
-                   int64_t max_tiles, hipStream_t st);
-int launch_grl_bwd(const float* xz, int64_t xz_rs, const float* conv_w, int KC,
-                   const float* conv_b, const void* wf, const void* wft, const float* gate_b,
-                   const float* lam, const float* h0, const int* pieces, int64_t B, int64_t G,
-                   int64_t ntok, const float* tile_carries, int64_t max_tiles, const float* dy,
-                   const float* dy_last, float* dxz, int64_t dxz_rs, float* drg, float* xc_out,
-                   float* drg_rmax, float* xc_rmax, float* part, float* cpart, hipStream_t st);
 int launch_gemm_tn_hs(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
                       int K, float* dw, int accumulate, hipStream_t st);
 int64_t emb_workspace_bytes(int64_t M, int64_t V, int64_t d);
@@ -415,10 +389,6 @@ int launch_item_split_h(const float* X, int64_t N, int64_t D, void* img, int* ex
 int launch_item_ce_fwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                          const int64_t* tgt, int64_t B, int64_t V, int64_t D, float* lse,
                          float* loss, void* ws, int64_t ws_bytes, hipStream_t st);
-int launch_item_ce_bwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
-                         const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
-                         int64_t V, int64_t D, float* dE, float* dW, void* ws, int64_t ws_bytes,
-                         hipStream_t st);
 int launch_item_ce_probs_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
                            const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
                            int64_t V, int64_t D, int64_t v_off, float* out, int64_t ld,

@@ -14,10 +14,12 @@
 //   The weight gradients of the same Linears over row chunks; the fixed-order
 //   column sum (rb_colsum) adds the partials.
 //
-// Both: one 512-thread workgroup per CU (128 KB of LDS: 2 stages of A and B),
-// 256 x 256 output tiles, waves 4 x 2 owning 64 x 128 each (2 x 4 blocks of
-// 32 x 32), every operand global -> LDS by LDS-DMA, the next k-step issued
-// right after the barrier that frees its slot.
+// Both: one 512-thread workgroup per CU, 256 x 256 output tiles, waves 4 x 2
+// owning 64 x 128 each (2 x 4 blocks of 32 x 32), every operand global -> LDS
+// by LDS-DMA, the next k-step issued right after the barrier that frees its
+// slot.  LDS: the NT kernel 160 KB, all of a gfx950 CU (3 A stages, A two
+// k-steps ahead, + 2 weight stages); the TN kernel 128 KB (2 stages of both
+// operands).  The launchers check that the device grants it.
 #include "common.h"
 
 #include <type_traits>
@@ -439,8 +441,9 @@ k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict
 }
 
 template <typename F>
-void set_lds(F* f, int bytes) {
-  (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+bool set_lds(F* f, int bytes) {
+  return hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) ==
+         hipSuccess;
 }
 
 }  // namespace
@@ -457,8 +460,8 @@ int launch_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int R, const void
                         const float* bias, void* out, int64_t ldo, hipStream_t st) {
   static bool attr = false;   // benign race: idempotent
   if (!attr) {
-    set_lds(k_gemm_nt_bf<true>, BF_LDS);
-    set_lds(k_gemm_nt_bf<false>, BF_LDS);
+    if (!set_lds(k_gemm_nt_bf<true>, BF_LDS) || !set_lds(k_gemm_nt_bf<false>, BF_LDS))
+      return fail("rb_gemm_nt_bf16: the device refused 160 KB of LDS per workgroup (gfx950 only)");
     attr = true;
   }
   const int m_tiles = (int)((M + BF_BM - 1) / BF_BM);
@@ -478,7 +481,8 @@ int launch_gemm_tn_bf16(const void* Y, int64_t ldy, const void* X, int64_t ldx, 
                         int K, float* parts, int S, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    set_lds(k_gemm_tn_bf, TB_LDS);
+    if (!set_lds(k_gemm_tn_bf, TB_LDS))
+      return fail("rb_gemm_tn_bf16: the device refused 128 KB of LDS per workgroup (gfx950 only)");
     attr = true;
   }
   const int64_t per = (M + S - 1) / S;

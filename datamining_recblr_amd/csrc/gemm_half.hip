@@ -5,7 +5,7 @@
 // at the HBM roofline they are bound by their row streams (the fp32 output
 // write or the fp32 input read), not by arithmetic, as soon as the
 // arithmetic runs at >= 1/3 of the bf16 pipe.  The six-product bf16 split
-// (gemm_split.hip) needs 6x the bf16 flops and is MFMA-bound at the tile
+// (round 1's gemm_split.hip, since removed) needs 6x the bf16 flops and is MFMA-bound at the tile
 // level; here each operand is split into TWO fp16 parts and three products
 // are accumulated:
 //     x = 2^-s (x0 + x1),  x0 = f16(x 2^s),  x1 = f16(x 2^s - x0)

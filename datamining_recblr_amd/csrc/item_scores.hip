@@ -35,7 +35,6 @@ namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kWaves = 4;            // waves per workgroup
-constexpr int kThreads = kWaves * 64;
 constexpr int kTile = 32;            // rows (items or sequences) per wave tile
 constexpr int64_t kTargetWgs = 512;  // ~2 workgroups per CU over 256 CUs
 
@@ -1000,249 +999,6 @@ __global__ __launch_bounds__(256) void k_ce_probs_h(const _Float16* __restrict__
   }
 }
 
-// ---- the CE backward's products on the f16 pipe, P never stored -------------------
-// dseq = P W (row-stationary, k_ce_bwd_seq_h) and ditems = P^T seq
-// (item-stationary, k_ce_bwd_item_h), P = (softmax - onehot) * dloss / B,
-// each kernel recomputing the logits of its tiles exactly as k_ce_fwd_h /
-// k_ce_probs_h do (the same split images, products, order and un-scaling:
-// bit-identical logits) and feeding P straight from the accumulators into a
-// second f16x3 product — the fp32 kernels k_ce_bwd_seq / _item on the f16
-// pipe.  The second product sums over the streamed tile's 32 rows: the
-// accumulator tile holds them in its 16 registers (rows crow(r, h)), so
-// registers 8kb .. 8kb + 7 of a lane are its 8 K values of K-block kb and
-// the other operand's fragment gathers the same rows (crow(8kb + k, h), k <
-// 8) of the tile's image (ds_read_u16 per element, tile_gather_h).  The
-// tile's rows carry their own power-of-two scales (image = x 2^(kTS - e)),
-// which do not factor out of a sum over rows: they are folded into P,
-//   P' = P 2^(e_row - emax) 2^(kTS - e_g)   (|P'| < 2^kTS, e_g: frexp of |dloss / B|),
-// split into two f16 planes like every other operand; the partial sums are
-// un-scaled once by 2^(emax + e_g - 2 kTS) (exact).  emax = the streamed
-// operand's largest row exponent (each workgroup reduces the exponent array).
-// (A ds_read_b64_tr_b16 form of the gather, two reads per fragment instead of
-// eight, returned wrong operands on this XOR-swizzled tile image:
-// profiles/r04_ce_pytest_items_tr16.log.)
-// At d = 128 a wave holds its fixed operand's fragments (64 registers) and
-// the second product's four accumulators (64) beside the first's: one wave
-// per SIMD (the accumulator chains keep the MFMA pipe fed); d <= 64 two.
-
-// the largest of n int32 exponents (every thread of the workgroup)
-__device__ __forceinline__ int block_max_exp(const int* e, int64_t n) {
-  __shared__ int sm[kWaves];
-  int m = -100000;
-  for (int64_t i = threadIdx.x; i < n; i += kThreads) m = max(m, e[i]);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = m;
-  __syncthreads();
-  m = sm[0];
-#pragma unroll
-  for (int w = 1; w < kWaves; ++w) m = max(m, sm[w]);
-  return m;
-}
-
-// the 8 halfs of image column `ch` (plane p: ch = p D + col) at rows
-// crow(8 kb + k, h), k < 8, of a swizzled LDS image tile
-template <int D>
-__device__ __forceinline__ f16x8 tile_gather_h(const _Float16* tile, int ch, int kb, int h) {
-  constexpr int NS = Stream<D>::NS;
-  f16x8 r;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int row = 16 * kb + 8 * (k >> 2) + 4 * h + (k & 3);
-    r[k] = tile[row * 2 * D + ((((ch >> 3) ^ (row % NS))) << 3) + (ch & 7)];
-  }
-  return r;
-}
-
-// P' (16 values, the accumulator tile's rows) -> the two f16 planes of each
-// K-block
-__device__ __forceinline__ void split_p(const float (&pv)[16], f16x8 (&p0)[2], f16x8 (&p1)[2]) {
-#pragma unroll
-  for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float v = pv[8 * kb + k];
-      const _Float16 a = (_Float16)v;
-      p0[kb][k] = a;
-      p1[kb][k] = (_Float16)(v - (float)a);
-    }
-}
-
-// acc[n] += P' x (the tile's image rows, columns n*32 + j), the small
-// products first as everywhere on the f16 pipe
-template <int D>
-__device__ __forceinline__ void gemm2_h(f32x16 (&acc)[D / 32], const f16x8 (&p0)[2],
-                                        const f16x8 (&p1)[2], const _Float16* tile, int j, int h) {
-#pragma unroll
-  for (int n = 0; n < D / 32; ++n)
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const f16x8 t0 = tile_gather_h<D>(tile, n * 32 + j, kb, h);
-      const f16x8 t1 = tile_gather_h<D>(tile, D + n * 32 + j, kb, h);
-      acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(p1[kb], t0, acc[n], 0, 0, 0);
-      acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(p0[kb], t1, acc[n], 0, 0, 0);
-      acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(p0[kb], t0, acc[n], 0, 0, 0);
-      // one fragment pair in flight: the gathers of every (n, kb) hoisted
-      // together would hold 64 more registers than two waves per SIMD allow
-      __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// X[b][v] with the sequence rows from the tile (A) and the item row in
-// registers (B), the three products in the forward's order (item1.seq0,
-// item0.seq1, item0.seq0): the transposed orientation of k_ce_fwd_h's X^T
-template <int D>
-__device__ __forceinline__ f32x16 lds_dot_h_seqA(const float* tile, int j, int h,
-                                                 const f16x8 (&r0)[D / 16], const f16x8 (&r1)[D / 16]) {
-  constexpr int KS = D / 16;
-  const float* row = tile + j * D;
-  int sw = j % Stream<D>::NS;
-  asm volatile("" : "+v"(sw));
-  auto rd = [&](int slot) {
-    return __builtin_bit_cast(f16x8, *reinterpret_cast<const float4*>(row + ((slot ^ sw) << 2)));
-  };
-  f16x8 w0[KS], w1[KS];
-  w0[0] = rd(h);
-  w1[0] = rd(D / 8 + h);
-  f32x16 acc = {};
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (s + 1 < KS) {
-      w0[s + 1] = rd(2 * (s + 1) + h);
-      w1[s + 1] = rd(D / 8 + 2 * (s + 1) + h);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0[s], r1[s], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w1[s], r0[s], acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(w0[s], r0[s], acc, 0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  return acc;
-}
-
-// dseq partials per item split: de_part[split][b][d]
-template <int D>
-__global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void k_ce_bwd_seq_h(const _Float16* __restrict__ Ei,
-                                                      const int* __restrict__ Ee,
-                                                      const _Float16* __restrict__ Wi,
-                                                      const int* __restrict__ We,
-                                                      const float* __restrict__ lse,
-                                                      const int64_t* __restrict__ tgt,
-                                                      const float* __restrict__ dloss, float inv_n,
-                                                      int64_t B, int64_t V, int64_t per, int64_t RB,
-                                                      int64_t NS, float* __restrict__ de_part) {
-  constexpr int NT = D / 32;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
-  Place pl;
-  if (!place(RB, NS, pl)) return;
-  const int emax = block_max_exp(We, V);
-  const int64_t b0 = (pl.rb * kWaves + wave) * kTile;
-  const int64_t bc = min(b0 + j, B - 1);
-  f16x8 e0[D / 16], e1[D / 16];
-  ld_frag_h<D>(e0, e1, Ei, bc, h);
-  const int eb = Ee[bc] - 2 * kTS;
-  const float lb = lse[bc];
-  const int64_t tb = tgt[bc];
-  const float g = dloss[0] * inv_n;
-  const int eg = g != 0.0f ? __builtin_amdgcn_frexp_expf(fabsf(g)) : 0;
-  f32x16 acc[NT];
-#pragma unroll
-  for (int n = 0; n < NT; ++n) acc[n] = f32x16{};
-  stream_tiles<D, 2>(reinterpret_cast<const float*>(Wi), V, per, pl.split,
-                     reinterpret_cast<const float*>(We), nullptr,
-                     [&](int64_t t, const float* tile, const float* ebuf, const int64_t*) {
-    const int64_t v0 = t * kTile;
-    const f32x16 x = lds_dot_h<D, true>(tile, j, h, e0, e1);   // X^T[v][b], k_ce_fwd_h's
-    const int4* ev = reinterpret_cast<const int4*>(ebuf);
-    const int hi = rel32(V, v0), tt = rel32(tb, v0);
-    float pv[16];
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) {
-      const int4 q = ev[2 * q4 + h];   // items 8 q4 + 4h .. + 3 = rows crow(4 q4 .. 4 q4 + 3, h)
-      const int qe[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = 4 * q4 + u, c = crow(r, h);
-        const float xs = __builtin_amdgcn_ldexpf(x[r], qe[u] + eb);
-        const float pr = c < hi ? (fexp(xs - lb) - (c == tt ? 1.0f : 0.0f)) * g : 0.0f;
-        pv[r] = __builtin_amdgcn_ldexpf(pr, qe[u] - emax + kTS - eg);
-      }
-    }
-    f16x8 p0[2], p1[2];
-    split_p(pv, p0, p1);
-    gemm2_h<D>(acc, p0, p1, reinterpret_cast<const _Float16*>(tile), j, h);
-  });
-  if (b0 >= B) return;
-  float* out = de_part + pl.split * B * D;
-  const int sh = emax + eg - 2 * kTS;
-#pragma unroll
-  for (int n = 0; n < NT; ++n)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t row = b0 + crow(r, h);
-      if (row < B) out[row * D + n * 32 + j] = __builtin_amdgcn_ldexpf(acc[n][r], sh);
-    }
-}
-
-// ditems partials per sequence split: dw_part[split][v][d]
-template <int D>
-__global__ __launch_bounds__(256, D <= 64 ? 2 : 1) void k_ce_bwd_item_h(const _Float16* __restrict__ Ei,
-                                                       const int* __restrict__ Ee,
-                                                       const _Float16* __restrict__ Wi,
-                                                       const int* __restrict__ We,
-                                                       const float* __restrict__ lse,
-                                                       const int64_t* __restrict__ tgt,
-                                                       const float* __restrict__ dloss, float inv_n,
-                                                       int64_t B, int64_t V, int64_t per, int64_t RB,
-                                                       int64_t NS, float* __restrict__ dw_part) {
-  constexpr int NT = D / 32;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, j = lane & 31, h = lane >> 5;
-  Place pl;
-  if (!place(RB, NS, pl)) return;
-  const int emax = block_max_exp(Ee, B);
-  const int64_t v0 = (pl.rb * kWaves + wave) * kTile;
-  const int64_t v = v0 + j;
-  const int64_t vc = min(v, V - 1);
-  f16x8 w0[D / 16], w1[D / 16];
-  ld_frag_h<D>(w0, w1, Wi, vc, h);
-  const int ev = We[vc];
-  const float g = dloss[0] * inv_n;
-  const int eg = g != 0.0f ? __builtin_amdgcn_frexp_expf(fabsf(g)) : 0;
-  f32x16 acc[NT];
-#pragma unroll
-  for (int n = 0; n < NT; ++n) acc[n] = f32x16{};
-  stream_tiles<D, 3>(reinterpret_cast<const float*>(Ei), B, per, pl.split, lse, tgt,
-                     [&](int64_t t, const float* tile, const float* lt, const int64_t* tt,
-                         const float* xb) {
-    const int64_t bt0 = t * kTile;
-    const f32x16 x = lds_dot_h_seqA<D>(tile, j, h, w0, w1);   // X[b][v]
-    const int* eb = reinterpret_cast<const int*>(xb);
-    const int hi = rel32(B, bt0);
-    float pv[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int c = crow(r, h);
-      const int er = eb[c];
-      const float xs = __builtin_amdgcn_ldexpf(x[r], ev + (er - 2 * kTS));
-      const float pr = c < hi ? (fexp(xs - lt[c]) - (v == tt[c] ? 1.0f : 0.0f)) * g : 0.0f;
-      pv[r] = __builtin_amdgcn_ldexpf(pr, er - emax + kTS - eg);
-    }
-    f16x8 p0[2], p1[2];
-    split_p(pv, p0, p1);
-    gemm2_h<D>(acc, p0, p1, reinterpret_cast<const _Float16*>(tile), j, h);
-  }, reinterpret_cast<const float*>(Ee));
-  if (v0 >= V) return;
-  float* out = dw_part + pl.split * V * D;
-  const int sh = emax + eg - 2 * kTS;
-#pragma unroll
-  for (int n = 0; n < NT; ++n)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t row = v0 + crow(r, h);
-      if (row < V) out[row * D + n * 32 + j] = __builtin_amdgcn_ldexpf(acc[n][r], sh);
-    }
-}
-
 // ---- host side ---------------------------------------------------------------------
 size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -1390,20 +1146,6 @@ void probs_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, int
                        (int64_t)0, nullptr);
 }
 
-template <int D>
-void ce_bwd_h_t(const void* Ei, const int* Ee, const void* Wi, const int* We, const float* lse,
-                const int64_t* tgt, const float* dloss, float inv_n, int64_t B, int64_t V,
-                const Grid2& g, float* part, bool items, hipStream_t st) {
-  if (items)
-    hipLaunchKernelGGL(k_ce_bwd_item_h<D>, dim3(g.wgs()), dim3(256), 0, st, (const _Float16*)Ei,
-                       Ee, (const _Float16*)Wi, We, lse, tgt, dloss, inv_n, B, V, g.per, g.blocks,
-                       g.splits, part);
-  else
-    hipLaunchKernelGGL(k_ce_bwd_seq_h<D>, dim3(g.wgs()), dim3(256), 0, st, (const _Float16*)Ei,
-                       Ee, (const _Float16*)Wi, We, lse, tgt, dloss, inv_n, B, V, g.per, g.blocks,
-                       g.splits, part);
-}
-
 void sum_parts(const float* parts, int64_t P, int64_t n, float* out, hipStream_t st) {
   const int64_t threads = (n + 3) / 4;
   hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, parts,
@@ -1458,30 +1200,6 @@ int launch_item_ce_bwd(const float* E, const float* W, const int64_t* tgt, const
     sum_parts(part, g.splits, V * D, dW, st);
   }
   return launch_status("rb_item_ce_bwd");
-}
-
-int launch_item_ce_bwd_h(const void* Ei, const int* Ee, const void* Wi, const int* We,
-                         const int64_t* tgt, const float* lse, const float* dloss, int64_t B,
-                         int64_t V, int64_t D, float* dE, float* dW, void* ws, int64_t ws_bytes,
-                         hipStream_t st) {
-  const CeWs L = ce_layout(B, V, D);
-  if (ws_bytes < (int64_t)L.total) return fail("rb_item_ce_bwd_h: workspace too small");
-  if (D != 32 && D != 64 && D != 128) return fail("rb_item_ce_bwd_h: d must be 32, 64 or 128");
-  char* w = static_cast<char*>(ws);
-  const float inv_n = 1.0f / (float)B;
-  for (int items = 0; items < 2; ++items) {
-    float* out = items ? dW : dE;
-    if (!out) continue;
-    float* part = reinterpret_cast<float*>(w + (items ? L.dw : L.de));
-    const Grid2 g = items ? plan(V, ntiles(B)) : plan(B, ntiles(V));
-    switch (D) {
-      case 32: ce_bwd_h_t<32>(Ei, Ee, Wi, We, lse, tgt, dloss, inv_n, B, V, g, part, items, st); break;
-      case 64: ce_bwd_h_t<64>(Ei, Ee, Wi, We, lse, tgt, dloss, inv_n, B, V, g, part, items, st); break;
-      default: ce_bwd_h_t<128>(Ei, Ee, Wi, We, lse, tgt, dloss, inv_n, B, V, g, part, items, st); break;
-    }
-    sum_parts(part, g.splits, (items ? V : B) * D, out, st);
-  }
-  return launch_status("rb_item_ce_bwd_h");
 }
 
 int launch_item_rank(const float* E, const float* W, const int64_t* tgt, int64_t B, int64_t V,

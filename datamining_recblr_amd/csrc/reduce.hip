@@ -129,13 +129,15 @@ __global__ __launch_bounds__(64 * RG) void k_colsum_2l(const float* __restrict__
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the fence's own wait may be dropped
-    const unsigned old = __hip_atomic_fetch_add(&cnt[mc], 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
+    // wrapping increment (old >= nch - 1 ? 0 : old + 1): the ticket is back
+    // at 0 after the last arrival without a separate reset store, and a
+    // ticket outside [0, nch) is pulled back into range by the next launch
+    const unsigned old = __builtin_amdgcn_atomic_inc32(&cnt[mc], (unsigned)(nch - 1),
+                                                       __ATOMIC_RELAXED, "agent");
     const int last = old == (unsigned)(nch - 1);
     if (last) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&cnt[mc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     s_last = last;
   }

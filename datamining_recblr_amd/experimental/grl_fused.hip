@@ -27,7 +27,8 @@
 //   D  in the MFMA accumulator layout (lane: one channel, 16 rows per
 //      block): bias, alpha, beta, b' = beta xc, the scan (each lane chains its
 //      eight 4-row groups with its partner lane's), y = silu(z) h.
-#include "common.h"
+#include "../csrc/common.h"
+#include "recblr_exp.h"
 
 namespace rb {
 namespace {
@@ -58,36 +59,6 @@ constexpr int LDS_CW = LDS_LAST + GT * 4;       // conv weights [H][KC] and bias
 constexpr int LDS_BYTES = LDS_CW + GH * 4 * 4 + GH * 4;
 
 typedef int i32x4g __attribute__((ext_vector_type(4)));
-
-// Ablation switches of tools/grlbench.hip (wrong results; never set in the
-// library build): 1 weight fragments not loaded, 2 no gates GEMM at all,
-// 4 no x / xz row loads, 8 no per-channel z / dy loads and y / dz / drg stores,
-// 16 no y stores (forward), 32 no xc / dx row stores (backward)
-#ifndef GRL_PROBE
-#define GRL_PROBE 0
-#endif
-// -DGRL_STAMPS (tools/grlbench.hip only): per-phase cycle sums of every wave
-// (the stamps' lgkmcnt(0) waits perturb the overlap: read shares)
-#ifdef GRL_STAMPS
-__device__ unsigned long long grl_stamps[2][20];
-#define GRL_STAMP(k)                                                           \
-  do {                                                                         \
-    __builtin_amdgcn_sched_barrier(0);                                         \
-    unsigned long long t_;                                                     \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                         \
-    if ((k) >= 0) st_acc[(k) < 0 ? 0 : (k)] += t_ - st_prev;                   \
-    st_prev = t_;                                                              \
-  } while (0)
-#define GRL_STAMP_DECL unsigned long long st_acc[20] = {}, st_prev = 0
-#define GRL_STAMP_FLUSH(w) \
-  if (lane == 0)           \
-    for (int k_ = 0; k_ < 20; ++k_) atomicAdd(&grl_stamps[w][k_], st_acc[k_])
-#else
-#define GRL_STAMP(k) do {} while (0)
-#define GRL_STAMP_DECL do {} while (0)
-#define GRL_STAMP_FLUSH(w) do {} while (0)
-#endif
 
 __device__ __forceinline__ f32x16g mfma_g(f16x8g a, f16x8g b, f32x16g c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -228,7 +199,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
       const int vr = 8 * wave + j;
       const int grow = __builtin_amdgcn_readlane(mrow, vr);
       const int pos = __builtin_amdgcn_readlane(mpos, vr);
-      xo[j] = pos >= 0 && !(GRL_PROBE & 4)
+      xo[j] = pos >= 0
                   ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)(grow * xzr + 4 * lane))
                   : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
     }
@@ -237,7 +208,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
 #pragma unroll
     for (int i = 0; i < KC - 1; ++i) {   // row g0 - (KC - 1 - i)
       const int l = KC - 1 - i;
-      xh[i] = p0 >= l && !(GRL_PROBE & 4)
+      xh[i] = p0 >= l
                   ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((g0 - l) * xzr + 4 * lane))
                   : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
     }
@@ -249,7 +220,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
         const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
         const int r0 = __builtin_amdgcn_readlane(rv, rc), r1 = __builtin_amdgcn_readlane(rv, rc + 4);
         const int grow = h ? r1 : r0;
-        zp[rb][e] = grow >= 0 && !(GRL_PROBE & 8) ? a.xz[(uint32_t)(grow * xzr + GH + c)] : 0.0f;
+        zp[rb][e] = grow >= 0 ? a.xz[(uint32_t)(grow * xzr + GH + c)] : 0.0f;
       }
   };
   // conv weights and bias -> LDS once (phase A then issues no global loads
@@ -267,14 +238,12 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int vr = 8 * wave + j;
-      if (s_pos[vr] >= 0 && !(GRL_PROBE & 24))
+      if (s_pos[vr] >= 0)
         __builtin_nontemporal_store(*reinterpret_cast<const f32x4g*>(yb + vr * XC_PITCH),
                                     reinterpret_cast<f32x4g*>(a.y + (uint32_t)(s_row[vr] * yr + 4 * lane)));
     }
   };
 
-  GRL_STAMP_DECL;
-  GRL_STAMP(-1);
   for (int v0 = 0; v0 < span_rows; v0 += GT) {
     if (a.tile_carries && h == 0)
       a.tile_carries[((int64_t)g * a.max_tiles + v0 / GT) * GH + c] = carry;
@@ -289,7 +258,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
     char* const db = smem + opaque(LDS_ER + 16 * h);               // per-row int arrays
     char* const xb = smem + opaque(LDS_XC + 4 * h * XC_PITCH + 4 * c);   // s_xc[4h][c]
     char* const gb = smem + opaque(LDS_PLANE0 + lane * 16);         // GEMM A fragments
-    GRL_STAMP(0);
     // the previous tile's y rows, whole 1 KB rows from LDS (phase D left
     // them in the xc slots: per-lane 4-byte stores there cost 20 % more)
     if (a.y && v0 > 0) store_y();
@@ -355,9 +323,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
       *reinterpret_cast<f16x4g*>(ab_fr + fo) = h0v;
       *reinterpret_cast<f16x4g*>(ab_fr + PLANE_BYTES + fo) = h1v;
     }
-    GRL_STAMP(1);
     lds_sync();
-    GRL_STAMP(2);
 
     // ---- phase C: r / i columns of channels 32w.. for the 64 rows
     f32x16g ar[2], ai[2];
@@ -368,17 +334,13 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
     // weight fragments: a wave-uniform base (kb advances it) + the lane's 16 B
     const int wl = opaque(lane * 16);
     auto wfrag = [&](const char* base, int kb, int p) {
-#if GRL_PROBE & 1
-      return f16x8g{} + (_Float16)(kb + p);
-#else
       return *reinterpret_cast<const f16x8g*>(base + kb * 2048 + p * 1024 + wl);
-#endif
     };
     // weight fragments two k16 steps ahead (L2 latency over one step's MFMAs)
     f16x8g br0 = wfrag(wr, 0, 0), br1 = wfrag(wr, 0, 1), bi0 = wfrag(wi, 0, 0), bi1 = wfrag(wi, 0, 1);
     f16x8g nr0 = wfrag(wr, 1, 0), nr1 = wfrag(wr, 1, 1), ni0 = wfrag(wi, 1, 0), ni1 = wfrag(wi, 1, 1);
 #pragma unroll 1
-    for (int kb = 0; kb < ((GRL_PROBE & 2) ? 0 : KBG); ++kb) {
+    for (int kb = 0; kb < KBG; ++kb) {
       f16x8g mr0, mr1, mi0, mi1;
       if (kb + 2 < KBG) {
         mr0 = wfrag(wr, kb + 2, 0); mr1 = wfrag(wr, kb + 2, 1);
@@ -412,7 +374,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
 #define DSEQ(rc) (*reinterpret_cast<const int*>(db + (LDS_SEQ - LDS_ER) + 4 * (rc)))
 #define DLAST(rc) (*reinterpret_cast<const int*>(db + (LDS_LAST - LDS_ER) + 4 * (rc)))
 #define DER(rc) (*reinterpret_cast<const int*>(db + 4 * (rc)))
-    GRL_STAMP(3);
     // ---- phase D: gates, scan, merge (lane: channel c, rows of its C layout),
     // one 32-row block at a time; alpha -> ar, b' -> ai in place
     float run = carry;
@@ -482,7 +443,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
           const float yv = fsilu(zp[rb][e]) * hn;
           if (a.y)   // over this (row, channel)'s xc, read above
             *reinterpret_cast<float*>(xb + rc * XC_PITCH) = yv;
-          else if (pos >= 0 && a.y_last && DLAST(rc) && !(GRL_PROBE & 24))
+          else if (pos >= 0 && a.y_last && DLAST(rc))
             a.y_last[(uint32_t)(DSEQ(rc) * GH + c)] = yv;
         }
       }
@@ -494,12 +455,9 @@ __global__ void __launch_bounds__(512, 1) k_grl_fwd(const GrlFwdArgs a) {
 #undef DSEQ
 #undef DLAST
 #undef DER
-    GRL_STAMP(4);
     lds_sync();   // LDS is rewritten by the next tile
-    GRL_STAMP(5);
   }
   if (a.y) store_y();
-  GRL_STAMP_FLUSH(0);
 }
 
 // ---------------------------------------------------------------------------
@@ -638,8 +596,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
     for (int v = 0; v < 4; ++v) cbv[v] = b4[v];
   };
 
-  GRL_STAMP_DECL;
-  GRL_STAMP(-1);
   for (int t = n_tiles - 1; t >= 0; --t) {
     if (t != n_tiles - 1) {   // move the cursor back by one tile
       cur_off -= GT;
@@ -653,7 +609,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
     const int rseq = rvalid ? p_seq[rp] : 0;
     const int rrem = rvalid ? p_len[rp] - 1 - roff : -1;     // rows to the sequence's end
 
-    GRL_STAMP(0);
     // ---- A: xc (fp32 -> R0, HBM), its f16 planes (-> R1)
     {
       float cw[KC][4], cbv[4];
@@ -671,7 +626,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
           f32x4g xs[KC];
 #pragma unroll
           for (int k = 0; k < KC; ++k)
-            xs[k] = KC - 1 - k <= pos && !(GRL_PROBE & 4)
+            xs[k] = KC - 1 - k <= pos
                         ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((grow - (KC - 1 - k)) * xzr + 4 * lane))
                         : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
@@ -682,7 +637,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
               acc = acc + (KC - 1 - k <= pos ? cw[k][v] * xs[k][v] : 0.0f);
             xcv[v] = fsilu(acc);
           }
-          if (!(GRL_PROBE & 32))
           __builtin_nontemporal_store(xcv, reinterpret_cast<f32x4g*>(a.xc_out + (uint32_t)(grow * GH + 4 * lane)));
         }
         *reinterpret_cast<f32x4g*>(ab_xc + vr * XC_PITCH) = xcv;
@@ -712,9 +666,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         *reinterpret_cast<f16x4g*>(ab_fr + PLANE_BYTES + fo) = h1v;
       }
     }
-    GRL_STAMP(1);
     lds_sync();
-    GRL_STAMP(2);
 
     // ---- C: GEMM 1 (r, i)
     f32x16g ar[2], ai[2];
@@ -726,16 +678,12 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
       const int wl = opaque(lane * 16);
       const char* const gb = smem + opaque(B_R1 + lane * 16);
       auto wfrag = [&](const char* base, int kb, int p) {
-#if GRL_PROBE & 1
-        return f16x8g{} + (_Float16)(kb + p);
-#else
         return *reinterpret_cast<const f16x8g*>(base + kb * 2048 + p * 1024 + wl);
-#endif
       };
       f16x8g br0 = wfrag(wr, 0, 0), br1 = wfrag(wr, 0, 1), bi0 = wfrag(wi, 0, 0), bi1 = wfrag(wi, 0, 1);
       f16x8g nr0 = wfrag(wr, 1, 0), nr1 = wfrag(wr, 1, 1), ni0 = wfrag(wi, 1, 0), ni1 = wfrag(wi, 1, 1);
 #pragma unroll 1
-      for (int kb = 0; kb < ((GRL_PROBE & 2) ? 0 : KBG); ++kb) {
+      for (int kb = 0; kb < KBG; ++kb) {
         f16x8g mr0, mr1, mi0, mi1;
         if (kb + 2 < KBG) {
           mr0 = wfrag(wr, kb + 2, 0); mr1 = wfrag(wr, kb + 2, 1);
@@ -757,9 +705,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         if (kb + 2 < KBG) { nr0 = mr0; nr1 = mr1; ni0 = mi0; ni1 = mi1; }
       }
     }
-    GRL_STAMP(3);
     lds_sync();   // R1's planes are spent: gy goes there
-    GRL_STAMP(4);
 
 // each phase takes fresh (opaque) bases: per-row values are re-read from
 // LDS, never kept in registers from one phase to the next
@@ -795,7 +741,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
           if ((e & 3) == 0) __builtin_amdgcn_sched_barrier(0);
           const int rc = 32 * rb + 8 * (e >> 2) + (e & 3);
           zv[e] = gv[e] = 0.0f;
-          if (BPOS(rc) >= 0 && !(GRL_PROBE & 8)) {
+          if (BPOS(rc) >= 0) {
             const int grow = BROW(rc);
             zv[e] = a.xz[(uint32_t)(grow * xzr + GH + c)];
             gv[e] = !LASTDY ? a.dy[(uint32_t)(grow * GH + c)]
@@ -857,7 +803,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
             hp = hn;
             const float zz = zv[e];
             const float sz = fsigm(zz);
-            if (pos >= 0 && !(GRL_PROBE & 8))
+            if (pos >= 0)
               a.dxz[(uint32_t)(BROW(rc) * dxr + GH + c)] = (gv[e] * hn) * (sz * (1.0f + zz * (1.0f - sz)));
             HPV(rc) = gv[e] * (zz * sz);   // 0 past the span (gv = 0)
           }
@@ -865,7 +811,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
       }
     }
 
-    GRL_STAMP(5);
     // ---- D (reverse part): adjoint, gate gradients; dr, di -> ar, ai; dxc's
     // direct term -> dxd
     float dxd[2][16];
@@ -965,9 +910,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
       }
       eadj = run;
     }
-    GRL_STAMP(6);
     lds_sync();   // every wave is past its reads of xc (R0) and gy (R1)
-    GRL_STAMP(7);
 
     // ---- E: dr -> R0, di -> R1 (fp32, row-major), then row-wide
     {
@@ -993,7 +936,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         const f32x4g dr4 = *reinterpret_cast<const f32x4g*>(e0 + vr * XC_PITCH);
         const f32x4g di4 = *reinterpret_cast<const f32x4g*>(e1 + vr * XC_PITCH);
         const int grow = *reinterpret_cast<const int*>(smem + B_ROW + 4 * vr);
-        if (pos >= 0 && !(GRL_PROBE & 8)) {
+        if (pos >= 0) {
           __builtin_nontemporal_store(dr4, reinterpret_cast<f32x4g*>(a.drg + (uint32_t)(grow * (2 * GH) + 4 * lane)));
           __builtin_nontemporal_store(di4, reinterpret_cast<f32x4g*>(a.drg + (uint32_t)(grow * (2 * GH) + GH + 4 * lane)));
         }
@@ -1028,9 +971,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         *reinterpret_cast<f16x4g*>(e1 - 8 * lane + vr * XC_PITCH + PL_LO) = il;
       }
     }
-    GRL_STAMP(8);
     lds_sync();
-    GRL_STAMP(9);
 
     // ---- F: GEMM 2, dxc_g for channels 32w.. (K = 512: dr's planes in R0,
     // di's in R1)
@@ -1044,15 +985,11 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
       // A fragment of lane l: row l % 32, halfs 8 (l / 32) .. + 7 of a k16 block
       const char* const g2 = smem + opaque((lane & 31) * XC_PITCH + 16 * (lane >> 5));
       auto tfrag = [&](int kk, int p) {
-#if GRL_PROBE & 1
-        return f16x8g{} + (_Float16)(kk + p);
-#else
         return *reinterpret_cast<const f16x8g*>(wt + kk * 2048 + p * 1024 + wl);
-#endif
       };
       f16x8g b0 = tfrag(0, 0), b1 = tfrag(0, 1), n0 = tfrag(1, 0), n1 = tfrag(1, 1);
 #pragma unroll 1
-      for (int kk = 0; kk < ((GRL_PROBE & 2) ? 0 : 2 * KBG); ++kk) {
+      for (int kk = 0; kk < 2 * KBG; ++kk) {
         f16x8g m0, m1;
         if (kk + 2 < 2 * KBG) { m0 = tfrag(kk + 2, 0); m1 = tfrag(kk + 2, 1); }
         const char* const ga = g2 + (kk < KBG ? B_R0 + kk * 32 : B_R1 + (kk - KBG) * 32);
@@ -1068,9 +1005,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         if (kk + 2 < 2 * KBG) { n0 = m0; n1 = m1; }
       }
     }
-    GRL_STAMP(10);
     lds_sync();   // the planes are spent: dxc goes to R0
-    GRL_STAMP(11);
 
     // ---- G: dxc = dxc_g + the direct term -> R0 (C layout)
     {
@@ -1085,9 +1020,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
               __builtin_amdgcn_ldexpf(ax[rb][e], BER2(rc) + ec_t - 2 * kSWg) + dxd[rb][e];
         }
     }
-    GRL_STAMP(12);
     lds_sync();
-    GRL_STAMP(13);
 
     // ---- H: conv backward, row-wide (channels 4*lane..).  H1: the
     // pre-activation again from x (the rows dW needs anyway), dpre = dxc
@@ -1108,7 +1041,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
           f32x4g xs[KC];
 #pragma unroll
           for (int k = 0; k < KC; ++k)
-            xs[k] = KC - 1 - k <= pos && !(GRL_PROBE & 4)
+            xs[k] = KC - 1 - k <= pos
                         ? *reinterpret_cast<const f32x4g*>(a.xz + (uint32_t)((grow - (KC - 1 - k)) * xzr + 4 * lane))
                         : f32x4g{0.0f, 0.0f, 0.0f, 0.0f};
           const f32x4g g1 = *reinterpret_cast<const f32x4g*>(dp + vr * XC_PITCH);
@@ -1125,9 +1058,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
         }
         *reinterpret_cast<f32x4g*>(dp + vr * XC_PITCH) = dpv;
       }
-      GRL_STAMP(14);
       lds_sync();
-      GRL_STAMP(15);
 #pragma unroll 2
       for (int j = 0; j < 8; ++j) {
         const int vr = 8 * wave + j;
@@ -1147,11 +1078,9 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
             for (int v = 0; v < 4; ++v) dxv[v] = dxv[v] + cw[k][v] * dn[v];
           }
         }
-        if (!(GRL_PROBE & 32))
-          __builtin_nontemporal_store(dxv, reinterpret_cast<f32x4g*>(a.dxz + (uint32_t)(grow * dxr + 4 * lane)));
+        __builtin_nontemporal_store(dxv, reinterpret_cast<f32x4g*>(a.dxz + (uint32_t)(grow * dxr + 4 * lane)));
       }
     }
-    GRL_STAMP(16);
     lds_sync();
     if (wave == 0) {   // this tile's first 3 rows of dpre: the halo of the next (earlier) tile
 #pragma unroll
@@ -1168,9 +1097,7 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
 #undef BER2
 #undef XCV
 #undef HPV
-    GRL_STAMP(17);
   }
-  GRL_STAMP_FLUSH(1);
   // ---- partial sums of this workgroup
   acc_v += __shfl_xor(acc_v, 32);
   acc_r += __shfl_xor(acc_r, 32);
@@ -1193,7 +1120,6 @@ __global__ void __launch_bounds__(512, 1) k_grl_bwd(const GrlBwdArgs a) {
 
 }  // namespace
 
-int grl_fwd_lds_bytes() { return LDS_BYTES; }
 
 int launch_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int KC,
                    const float* conv_b, const void* wf, const float* gate_b, const float* lam,

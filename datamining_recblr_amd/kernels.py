@@ -75,14 +75,16 @@ def kernel_timing(only=None):
         _timer = prev
 
 
-def _launch(name: str, nbytes: int, *args, _fn: str | None = None, _flops: bool = False) -> None:
+def _launch(name: str, nbytes: int, *args, _fn: str | None = None, _flops: bool = False,
+            _exp: bool = False) -> None:
     """Call C-ABI entry point `_fn or name`; timed under `name` in bench runs.
     `nbytes` is the launch's algorithmic HBM bytes, or its algorithmic FLOPs
     where `_flops` is set — exactly the names in FLOP_KERNELS (checked when
     timed, and statically by tests/test_host_logic.py)."""
     t = _timer
+    call = _lib.call_exp if _exp else _lib.call
     if t is None or (t.only is not None and name not in t.only):
-        _lib.call(_fn or name, *args)
+        call(_fn or name, *args)
         return
     if _flops != (name in FLOP_KERNELS):
         raise AssertionError(f"{name}: counted in {'FLOPs' if _flops else 'bytes'} but "
@@ -90,18 +92,22 @@ def _launch(name: str, nbytes: int, *args, _fn: str | None = None, _flops: bool 
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    _lib.call(_fn or name, *args)
+    call(_fn or name, *args)
     e1.record()
     t.records.append((name, nbytes, e0, e1))
 
 
 _tickets = {}
+_lib.on_failure(_tickets.clear)
 
 
 def _colsum_tickets(x: torch.Tensor, n: int) -> torch.Tensor:
     """rb_colsum_chunked's ticket counters for torch's current stream on x's
-    device: zeroed once here, left zero by every call (calls on one stream
-    are ordered; another stream gets its own)."""
+    device: zeroed once here, back at zero after every complete launch (the
+    kernel's wrapping increment; calls on one stream are ordered, another
+    stream gets its own).  A counter found out of range is pulled back into
+    range by the launch that meets it; a failed native call drops every cached
+    counter (_lib.on_failure), so the next call starts from fresh zeros."""
     key = (x.device, _stream(x))
     t = _tickets.get(key)
     if t is None or t.numel() < n:
@@ -677,8 +683,7 @@ def embedding_plan(idx, num_rows, d, stream=None):
 # MFMA roofline).
 FLOP_KERNELS = frozenset({"rb_item_ce_fwd", "rb_item_ce_bwd", "rb_item_ce_probs", "rb_item_rank",
                           "rb_item_scores", "rb_item_ce_fwd_h", "rb_item_ce_probs_h",
-                          "rb_item_ce_probs_h_t", "rb_item_ce_probs_h_both",
-                          "rb_item_ce_bwd_h"})
+                          "rb_item_ce_probs_h_t", "rb_item_ce_probs_h_both"})
 
 
 def f16_split_kernel(name: str) -> bool:
@@ -865,32 +870,6 @@ def item_ce_probs_h_t(seq: SplitRows, items: SplitRows, target, lse, dloss, item
     return pt, gmax
 
 
-def item_ce_bwd_h(seq: SplitRows, items: SplitRows, target, lse, dloss, want_seq=True,
-                  want_items=True):
-    """(dseq [B, d], ditems [V, d]) of the CE on split images with P never
-    stored (rb_item_ce_bwd_h: each product from a kernel that recomputes the
-    logits and multiplies P from its accumulators, f16x3); d in {32, 64, 128}."""
-    B, V, d, target = _split_operands(seq, items, target)
-    if d not in (32, 64, 128):
-        raise ValueError("item_ce_bwd_h: d must be 32, 64 or 128")
-    _check(lse, "lse")
-    _check(dloss, "dloss")
-    dev = seq.img.device
-    lib = _lib.load()
-    ws_bytes = int(lib.rb_item_ce_workspace(B, V, d))
-    ws = torch.empty((ws_bytes,), device=dev, dtype=torch.uint8)
-    dseq = torch.empty((B, d), device=dev, dtype=torch.float32) if want_seq else None
-    ditems = torch.empty((V, d), device=dev, dtype=torch.float32) if want_items else None
-    flops = 4 * B * V * d * (int(want_seq) + int(want_items))   # logits + product, each
-    _launch("rb_item_ce_bwd_h", flops, seq.img.data_ptr(), seq.exps.data_ptr(),
-            items.img.data_ptr(), items.exps.data_ptr(), target.data_ptr(),
-            lse.contiguous().data_ptr(), dloss.reshape(1).contiguous().data_ptr(), B, V, d,
-            None if dseq is None else dseq.data_ptr(),
-            None if ditems is None else ditems.data_ptr(), ws.data_ptr(), ws_bytes,
-            _stream(seq.img), _flops=True)
-    return dseq, ditems
-
-
 def item_ce_probs_h_both(seq: SplitRows, items: SplitRows, target, lse, dloss, item_offset=0,
                         pad_to: int = 1):
     """Both layouts of the logits' gradient in one pass
@@ -1010,22 +989,6 @@ def pad_prefix_bwd(conv_b, gate_w, gate_b, lam, pad_len, dh0, into=None):
     return dcb, dgw, dgb, dlam
 
 
-# ---- projection GEMMs on the bf16 MFMA pipe (exact 3-way split, fp32-accurate) ----
-
-def gemm_split_weight(w: torch.Tensor, transpose: bool = False) -> torch.Tensor:
-    """Fragment-ordered bf16 split image of Bm = w (transpose=False, w [C, R])
-    or Bm = w^T (w [R, C]) for gemm_nt (rb_gemm_split_weight)."""
-    _check(w, "weight")
-    if w.dim() != 2 or w.stride(1) != 1:
-        raise ValueError("weight must be a 2-D row-major tensor")
-    R, C = (w.shape[0], w.shape[1]) if transpose else (w.shape[1], w.shape[0])
-    nbytes = _lib.load().rb_gemm_split_weight_bytes(C, R)
-    wf = torch.empty(nbytes // 2, device=w.device, dtype=torch.bfloat16)
-    _lib.call("rb_gemm_split_weight", w.data_ptr(), w.stride(0), C, R, int(transpose),
-              wf.data_ptr(), _stream(w))
-    return wf
-
-
 def pack_plan(item_seq: torch.Tensor, offsets: torch.Tensor, order: torch.Tensor, ntok: int):
     """rb_pack_plan: (ids [ntok], row_pos [ntok], inv [B], last [B]) of the
     packed layout (sequence s = batch row order[s] at rows offsets[s] ..
@@ -1055,48 +1018,6 @@ class _SplitJob(ctypes.Structure):
 
 
 MAX_SPLIT_JOBS = 32   # RB_MAX_SPLIT_JOBS
-
-
-def gemm_split_weights(jobs) -> None:
-    """Refresh several split images in one launch (rb_gemm_split_weights):
-    jobs = [(w, transpose, wf)], wf from gemm_split_weight's layout."""
-    jobs = list(jobs)
-    for k in range(0, len(jobs), MAX_SPLIT_JOBS):
-        chunk = jobs[k:k + MAX_SPLIT_JOBS]
-        arr = (_SplitJob * len(chunk))()
-        for d, (w, transpose, wf) in zip(arr, chunk):
-            _check(w, "weight")
-            if w.dim() != 2 or w.stride(1) != 1:
-                raise ValueError("weight must be a 2-D row-major tensor")
-            R, C = (w.shape[0], w.shape[1]) if transpose else (w.shape[1], w.shape[0])
-            if wf.numel() * 2 != C * R * 6 or wf.device != w.device:
-                raise ValueError("split image buffer does not match the weight")
-            d.W, d.ldw, d.C, d.R = w.data_ptr(), w.stride(0), C, R
-            d.transpose, d.Wf = int(transpose), wf.data_ptr()
-        _lib.call("rb_gemm_split_weights", ctypes.addressof(arr), len(chunk),
-                  _stream(chunk[0][0]))
-
-
-def gemm_nt(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None = None,
-            out: torch.Tensor | None = None, accumulate: bool = False) -> torch.Tensor:
-    """out[M, C] (+)= a[M, R] @ Bm^T (+ bias) with Bm's split image wf
-    (rb_gemm_nt).  a: 2-D, unit inner stride, row stride a multiple of 4."""
-    _check(a, "a")
-    if a.dim() != 2 or a.stride(1) != 1:
-        raise ValueError("a must be a 2-D tensor with unit inner stride")
-    M, R = a.shape
-    if out is None:
-        if accumulate:
-            raise ValueError("accumulate needs out")
-        out = torch.empty((M, C), device=a.device, dtype=torch.float32)
-    elif out.shape != (M, C) or out.stride(1) != 1:
-        raise ValueError("out must be [M, C] with unit inner stride")
-    if bias is not None:
-        _check(bias, "bias")
-    _lib.call("rb_gemm_nt", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
-              0 if bias is None else bias.data_ptr(), out.data_ptr(), out.stride(0),
-              int(accumulate), _stream(a))
-    return out
 
 
 # ---- fp16 two-part split GEMMs (csrc/gemm_half.hip) --------------------------
@@ -1392,7 +1313,7 @@ def grl_fwd(xz, conv_w, conv_b, wg_img, gate_b, lam, h0, seq: Packed, want_y=Tru
             0 if xc is None else xc.data_ptr(), 0 if rg is None else rg.data_ptr(),
             0 if carries is None else carries.data_ptr(), nT,
             0 if rmax is None else rmax.data_ptr(), _ptr(tc), seq.max_tiles if tc is not None else 0,
-            _stream(xz))
+            _stream(xz), _exp=True)
     if tc is not None:
         carries = tc
     return (y if want_y else y_last), carries, xc, rg, rmax
@@ -1435,7 +1356,7 @@ def grl_bwd(xz, conv_w, conv_b, wg_img, wgt_img, gate_b, lam, h0, seq: Packed, t
             0 if last_only else dy.data_ptr(), dy.data_ptr() if last_only else 0,
             dxz.data_ptr(), H2, drg.data_ptr(), xc.data_ptr(),
             0 if rmax is None else rmax.data_ptr(), 0 if rmax is None else rmax[nr:].data_ptr(),
-            part.data_ptr(), cpart.data_ptr(), _stream(xz))
+            part.data_ptr(), cpart.data_ptr(), _stream(xz), _exp=True)
     sums = colsum(part.view(seq.G, 4 * H)).view(4, H)
     csum = colsum(cpart)
     return (dxz, drg, xc, None if rmax is None else rmax[:nr], None if rmax is None else rmax[nr:],

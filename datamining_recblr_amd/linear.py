@@ -15,8 +15,9 @@ RECBLR_GEMM:
   f16x3  (default, csrc/gemm_half.hip): every fp32 operand scaled by an exact
          power of two and split into two fp16 parts, three products, fp32
          accumulation — error vs fp64 at or below hipBLASLt's fp32 kernels;
-  bf16x6 (csrc/gemm_split.hip): three exact bf16 parts, six products;
   torch  (or RECBLR_SPLIT_GEMM=0): hipBLASLt/rocBLAS fp32 through torch.
+(Round 1's bf16x6 kernel — three exact bf16 parts, six products — was kept
+for A/B until round 4 and is in git history.)
 Their speed does not depend on the row count, which changes every batch once
 the sequences are packed (RecBLR._forward_packed): there hipBLASLt's untuned
 heuristic picks run at 86-117 TFLOP/s.  Shapes they do not
@@ -37,10 +38,9 @@ from . import gemm_tuning, kernels
 __all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled",
            "HipLinearForward", "has_hooks", "fire_hooks"]
 
-SPLIT_MIN_ROWS = 4096
 _GEMM = os.environ.get("RECBLR_GEMM", "f16x3")
-if _GEMM not in ("f16x3", "bf16x6", "torch"):
-    raise ValueError(f"RECBLR_GEMM must be f16x3, bf16x6 or torch, got {_GEMM!r}")
+if _GEMM not in ("f16x3", "torch"):
+    raise ValueError(f"RECBLR_GEMM must be f16x3 or torch, got {_GEMM!r}")
 _split_on = os.environ.get("RECBLR_SPLIT_GEMM", "1") != "0" and _GEMM != "torch"
 _half = _GEMM == "f16x3"
 # weight gradients on the f16 pipe (rb_gemm_tn_h) when both operands' row-group
@@ -59,7 +59,7 @@ _small_tn = os.environ.get("RECBLR_SMALL_TN", "0") == "1"
 # taken anywhere (torch.optim step hook: also covers optimizers that write
 # through .data) are unchanged; the first stale lookup of a training step
 # refreshes every stale entry of that device in one launch
-# (rb_gemm_split_weights) instead of one launch per GEMM call.  Code that
+# (rb_gemm_h_split_weights) instead of one launch per GEMM call.  Code that
 # rewrites weights through .data outside torch.optim calls
 # invalidate_split_cache() (or sets RECBLR_SPLIT_CACHE=0).
 _split_cache: dict = {}
@@ -96,12 +96,11 @@ def _stamp(w: torch.Tensor):
 
 
 def _make_image(w, transpose):
-    return (kernels.gemm_h_weight(w, transpose=transpose) if _half
-            else kernels.gemm_split_weight(w, transpose=transpose))
+    return kernels.gemm_h_weight(w, transpose=transpose)
 
 
 def _weight_split(w: torch.Tensor, transpose: bool) -> torch.Tensor:
-    """The split weight image of the selected format (f16x3 or bf16x6)."""
+    """The f16 weight image of w (transpose: of w^T), cached."""
     if not _cache_on:
         return _make_image(w, transpose)
     key = (id(w), transpose)
@@ -127,7 +126,7 @@ def _weight_split(w: torch.Tensor, transpose: bool) -> torch.Tensor:
         if _stamp(ww) != ent[2] and ww.device == w.device:
             jobs.append((ww, k[1], ent[3]))
             fresh.append(ent)
-    (kernels.gemm_h_split_weights if _half else kernels.gemm_split_weights)(jobs)
+    kernels.gemm_h_split_weights(jobs)
     for ent in fresh:
         ent[2] = _stamp(ent[0]())
     return e[3]
@@ -143,15 +142,13 @@ HALF_MIN_ROWS = 1
 
 
 def _split_ok(a: torch.Tensor, C: int, R: int) -> bool:
-    min_rows = HALF_MIN_ROWS if _half else SPLIT_MIN_ROWS
-    return (_split_on and a.is_cuda and a.dim() == 2 and a.shape[0] >= max(min_rows, 1)
-            and C % (32 if _half else 128) == 0 and R % 32 == 0 and a.stride(1) == 1
-            and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0 and a.dtype == torch.float32
-            and (not _half or C <= 1024))
+    return (_split_on and _half and a.is_cuda and a.dim() == 2 and a.shape[0] >= HALF_MIN_ROWS
+            and C % 32 == 0 and R % 32 == 0 and a.stride(1) == 1 and a.stride(0) % 4 == 0
+            and a.data_ptr() % 16 == 0 and a.dtype == torch.float32 and C <= 1024)
 
 
 def gemm_format() -> str:
-    """The split GEMM format in use: 'f16x3', 'bf16x6' or 'torch'."""
+    """The split GEMM format in use: 'f16x3' or 'torch'."""
     return _GEMM if _split_on else "torch"
 
 
@@ -204,7 +201,7 @@ def _bf16_image(w: torch.Tensor, transpose: bool) -> torch.Tensor:
 
 def _bf16_ok(a: torch.Tensor, w: torch.Tensor, C: int, R: int) -> bool:
     return (_bf16_gemm and a.dtype == torch.bfloat16 and w.dtype == torch.float32 and a.is_cuda
-            and a.dim() == 2 and a.stride(1) == 1 and a.stride(0) % 8 == 0
+            and a.dim() == 2 and a.shape[0] > 0 and a.stride(1) == 1 and a.stride(0) % 8 == 0
             and a.data_ptr() % 16 == 0 and w.stride(1) == 1 and R % 64 == 0 and C % 256 == 0)
 
 
@@ -221,9 +218,7 @@ def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
         return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
     N, K = w.shape
     if _split_ok(a, N, K):
-        if _half:
-            return kernels.gemm_nt_h(a, _weight_split(w, False), N, bias=bias, rmax=rmax)
-        return kernels.gemm_nt(a, _weight_split(w, False), N, bias=bias)
+        return kernels.gemm_nt_h(a, _weight_split(w, False), N, bias=bias, rmax=rmax)
     return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
 
 
@@ -286,12 +281,9 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
         wb = w.to(dy.dtype)
         return out.addmm_(dy, wb) if out is not None else dy @ wb
     N, K = w.shape
-    if _split_ok(dy, K, N) and _half:
+    if _split_ok(dy, K, N):
         r = kernels.gemm_nt_h(dy, _weight_split(w, True), K, rmax=rmax)
         return r if out is None else out.add_(r)
-    if _split_ok(dy, K, N) and (out is None or (out.stride(1) == 1 and out.shape == (dy.shape[0], K))):
-        return kernels.gemm_nt(dy, _weight_split(w, True), K, out=out,
-                               accumulate=out is not None)
     if out is not None:
         return out.addmm_(dy, w)
     return torch.mm(dy, w)

@@ -83,3 +83,27 @@ class Adam(torch.optim.Optimizer):
                               float(group["weight_decay"]), float(bc1), float(bc2),
                               kernels._stream(chunk[0]))
         return loss
+
+
+def native_ok(params) -> bool:
+    """Whether every parameter meets rb_adam_step's requirements (contiguous
+    fp32 CUDA tensors)."""
+    return all(p.dtype == torch.float32 and p.is_cuda and p.is_contiguous() for p in params)
+
+
+def make_adam(params, lr: float = 1e-3, weight_decay: float = 0.0, kind: str | None = None):
+    """The training loop's Adam (RecBole's learner 'adam'): the native
+    one-launch Adam, or torch.optim.Adam with RECBLR_ADAM=torch (kind
+    overrides the variable).  Parameters the native kernel cannot take
+    (CPU, non-fp32 or non-contiguous) fall back to torch.optim.Adam — the
+    same semantics, checked against each other in tests/test_gpu_optim.py."""
+    import os
+
+    params = list(params)
+    kind = kind or os.environ.get("RECBLR_ADAM", "native")
+    if kind not in ("native", "torch"):
+        raise ValueError(f"RECBLR_ADAM must be native or torch, got {kind!r}")
+    if kind == "native" and native_ok(params):
+        return Adam(params, lr=lr, weight_decay=weight_decay)
+    fused = all(p.is_cuda and p.dtype == torch.float32 for p in params)
+    return torch.optim.Adam(params, lr=lr, weight_decay=weight_decay, fused=fused or None)

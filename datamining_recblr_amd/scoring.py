@@ -45,18 +45,19 @@ PROBS_SLICE_BYTES = 1 << 30
 CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
 # The backward's two products dseq = P W, ditems = P^T seq: "f16" (default:
 # P written in both layouts, both products on the f16x3 weight-gradient
-# kernel, _bwd_f16), "fused" (rb_item_ce_bwd_h, each product inside a kernel
-# that recomputes the logits, P never stored; d in {32, 64, 128}: equal step
-# time, profiles/r04_ce_bench_*.log) or "torch" (hipBLASLt fp32 on P, sliced).  An earlier f16 variant ran ditems as the NT
-# kernel on P^T: 2.2x slower (42 row tiles with K = 2048 and online row
-# scales that P^T's rows outgrow; profiles/r03_ce_grads_probe.log).
+# kernel, _bwd_f16) or "torch" (hipBLASLt fp32 on P, sliced).  Measured and
+# removed: an f16 variant running ditems as the NT kernel on P^T (2.2x
+# slower: 42 row tiles with K = 2048 and online row scales that P^T's rows
+# outgrow; profiles/r03_ce_grads_probe.log), and rb_item_ce_bwd_h (round 4:
+# each product inside a kernel that recomputes the logits, P never stored —
+# equal step time, profiles/r04_ce_bench_*.log; in git history up to round 4).
 CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "f16")
 
 
 def set_ce_grads(mode: str) -> str:
     """Set the backward's product strategy (bench A/B); returns the previous one."""
     global CE_GRADS
-    if mode not in ("fused", "f16", "torch"):
+    if mode not in ("f16", "torch"):
         raise ValueError(mode)
     prev, CE_GRADS = CE_GRADS, mode
     return prev
@@ -175,10 +176,6 @@ class _ItemCE(torch.autograd.Function):
         if CE_BACKWARD == "fused":
             dseq, dtable = kernels.item_ce_bwd(seq, table, target, lse, dloss.float(),
                                                want_seq=want_seq, want_items=want_items)
-        elif ctx.split is not None and CE_GRADS == "fused" and seq.shape[1] in (32, 64, 128):
-            s_seq, s_tab = ctx.split
-            dseq, dtable = kernels.item_ce_bwd_h(s_seq, s_tab, target, lse, dloss.float(),
-                                                 want_seq=want_seq, want_items=want_items)
         elif ctx.split is not None and _f16_grads_ok(seq, table):
             dseq, dtable = _bwd_f16(seq, table, target, lse, dloss.float(), want_seq,
                                     want_items, ctx.split)

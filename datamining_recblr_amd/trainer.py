@@ -65,9 +65,10 @@ def fit(model, data, env: DistEnv, epochs: int = 100, batch_size: int = 2048,
         log=print) -> dict:
     """Train with early stopping; returns best valid / test metrics."""
     step = wrap_ddp(model, env)
-    # RecBole's learner 'adam' (torch.optim.Adam semantics) as one native launch
-    from .optim import Adam
-    opt = Adam(model.parameters(), lr=lr, weight_decay=weight_decay)
+    # RecBole's learner 'adam' (torch.optim.Adam semantics): one native launch,
+    # or torch.optim.Adam (RECBLR_ADAM=torch, or parameters it cannot take)
+    from .optim import make_adam
+    opt = make_adam(model.parameters(), lr=lr, weight_decay=weight_decay)
     loader = SequentialLoader(data, "train", batch_size=batch_size, shuffle=True, seed=seed,
                               rank=env.rank, world=env.world_size, drop_last=env.distributed)
     best, best_state, bad, history = -1.0, None, 0, []

@@ -385,18 +385,6 @@ int rb_item_ce_probs_h_both(const void* seq_img, const int* seq_exp, const void*
                             int64_t ldt, float* row_group_max, float* item_group_max,
                             void* stream);
 
-/* The CE backward (RecBLR.py:100-102: nn.CrossEntropyLoss over the item
- * table, its input gradients) on split images with P never stored: dseq [B,
- * d] = P W and ditems [V, d] = P^T seq (either NULL to skip), P = (softmax -
- * onehot) * dloss / B, each from a kernel that recomputes the logits exactly
- * as rb_item_ce_fwd_h (bit-identical) and feeds P from its accumulators into
- * a second f16x3 product, fixed-order split partials summed in the
- * workspace (rb_item_ce_workspace).  d in {32, 64, 128}. */
-int rb_item_ce_bwd_h(const void* seq_img, const int* seq_exp, const void* item_img,
-                     const int* item_exp, const int64_t* target, const float* lse,
-                     const float* dloss, int64_t B, int64_t V, int64_t d, float* dseq,
-                     float* ditems, void* workspace, int64_t workspace_bytes, void* stream);
-
 /* out [ceil(n/32)] = max |x| over each 32-row group of x [n, c] (row stride
  * ld): rb_gemm_tn_h's operand scales for a tensor no f16 GEMM has read. */
 int rb_group_absmax(const float* x, int64_t n, int64_t c, int64_t ld, float* out, void* stream);
@@ -455,22 +443,6 @@ int rb_gate_scan_bwd_bf16(const rb_bf16* rg, int64_t rg_rs, const rb_bf16* xc, i
                           rb_bf16* dxc, int64_t dxc_rs, rb_bf16* dz, int64_t dz_rs, float* part,
                           float* dh0_part, int64_t B, int64_t L, int64_t H, const int64_t* seq_offsets, void* stream);
 
-/* ---- projection GEMMs (RecBLR.py:162,165,167,213,214: nn.Linear, fp32) ----
- * fp32 GEMMs on the bf16 MFMA pipe: every fp32 operand is split exactly into
- * three bf16 parts and the six partial products of weight >= 2^-18 are
- * accumulated in fp32 (fp32-level accuracy; csrc/gemm_split.hip).
- *
- * Bytes of the pre-split weight image of Bm [C, R]. */
-int64_t rb_gemm_split_weight_bytes(int64_t C, int64_t R);
-
-/* Split Bm into the fragment-ordered bf16 image Wf consumed by rb_gemm_nt:
- * Bm = W (transpose = 0; W [C, R], row stride ldw) or Bm = W^T (transpose = 1;
- * W [R, C]).  C % 32 == 0, R % 16 == 0; Wf 16-B aligned,
- * rb_gemm_split_weight_bytes(C, R) bytes.  Replaces the weight operand of
- * F.linear (forward: Bm = W) and of its input gradient (Bm = W^T). */
-int rb_gemm_split_weight(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
-                         void* Wf, void* stream);
-
 /* Packed-sequence plan (RecBLR.forward on RecBole's right-padded batch,
  * RecBLR.py:75, run on each sequence's first len_b positions only): item_seq
  * [B, L] int64 (row stride seq_rs), seq_offsets [B+1] and order [B] (packed
@@ -501,30 +473,8 @@ typedef struct {
 int rb_adam_step(const rb_adam_job* jobs, int64_t n, double lr, double beta1, double beta2,
                  double eps, double weight_decay, double bc1, double bc2, void* stream);
 
-/* rb_gemm_split_weight for up to RB_MAX_SPLIT_JOBS weights in one launch
- * (jobs: a HOST array of n descriptors, each with rb_gemm_split_weight's
- * arguments and constraints).  The host side refreshes every split image a
- * training step made stale (the optimizer changed the weights) at once. */
-#define RB_MAX_SPLIT_JOBS 32
-typedef struct {
-  const float* W;
-  int64_t ldw;
-  int64_t C;
-  int64_t R;
-  int64_t transpose;
-  void* Wf;
-} rb_split_job;
-int rb_gemm_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
-
-/* out[m, c] = sum_r A[m, r] Bm[c, r] (+ bias[c] if bias) (+ out[m, c] if
- * accumulate), m < M, c < C: F.linear's forward (A = x, Bm = W) and input
- * gradient (A = dy, Bm = W^T, accumulate adds a residual gradient in place).
- * A row stride lda (multiple of 4, A 16-B aligned), out row stride ldo;
- * R % 32 == 0, C % 128 == 0. */
-int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
-               const float* bias, float* out, int64_t ldo, int accumulate, void* stream);
-
-/* ---- the same GEMMs on the f16 pipe, two-part split (csrc/gemm_half.hip) ----
+/* ---- projection GEMMs (RecBLR.py:162,165,167,213,214: nn.Linear, fp32) ----
+ * fp32 GEMMs on the f16 pipe, two-part split (csrc/gemm_half.hip).
  * Every fp32 operand is scaled by an exact power of two and split into two
  * fp16 parts, x = 2^-s (x0 + x1) (22 significant bits); the three products
  * a0b0 + a0b1 + a1b0 accumulate in fp32 (error vs fp64 within a few fp32
@@ -534,12 +484,29 @@ int rb_gemm_nt(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf
  * Bytes of the f16 weight image of Bm [C, R] (two planes + C exponents). */
 int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R);
 
-/* Build the f16 weight images of up to RB_MAX_SPLIT_JOBS weights (jobs as for
- * rb_gemm_split_weights; each Wf rb_gemm_h_weight_bytes(C, R) bytes). */
+/* Build the f16 weight images of up to RB_MAX_SPLIT_JOBS weights in one
+ * launch (jobs: a HOST array of n descriptors; Bm = W (transpose = 0; W [C,
+ * R], row stride ldw) or Bm = W^T (transpose = 1; W [R, C]); C % 32 == 0,
+ * R % 16 == 0; each Wf 16-B aligned, rb_gemm_h_weight_bytes(C, R) bytes).
+ * The host side refreshes every image a training step made stale (the
+ * optimizer changed the weights) at once.  Replaces the weight operand of
+ * F.linear (forward: Bm = W) and of its input gradient (Bm = W^T). */
+#define RB_MAX_SPLIT_JOBS 32
+typedef struct {
+  const float* W;
+  int64_t ldw;
+  int64_t C;
+  int64_t R;
+  int64_t transpose;
+  void* Wf;
+} rb_split_job;
 int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
 
-/* rb_gemm_nt's contract on the f16 image (R % 32 == 0, C % 32 == 0,
- * C <= 1024; accumulate must be 0).  rmax (optional, [ceil(M/32)] floats): max |A| over each
+/* out[m, c] = sum_r A[m, r] Bm[c, r] (+ bias[c] if bias), m < M, c < C, on
+ * the f16 image Wf of Bm: F.linear's forward (A = x, Bm = W) and input
+ * gradient (A = dy, Bm = W^T).  A row stride lda (multiple of 4, A 16-B
+ * aligned), out row stride ldo; R % 32 == 0, C % 32 == 0, C <= 1024;
+ * accumulate must be 0.  rmax (optional, [ceil(M/32)] floats): max |A| over each
  * 32-row group, the operand scale of rb_gemm_tn_h on the same rows.  Replaces
  * nn.Linear's forward / input-gradient GEMM (RecBLR.py:162,165,167,213,214).
  * Whole rounds of 256-row tiles run on the persistent kernel; the rows past
@@ -584,7 +551,10 @@ int rb_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int64_t R, const v
  * ymax / xmax [ceil(M/32)]: max |dY| / |X| over each 32-row group — the rmax
  * side outputs of the rb_gemm_nt_h calls that read the same operands (the
  * operand scales).  N % 128 == 0, K % 128 == 0, splits % 8 == 0, row strides
- * multiples of 4, operands 16-B aligned. */
+ * multiples of 4, operands 16-B aligned.  A row chunk (ceil(ceil(M/splits)/32)
+ * * 32 rows) must span < 2 GiB of either operand, max(ldy, ldx) * 4 bytes per
+ * row: the kernel addresses a chunk with 32-bit offsets; pass more splits
+ * otherwise (an argument error, never a silent wrap). */
 int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
                  int64_t K, const float* ymax, const float* xmax, float* parts, int64_t splits,
                  void* stream);
@@ -625,51 +595,6 @@ int rb_gemm_tn_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx, int
  * strides and alignment.  Deterministic (fixed-order partial sums). */
 int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
                   int64_t K, float* dw, int accumulate, void* stream);
-
-/* GatedRecurrentLayer's core in one launch (RecBLR.py:182-206 between the
- * in- and out-projections), forward, packed sequences, fp32, H == 256:
- * xc = silu(causal depthwise conv(x) + b) (conv_w [H, kc], kc in 2..4),
- * rg = xc W_g^T (W_g's f16 image: rb_gemm_h_split_weights, C = 2H, R = H;
- * three fp16 products, fp32 accumulate) + gate_b, alpha / beta gates, the
- * BD-LRU scan from h0 ([H], shared; NULL = zeros) and y = silu(z) h.
- * xz [ntok, 2H] (x | z), row stride xz_rs.  pieces: int32 [3B + G + 1] =
- * each work piece's start row, length and packed sequence index (whole
- * sequences, B of them), then G + 1 offsets into the piece list, one span
- * per workgroup.  Outputs: y [ntok, H] (y_rs) or y_last [B, H] (each
- * sequence's last row, packed order) — exactly one; optional xc [ntok, H],
- * rg [ntok, 2H] (the GEMM without gate_b), carries [B, n_tiles, H] (the
- * state entering every 16-step tile: rb_gate_scan_bwd's checkpoints) and
- * xc_rmax [ceil(ntok/32)] (max |xc| per 32-row group, the caller zeroes
- * it).  tile_carries [G, max_tiles, H] (optional): the state entering each
- * of a workgroup's 64-row tiles, the checkpoints of rb_grl_bwd.  Replaces
- * the reference's conv / gates Linear / gate math / parallel_scan chain
- * (RecBLR.py:173-206, parallel_scan.py:117). */
-int rb_grl_fwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
-               const float* conv_b, const void* wg_img, const float* gate_b, const float* lam,
-               const float* h0, const int32_t* pieces, int64_t B, int64_t G, int64_t ntok,
-               int64_t H, float* y, int64_t y_rs, float* y_last, float* xc, float* rg,
-               float* carries, int64_t n_tiles, float* xc_rmax, float* tile_carries,
-               int64_t max_tiles, void* stream);
-
-/* Backward of rb_grl_fwd in one launch (autograd of RecBLR.py:182-206 and
- * parallel_scan.py:117's backward): the same pieces and 64-row tiles walked
- * in reverse; conv, gates GEMM and the forward scan recomputed from xz and
- * the forward's tile_carries; dy [ntok, H] or dy_last [B, H] (exactly one).
- * Writes dxz [ntok, 2H] (dx | dz; row stride dxz_rs), drg [ntok, 2H] (the
- * gates GEMM's output gradient), xc [ntok, H] (its input, for the weight
- * gradient drg^T xc), optional drg_rmax / xc_rmax [ceil(ntok/32)] (32-row
- * group maxima, zeroed by the caller), part [G, 4, H] (per workgroup:
- * dLambda, d gate_b r and i halves, dh0) and cpart [8G, H kc + H] (per
- * wave: d conv_w in [H, kc] order, d conv_b); column sums of part and cpart
- * are the parameter gradients.  dxc = drg W_g runs inside on W_g^T's f16
- * image (wgt_img: rb_gemm_h_split_weights of W_g^T, C = H, R = 2H). */
-int rb_grl_bwd(const float* xz, int64_t xz_rs, const float* conv_w, int64_t kc,
-               const float* conv_b, const void* wg_img, const void* wgt_img, const float* gate_b,
-               const float* lam, const float* h0, const int32_t* pieces, int64_t B, int64_t G,
-               int64_t ntok, int64_t H, const float* tile_carries, int64_t max_tiles,
-               const float* dy, const float* dy_last, float* dxz, int64_t dxz_rs, float* drg,
-               float* xc, float* drg_rmax, float* xc_rmax, float* part, float* cpart,
-               void* stream);
 
 #ifdef __cplusplus
 }

@@ -32,15 +32,14 @@ def cuda():
 
 @pytest.fixture
 def split_gemm_calls(monkeypatch):
-    """Records every launch of the split-operand GEMM of the selected format
-    (kernels.gemm_nt_h / rb_gemm_nt_h and its fused-activation variants
-    kernels.gemm_nt_h_act / gemm_nt_h_dact for f16x3, kernels.gemm_nt / rb_gemm_nt for bf16x6)
-    as (M, R, C): tests use it to assert that the path they claim
-    to check actually ran the kernel."""
+    """Records every launch of the f16x3 split-operand GEMM (kernels.gemm_nt_h
+    / rb_gemm_nt_h and its fused-activation variants kernels.gemm_nt_h_act /
+    gemm_nt_h_dact) as (M, R, C): tests use it to assert that the path they
+    claim to check actually ran the kernel."""
     from datamining_recblr_amd import kernels
 
     calls = []
-    for name in ("gemm_nt", "gemm_nt_h", "gemm_nt_h_act", "gemm_nt_h_dact"):
+    for name in ("gemm_nt_h", "gemm_nt_h_act", "gemm_nt_h_dact"):
         orig = getattr(kernels, name)
 
         def counted(a, wf, C, *args, _orig=orig, **kw):

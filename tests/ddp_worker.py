@@ -18,7 +18,6 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from datamining_recblr_amd import linear
     from datamining_recblr_amd.distributed import init_from_env, shard_range, wrap_ddp
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
@@ -26,7 +25,6 @@ def main():
 
     from datamining_recblr_amd import kernels
 
-    linear.SPLIT_MIN_ROWS = 0          # every projection through rb_gemm_nt
     tn_rows = []                       # M of every rb_gemm_tn_h launch (weight gradients)
     _tn = kernels.gemm_tn_h
 

@@ -60,11 +60,11 @@ def test_row_conv_and_batched_split_argument_errors():
 
     jobs = (kernels._SplitJob * 1)()
     jobs[0].W, jobs[0].ldw, jobs[0].C, jobs[0].R, jobs[0].transpose, jobs[0].Wf = 16, 40, 32, 40, 0, 16
-    rc = lib.rb_gemm_split_weights(ctypes.addressof(jobs), 1, None)
+    rc = lib.rb_gemm_h_split_weights(ctypes.addressof(jobs), 1, None)
     assert rc == _lib.RB_EINVAL and b"multiple of" in lib.rb_last_error_string()   # R % 16
-    rc = lib.rb_gemm_split_weights(ctypes.addressof(jobs), 0, None)
+    rc = lib.rb_gemm_h_split_weights(ctypes.addressof(jobs), 0, None)
     assert rc == _lib.RB_EINVAL
-    rc = lib.rb_gemm_split_weights(ctypes.addressof(jobs), 33, None)
+    rc = lib.rb_gemm_h_split_weights(ctypes.addressof(jobs), 33, None)
     assert rc == _lib.RB_EINVAL
 
 
@@ -103,6 +103,43 @@ def test_probe_library_is_separate_and_exports_its_header():
     # argument errors are reported without touching the GPU
     try:
         _lib.call_probe("rb_probe_gemm_pattern", None, 1, 4, None, 4, None)
+    except _lib.RecBLRNativeError as e:
+        assert "null pointer" in str(e)
+    else:
+        raise AssertionError("null pointers accepted")
+
+
+def test_tn_weight_gradient_rejects_row_chunks_of_2_gib():
+    """rb_gemm_tn_h addresses a row chunk with 32-bit offsets through a buffer
+    descriptor: a chunk spanning 2 GiB of an operand is an argument error
+    naming the limit (checked before any HIP call), never a silent wrap."""
+    lib = _lib.load()
+    M, N, K = 1 << 22, 128, 128
+    # 8 splits of 2^22 rows: 2^19-row chunks; at a 2^13-float row stride of dY
+    # a chunk spans 2^19 x 32 KiB = 16 GiB
+    rc = lib.rb_gemm_tn_h(16, 1 << 13, 16, K, M, N, K, 16, 16, 16, 8, None)
+    assert rc == _lib.RB_EINVAL and b"2 GiB" in lib.rb_last_error_string()
+
+
+def test_experimental_library_is_separate_and_exports_its_header():
+    """The opt-in fused GatedRecurrentLayer kernels (RECBLR_FUSED_GRL*) live
+    in their own library (experimental/recblr_exp.h, lib/libdmrecblr_exp.so):
+    the product library exports none of them, the experimental library
+    exactly its header's, at the product's ABI version; argument errors are
+    reported without touching the GPU."""
+    import os
+    hdr = os.path.join(os.path.dirname(_lib.__file__), "experimental", "recblr_exp.h")
+    text = re.sub(r"/\*.*?\*/", "", open(hdr).read(), flags=re.S)
+    names = re.findall(r"\b(rb_[a-z0-9_]+)\s*\(", text)
+    assert set(names) == set(_lib.EXP_SIGNATURES)
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    for n in names:
+        assert not hasattr(raw, n), n
+    exp = _lib.load_exp()
+    assert exp.rb_exp_version() == _lib.ABI_VERSION
+    try:
+        _lib.call_exp("rb_grl_fwd", *[0 if t is ctypes.c_int64 else None
+                                      for t in _lib.EXP_SIGNATURES["rb_grl_fwd"][1]])
     except _lib.RecBLRNativeError as e:
         assert "null pointer" in str(e)
     else:

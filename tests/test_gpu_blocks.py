@@ -176,8 +176,7 @@ def test_silu_dropout(cuda, mode):
 def test_fused_feed_forward(cuda, p, split_gemm_calls):
     """_FeedForward (two GEMMs, SiLU+dropout, dropout+residual+LN, folded bias
     grads, residual grad through addmm) == the reference FeedForward math.
-    M = 5000 rows: above SPLIT_MIN_ROWS, so all four fwd/dX GEMMs run the
-    split-bf16 kernel (asserted)."""
+    M = 5000 rows: all four fwd/dX GEMMs run the f16x3 kernel (asserted)."""
     from datamining_recblr_amd import kernels
     from datamining_recblr_amd.blocks import _FeedForward
 
@@ -671,3 +670,23 @@ def test_colsum_chunked_one_launch_equals_two_passes(cuda, shape):
         assert torch.equal(out.reshape(M, C), ref), it
     tickets = kernels._tickets[(x.device, _stream(x))]
     assert int(tickets.abs().sum()) == 0
+
+
+
+def test_colsum_chunked_tickets_dropped_after_a_failed_call(cuda):
+    """The tickets stay in [0, nch) (the kernel's wrapping increment) and are
+    back at 0 after every complete launch; a failed native call drops the
+    cached counters altogether (_lib.on_failure), so the next call starts
+    from fresh zeros and is exact."""
+    from datamining_recblr_amd import _lib, kernels
+    from datamining_recblr_amd.kernels import _stream
+
+    x = torch.randn(2048, 256, device=cuda)
+    ref = kernels.colsum(x).clone()
+    key = (x.device, _stream(x))
+    assert int(kernels._tickets[key].abs().sum()) == 0
+    with pytest.raises(_lib.RecBLRNativeError):
+        _lib.call("rb_colsum", 0, 1, 1, 1, 1, 1, 0, 0)
+    assert key not in kernels._tickets
+    assert torch.equal(kernels.colsum(x), ref)
+    assert int(kernels._tickets[key].abs().sum()) == 0

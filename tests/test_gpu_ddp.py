@@ -10,8 +10,7 @@ the encoder, the ResidualGrad slots whose residual gradient the producing
 LayerNorm backward adds (rb_add_ln_bwd2), the folded pad-prefix backward that adds into the conv-bias /
 gate / Lambda gradients in place, the split-weight cache invalidated by the
 optimizer-step hook (3 Adam steps), and host-staged packing.  Every
-projection runs the split GEMM (SPLIT_MIN_ROWS = 0 in the ranks and here);
-at L = 200 the weight gradients run on rb_gemm_tn_h (asserted).
+projection runs the f16x3 split GEMM; at L = 200 the weight gradients run on rb_gemm_tn_h (asserted).
 
 Bar: each step's loss and every parameter gradient equal the full-batch
 run's within 1e-5 of the tensor's max at step 0 (the only difference is the
@@ -71,7 +70,6 @@ def _run_ranks(tmp_path, GB, L, world=2):
 
 
 def _full_batch_reference(cuda, GB, L):
-    from datamining_recblr_amd import linear
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
 
@@ -79,21 +77,16 @@ def _full_batch_reference(cuda, GB, L):
     model = RecBLR(dict(CFG, MAX_ITEM_LIST_LENGTH=L), SyntheticDataset(N_ITEMS)).to(cuda).train()
     opt = torch.optim.Adam(model.parameters(), lr=1e-3, fused=True)
     rec = {}
-    old = linear.SPLIT_MIN_ROWS
-    linear.SPLIT_MIN_ROWS = 0
-    try:
-        for i, full in enumerate(batches(GB, L, N_ITEMS, STEPS)):
-            opt.zero_grad(set_to_none=True)
-            loss = model.calculate_loss(to_device(full, 0, GB, cuda))
-            loss.backward()
-            rec[f"loss.{i}"] = loss.detach().cpu().reshape(1)
-            for n, p in model.named_parameters():
-                rec[f"grad.{i}.{n}"] = p.grad.detach().cpu().clone()
-            opt.step()
+    for i, full in enumerate(batches(GB, L, N_ITEMS, STEPS)):
+        opt.zero_grad(set_to_none=True)
+        loss = model.calculate_loss(to_device(full, 0, GB, cuda))
+        loss.backward()
+        rec[f"loss.{i}"] = loss.detach().cpu().reshape(1)
         for n, p in model.named_parameters():
-            rec[f"param.{n}"] = p.detach().cpu().clone()
-    finally:
-        linear.SPLIT_MIN_ROWS = old
+            rec[f"grad.{i}.{n}"] = p.grad.detach().cpu().clone()
+        opt.step()
+    for n, p in model.named_parameters():
+        rec[f"param.{n}"] = p.detach().cpu().clone()
     return rec
 
 

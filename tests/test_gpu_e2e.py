@@ -14,9 +14,8 @@ Shapes:
   threshold, so the bench's own routing is exercised);
 * C3 (configs[2], amazon-beauty shape; the dataset is absent, synthetic
   stand-in): d = 128, L = 50, B = 2048 (train_batch_size), n_items = 10,544.
-Each runs packed (the benchmark's default) and dense, with the split
-threshold as shipped and at 0 (every projection, the gathered last-layer
-tail included, through the split kernels).  Eval mode: dropout streams differ
+Each runs packed (the benchmark's default) and dense; every projection, the
+gathered last-layer tail included, runs on the split kernels.  Eval mode: dropout streams differ
 between implementations.
 """
 import pytest
@@ -69,14 +68,9 @@ def _run(cuda, B, L, packed, gather, seed, loss_type="CE", fixed_len=False):
 
 
 @pytest.mark.parametrize("packed", [True, False], ids=["packed", "dense"])
-@pytest.mark.parametrize("threshold", ["shipped", 0])
 @pytest.mark.parametrize("B,L", [(64, 200), (2048, 50)], ids=["C2", "C3"])
 def test_train_step_matches_oracle_with_split_gemm(cuda, split_gemm_calls, monkeypatch, B, L,
-                                                   packed, threshold):
-    from datamining_recblr_amd import linear
-
-    if threshold != "shipped":
-        monkeypatch.setattr(linear, "SPLIT_MIN_ROWS", threshold)
+                                                   packed):
     from datamining_recblr_amd import kernels, recurrence
 
     fused, fused_b = [], []
@@ -99,8 +93,7 @@ def test_train_step_matches_oracle_with_split_gemm(cuda, split_gemm_calls, monke
         assert s in shapes, (s, shapes)
     assert len(fused) == 2 * on and len(fused_b) == 2 * on_b, (fused, fused_b)
     assert ((256, 512) in shapes) != on and ((512, 256) in shapes) != on_b, shapes
-    if threshold == 0:
-        assert any(c[0] == B for c in split_gemm_calls), "gathered tail not on the kernel"
+    assert any(c[0] == B for c in split_gemm_calls), "gathered tail not on the kernel"
 
 
 @pytest.mark.parametrize("fixed_len", [False, True], ids=["ragged", "fixed_len"])

@@ -1,4 +1,4 @@
-"""The fused GatedRecurrentLayer forward and backward (csrc/grl_fused.hip,
+"""The fused GatedRecurrentLayer forward and backward (experimental/grl_fused.hip,
 rb_grl_fwd / rb_grl_bwd): conv + SiLU, the behaviour-gate projection and the
 BD-LRU scan with the silu(z) merge in one launch each way (RecBLR.py:182-206),
 against the three-launch path they replace (rb_conv_silu_fwd_rows,

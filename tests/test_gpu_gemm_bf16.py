@@ -156,3 +156,38 @@ def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     assert rel(dx1, dx0) < 2e-2
     for n in g0:
         assert rel(g1[n], g0[n]) < 2e-2, n
+
+
+def test_gemm_tn_bf16_operands_above_bit_31(cuda):
+    """rb_gemm_tn_bf16 with both operands at device addresses whose bit 31 is
+    set (the descriptor base of round 4's TN fault), bitwise
+    equal to the same operands placed by the allocator."""
+    M, N, K, S = 100000, 256, 512, 16
+    g = torch.Generator(device=cuda).manual_seed(31)
+    dy0 = torch.randn(M, N, device=cuda, generator=g).to(BF)
+    x0 = torch.randn(M, K, device=cuda, generator=g).to(BF)
+    need = 2 * M * (N + K) + 1024
+    buf = torch.empty((1 << 31) + need, dtype=torch.uint8, device=cuda)
+    base = buf.data_ptr()
+    off = 0 if (base >> 31) & 1 else ((1 << 31) - (base & 0x7FFFFFFF))
+    off += (-(base + off)) % 256
+    dy = buf[off: off + 2 * M * N].view(BF).view(M, N)
+    off += 2 * M * N
+    x = buf[off: off + 2 * M * K].view(BF).view(M, K)
+    for t in (dy, x):
+        assert (t.data_ptr() >> 31) & 1 and t.data_ptr() % 16 == 0
+    dy.copy_(dy0)
+    x.copy_(x0)
+    assert torch.equal(kernels.gemm_tn_bf16(dy, x, S), kernels.gemm_tn_bf16(dy0, x0, S))
+
+
+def test_bf16_linear_with_no_rows(cuda, monkeypatch):
+    """An empty activation (M = 0) with the bf16 kernels selected returns an
+    empty output like torch's GEMM instead of reaching the kernel's shape
+    check."""
+    monkeypatch.setattr(linear, "_bf16_gemm", True)
+    w = torch.randn(1024, 256, device=cuda)
+    a = torch.empty(0, 256, device=cuda, dtype=BF)
+    assert linear.mm_nt(a, w).shape == (0, 1024)
+    dy = torch.empty(0, 1024, device=cuda, dtype=BF)
+    assert linear.mm_nn(dy, w).shape == (0, 256)

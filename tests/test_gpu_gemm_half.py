@@ -486,3 +486,48 @@ def test_few_rows_weight_gradient(cuda, M, N, K):
     kernels.gemm_tn_hs(dy, x, out=acc, accumulate=True)
     assert torch.equal(acc, base + dw)
     assert torch.equal(kernels.gemm_tn_hs(dy, x), dw)   # deterministic
+
+
+def _bit31_views(cuda, shapes):
+    """fp32 views, 16-B aligned, whose device addresses all have bit 31 set,
+    sliced from one allocation of 2 GiB + the operands (some offset of any
+    2 GiB window has its low address word at or above 2^31).  Round 4's TN
+    fault: the buffer descriptor's base went through readfirstlane's int and
+    was sign-extended into the high word for exactly such addresses."""
+    need = sum(4 * (r * c) + 256 for r, c in shapes)
+    buf = torch.empty((1 << 31) + need + 256, dtype=torch.uint8, device=cuda)
+    base = buf.data_ptr()
+    off = 0 if (base >> 31) & 1 else ((1 << 31) - (base & 0x7FFFFFFF))
+    off += (-(base + off)) % 256
+    views = []
+    for r, c in shapes:
+        v = buf[off: off + 4 * r * c].view(torch.float32).view(r, c)
+        assert (v.data_ptr() >> 31) & 1 and v.data_ptr() % 16 == 0
+        views.append(v)
+        off += 4 * r * c + ((-(4 * r * c)) % 256)
+    assert off <= buf.numel()
+    return buf, views
+
+
+@pytest.mark.parametrize("M,N,K,S", [(204632, 512, 256, 64), (5000, 128, 512, 8)])
+def test_weight_gradient_tn_operands_above_bit_31(cuda, M, N, K, S):
+    """rb_gemm_tn_h with both operands and the partials at addresses with
+    bit 31 set, against fp64 and bitwise against the same operands placed by
+    the allocator."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(31 + M)
+    dy0 = (torch.randn(M, N, generator=g) * 1e-3).to(cuda)
+    x0 = torch.randn(M, K, generator=g).to(cuda)
+    buf, (dy, x) = _bit31_views(cuda, [(M, N), (M, K)])
+    dy.copy_(dy0)
+    x.copy_(x0)
+    ymax, xmax = _row_group_max(dy0), _row_group_max(x0)
+    parts = kernels.gemm_tn_h(dy, x, ymax, xmax, S)
+    dw = kernels.colsum(parts.view(S, -1)).view(N, K)
+    ref = dy0.double().t() @ x0.double()
+    e_h = _rel_err(dw, ref)
+    assert e_h < 2e-6 and e_h < 4 * max(_rel_err(dy0.t() @ x0, ref), 1e-7), e_h
+    assert torch.equal(parts, kernels.gemm_tn_h(dy0, x0, ymax, xmax, S))
+    del buf
+

@@ -416,52 +416,3 @@ def test_item_ce_f16_grads_vs_fp64(cuda, monkeypatch, B, V, slice_bytes, on):
     (0.7 * F.cross_entropy(s2 @ w2.t(), tgt)).backward()
     normwise(s1.grad, s2.grad, 2e-5, "dseq")
     normwise(w1.grad, w2.grad, 2e-5, "ditems")
-
-
-@pytest.mark.parametrize("B,V,d", [(2048, 10544, 128), (512, 1000, 128), (300, 515, 64),
-                                   (37, 33, 32), (1, 1, 64), (130, 97, 128)])
-def test_item_ce_fused_h_grads_vs_fp64(cuda, monkeypatch, B, V, d):
-    """RECBLR_CE_GRADS=fused: both products inside kernels that recompute
-    the logits (rb_item_ce_bwd_h, P never stored) — no P buffer, no
-    weight-gradient GEMM, no library GEMM — against torch fp64 at the suite's
-    normwise 2e-5, partial tiles of both axes included."""
-    from datamining_recblr_amd import kernels, scoring
-
-    monkeypatch.setattr(scoring, "CE_GRADS", "fused")
-    seq, W, tgt = _data(B, V, d, cuda, seed=17, scale=0.5)
-    s1 = seq.clone().requires_grad_()
-    w1 = W.clone().requires_grad_()
-    with kernels.kernel_timing() as t:
-        (0.7 * scoring.item_cross_entropy(s1, w1, tgt)).backward()
-    names = {r[0] for r in t.records}
-    assert "rb_item_ce_bwd_h" in names and not any("probs" in n for n in names), names
-    s2 = seq.double().requires_grad_()
-    w2 = W.double().requires_grad_()
-    (0.7 * F.cross_entropy(s2 @ w2.t(), tgt)).backward()
-    normwise(s1.grad, s2.grad, 2e-5, "dseq")
-    normwise(w1.grad, w2.grad, 2e-5, "ditems")
-
-
-def test_item_ce_fused_h_row_scales_and_parts(cuda):
-    """Rows of seq and of the table scaled over 2^-20 .. 2^20 (the second
-    product folds each streamed row's scale into P against the largest one),
-    only one of the two gradients wanted, and bitwise determinism."""
-    from datamining_recblr_amd import kernels
-
-    B, V, d = 256, 700, 128
-    seq, W, tgt = _data(B, V, d, cuda, seed=18, scale=0.5)
-    g = torch.Generator().manual_seed(5)
-    seq = seq * torch.exp2(torch.randint(-20, 21, (B, 1), generator=g).float()).to(cuda) / 2 ** 20
-    W = W * torch.exp2(torch.randint(-20, 21, (V, 1), generator=g).float()).to(cuda) / 2 ** 20
-    ss, sw = kernels.item_split_h(seq), kernels.item_split_h(W)
-    _, lse = kernels.item_ce_fwd_h(ss, sw, tgt)
-    dl = torch.full((), 1.3, device=cuda)
-    dseq, ditems = kernels.item_ce_bwd_h(ss, sw, tgt, lse, dl)
-    logits = seq.double() @ W.double().t()
-    p = (torch.softmax(logits, 1) - F.one_hot(tgt, V).double()) * 1.3 / B
-    normwise(dseq, p @ W.double(), 2e-5, "dseq")
-    normwise(ditems, p.t() @ seq.double(), 2e-5, "ditems")
-    d1, n1 = kernels.item_ce_bwd_h(ss, sw, tgt, lse, dl, want_items=False)
-    n2, d2 = kernels.item_ce_bwd_h(ss, sw, tgt, lse, dl, want_seq=False)
-    assert n1 is None and n2 is None
-    assert torch.equal(d1, dseq) and torch.equal(d2, ditems)

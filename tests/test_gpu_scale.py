@@ -59,17 +59,11 @@ def test_c5_scan_reference_layout(cuda):
     close(x.grad, xr.grad, what="d_tokens")
 
 
-@pytest.mark.parametrize("threshold", ["shipped", 0])
 @pytest.mark.parametrize("loss_type", ["CE", "BPR"])
-def test_c1_train_step_matches_oracle(cuda, loss_type, threshold, monkeypatch, split_gemm_calls):
+def test_c1_train_step_matches_oracle(cuda, loss_type, split_gemm_calls):
     """C1-shaped step (B=128, L=50, d=64) in eval mode: loss and every
-    parameter gradient vs the oracle.  ntok ~ 3.3k is below SPLIT_MIN_ROWS;
-    with the threshold at 0 the projections whose output width is a multiple
-    of 128 run the split-bf16 kernel (asserted)."""
-    from datamining_recblr_amd import linear
-
-    if threshold != "shipped":
-        monkeypatch.setattr(linear, "SPLIT_MIN_ROWS", threshold)
+    parameter gradient vs the oracle, every projection on the f16x3 kernel
+    (asserted)."""
     from datamining_recblr_amd.distributed import synthetic_interaction
     from datamining_recblr_amd.model import RecBLR
     from datamining_recblr_amd.recbole_compat import SyntheticDataset
@@ -91,5 +85,4 @@ def test_c1_train_step_matches_oracle(cuda, loss_type, threshold, monkeypatch, s
     close(loss, ref, what="loss")
     for n, p in model.named_parameters():
         close(p.grad, params[n].grad, what=f"d{n}")
-    if threshold == 0:
-        assert len(split_gemm_calls) >= 8, split_gemm_calls
+    assert len(split_gemm_calls) >= 8, split_gemm_calls

@@ -13,7 +13,6 @@
 #include "../datamining_recblr_amd/csrc/item_scores.hip"
 #include "../datamining_recblr_amd/csrc/pad_prefix.hip"
 #include "../datamining_recblr_amd/csrc/reduce.hip"
-#include "../datamining_recblr_amd/csrc/gemm_split.hip"
 
 #include <algorithm>
 #include <cstdio>

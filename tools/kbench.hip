@@ -14,12 +14,10 @@
 #include "../datamining_recblr_amd/csrc/item_scores.hip"
 #include "../datamining_recblr_amd/csrc/pad_prefix.hip"
 #include "../datamining_recblr_amd/csrc/reduce.hip"
-#include "../datamining_recblr_amd/csrc/gemm_split.hip"
 #include "../datamining_recblr_amd/csrc/gemm_half.hip"
 #include "../datamining_recblr_amd/csrc/pack.hip"
 #include "../datamining_recblr_amd/csrc/probe.hip"
 #include "../datamining_recblr_amd/csrc/gemm_small.hip"
-#include "../datamining_recblr_amd/csrc/grl_fused.hip"
 
 #include <algorithm>
 #include <cstdio>
