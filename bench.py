@@ -180,8 +180,29 @@ def cpu_baseline(args, state_dict):
         orc.serial_scan(gates, tokens)
         st.append(time.perf_counter() - t0)
     smed = sorted(st)[1]
+    # BASELINE.md's CPU plan (ii): the whole C1 train step (configs[0]: B=128,
+    # L=50, d=64; ml-1m's 3,706 items + padding, synthetic ids)
+    cfg1 = dict(cfg, hidden_size=64, MAX_ITEM_LIST_LENGTH=50)
+    torch.manual_seed(2020)
+    m1 = RecBLR(cfg1, SyntheticDataset(3707))
+    p1 = {k: v.detach().clone().requires_grad_(v.dtype.is_floating_point)
+          for k, v in m1.state_dict().items()}
+    opt1 = torch.optim.Adam([p for p in p1.values() if p.requires_grad], lr=1e-3)
+    i1 = synthetic_interaction(128, 50, 3707, "cpu", seed=0)
+    t1s = []
+    for _ in range(4):
+        t0 = time.perf_counter()
+        opt1.zero_grad(set_to_none=True)
+        orc.calculate_loss(p1, cfg1, i1["item_id_list"], i1["item_length"], i1["item_id"],
+                           p_drop=args.dropout).backward()
+        opt1.step()
+        t1s.append(time.perf_counter() - t0)
+    c1med = sorted(t1s[1:])[1]
+    cap = os.environ.get("OMP_NUM_THREADS")
     where = (f"{threads} threads ({phys} physical cores / {logical} logical CPUs in this "
-             f"process's affinity set; OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')})")
+             f"process's affinity set; OMP_NUM_THREADS={cap}"
+             + (": the box's CPU share for a one-GPU job, which caps the thread count"
+                if cap and phys and int(cap) < phys else "") + ")")
     return {"value": round(args.cpu_sample / med, 3), "unit": "sequences/sec", "cores": threads,
             "kind": "port",
             "sample": (f"oracle (serial-scan CPU restatement of RecBLR.py + parallel_scan.py) "
@@ -189,6 +210,12 @@ def cpu_baseline(args, state_dict):
                        f"sequences, L={args.seq_len}, d={args.hidden}, n_items={args.n_items}, "
                        f"dropout {args.dropout} as the GPU step; median of 3 after 1 warm-up; "
                        f"{med:.2f} s/step on {where}"),
+            "c1_train_step": {"config": "configs[0] shape: B=128, L=50, d=64, n_items=3707 "
+                                        "(synthetic ids), CE, dropout as the GPU step",
+                              "s_per_step": round(c1med, 3),
+                              "sequences_per_sec": round(128 / c1med, 1),
+                              "note": "the whole oracle train step (fwd+bwd+Adam), median of 3 "
+                                      "after 1 warm-up, same threads"},
             "scan_fwd_only": {"shape_BCT": [B, C, T], "s": round(smed, 3),
                               "sequences_per_sec": round(B / smed, 1),
                               "note": "serial_scan (parallel_scan.py:44-60 order, no FMA), "

@@ -10,7 +10,14 @@
 // default cache policy (ldc)
 //
 // steps per lane of the row-tiled packed forward at K = 4 (tile = 4 x TC rows;
-// each tile re-fetches K-1 halo rows its predecessor loaded)
+// each tile re-fetches K-1 halo rows its predecessor loaded).  Round 5 cut
+// the halo's measured re-reads two ways, and both ran slower at the bench
+// shape (0.61-0.62 of 8 TB/s against 0.69; profiles/r05_conv_ab_*.txt):
+// a workgroup's 4 waves on 4 consecutive tiles of one channel group (PMC
+// read 1.09x the algorithmic bytes instead of 1.20x, but each workgroup reads
+// 256-B pieces of 64 rows instead of whole 1-KB rows) and a wave walking 4
+// consecutive tiles (1.12x; a quarter of the waves in flight).  The kernel
+// already streams at the 1R + 1W copy rate of these boxes (0.66-0.73).
 constexpr int kConvRowsTC = 4;
 
 namespace rb {

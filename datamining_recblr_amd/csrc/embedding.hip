@@ -309,33 +309,48 @@ __device__ void emb_offsets(const int* __restrict__ tot, int V, int* __restrict_
   }
 }
 
-// One thread per key: cnt[t][v] becomes the exclusive prefix over the
-// blocks (in block order), tot[v] the key's count; the lanes of a wave read
-// and write 64 consecutive keys per block, 16 blocks in flight.  The last
-// workgroup to finish (arrival ticket, zeroed by k_emb_hist) then runs
-// emb_offsets over all keys.
+// cnt[t][v] becomes the exclusive prefix over the blocks (in block order),
+// tot[v] the key's count.  64 keys per 1024-thread workgroup: thread (key j =
+// tid & 63, block group q = tid >> 6) loads its key's counts of blocks
+// 16q .. 16q + 15 (a wave reads 64 consecutive keys of one block per load,
+// all 16 loads in flight), the 16 group totals of each key are combined
+// through LDS in block order, then every thread writes its prefixes.  (Round
+// 4's form, one thread per key walking all 256 blocks, ran on V / 1024 = 11
+// workgroups: 63 us at the bench's V = 10,544.)  The last workgroup to finish
+// (arrival ticket, zeroed by k_emb_hist) then runs emb_offsets over all keys.
+constexpr int kKeysPerWg = 64;
+constexpr int kKeyGroups = 1024 / kKeysPerWg;            // 16
+constexpr int kBlocksPerGroup = kPlanBlocks / kKeyGroups; // 16
+static_assert(kKeyGroups * kBlocksPerGroup == kPlanBlocks, "block groups cover the blocks");
 __global__ void __launch_bounds__(1024) k_emb_keys(int* __restrict__ cnt, int V,
                                                    int* __restrict__ tot, int* __restrict__ seg,
                                                    int* __restrict__ nch, int* __restrict__ choff,
                                                    int4* __restrict__ desc,
                                                    unsigned* __restrict__ ticket) {
   __shared__ int ts[kPlanMaxKeys];
+  __shared__ int gsum[kKeyGroups][kKeysPerWg];
   __shared__ int sh[32];
   __shared__ int s_last;
-  const int v = blockIdx.x * 1024 + threadIdx.x;
+  const int j = threadIdx.x & (kKeysPerWg - 1), q = threadIdx.x / kKeysPerWg;
+  const int v = blockIdx.x * kKeysPerWg + j;
+  const int t0 = q * kBlocksPerGroup;
+  int c[kBlocksPerGroup];
+  int s = 0;
+#pragma unroll
+  for (int t = 0; t < kBlocksPerGroup; ++t) c[t] = v < V ? cnt[(int64_t)(t0 + t) * V + v] : 0;
+#pragma unroll
+  for (int t = 0; t < kBlocksPerGroup; ++t) s += c[t];
+  gsum[q][j] = s;
+  __syncthreads();
+  int carry = 0;
+  for (int g = 0; g < q; ++g) carry += gsum[g][j];
   if (v < V) {
-    int carry = 0;
-    for (int t0 = 0; t0 < kPlanBlocks; t0 += 16) {
-      int c[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) c[q] = cnt[(int64_t)(t0 + q) * V + v];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        cnt[(int64_t)(t0 + q) * V + v] = carry;
-        carry += c[q];
-      }
+    for (int t = 0; t < kBlocksPerGroup; ++t) {
+      cnt[(int64_t)(t0 + t) * V + v] = carry;
+      carry += c[t];
     }
-    tot[v] = carry;
+    if (q == kKeyGroups - 1) tot[v] = carry;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains
   __syncthreads();
@@ -360,7 +375,12 @@ __global__ void __launch_bounds__(1024) k_emb_keys(int* __restrict__ cnt, int V,
 // + the key's positions in earlier blocks + its earlier positions in this
 // block; inside a 64-row step the lanes with equal keys are found from
 // ballots over the key bits, and each key's running count stays in LDS
-// across the block's steps.
+// across the block's steps.  The global loads are batched kPlaceSteps steps
+// at a time (the ids, then seg[k] and cnt[t][k] of all of them in flight) so
+// only the LDS ranking runs step by step: round 4's form waited for two
+// dependent global loads per 64-row step (119 us for the bench's 800-row
+// blocks, latency-bound at one wave per block).
+constexpr int kPlaceSteps = 8;
 __global__ void __launch_bounds__(64) k_emb_place(const int64_t* __restrict__ idx, int64_t M,
                                                   int V, int bits, int64_t per,
                                                   const int* __restrict__ seg,
@@ -372,24 +392,35 @@ __global__ void __launch_bounds__(64) k_emb_place(const int64_t* __restrict__ id
   __syncthreads();
   const int64_t beg = (int64_t)blockIdx.x * per, end = min(M, beg + per);
   const uint64_t lt = (uint64_t(1) << lane) - 1;
-  for (int64_t r0 = beg; r0 < end; r0 += 64) {
-    const int64_t i = r0 + lane;
-    const int64_t kk = i < end ? idx[i] : -1;
-    const bool ok = kk >= 0 && kk < V;
-    const int k = ok ? (int)kk : 0;
-    uint64_t same = __builtin_amdgcn_ballot_w64(ok);
-    for (int b = 0; b < bits; ++b) {
-      const bool bit = (k >> b) & 1;
-      const uint64_t m = __builtin_amdgcn_ballot_w64(ok && bit);
-      same &= bit ? m : ~m;
+  const int* crow = cnt + (int64_t)blockIdx.x * V;
+  for (int64_t r0 = beg; r0 < end; r0 += 64 * kPlaceSteps) {
+    int k[kPlaceSteps], base[kPlaceSteps];
+    bool ok[kPlaceSteps];
+#pragma unroll
+    for (int st = 0; st < kPlaceSteps; ++st) {
+      const int64_t i = r0 + st * 64 + lane;
+      const int64_t kk = i < end ? idx[i] : -1;
+      ok[st] = kk >= 0 && kk < V;
+      k[st] = ok[st] ? (int)kk : 0;
     }
-    if (ok) {
-      const int before = run[k];
-      const int64_t slot = (int64_t)seg[k] + cnt[(int64_t)blockIdx.x * V + k] + before +
-                           __popcll(same & lt);
-      if (slot < M) vals[slot] = (int)i;   // always (the slots are a permutation)
-      // the group's lowest lane advances the key's count (groups: distinct keys)
-      if ((same & lt) == 0) run[k] = before + __popcll(same);
+#pragma unroll
+    for (int st = 0; st < kPlaceSteps; ++st) base[st] = seg[k[st]] + crow[k[st]];
+#pragma unroll
+    for (int st = 0; st < kPlaceSteps; ++st) {
+      if (r0 + st * 64 >= end) break;   // wave-uniform
+      uint64_t same = __builtin_amdgcn_ballot_w64(ok[st]);
+      for (int b = 0; b < bits; ++b) {
+        const bool bit = (k[st] >> b) & 1;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(ok[st] && bit);
+        same &= bit ? m : ~m;
+      }
+      if (ok[st]) {
+        const int before = run[k[st]];
+        const int64_t slot = (int64_t)base[st] + before + __popcll(same & lt);
+        if (slot < M) vals[slot] = (int)(r0 + st * 64 + lane);   // always (a permutation)
+        // the group's lowest lane advances the key's count (groups: distinct keys)
+        if ((same & lt) == 0) run[k[st]] = before + __popcll(same);
+      }
     }
   }
 }
@@ -499,7 +530,7 @@ int launch_embedding_plan(const int64_t* idx, int64_t M, int64_t d, int64_t V, v
     const int64_t per = (M + kPlanBlocks - 1) / kPlanBlocks;
     hipLaunchKernelGGL(k_emb_hist, dim3(kPlanBlocks), dim3(1024), 0, st, idx, M, (int)V, per, cnt,
                        ticket);
-    hipLaunchKernelGGL(k_emb_keys, dim3((unsigned)((V + 1023) / 1024)), dim3(1024), 0, st, cnt,
+    hipLaunchKernelGGL(k_emb_keys, dim3((unsigned)((V + kKeysPerWg - 1) / kKeysPerWg)), dim3(1024), 0, st, cnt,
                        (int)V, tot, seg, nch, choff, reinterpret_cast<int4*>(ws + w.desc), ticket);
     hipLaunchKernelGGL(k_emb_place, dim3(kPlanBlocks), dim3(64), 0, st, idx, M, (int)V,
                        key_bits(V), per, seg, cnt, vals_out);

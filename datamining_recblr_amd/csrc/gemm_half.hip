@@ -119,17 +119,41 @@ __global__ void __launch_bounds__(256) k_split_weights_h(const SplitJobsH jobs) 
   auto bm = [&](int c, int r) -> float {
     return tr ? W[(int64_t)r * ldw + c] : W[(int64_t)c * ldw + r];
   };
-  {
+  // column maxima: 8 threads per column, consecutive threads on consecutive
+  // addresses (W^T: 32 columns are one 128-B row piece; W: each column is a
+  // row of W, read as float4 runs), four independent loads in flight
+  const bool vec = (reinterpret_cast<uintptr_t>(W) & 15) == 0 && (ldw & 3) == 0;
+  if (tr || !vec) {
     const int c = cb * 32 + (tid & 31);
-    float m = 0.0f;
-    for (int r = tid >> 5; r < R; r += 8) m = fmaxf(m, fabsf(bm(c, r)));
-    smax[tid] = m;
+    float m0 = 0.0f, m1 = 0.0f;
+    int r = tid >> 5;
+    for (; r + 8 < R; r += 16) {
+      m0 = fmaxf(m0, fabsf(bm(c, r)));
+      m1 = fmaxf(m1, fabsf(bm(c, r + 8)));
+    }
+    if (r < R) m0 = fmaxf(m0, fabsf(bm(c, r)));
+    smax[(tid & 31) * 8 + (tid >> 5)] = fmaxf(m0, m1);
+  } else {
+    const int cl = tid >> 3, c = cb * 32 + cl;
+    const float* row = W + (int64_t)c * ldw;
+    float m0 = 0.0f, m1 = 0.0f;
+    for (int r = (tid & 7) * 4; r < R; r += 64) {   // R % 16 == 0: whole float4 runs
+      const f32x4 a = *reinterpret_cast<const f32x4*>(row + r);
+      m0 = fmaxf(m0, fmaxf(fabsf(a[0]), fabsf(a[1])));
+      m1 = fmaxf(m1, fmaxf(fabsf(a[2]), fabsf(a[3])));
+      if (r + 32 < R) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(row + r + 32);
+        m0 = fmaxf(m0, fmaxf(fabsf(b[0]), fabsf(b[1])));
+        m1 = fmaxf(m1, fmaxf(fabsf(b[2]), fabsf(b[3])));
+      }
+    }
+    smax[cl * 8 + (tid & 7)] = fmaxf(m0, m1);
   }
   __syncthreads();
   if (tid < 32) {
-    float m = smax[tid];
+    float m = smax[tid * 8];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) m = fmaxf(m, smax[tid + 32 * q]);
+    for (int q = 1; q < 8; ++q) m = fmaxf(m, smax[tid * 8 + q]);
     const int e = m > 0.0f ? __builtin_amdgcn_frexp_expf(m) : 0;
     sexp[tid] = e;
     int* ew = reinterpret_cast<int*>(reinterpret_cast<char*>(jobs.Wf[j]) + (int64_t)C * R * 4);

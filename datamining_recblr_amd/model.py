@@ -59,8 +59,8 @@ class _PinnedRing:
         if buf is None or buf.numel() < n or buf.dtype != host.dtype:
             buf = self.bufs[i] = torch.empty(max(n, 4096), dtype=host.dtype, pin_memory=True)
             self.events[i] = None
-        if self.events[i] is not None:
-            self.events[i].synchronize()
+        if self.events[i] is not None and not torch.cuda.is_current_stream_capturing():
+            self.events[i].synchronize()   # (under graph capture: no host sync allowed)
         buf[:n].copy_(host)
         # the copy and its event on the TARGET device's current stream (the
         # current device may be another one)

@@ -531,3 +531,29 @@ def test_weight_gradient_tn_operands_above_bit_31(cuda, M, N, K, S):
     assert torch.equal(parts, kernels.gemm_tn_h(dy0, x0, ymax, xmax, S))
     del buf
 
+
+
+@pytest.mark.parametrize("C,R", [(512, 128), (128, 512), (256, 48), (96, 16)])
+def test_weight_image_strided_views_and_column_exponents(cuda, C, R):
+    """rb_gemm_h_split_weights reads W along its rows (float4 runs when W is
+    16-B aligned with ldw % 4 == 0, scalar loads otherwise): a row-strided
+    view (ldw = R + 1) and a misaligned one give the image of the contiguous
+    copy bit for bit, and the column exponents are frexp of each column's
+    max |Bm| (both orientations)."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(C + R)
+    base = (torch.randn(C, R + 1, generator=g) *
+            torch.exp2(torch.randint(-30, 30, (C, 1), generator=g).float())).to(cuda)
+    wv = base[:, :R]                 # ldw = R + 1
+    wm = base[:, 1:]                 # ldw = R + 1, 4-B offset: not 16-B aligned
+    for w in (wv, wm):
+        ref = kernels.gemm_h_weight(w.contiguous())
+        assert torch.equal(kernels.gemm_h_weight(w).view(torch.int16), ref.view(torch.int16))
+        e = ref.view(torch.int32)[C * R:C * R + C]
+        m = w.abs().amax(1)
+        assert torch.equal(e.cpu(), torch.frexp(m.cpu())[1].to(torch.int32))
+    bt = torch.randn(R, C + 1, generator=g).to(cuda)[:, :C]   # W [R, C], ldw = C + 1
+    wt = kernels.gemm_h_weight(bt, transpose=True)             # Bm = W^T
+    assert torch.equal(wt.view(torch.int16),
+                       kernels.gemm_h_weight(bt.t().contiguous()).view(torch.int16))
