@@ -599,8 +599,8 @@ int rb_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int64_t 
                       int64_t chunk_rows, float* part, uint32_t* counters, int64_t n_counters,
                       float* out, void* stream) {
   if (!in || !out || !part || !counters) return fail("rb_colsum_chunked: null pointer");
-  if (M <= 0 || P <= 0 || C <= 0 || rs < C || chunk_rows <= 0 || chunk_rows > 256 ||
-      P % chunk_rows)
+  if (M <= 0 || P <= 0 || C <= 0 || rs < C ||
+      (chunk_rows != 64 && chunk_rows != 128 && chunk_rows != 256) || P % chunk_rows)
     return fail("rb_colsum_chunked: bad shape, stride or chunk size");
   const int64_t cblocks = (C + 63) / 64;
   if (n_counters < M * cblocks) return fail("rb_colsum_chunked: too few counters");

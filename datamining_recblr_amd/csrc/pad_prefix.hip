@@ -61,6 +61,7 @@ __device__ __forceinline__ float pad_gate(const float* __restrict__ conv_b,
                                           const float* __restrict__ gb, int H, int o, int lane) {
   const float* w = gw + (int64_t)o * H;
   float acc = 0.0f;
+#pragma unroll 4   // H = 256: all four loads of the row in flight at once
   for (int k = lane; k < H; k += 64) acc = fmaf(w[k], silu_f(conv_b[k]), acc);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
@@ -137,6 +138,7 @@ __global__ __launch_bounds__(256) void k_pad_prefix_bwd1(
   di = __shfl(di, 0);
   float* wr = dgw + (int64_t)c * H;
   float* wi = dgw + (int64_t)(H + c) * H;
+#pragma unroll 4
   for (int kk = lane; kk < H; kk += 64) {
     const float x = silu_f(conv_b[kk]);
     const float vr = dr * x, vi = di * x;
@@ -156,8 +158,22 @@ __global__ __launch_bounds__(1024) void k_pad_prefix_bwd3(const float* __restric
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float acc = 0.0f;
-  if (c < H)
-    for (int o = ty; o < 2 * H; o += 16) acc = fmaf(gw[(int64_t)o * H + c], drg[o], acc);
+  if (c < H) {
+    // 8 rows' loads in flight per batch (a dependent chain of 2H / 16 = 32
+    // load round trips before), the fma order unchanged
+    int o = ty;
+    for (; o + 7 * 16 < 2 * H; o += 8 * 16) {
+      float w[8], g[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        w[q] = gw[(int64_t)(o + 16 * q) * H + c];
+        g[q] = drg[o + 16 * q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc = fmaf(w[q], g[q], acc);
+    }
+    for (; o < 2 * H; o += 16) acc = fmaf(gw[(int64_t)o * H + c], drg[o], acc);
+  }
   red[ty][tx] = acc;
   __syncthreads();
   if (ty == 0 && c < H) {

@@ -89,12 +89,15 @@ __global__ __launch_bounds__(64 * RG) void k_colsum4(const float* __restrict__ i
 // the last arriver acquires before reading (cdna_hip_programming.md §6
 // Guideline 16, the counter form) and resets its ticket for the next call
 // (the tickets are zeroed once when the caller allocates them).
-template <int RG>
+template <int RG, int CH>
 __global__ __launch_bounds__(64 * RG) void k_colsum_2l(const float* __restrict__ in, int64_t C,
                                                        int64_t rs, int64_t cblocks, int nch,
-                                                       int CH, float* __restrict__ part,
+                                                       float* __restrict__ part,
                                                        unsigned* __restrict__ cnt,
                                                        float* __restrict__ out) {
+  constexpr int NL = CH / RG;   // rows per thread, all loads in flight at once (one
+                                // round trip: a runtime chunk size left the compiler
+                                // four dependent batches of four, ~8-13 us per call)
   __shared__ float red[RG][64];
   __shared__ int s_last;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -107,13 +110,11 @@ __global__ __launch_bounds__(64 * RG) void k_colsum_2l(const float* __restrict__
     const float* base = in + ((m * nch + ch) * (int64_t)CH) * rs + c;
     float s = 0.0f;
     if (c < C) {
-      int p = ty;
-      for (; p + 3 * RG < CH; p += 4 * RG) {
-        const float a = base[p * rs], q = base[(p + RG) * rs];
-        const float d = base[(p + 2 * RG) * rs], e = base[(p + 3 * RG) * rs];
-        s = (((s + a) + q) + d) + e;
-      }
-      for (; p < CH; p += RG) s += base[p * rs];
+      float v[NL];
+#pragma unroll
+      for (int i = 0; i < NL; ++i) v[i] = base[(int64_t)(ty + i * RG) * rs];
+#pragma unroll
+      for (int i = 0; i < NL; ++i) s += v[i];   // increasing p: k_colsum<RG>'s order
     }
     red[ty][tx] = s;
     __syncthreads();
@@ -147,10 +148,12 @@ __global__ __launch_bounds__(64 * RG) void k_colsum_2l(const float* __restrict__
   float s = 0.0f;
   if (c < C) {
     int p = ty;
-    for (; p + 3 * RG < nch; p += 4 * RG) {
-      const float a = base[(int64_t)p * C], q = base[(int64_t)(p + RG) * C];
-      const float d = base[(int64_t)(p + 2 * RG) * C], e = base[(int64_t)(p + 3 * RG) * C];
-      s = (((s + a) + q) + d) + e;
+    for (; p + 7 * RG < nch; p += 8 * RG) {   // 8 independent loads in flight, order kept
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = base[(int64_t)(p + i * RG) * C];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s += v[i];
     }
     for (; p < nch; p += RG) s += base[(int64_t)p * C];
   }
@@ -245,8 +248,23 @@ int launch_colsum_chunked(const float* in, int64_t M, int64_t P, int64_t C, int6
                           float* part, unsigned* cnt, float* out, hipStream_t st) {
   const int64_t cblocks = (C + 63) / 64;
   const int nch = (int)(P / CH);
-  hipLaunchKernelGGL(k_colsum_2l<4>, dim3((unsigned)(M * cblocks * nch)), dim3(256), 0, st, in, C,
-                     rs, cblocks, nch, CH, part, cnt, out);
+  const dim3 grid((unsigned)(M * cblocks * nch));
+  switch (CH) {
+    case 64:
+      hipLaunchKernelGGL((k_colsum_2l<4, 64>), grid, dim3(256), 0, st, in, C, rs, cblocks, nch,
+                         part, cnt, out);
+      break;
+    case 128:
+      hipLaunchKernelGGL((k_colsum_2l<4, 128>), grid, dim3(256), 0, st, in, C, rs, cblocks, nch,
+                         part, cnt, out);
+      break;
+    case 256:
+      hipLaunchKernelGGL((k_colsum_2l<4, 256>), grid, dim3(256), 0, st, in, C, rs, cblocks, nch,
+                         part, cnt, out);
+      break;
+    default:
+      return fail("rb_colsum_chunked: chunk_rows must be 64, 128 or 256");
+  }
   return launch_status("rb_colsum_chunked");
 }
 

@@ -287,7 +287,7 @@ int rb_colsum(const float* in, int64_t M, int64_t P, int64_t C, int64_t rs, int6
 
 /* rb_colsum for few columns and many rows in one launch: the rows of each of
  * the M matrices (contiguous: matrix m starts at in + m*P*rs) are summed in
- * chunks of `chunk_rows` (P % chunk_rows == 0, chunk_rows <= 256), each chunk
+ * chunks of `chunk_rows` (64, 128 or 256; P % chunk_rows == 0), each chunk
  * as rb_colsum(P = chunk_rows) does, then the chunk sums as
  * rb_colsum(P = P / chunk_rows) does — bitwise the two-launch result.  part:
  * [M, P / chunk_rows, C] fp32 workspace; counters: M * ceil(C / 64) uint32
