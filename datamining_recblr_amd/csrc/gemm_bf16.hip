@@ -113,7 +113,14 @@ constexpr int BF_LDS = BF_NSA * BF_A_STAGE + 2 * BF_B_STAGE;    // 160 KB
 // one row tile are neighbouring workgroups of one XCD (same blockIdx % 8), so
 // their A re-reads hit that XCD's L2.  A tile's results are rounded and
 // stored at its end; the next k-step's wait counts them (they drain during
-// that k-step, behind its MFMAs).
+// that k-step, behind its MFMAs).  The MFMAs take the weight fragment as
+// their first operand (round 5), so each accumulator block holds the tile
+// transposed: lane l owns one row (l % 32) and four groups of four
+// consecutive columns; after packing to bf16, v_permlane32_swap of group
+// pairs gives each lane 8 consecutive columns, one 16-B store — half the
+// store instructions of the quad-transposed 8-B stores, no DPP transposes
+// (cdna_hip_programming.md T21): 5-21% per shape at configs[4]
+// (profiles/r05_bfswap_shapes.txt).
 template <bool BIAS>
 __global__ void __launch_bounds__(BF_THREADS, 1)
 k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
@@ -217,9 +224,9 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
     // own DMAs A(u), B(u) landed; younger than B(u): A(u + 1) (4, when it
     // exists) and the 32 stores at the end of step u - 1 (a whole tile's)
     if (u + 1 < U) {
-      if (stored_prev) bwait_vm<36>(); else bwait_vm<4>();
+      if (stored_prev) bwait_vm<20>(); else bwait_vm<4>();
     } else {
-      if (stored_prev) bwait_vm<32>(); else bwait_vm<0>();
+      if (stored_prev) bwait_vm<16>(); else bwait_vm<0>();
     }
     bbarrier();
     if (u + 1 < U) issueB((u + 1) & 1);
@@ -245,8 +252,10 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
       constexpr int p = decltype(P_)::value;
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        acc[0][cb] = mfma_bf(fa[p][0], fb[p][cb], acc[0][cb]);
-        acc[1][cb] = mfma_bf(fa[p][1], fb[p][cb], acc[1][cb]);
+        // swapped operands: acc holds the block transposed (lane: one row,
+        // registers: 4 groups of 4 consecutive columns)
+        acc[0][cb] = mfma_bf(fb[p][cb], fa[p][0], acc[0][cb]);
+        acc[1][cb] = mfma_bf(fb[p][cb], fa[p][1], acc[1][cb]);
       }
     };
     using I0 = std::integral_constant<int, 0>;
@@ -277,28 +286,44 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
       tile_of(i, mt, ct);
       const bool full = (int64_t)mt * BF_BM + BF_BM <= M;
       if (mt < m_tiles) {
+        // lane l holds row 64 wm + 32 rb + l % 32 of the tile, columns
+        // 8g + 4h .. 8g + 4h + 3 of each 32-column block in registers 4g..4g+3
+        // (h = l / 32); bf16 pairs packed, then v_permlane32_swap of groups
+        // (g, g + 1): lanes 0-31 hold columns 8g .. 8g + 7, lanes 32-63
+        // 8g + 8 .. 8g + 15 -> one 16-B store per group pair
+        const int h = lane >> 5;
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-          const int col = ct * BF_BN + wn * 128 + cb * 32 + (lane & 28);
-          const f32x4 b4 = BIAS ? *reinterpret_cast<const f32x4*>(bias + col) : f32x4{0, 0, 0, 0};
+          const int colb = ct * BF_BN + wn * 128 + cb * 32;
 #pragma unroll
           for (int rb = 0; rb < 2; ++rb) {
-            const int64_t rbase = (int64_t)mt * BF_BM + wm * 64 + rb * 32 + 4 * (lane >> 5) + (lane & 3);
+            const int64_t row = (int64_t)mt * BF_BM + wm * 64 + rb * 32 + (lane & 31);
+            uint32_t pk[4][2];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-              float v[4];
+              const int c0 = colb + 8 * g + 4 * h;
+              const f32x4 b4 = BIAS ? *reinterpret_cast<const f32x4*>(bias + c0) : f32x4{0, 0, 0, 0};
+              const f32x4 x = {acc[rb][cb][4 * g] + b4[0], acc[rb][cb][4 * g + 1] + b4[1],
+                               acc[rb][cb][4 * g + 2] + b4[2], acc[rb][cb][4 * g + 3] + b4[3]};
+              const u32x2 w = __builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4));
+              pk[g][0] = w[0];
+              pk[g][1] = w[1];
+            }
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][4 * g + r];
-              quad_t(v, lane);
-              const f32x4 x = {v[0] + b4[0], v[1] + b4[1], v[2] + b4[2], v[3] + b4[3]};
-              const int64_t row = rbase + 8 * g;
+            for (int g = 0; g < 4; g += 2) {
+#pragma unroll
+              for (int q = 0; q < 2; ++q) {
+                const auto r = __builtin_amdgcn_permlane32_swap(pk[g][q], pk[g + 1][q], false, false);
+                pk[g][q] = r[0];
+                pk[g + 1][q] = r[1];
+              }
               if (full || row < M)
-                *reinterpret_cast<u32x2*>(out + row * ldo + col) =
-                    __builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4));
+                *reinterpret_cast<uint4*>(out + row * ldo + colb + 8 * g + 8 * h) =
+                    make_uint4(pk[g][0], pk[g][1], pk[g + 1][0], pk[g + 1][1]);
             }
           }
         }
-        stored_prev = full;   // 32 stores issued (partial tiles: fewer, not counted)
+        stored_prev = full;   // 16 stores issued (partial tiles: fewer, not counted)
       }
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)

@@ -50,6 +50,18 @@ def short(name):
     return n.split("(")[0]
 
 
+def modes(vals, tol=0.03):
+    """[{"bytes": mean, "launches": n}] of the values grouped within tol."""
+    out = []
+    for v in sorted(vals):
+        if out and abs(v - out[-1]["_ref"]) <= tol * max(out[-1]["_ref"], 1.0):
+            out[-1]["_sum"] += v
+            out[-1]["launches"] += 1
+        else:
+            out.append({"_ref": v, "_sum": v, "launches": 1})
+    return [{"bytes": round(m["_sum"] / m["launches"]), "launches": m["launches"]} for m in out]
+
+
 def main():
     fdir, wdir = sys.argv[1], sys.argv[2]
     fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
@@ -93,6 +105,11 @@ def main():
         k = res["kernels"][short(name)]
         if k["fetch_bytes"] is not None and k["write_bytes"] is not None:
             k["traffic_bytes"] = k["fetch_bytes"] + k["write_bytes"]
+        # launches of one kernel that move different byte counts at the same
+        # grid (e.g. the LayerNorm forward in gather mode vs with a residual):
+        # the distinct per-launch values, clustered within 3%, with counts
+        k["fetch_modes"] = modes([v * 1024 * (cal_read or 1) for v in fsel])
+        k["write_modes"] = modes([v * 1024 * (cal_write or 1) for v in wsel])
     json.dump(res, sys.stdout, indent=1)
     print()
 
