@@ -733,8 +733,8 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
 int rb_gemm_bf16_weight_image(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
                               void* img, void* stream) {
   if (!W || !img) return fail("rb_gemm_bf16_weight_image: null pointer");
-  if (C <= 0 || R <= 0 || C % 32 || R % 16 || C > 65536 || R > 65536)
-    return fail("rb_gemm_bf16_weight_image: C % 32 == 0 and R % 16 == 0 required (<= 65536)");
+  if (C <= 0 || R <= 0 || C % 16 || R % 32 || C > 65536 || R > 65536)
+    return fail("rb_gemm_bf16_weight_image: C % 16 == 0 and R % 32 == 0 required (<= 65536)");
   if (ldw < (transpose ? C : R)) return fail("rb_gemm_bf16_weight_image: bad row stride");
   if (!aligned16(img)) return fail("rb_gemm_bf16_weight_image: img must be 16-byte aligned");
   return launch_bf16_weight_image(W, ldw, (int)C, (int)R, transpose ? 1 : 0, img,
@@ -747,11 +747,10 @@ int rb_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int64_t R, const void
   if (M <= 0 || R <= 0 || C <= 0) return fail("rb_gemm_nt_bf16: empty shape");
   if (R % 64 || C % 256 || R > 16384 || C > 65536)
     return fail("rb_gemm_nt_bf16: R % 64 == 0 (<= 16384) and C % 256 == 0 required");
-  if (lda < R || lda % 8 || lda > (1 << 20) || ldo < C || ldo % 4)
-    return fail("rb_gemm_nt_bf16: bad row strides (lda % 8 == 0, ldo % 4 == 0)");
-  if (!aligned16(A) || !aligned16(img) || (reinterpret_cast<uintptr_t>(out) & 7) ||
-      (bias && !aligned16(bias)))
-    return fail("rb_gemm_nt_bf16: A, img and bias must be 16-byte aligned, out 8-byte aligned");
+  if (lda < R || lda % 8 || lda > (1 << 20) || ldo < C || ldo % 8)
+    return fail("rb_gemm_nt_bf16: bad row strides (lda % 8 == 0, ldo % 8 == 0)");
+  if (!aligned16(A) || !aligned16(img) || !aligned16(out) || (bias && !aligned16(bias)))
+    return fail("rb_gemm_nt_bf16: A, img, out and bias must be 16-byte aligned");
   if ((M + 255) / 256 > 0x7fffffffLL / (C / 256) / 2) return fail("rb_gemm_nt_bf16: too many tiles");
   return launch_gemm_nt_bf16(A, lda, M, (int)R, img, (int)C, bias, out, ldo,
                              reinterpret_cast<hipStream_t>(stream));

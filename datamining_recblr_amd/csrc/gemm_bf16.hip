@@ -1,21 +1,23 @@
 // gemm_bf16.hip — the projections of bf16 activations (BASELINE configs[4]:
-// L = 2,048, d = 256, H = 512, 2M rows per step) on the bf16 MFMA pipe: one
-// v_mfma_f32_32x32x16_bf16 per fragment pair, fp32 accumulation.
+// L = 2,048, d = 256, H = 512, 2M rows per step) on the bf16 MFMA pipe
+// (NT: v_mfma_f32_16x16x32_bf16, TN: 32x32x16), fp32 accumulation.
 //
 // rb_gemm_nt_bf16: out[M, C] = A[M, R] . Bm[C, R]^T (+ bias[C]), bf16 out
 //   nn.Linear's forward (Bm = W) and input gradient (Bm = W^T) on bf16
 //   activations (RecBLR.py:162,165,167 and their autograd).  Bm is the fp32
 //   weight rounded to bf16 once per call, in MFMA fragment order
-//   (rb_gemm_bf16_weight_image: fragment (column block cb, k16 block kb) =
-//   64 lanes x 16 B, lane l: column 32 cb + l % 32, k 16 kb + 8 (l / 32) ..
-//   + 7), so a k-step's weight slice is a run of contiguous 1 KB DMAs from L2.
+//   (rb_gemm_bf16_weight_image: fragment (16-column block cb, k32 block kb)
+//   = 64 lanes x 16 B, lane l: column 16 cb + l % 16, k 32 kb + 8 (l / 16)
+//   .. + 7), so a k-step's weight slice is a run of contiguous 1 KB DMAs
+//   from L2.
 //   The bias is added in fp32 before the one rounding to bf16.
 // rb_gemm_tn_bf16: part[s][N, K] = dY[chunk_s]^T . X[chunk_s], fp32
 //   The weight gradients of the same Linears over row chunks; the fixed-order
 //   column sum (rb_colsum) adds the partials.
 //
 // Both: one 512-thread workgroup per CU, 256 x 256 output tiles, waves 4 x 2
-// owning 64 x 128 each (2 x 4 blocks of 32 x 32), every operand global -> LDS
+// owning 64 x 128 each (NT: 4 x 8 blocks of 16 x 16, TN: 2 x 4 blocks of
+// 32 x 32), every operand global -> LDS
 // by LDS-DMA, the next k-step issued right after the barrier that frees its
 // slot.  LDS: the NT kernel 160 KB, all of a gfx950 CU (3 A stages, A two
 // k-steps ahead, + 2 weight stages); the TN kernel 128 KB (2 stages of both
@@ -38,6 +40,9 @@ typedef __attribute__((address_space(3))) fp16x4_t* lds_h4_ptr;
 
 __device__ __forceinline__ f32x16 mfma_bf(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_bf16x16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
 template <typename T>
@@ -83,17 +88,19 @@ __device__ __forceinline__ void quad_t(float (&v)[4], int lane) {
 
 // ---------------------------------------------------------------------------
 // weight image: Bm[c][k] = W[c * ldw + k] (transpose = 0) or W[k * ldw + c]
-// (transpose = 1: Bm = W^T), rounded to bf16, fragment order
+// (transpose = 1: Bm = W^T), rounded to bf16, in 16x16x32 fragment order:
+// fragment (16-column block cb, k32 block kb) = 64 lanes x 16 B, lane l:
+// column 16 cb + l % 16, k 32 kb + 8 (l / 16) .. + 7
 __global__ void __launch_bounds__(256) k_bf16_weight_image(const float* __restrict__ W, int64_t ldw,
                                                            int C, int R, int transpose,
                                                            bf16x8* __restrict__ img) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int KB = R / 16;
-  if (t >= (int64_t)(C / 32) * KB * 64) return;
+  const int KB = R / 32;
+  if (t >= (int64_t)(C / 16) * KB * 64) return;
   const int lane = (int)(t & 63);
   const int64_t fi = t >> 6;
   const int cb = (int)(fi / KB), kb = (int)(fi % KB);
-  const int c = cb * 32 + (lane & 31), k0 = kb * 16 + 8 * (lane >> 5);
+  const int c = cb * 16 + (lane & 15), k0 = kb * 32 + 8 * (lane >> 4);
   bf16x8 o;
 #pragma unroll
   for (int j = 0; j < 8; ++j)
@@ -113,14 +120,13 @@ constexpr int BF_LDS = BF_NSA * BF_A_STAGE + 2 * BF_B_STAGE;    // 160 KB
 // one row tile are neighbouring workgroups of one XCD (same blockIdx % 8), so
 // their A re-reads hit that XCD's L2.  A tile's results are rounded and
 // stored at its end; the next k-step's wait counts them (they drain during
-// that k-step, behind its MFMAs).  The MFMAs take the weight fragment as
-// their first operand (round 5), so each accumulator block holds the tile
-// transposed: lane l owns one row (l % 32) and four groups of four
-// consecutive columns; after packing to bf16, v_permlane32_swap of group
-// pairs gives each lane 8 consecutive columns, one 16-B store — half the
-// store instructions of the quad-transposed 8-B stores, no DPP transposes
-// (cdna_hip_programming.md T21): 5-21% per shape at configs[4]
-// (profiles/r05_bfswap_shapes.txt).
+// that k-step, behind its MFMAs).  v_mfma_f32_16x16x32_bf16 blocks (round 5:
+// the chip holds a higher clock under them than under 32x32x16 at equal
+// cycles per FLOP, MI355X_MICROARCH.md DVFS item 7), the weight fragment as
+// the first operand, so each accumulator block holds the tile transposed:
+// lane l owns one row (l % 16) and 4 consecutive columns 4 (l / 16) ..;
+// after packing to bf16, v_permlane16_swap of block pairs gives each lane 8
+// consecutive columns, one 16-B store (cdna_hip_programming.md T21).
 template <bool BIAS>
 __global__ void __launch_bounds__(BF_THREADS, 1)
 k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
@@ -131,7 +137,7 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nct = C / BF_BN, KT = R / BF_BK, KB16 = R / 16;
+  const int nct = C / BF_BN, KT = R / BF_BK, KB32 = R / 32;
   const int n_tiles = ((m_tiles + 7) >> 3) * 8 * nct;
   const int G = gridDim.x, bid = blockIdx.x;
   const int my_tiles = bid < n_tiles ? (n_tiles - 1 - bid) / G + 1 : 0;
@@ -147,7 +153,8 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   // ---- DMA of one k-step into stage `slot`.  A image: 128-B rows, 16-B
   // chunk c of row r at chunk c ^ ((r >> 1) & 7) (conflict-free fragment
   // reads); wave w moves rows 32w .. 32w + 31 (4 x 8 rows).  B image:
-  // fragment (cb, s) at (4 cb + s) KB; wave w moves column block w.
+  // fragment (16-column block j, k32 half s) at (2 j + s) KB; wave w moves
+  // blocks 2w, 2w + 1.
   int d_i = 0, d_kt = 0, d_mt, d_ct, a_slot = 0;
   const char* d_base = nullptr;   // the wave's first row of the tile (uniform)
   uint32_t d_off[4];              // + 32-bit lane offsets (rows past M repeat row M - 1)
@@ -184,37 +191,37 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   tile_of(0, b_mt, b_ct);
   auto issueB = [&](int slot) {
     char* sb = smem + BF_NSA * BF_A_STAGE + slot * BF_B_STAGE + wave * 4096;
-    const bf16x8* ws = Wf + ((int64_t)(b_ct * 8 + wave) * KB16 + b_kt * 4) * 64 + lane;
+    const bf16x8* ws = Wf + ((int64_t)(b_ct * 16 + 2 * wave) * KB32 + b_kt * 2) * 64 + lane;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
-      __builtin_amdgcn_global_load_lds((const void*)(ws + q * 64), (lds_ptr_t)(sb + q * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(ws + ((q >> 1) * KB32 + (q & 1)) * 64),
+                                       (lds_ptr_t)(sb + q * 1024), 16, 0, 0);
     if (++b_kt == KT) {
       b_kt = 0;
       if (++b_i < my_tiles) tile_of(b_i, b_mt, b_ct);
     }
   };
 
-  f32x16 acc[2][4];
+  // wave tile 64 rows x 128 columns = 4 x 8 blocks of 16 x 16
+  f32x4 acc[4][8];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[m][n][e] = 0.0f;
+    for (int n = 0; n < 8; ++n) acc[m][n] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
 
   const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  // A fragment (rows 64 wm + 32 rb + lane % 32, k 16 s + 8 (lane / 32) ..):
-  // logical chunk 2s + lane / 32 of its row
-  // ((2s + h) ^ sw) << 4 = ((h ^ sw) << 4) ^ (s << 5): one register per rb
-  uint32_t a_off[2];
+  // A fragment (rows 64 wm + 16 rb + lane % 16, k 32 s + 8 (lane / 16) ..):
+  // logical chunk 4s + lane / 16 of its row;
+  // ((4s + h) ^ sw) << 4 = ((h ^ sw) << 4) ^ (s << 6): one register per rb
+  uint32_t a_off[4];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb) {
-    const int row = wm * 64 + rb * 32 + (lane & 31);
-    a_off[rb] = row * 128 + (((lane >> 5) ^ ((row >> 1) & 7)) << 4);
+  for (int rb = 0; rb < 4; ++rb) {
+    const int row = wm * 64 + rb * 16 + (lane & 15);
+    a_off[rb] = row * 128 + (((lane >> 4) ^ ((row >> 1) & 7)) << 4);
   }
 
   // issue order: A(0), B(0), A(1); then in step u: B(u + 1), A(u + 2); a
-  // tile's 32 result stores (per wave) follow its last step's MFMAs
+  // tile's 16 result stores (per wave) follow its last step's MFMAs
   issueA();
   issueB(0);
   if (U > 1) issueA();
@@ -222,7 +229,7 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   bool stored_prev = false;
   for (int u = 0; u < U; ++u) {
     // own DMAs A(u), B(u) landed; younger than B(u): A(u + 1) (4, when it
-    // exists) and the 32 stores at the end of step u - 1 (a whole tile's)
+    // exists) and the 16 stores at the end of step u - 1 (a whole tile's)
     if (u + 1 < U) {
       if (stored_prev) bwait_vm<20>(); else bwait_vm<4>();
     } else {
@@ -236,101 +243,87 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
     const uint32_t sb =
         smem_base + BF_NSA * BF_A_STAGE + (u & 1) * BF_B_STAGE + wn * 16384 + lane * 16;
     stored_prev = false;
-    // fragments double-buffered: substep s + 1's six reads are in flight
-    // during substep s's eight MFMAs
-    bf16x8 fa[2][2], fb[2][4];
-    auto load = [&](auto S_, auto P_) {
-      constexpr int s = decltype(S_)::value, p = decltype(P_)::value;
-      fa[p][0] = bds_read16<bf16x8>(sa + (a_off[0] ^ (s << 5)));
-      fa[p][1] = bds_read16<bf16x8>(sa + (a_off[1] ^ (s << 5)));
-      fb[p][0] = bds_read16o<(0 + s) * 1024, bf16x8>(sb);
-      fb[p][1] = bds_read16o<(4 + s) * 1024, bf16x8>(sb);
-      fb[p][2] = bds_read16o<(8 + s) * 1024, bf16x8>(sb);
-      fb[p][3] = bds_read16o<(12 + s) * 1024, bf16x8>(sb);
-    };
-    auto mma = [&](auto P_) {
-      constexpr int p = decltype(P_)::value;
+    // two k32 halves; the second half's 12 reads are in flight during the
+    // first half's 32 MFMAs
+    bf16x8 fa[2][4], fb[2][8];
+    auto load = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
 #pragma unroll
-      for (int cb = 0; cb < 4; ++cb) {
-        // swapped operands: acc holds the block transposed (lane: one row,
-        // registers: 4 groups of 4 consecutive columns)
-        acc[0][cb] = mfma_bf(fb[p][cb], fa[p][0], acc[0][cb]);
-        acc[1][cb] = mfma_bf(fb[p][cb], fa[p][1], acc[1][cb]);
-      }
+      for (int rb = 0; rb < 4; ++rb) fa[s][rb] = bds_read16<bf16x8>(sa + (a_off[rb] ^ (s << 6)));
+      fb[s][0] = bds_read16o<(0 + s) * 1024, bf16x8>(sb);
+      fb[s][1] = bds_read16o<(2 + s) * 1024, bf16x8>(sb);
+      fb[s][2] = bds_read16o<(4 + s) * 1024, bf16x8>(sb);
+      fb[s][3] = bds_read16o<(6 + s) * 1024, bf16x8>(sb);
+      fb[s][4] = bds_read16o<(8 + s) * 1024, bf16x8>(sb);
+      fb[s][5] = bds_read16o<(10 + s) * 1024, bf16x8>(sb);
+      fb[s][6] = bds_read16o<(12 + s) * 1024, bf16x8>(sb);
+      fb[s][7] = bds_read16o<(14 + s) * 1024, bf16x8>(sb);
+    };
+    auto mma = [&](auto S_) {
+      constexpr int s = decltype(S_)::value;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[rb][j] = mfma_bf16x16(fb[s][j], fa[s][rb], acc[rb][j]);
     };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    load(I0{}, I0{});
-    load(I1{}, I1{});
-    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fb[0][0]),
-                 "+v"(fb[0][1]), "+v"(fb[0][2]), "+v"(fb[0][3]));
+    load(I0{});
+    load(I1{});
+    asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fa[0][2]),
+                 "+v"(fa[0][3]), "+v"(fb[0][0]), "+v"(fb[0][1]), "+v"(fb[0][2]), "+v"(fb[0][3]),
+                 "+v"(fb[0][4]), "+v"(fb[0][5]), "+v"(fb[0][6]), "+v"(fb[0][7]));
     mma(I0{});
-    load(I2{}, I0{});
-    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[1][0]),
-                 "+v"(fb[1][1]), "+v"(fb[1][2]), "+v"(fb[1][3]));
-    mma(I1{});
-    load(I3{}, I1{});
-    asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(fa[0][0]), "+v"(fa[0][1]), "+v"(fb[0][0]),
-                 "+v"(fb[0][1]), "+v"(fb[0][2]), "+v"(fb[0][3]));
-    mma(I0{});
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fb[1][0]),
-                 "+v"(fb[1][1]), "+v"(fb[1][2]), "+v"(fb[1][3]));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(fa[1][0]), "+v"(fa[1][1]), "+v"(fa[1][2]),
+                 "+v"(fa[1][3]), "+v"(fb[1][0]), "+v"(fb[1][1]), "+v"(fb[1][2]), "+v"(fb[1][3]),
+                 "+v"(fb[1][4]), "+v"(fb[1][5]), "+v"(fb[1][6]), "+v"(fb[1][7]));
     mma(I1{});
 
     if (kt == KT - 1) {
-      // the tile's results: + bias in fp32, one rounding to bf16, quad
-      // transposes (a lane: 4 consecutive columns of one row), 8-B stores
+      // the tile's results: + bias in fp32, one rounding to bf16, 16-B stores
       int mt, ct;
       tile_of(i, mt, ct);
       const bool full = (int64_t)mt * BF_BM + BF_BM <= M;
       if (mt < m_tiles) {
-        // lane l holds row 64 wm + 32 rb + l % 32 of the tile, columns
-        // 8g + 4h .. 8g + 4h + 3 of each 32-column block in registers 4g..4g+3
-        // (h = l / 32); bf16 pairs packed, then v_permlane32_swap of groups
-        // (g, g + 1): lanes 0-31 hold columns 8g .. 8g + 7, lanes 32-63
-        // 8g + 8 .. 8g + 15 -> one 16-B store per group pair
-        const int h = lane >> 5;
+        // lane l holds row 64 wm + 16 rb + l % 16 of the tile, columns
+        // 4g .. 4g + 3 (g = l / 16) of each 16-column block; bf16 pairs
+        // packed, then v_permlane16_swap of blocks (j, j + 1): 16-lane rows
+        // g = 0, 2 hold columns 8 (g / 2) .. + 7 of block j, rows g = 1, 3
+        // those of block j + 1 -> one 16-B store per block pair
+        const int g = lane >> 4;
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) {
-          const int colb = ct * BF_BN + wn * 128 + cb * 32;
+        for (int rb = 0; rb < 4; ++rb) {
+          const int64_t row = (int64_t)mt * BF_BM + wm * 64 + rb * 16 + (lane & 15);
 #pragma unroll
-          for (int rb = 0; rb < 2; ++rb) {
-            const int64_t row = (int64_t)mt * BF_BM + wm * 64 + rb * 32 + (lane & 31);
-            uint32_t pk[4][2];
+          for (int j = 0; j < 8; j += 2) {
+            const int colj = ct * BF_BN + wn * 128 + 16 * j;
+            uint32_t pk[2][2];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int c0 = colb + 8 * g + 4 * h;
+            for (int jj = 0; jj < 2; ++jj) {
+              const int c0 = colj + 16 * jj + 4 * g;
               const f32x4 b4 = BIAS ? *reinterpret_cast<const f32x4*>(bias + c0) : f32x4{0, 0, 0, 0};
-              const f32x4 x = {acc[rb][cb][4 * g] + b4[0], acc[rb][cb][4 * g + 1] + b4[1],
-                               acc[rb][cb][4 * g + 2] + b4[2], acc[rb][cb][4 * g + 3] + b4[3]};
+              const f32x4 x = acc[rb][j + jj] + b4;
               const u32x2 w = __builtin_bit_cast(u32x2, __builtin_convertvector(x, bf16x4));
-              pk[g][0] = w[0];
-              pk[g][1] = w[1];
+              pk[jj][0] = w[0];
+              pk[jj][1] = w[1];
             }
 #pragma unroll
-            for (int g = 0; g < 4; g += 2) {
-#pragma unroll
-              for (int q = 0; q < 2; ++q) {
-                const auto r = __builtin_amdgcn_permlane32_swap(pk[g][q], pk[g + 1][q], false, false);
-                pk[g][q] = r[0];
-                pk[g + 1][q] = r[1];
-              }
-              if (full || row < M)
-                *reinterpret_cast<uint4*>(out + row * ldo + colb + 8 * g + 8 * h) =
-                    make_uint4(pk[g][0], pk[g][1], pk[g + 1][0], pk[g + 1][1]);
+            for (int q = 0; q < 2; ++q) {
+              const auto r = __builtin_amdgcn_permlane16_swap(pk[0][q], pk[1][q], false, false);
+              pk[0][q] = r[0];
+              pk[1][q] = r[1];
             }
+            if (full || row < M)
+              *reinterpret_cast<uint4*>(out + row * ldo + colj + 16 * (g & 1) + 8 * (g >> 1)) =
+                  make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
           }
         }
         stored_prev = full;   // 16 stores issued (partial tiles: fewer, not counted)
       }
 #pragma unroll
-      for (int rb = 0; rb < 2; ++rb)
+      for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[rb][cb][e] = 0.0f;
+        for (int j = 0; j < 8; ++j) acc[rb][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       kt = 0;
       ++i;
     } else {
@@ -475,7 +468,7 @@ bool set_lds(F* f, int bytes) {
 
 int launch_bf16_weight_image(const float* W, int64_t ldw, int C, int R, int transpose, void* img,
                              hipStream_t st) {
-  const int64_t total = (int64_t)(C / 32) * (R / 16) * 64;
+  const int64_t total = (int64_t)(C / 16) * (R / 32) * 64;
   k_bf16_weight_image<<<(unsigned)((total + 255) / 256), 256, 0, st>>>(W, ldw, C, R, transpose,
                                                                        (bf16x8*)img);
   return launch_status("rb_gemm_bf16_weight_image");

@@ -561,21 +561,23 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
 
 /* ---- bf16 activations (BASELINE configs[4]: L = 2048, d = 256) ----------
  * The same Linears (RecBLR.py:162,165,167 and their autograd) when the
- * activations are bf16: bf16 operands on v_mfma_f32_32x32x16_bf16, fp32
- * accumulation (csrc/gemm_bf16.hip).  Replace torch.addmm / mm / bmm on
+ * activations are bf16: bf16 operands on the bf16 MFMA pipe (NT:
+ * v_mfma_f32_16x16x32_bf16, TN: 32x32x16), fp32 accumulation
+ * (csrc/gemm_bf16.hip).  Replace torch.addmm / mm / bmm on
  * bf16 tensors (hipBLASLt).
  *
  * The weight image: Bm [C, R] = W (transpose = 0; W row stride ldw) or W^T
- * (transpose = 1), rounded to bf16 (nearest even) in MFMA fragment order;
- * img holds C * R bf16 (2 C R bytes, 16-byte aligned); C % 32 == 0,
- * R % 16 == 0. */
+ * (transpose = 1), rounded to bf16 (nearest even) in 16x16x32 fragment
+ * order (fragment (16-column block cb, k32 block kb) = 64 lanes x 8 bf16,
+ * lane l: column 16 cb + l % 16, k 32 kb + 8 (l / 16) ..); img holds C * R
+ * bf16 (2 C R bytes, 16-byte aligned); C % 16 == 0, R % 32 == 0. */
 int rb_gemm_bf16_weight_image(const float* W, int64_t ldw, int64_t C, int64_t R, int transpose,
                               void* img, void* stream);
 
 /* out[M, C] (bf16, row stride ldo) = A[M, R] (bf16, row stride lda) . Bm^T
  * (+ bias[C], fp32, added before the one rounding to bf16).  R % 64 == 0,
- * C % 256 == 0, lda % 8 == 0, ldo % 4 == 0; A, img, bias 16-byte aligned,
- * out 8-byte aligned. */
+ * C % 256 == 0, lda % 8 == 0, ldo % 8 == 0; A, img, out, bias 16-byte
+ * aligned (16-B result stores). */
 int rb_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int64_t R, const void* img, int64_t C,
                     const float* bias, void* out, int64_t ldo, void* stream);
 

@@ -65,20 +65,20 @@ def test_gemm_nt_bf16_transposed_image(cuda):
 
 
 def test_bf16_weight_image_layout(cuda):
-    """Fragment (cb, kb), lane l: column 32 cb + l % 32, k 16 kb + 8 (l / 32) + j."""
+    """Fragment (cb, kb), lane l: column 16 cb + l % 16, k 32 kb + 8 (l / 16) + j."""
     C, R = 64, 96
     w = torch.arange(C * R, device=cuda, dtype=torch.float32).view(C, R) / 64.0
-    img = kernels.bf16_weight_image(w).view(C // 32, R // 16, 64, 8).cpu()
+    img = kernels.bf16_weight_image(w).view(C // 16, R // 32, 64, 8).cpu()
     wb = w.to(BF).cpu()
-    for cb in range(C // 32):
-        for kb in range(R // 16):
-            for lane in (0, 5, 31, 32, 63):
-                c, k0 = 32 * cb + lane % 32, 16 * kb + 8 * (lane // 32)
+    for cb in range(C // 16):
+        for kb in range(R // 32):
+            for lane in (0, 5, 15, 16, 31, 47, 63):
+                c, k0 = 16 * cb + lane % 16, 32 * kb + 8 * (lane // 16)
                 assert torch.equal(img[cb, kb, lane], wb[c, k0:k0 + 8])
-    imt = kernels.bf16_weight_image(w, transpose=True).view(R // 32, C // 16, 64, 8).cpu()
-    # Bm = w^T: fragment (cb=1, kb=2), lane 33: column 32 + 1 of Bm = w's
-    # column 33, k = 32 + 8 .. + 7 = w's rows 40 .. 47
-    assert torch.equal(imt[1, 2, 33], wb[40:48, 33])
+    imt = kernels.bf16_weight_image(w, transpose=True).view(R // 16, C // 32, 64, 8).cpu()
+    # Bm = w^T: fragment (cb=2, kb=1), lane 37: column 32 + 5 of Bm = w's
+    # column 37, k = 32 + 16 .. + 7 = w's rows 48 .. 55
+    assert torch.equal(imt[2, 1, 37], wb[48:56, 37])
 
 
 @pytest.mark.parametrize("M,N,K,S", [
