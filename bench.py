@@ -381,9 +381,10 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
     projections) forward + backward on synthetic input; sequences/s over all
     ranks (weak scaling, max-over-ranks time).  The HBM fraction is that of
     the bf16 conv + gate-scan kernels (algorithmic bytes 20*N*2 per step,
-    N = B*L*H).  The projections run on torch's bf16 GEMMs (hipBLASLt) unless
-    RECBLR_BF16_GEMM=1 (rb_gemm_nt_bf16 / rb_gemm_tn_bf16, measured slower);
-    projection_gemms_ab times both."""
+    N = B*L*H).  The projections run per shape on our bf16 kernels
+    (rb_gemm_nt_bf16 / rb_gemm_tn_bf16) or torch's bf16 GEMMs (hipBLASLt):
+    RECBLR_BF16_GEMM=auto (default: ours where faster), 1 (ours on all nine),
+    0 (hipBLASLt on all nine); projection_gemms_ab times the three."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     B, L, d = args.c5_batch, 2048, 256
@@ -414,9 +415,10 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
     # vs torch's bf16 GEMMs (hipBLASLt), alternated, best of 2 per variant
     from datamining_recblr_amd import linear as _lin
     saved_g = _lin.set_bf16_gemm(_lin._bf16_gemm)
-    runs = {"own_bf16_kernels": [], "torch_hipblaslt": []}
+    arms = (("per_shape_auto", "auto"), ("own_bf16_kernels", "1"), ("torch_hipblaslt", "0"))
+    runs = {name: [] for name, _ in arms}
     for _ in range(2):
-        for name, on in (("own_bf16_kernels", True), ("torch_hipblaslt", False)):
+        for name, on in arms:
             _lin.set_bf16_gemm(on)
             one()
             torch.cuda.synchronize()
@@ -430,7 +432,7 @@ def long_seq_c5(args, env, dev, steps=3, warmup=1):
                                     / steps, 3))
     _lin.set_bf16_gemm(saved_g)
     gemm_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
-    gemm_ab["headline"] = "own_bf16_kernels" if saved_g else "torch_hipblaslt"
+    gemm_ab["headline"] = {m: n for n, m in arms}[saved_g]
     path = [summ[n] for n in ("rb_conv_silu_fwd_bf16", "rb_conv_silu_bwd_bf16",
                               "rb_gate_scan_fwd_bf16", "rb_gate_scan_bwd_bf16") if n in summ]
     pb, pms = sum(p["bytes"] for p in path), sum(p["ms"] for p in path)

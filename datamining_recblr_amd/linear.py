@@ -166,22 +166,35 @@ def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
     return None
 
 
-# bf16 activations (BASELINE configs[4]): RECBLR_BF16_GEMM=1 runs the
-# projections on our bf16 MFMA kernels (csrc/gemm_bf16.hip), tested; the
-# weight gradient at parity, the NT kernel 5-23% slower per shape than torch's
-# bf16 GEMMs (hipBLASLt), which stay the default (configs[4] step 23.9 vs
-# 22.1 ms; profiles/r04_bf5_shapes.txt).  The
-# weight's bf16 fragment images (W for the forward, W^T for the input
+# bf16 activations (BASELINE configs[4]): the projections on our bf16 MFMA
+# kernels (csrc/gemm_bf16.hip) or torch's bf16 GEMMs (hipBLASLt), per shape.
+# RECBLR_BF16_GEMM:
+#   "auto" (default) — ours where they measured faster at configs[4]: the
+#     NT kernel for R <= 512 inputs (the three forward GEMMs and out's input
+#     gradient: 4-9% faster than hipBLASLt) and the weight-gradient kernel
+#     for N <= 512 (out.dW); hipBLASLt for the K = 1024 input gradients of
+#     the in / gates projections (7-14% faster there) and the N = 1024 weight
+#     gradients (profiles/r05_bfmid_shapes.txt);
+#   "1" — ours on every shape; "0" — hipBLASLt on every shape.
+# The weight's bf16 fragment images (W for the forward, W^T for the input
 # gradient) are cached per weight version like the split images.
-_bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "0") == "1"
+BF16_NT_MAX_R = 512
+BF16_TN_MAX_N = 512
+_BF16_MODES = ("auto", "1", "0")
+_bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "auto")
+if _bf16_gemm not in _BF16_MODES:
+    raise ValueError(f"RECBLR_BF16_GEMM must be one of {_BF16_MODES}, got {_bf16_gemm!r}")
 _bf16_cache: dict = {}
 
 
-def set_bf16_gemm(on: bool) -> bool:
-    """Switch the bf16 projection kernels (A/B in bench.py); returns the
-    previous setting."""
+def set_bf16_gemm(mode) -> str:
+    """Switch the bf16 projection kernels (A/B in bench.py): "auto", "1"
+    (True) or "0" (False); returns the previous mode."""
     global _bf16_gemm
-    prev, _bf16_gemm = _bf16_gemm, bool(on)
+    m = {True: "1", False: "0"}.get(mode, mode) if isinstance(mode, bool) else str(mode)
+    if m not in _BF16_MODES:
+        raise ValueError(f"bf16 GEMM mode must be one of {_BF16_MODES}, got {mode!r}")
+    prev, _bf16_gemm = _bf16_gemm, m
     return prev
 
 
@@ -200,7 +213,8 @@ def _bf16_image(w: torch.Tensor, transpose: bool) -> torch.Tensor:
 
 
 def _bf16_ok(a: torch.Tensor, w: torch.Tensor, C: int, R: int) -> bool:
-    return (_bf16_gemm and a.dtype == torch.bfloat16 and w.dtype == torch.float32 and a.is_cuda
+    return (_bf16_gemm != "0" and (_bf16_gemm == "1" or R <= BF16_NT_MAX_R)
+            and a.dtype == torch.bfloat16 and w.dtype == torch.float32 and a.is_cuda
             and a.dim() == 2 and a.shape[0] > 0 and a.stride(1) == 1 and a.stride(0) % 8 == 0
             and a.data_ptr() % 16 == 0 and w.stride(1) == 1 and R % 64 == 0 and C % 256 == 0)
 
@@ -335,7 +349,8 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
             S = max(8, min(S, M // 32 // 8 * 8))
         parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
         return kernels.colsum(parts.view(S, -1)).view(N, K)
-    if (_bf16_gemm and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
+    if (_bf16_gemm != "0" and (_bf16_gemm == "1" or N <= BF16_TN_MAX_N)
+            and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
             and M >= TN_BF16_MIN_ROWS and N % 256 == 0 and K % 256 == 0
             and dy2.stride(1) == 1 and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0
             and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0):

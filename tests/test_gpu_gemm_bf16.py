@@ -108,9 +108,10 @@ def test_gemm_tn_bf16_vs_fp64(cuda, M, N, K, S):
 
 def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     """configs[4]'s GatedRecurrentLayer (d = 256, L = 2048) with
-    RECBLR_BF16_GEMM on runs all three projections' forward, input-gradient and
-    weight-gradient GEMMs on the bf16 kernels, and agrees with the hipBLASLt
-    path (the default) to bf16 accuracy."""
+    RECBLR_BF16_GEMM=1 runs all three projections' forward, input-gradient and
+    weight-gradient GEMMs on the bf16 kernels, the default per-shape mode
+    (auto) five of the nine, and both agree with the hipBLASLt path
+    (RECBLR_BF16_GEMM=0) to bf16 accuracy."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     calls = {"nt": 0, "tn": 0}
@@ -148,14 +149,22 @@ def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     assert calls == {"nt": 6, "tn": 3}, calls
     y0, dx0, g0 = run(False)
     assert calls == {"nt": 6, "tn": 3}
+    # the default per-shape mode: ours for the R <= 512 NT GEMMs (in / gates /
+    # out forward, out's input gradient) and the N <= 512 weight gradient
+    # (out.dW); hipBLASLt for in.dX, gates.dX, in.dW, gates.dW
+    ya, dxa, ga = run("auto")
+    assert calls == {"nt": 10, "tn": 4}, calls
 
     def rel(a, b):
         return ((a - b).abs().max() / b.abs().max()).item()
 
     assert rel(y1, y0) < 2e-2
     assert rel(dx1, dx0) < 2e-2
+    assert rel(ya, y0) < 2e-2
+    assert rel(dxa, dx0) < 2e-2
     for n in g0:
         assert rel(g1[n], g0[n]) < 2e-2, n
+        assert rel(ga[n], g0[n]) < 2e-2, n
 
 
 def test_gemm_tn_bf16_operands_above_bit_31(cuda):
@@ -185,7 +194,7 @@ def test_bf16_linear_with_no_rows(cuda, monkeypatch):
     """An empty activation (M = 0) with the bf16 kernels selected returns an
     empty output like torch's GEMM instead of reaching the kernel's shape
     check."""
-    monkeypatch.setattr(linear, "_bf16_gemm", True)
+    monkeypatch.setattr(linear, "_bf16_gemm", "1")
     w = torch.randn(1024, 256, device=cuda)
     a = torch.empty(0, 256, device=cuda, dtype=BF)
     assert linear.mm_nt(a, w).shape == (0, 1024)

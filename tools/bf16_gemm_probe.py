@@ -40,6 +40,14 @@ def main(M=2097152):
         fl, by = 2 * M * R * C, 2 * M * (R + C)
         print(f"NT {name:10s} R={R:5d} C={C:5d}: own {t_own:7.3f} ms ({fl / t_own / 1e9:6.0f} TF/s, "
               f"{by / t_own / 1e6:6.0f} GB/s)  torch {t_ref:7.3f} ms", flush=True)
+        if name.endswith(".fwd"):
+            b = torch.randn(C, device=dev, generator=g)
+            bb = b.to(torch.bfloat16)
+            t_own = med(lambda: kernels.gemm_nt_bf16(a, img, C, bias=b))
+            t_ref = med(lambda: torch.addmm(bb, a, wb.t()))
+            print(f"NT {name + '+b':10s} R={R:5d} C={C:5d}: own {t_own:7.3f} ms "
+                  f"({fl / t_own / 1e9:6.0f} TF/s, {by / t_own / 1e6:6.0f} GB/s)  torch {t_ref:7.3f} ms",
+                  flush=True)
         del a
     tn = {"in.dW": (2 * H, d), "gates.dW": (2 * H, H), "out.dW": (d, H)}
     for name, (N, K) in tn.items():
