@@ -4,9 +4,11 @@ bench.py: every launch in issue order with its duration, the idle gap before
 it and its predecessor, plus the step's launch count and the time in launches
 under 20 us.  Steps end at the optimizer kernel (torch's fused Adam:
 multi_tensor_apply; rb_adam_step: k_adam); the median-length step of the last
-`steps` is printed.
+`steps` is printed — or of the `steps` steps starting at step `first`
+(0-based over the whole trace: bench.py's timed loop starts after its
+warmup steps, before the host-enqueue, breakdown and variant passes).
 
-    python tools/step_sequence.py <kernel_trace.csv> [steps] > out.txt"""
+    python tools/step_sequence.py <kernel_trace.csv> [steps] [first] > out.txt"""
 import csv
 import re
 import sys
@@ -28,13 +30,18 @@ def short(name: str) -> str:
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    first = int(sys.argv[3]) if len(sys.argv) > 3 else None
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     ends = [i for i, r in enumerate(rows)
             if "multi_tensor_apply" in r["Kernel_Name"] or "k_adam" in r["Kernel_Name"]]
     # a fused torch Adam may be several launches per step: keep the last of a run
     ends = [e for k, e in enumerate(ends) if k + 1 == len(ends) or ends[k + 1] != e + 1]
     steps = []
-    for a, b in zip(ends[-(S + 1):-1], ends[-S:]):
+    # step k spans (ends[k-1], ends[k]]; the first step (k = 0) has no
+    # predecessor end and is never selected
+    pairs = (list(zip(ends[first - 1:first + S - 1], ends[first:first + S])) if first
+             else list(zip(ends[-(S + 1):-1], ends[-S:])))
+    for a, b in pairs:
         seg = rows[a + 1:b + 1]
         t0 = int(rows[a]["End_Timestamp"])
         t1 = int(rows[b]["End_Timestamp"])
