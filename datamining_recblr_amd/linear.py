@@ -171,15 +171,16 @@ def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
 # RECBLR_BF16_GEMM:
 #   "auto" (default) — ours where they measured faster at configs[4]: the
 #     NT kernel for R <= 512 inputs (the three forward GEMMs and out's input
-#     gradient: 4-9% faster than hipBLASLt) and the weight-gradient kernel
-#     for N <= 512 (out.dW); hipBLASLt for the K = 1024 input gradients of
-#     the in / gates projections (7-14% faster there) and the N = 1024 weight
-#     gradients (profiles/r05_bfmid_shapes.txt);
+#     gradient: 4-9% faster than hipBLASLt, profiles/r05_bfmid_shapes.txt);
+#     hipBLASLt for the K = 1024 input gradients of the in / gates
+#     projections (7-14% faster there) and for the three weight gradients
+#     (torch's batched split-K + rb_colsum, 4-24% faster than
+#     rb_gemm_tn_bf16, profiles/r05_tn48_shapes.txt);
 #   "1" — ours on every shape; "0" — hipBLASLt on every shape.
 # The weight's bf16 fragment images (W for the forward, W^T for the input
 # gradient) are cached per weight version like the split images.
 BF16_NT_MAX_R = 512
-BF16_TN_MAX_N = 512
+BF16_TN_MAX_N = 0   # auto: no weight-gradient shape on rb_gemm_tn_bf16
 _BF16_MODES = ("auto", "1", "0")
 _bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "auto")
 if _bf16_gemm not in _BF16_MODES:
