@@ -163,6 +163,41 @@ def test_tuned_gemm_table_covers_bench_shapes():
     assert gemm_tuning.use_tuned_gemms() is False or torch.cuda.is_available()
 
 
+def test_tuned_gemm_table_lists_the_configs4_library_shapes():
+    """The table also carries the configs[4] GEMMs the per-shape bf16 mode
+    leaves on the library (round 5's TunableOp search): the K = 1,024 input
+    gradients and the three weight gradients' batched products, bf16."""
+    import csv
+
+    from datamining_recblr_amd import gemm_tuning
+
+    rows = [r for r in csv.reader(open(gemm_tuning.TABLE_PATH)) if r[0] != "Validator"]
+    bf16 = {r[1] for r in rows if "BFloat16" in r[0]}
+    for key in ("nn_512_2097152_1024", "nn_256_2097152_1024", "nt_512_256_32768_B_64",
+                "nt_512_1024_32768_B_64", "nt_256_1024_32768_B_64"):
+        assert any(k.startswith(key) for k in bf16), key
+    assert len({(r[0], r[1]) for r in rows}) == len(rows)   # no duplicate keys
+
+
+def test_bf16_gemm_modes_and_shape_rule(monkeypatch):
+    """RECBLR_BF16_GEMM: set_bf16_gemm takes "auto" / "1" / "0" or a bool and
+    returns the previous mode; anything else is rejected.  In "auto" only the
+    NT GEMMs with R <= 512 inputs run on our kernels, no weight gradient."""
+    from datamining_recblr_amd import linear
+
+    prev = linear.set_bf16_gemm("auto")
+    try:
+        assert linear.set_bf16_gemm(True) == "auto"
+        assert linear.set_bf16_gemm(False) == "1"
+        assert linear.set_bf16_gemm("auto") == "0"
+        with pytest.raises(ValueError):
+            linear.set_bf16_gemm("yes")
+        assert linear._bf16_gemm == "auto"
+        assert linear.BF16_NT_MAX_R == 512 and linear.BF16_TN_MAX_N == 0
+    finally:
+        linear.set_bf16_gemm(prev)
+
+
 def test_rank_metrics_match_sklearn_and_recbole():
     """rank_metrics from (n_greater, n_equal) equals sklearn's tie-averaged
     ndcg_score (run_with_unseen.py:247) and RecBole-style top-k metrics on an
