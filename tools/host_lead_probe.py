@@ -50,15 +50,19 @@ def main():
     print(json.dumps({"host_ms_per_step": d, "gpu_ms_per_step": round(1e3 * total / 40, 3),
                       "host_done_ms": round(1e3 * marks[-1], 2), "total_ms": round(1e3 * total, 2)}),
           flush=True)
-    # The same steps with the host certainly ahead: 4 steps queued behind a
-    # ~100 ms spin kernel (the pinned rings hold 4), timed by events between
-    # the spin's end and the 4th step's end.  Equal to the steady-state time
-    # per step = no host-induced GPU idle in the steady state.
+    # The same steps with the host certainly ahead: 4 steps queued behind
+    # ~50 ms of busy GEMMs (busy, so the clocks stay up; the pinned rings hold
+    # 4), timed by events between the GEMMs' end and the 4th step's end.
+    # Equal to the steady-state time per step = no host-induced GPU idle.
     pre = []
+    big = torch.randn(8192, 8192, device=dev)
     for trial in range(4):
+        for i in range(4):
+            step(i)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        torch.cuda._sleep(200_000_000)
+        for _ in range(6):
+            torch.mm(big, big)
         e0.record()
         for i in range(4):
             step(trial * 4 + i)
