@@ -222,6 +222,13 @@ def cpu_baseline(args, state_dict):
                                       "median of 3"}}
 
 
+def _newest_profiles(suffix):
+    """profiles/*<suffix>, oldest first by run tag (the name before the
+    suffix): r05_final < r05_final2 < r06_v0."""
+    files = glob.glob(os.path.join(ROOT, "profiles", "*" + suffix))
+    return sorted(files, key=lambda f: os.path.basename(f)[:-len(suffix)])
+
+
 def pmc_traffic(args, kernel_prefix):
     """HBM bytes per launch of `kernel_prefix` from the newest committed PMC
     summary (profiles/*_pmc_traffic.json, tools/pmc_traffic.py: FETCH_SIZE and
@@ -229,7 +236,7 @@ def pmc_traffic(args, kernel_prefix):
     correction applied).  None unless this run is that default shape."""
     if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    files = _newest_profiles("_pmc_traffic.json")
     if not files:
         return None, None
     data = json.load(open(files[-1]))
@@ -249,7 +256,7 @@ def pmc_mfma(args):
     cycles, whatever the dtype."""
     if (args.batch, args.seq_len, args.hidden) != (2048, 200, 128):
         return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_mfma.json")))
+    files = _newest_profiles("_pmc_mfma.json")
     if not files:
         return None
     data = json.load(open(files[-1]))
