@@ -218,6 +218,54 @@ __device__ __forceinline__ void unpack_raw(float (&o)[V], const RawVec<bf16_t, V
   }
 }
 
+// channels h0 .. h0 + VH - 1 of a raw image (h0 even for packed bf16), and
+// the reverse: VH results into a storage-format image (bf16: RNE pairs, as
+// stv); stv_raw stores a whole image with stv's policy
+template <int VH, typename T, int V>
+__device__ __forceinline__ void unpack_part(float (&o)[VH], const RawVec<T, V>& r, int h0) {
+  if constexpr (VH == V) {
+    unpack_raw(o, r);
+  } else if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int v = 0; v < VH; ++v) o[v] = r.w[h0 + v];
+  } else {
+#pragma unroll
+    for (int k = 0; k < VH / 2; ++k) unpack2(r.w[h0 / 2 + k], o[2 * k], o[2 * k + 1]);
+  }
+}
+template <int VH, typename T, int V>
+__device__ __forceinline__ void pack_part(RawVec<T, V>& r, const float (&o)[VH], int h0) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int v = 0; v < VH; ++v) r.w[h0 + v] = o[v];
+  } else {
+    static_assert(VH % 2 == 0, "packed bf16 pairs");
+#pragma unroll
+    for (int k = 0; k < VH / 2; ++k) r.w[h0 / 2 + k] = pack2(o[2 * k], o[2 * k + 1]);
+  }
+}
+// the words of channels h0 .. h0 + VH - 1 through an empty volatile asm (an
+// ordering point for the compiler; no instruction)
+template <int VH, typename T, int V>
+__device__ __forceinline__ void opaque_part(RawVec<T, V>& r, int h0) {
+  constexpr int per = sizeof(T) == 2 && V > 1 ? 2 : 1;   // channels per word
+#pragma unroll
+  for (int k = 0; k < VH / per; ++k) asm volatile("" : "+v"(r.w[h0 / per + k]));
+}
+template <int V>
+__device__ __forceinline__ void stv_raw(float* p, const RawVec<float, V>& r) { st_f32<kNT>(p, r.w); }
+template <int V>
+__device__ __forceinline__ void stv_raw(bf16_t* p, const RawVec<bf16_t, V>& r) {
+  if constexpr (V == 8) {
+    st_pol<kNT>(rb_u32x4{r.w[0], r.w[1], r.w[2], r.w[3]}, reinterpret_cast<rb_u32x4*>(p));
+  } else if constexpr (V == 4) {
+    st_pol<kNT>(rb_u32x2{r.w[0], r.w[1]}, reinterpret_cast<rb_u32x2*>(p));
+  } else {
+    static_assert(V == 2, "packed bf16 image");
+    st_pol<kNT>(r.w[0], reinterpret_cast<uint32_t*>(p));
+  }
+}
+
 // ---- dropout keep-flags ------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11): counter = element index / 4, key =
 // 64-bit seed, 4 uniform u32 per call -> keep flags of 4 consecutive elements.

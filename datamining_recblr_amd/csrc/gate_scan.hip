@@ -241,8 +241,8 @@ __device__ __forceinline__ void scan_from_upper(float& A, float& E, int q) {
   }
 }
 
-template <typename T, int VEC, int Q, int TC, bool PF>
-__global__ void __launch_bounds__(256)
+template <typename T, int VEC, int Q, int TC, bool PF, int VH = VEC>
+__global__ void __launch_bounds__(256, VH < VEC ? 2 : 1)   // channel passes: 2 waves per SIMD
 k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, int xc_rs,
                 const T* __restrict__ z, int z_rs, const float* __restrict__ lam,
                 const float* __restrict__ gbias, const float* __restrict__ carries,
@@ -326,131 +326,184 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
       }
     }
   };
-  auto process = [&](const BwdIn<T, VEC, TC>& raw, int tile, const float (&hc)[VEC]) {
+  // VH < VEC: the tile's math runs VH channels at a time (the per-channel
+  // recurrences are independent; the same operations in the same order, so
+  // bit-identical), its results collected in storage format and stored as
+  // VEC-wide vectors after the last pass — a third of the live registers.
+  constexpr bool SPLIT = VH < VEC;
+  static_assert(VEC % VH == 0 && (!SPLIT || VH % 2 == 0), "channel passes");
+  auto process = [&](const BwdIn<T, VEC, TC>& raw, int tile) {
     float hcar[VEC];
     ldc(hcar, carries + (b * nTc + tile) * H + cc);
-    struct {
-      float r[TC][VEC], i[TC][VEC], x[TC][VEC], z[TC][VEC], g[TC][VEC];
-    } in;
-#pragma unroll
-    for (int j = 0; j < TC; ++j) {
-      unpack_raw(in.r[j], raw.r[j]);
-      unpack_raw(in.i[j], raw.i[j]);
-      unpack_raw(in.x[j], raw.x[j]);
-      unpack_raw(in.z[j], raw.z[j]);
-      unpack_raw(in.g[j], raw.g[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < TC; ++j)
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        in.r[j][v] += br[v];
-        in.i[j][v] += bi[v];
-      }
     const int t0 = tile * TILE + q * TC;
-    // per-step derived values, each transcendental evaluated once
-    float al[TC][VEC], sr[TC][VEC], si[TC][VEC], sq[TC][VEC], bp[TC][VEC], gs[TC][VEC],
-        dsz[TC][VEC];
+    RawVec<T, VEC> odz[SPLIT ? TC : 1], odr[SPLIT ? TC : 1], odi[SPLIT ? TC : 1],
+        odx[SPLIT ? TC : 1];
 #pragma unroll
-    for (int j = 0; j < TC; ++j) {
-      const bool ok = t0 + j < L;
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        sr[j][v] = fsigm(in.r[j][v]);
-        const float a = ok ? fexp(nsp[v] * sr[j][v]) : 1.0f;
-        al[j][v] = a;
-        si[j][v] = fsigm(in.i[j][v]);
-        sq[j][v] = fsqrt(1.0f - a * a + 1e-8f);
-        bp[j][v] = ok ? sq[j][v] * si[j][v] * in.x[j][v] : 0.0f;
-        const float zz = in.z[j][v];
-        const float sz = fsigm(zz);
-        const float g = ok ? in.g[j][v] : 0.0f;   // dy past the end contributes nothing
-        in.g[j][v] = g;
-        gs[j][v] = g * (zz * sz);
-        dsz[j][v] = sz * (1.0f + zz * (1.0f - sz));
-      }
-    }
-    float cin[VEC], ein[VEC];
-#pragma unroll
-    for (int v = 0; v < VEC; ++v) {
-      float A = 1.0f, X = 0.0f, E = 0.0f;
+    for (int h0 = 0; h0 < VEC; h0 += VH) {
+      struct {
+        float r[TC][VH], i[TC][VH], x[TC][VH], z[TC][VH], g[TC][VH];
+      } in;
 #pragma unroll
       for (int j = 0; j < TC; ++j) {
-        X = X * al[j][v] + bp[j][v];
-        A = A * al[j][v];
+        // (channel passes: this pass's words through an empty volatile asm,
+        // ordered after the previous pass's results below, so the compiler
+        // cannot interleave the passes and the register saving is real)
+        RawVec<T, VEC> wr = raw.r[j], wi = raw.i[j], wx = raw.x[j], wz = raw.z[j], wg = raw.g[j];
+        if constexpr (SPLIT) {
+          opaque_part<VH>(wr, h0);
+          opaque_part<VH>(wi, h0);
+          opaque_part<VH>(wx, h0);
+          opaque_part<VH>(wz, h0);
+          opaque_part<VH>(wg, h0);
+        }
+        unpack_part(in.r[j], wr, h0);
+        unpack_part(in.i[j], wi, h0);
+        unpack_part(in.x[j], wx, h0);
+        unpack_part(in.z[j], wz, h0);
+        unpack_part(in.g[j], wg, h0);
+      }
+#pragma unroll
+      for (int j = 0; j < TC; ++j)
+#pragma unroll
+        for (int v = 0; v < VH; ++v) {
+          in.r[j][v] += br[h0 + v];
+          in.i[j][v] += bi[h0 + v];
+        }
+      // per-step derived values, each transcendental evaluated once
+      float al[TC][VH], sr[TC][VH], si[TC][VH], sq[TC][VH], bp[TC][VH], gs[TC][VH],
+          dsz[TC][VH];
+#pragma unroll
+      for (int j = 0; j < TC; ++j) {
+        const bool ok = t0 + j < L;
+#pragma unroll
+        for (int v = 0; v < VH; ++v) {
+          sr[j][v] = fsigm(in.r[j][v]);
+          const float a = ok ? fexp(nsp[h0 + v] * sr[j][v]) : 1.0f;
+          al[j][v] = a;
+          si[j][v] = fsigm(in.i[j][v]);
+          sq[j][v] = fsqrt(1.0f - a * a + 1e-8f);
+          bp[j][v] = ok ? sq[j][v] * si[j][v] * in.x[j][v] : 0.0f;
+          const float zz = in.z[j][v];
+          const float sz = fsigm(zz);
+          const float g = ok ? in.g[j][v] : 0.0f;   // dy past the end contributes nothing
+          in.g[j][v] = g;
+          gs[j][v] = g * (zz * sz);
+          dsz[j][v] = sz * (1.0f + zz * (1.0f - sz));
+        }
+      }
+      float cin[VH], ein[VH];
+#pragma unroll
+      for (int v = 0; v < VH; ++v) {
+        float A = 1.0f, X = 0.0f, E = 0.0f;
+#pragma unroll
+        for (int j = 0; j < TC; ++j) {
+          X = X * al[j][v] + bp[j][v];
+          A = A * al[j][v];
+        }
+#pragma unroll
+        for (int j = TC - 1; j >= 0; --j) {
+          const float d = E + gs[j][v];
+          E = d * al[j][v];
+        }
+        float Af = A, Xf = X;
+        scan_from_lower<Q>(Af, Xf, q);
+        float Ae = dpp_from_lower<1>(Af);
+        float Xe = dpp_from_lower<1>(Xf);
+        if (q == 0) {
+          Ae = 1.0f;
+          Xe = 0.0f;
+        }
+        cin[v] = hcar[h0 + v] * Ae + Xe;
+        float Ab = A, Eb = E;
+        scan_from_upper<Q>(Ab, Eb, q);
+        float Ase = dpp_from_upper<1>(Ab);
+        float Ese = dpp_from_upper<1>(Eb);
+        if (q == Q - 1) {
+          Ase = 1.0f;
+          Ese = 0.0f;
+        }
+        ein[v] = ecarry[h0 + v] * Ase + Ese;
+        const float At = group_first<Q>(Ab);
+        const float Et = group_first<Q>(Eb);
+        ecarry[h0 + v] = ecarry[h0 + v] * At + Et;
+      }
+      float hp[TC][VH];
+#pragma unroll
+      for (int j = 0; j < TC; ++j) {
+        const bool ok = t0 + j < L;
+        float dzo[VH];
+#pragma unroll
+        for (int v = 0; v < VH; ++v) {
+          hp[j][v] = cin[v];
+          cin[v] = cin[v] * al[j][v] + bp[j][v];
+          dzo[v] = (in.g[j][v] * cin[v]) * dsz[j][v];
+        }
+        if constexpr (SPLIT) pack_part(odz[j], dzo, h0);
+        else if (cv && ok) stv(dzb + (t0 + j) * dz_rs, dzo);
       }
 #pragma unroll
       for (int j = TC - 1; j >= 0; --j) {
-        const float d = E + gs[j][v];
-        E = d * al[j][v];
-      }
-      float Af = A, Xf = X;
-      scan_from_lower<Q>(Af, Xf, q);
-      float Ae = dpp_from_lower<1>(Af);
-      float Xe = dpp_from_lower<1>(Xf);
-      if (q == 0) {
-        Ae = 1.0f;
-        Xe = 0.0f;
-      }
-      cin[v] = hcar[v] * Ae + Xe;
-      float Ab = A, Eb = E;
-      scan_from_upper<Q>(Ab, Eb, q);
-      float Ase = dpp_from_upper<1>(Ab);
-      float Ese = dpp_from_upper<1>(Eb);
-      if (q == Q - 1) {
-        Ase = 1.0f;
-        Ese = 0.0f;
-      }
-      ein[v] = ecarry[v] * Ase + Ese;
-      const float At = group_first<Q>(Ab);
-      const float Et = group_first<Q>(Eb);
-      ecarry[v] = ecarry[v] * At + Et;
-    }
-    float hp[TC][VEC];
+        const bool ok = t0 + j < L;
+        float dro[VH], dio[VH], dxo[VH];
 #pragma unroll
-    for (int j = 0; j < TC; ++j) {
-      const bool ok = t0 + j < L;
-      float dzo[VEC];
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        hp[j][v] = cin[v];
-        cin[v] = cin[v] * al[j][v] + bp[j][v];
-        dzo[v] = (in.g[j][v] * cin[v]) * dsz[j][v];
+        for (int v = 0; v < VH; ++v) {
+          const float a = al[j][v];
+          const float d = ein[v] + gs[j][v];   // dL/dh_t
+          const float dbeta = d * in.x[j][v];
+          const float du = (dbeta * si[j][v]) * (0.5f * frcp(sq[j][v]));
+          const float da = hp[j][v] * d + (-du) * (2.0f * a);
+          const float dv = da * a;
+          dro[v] = (dv * nsp[h0 + v]) * ((1.0f - sr[j][v]) * sr[j][v]);
+          dio[v] = (dbeta * sq[j][v]) * ((1.0f - si[j][v]) * si[j][v]);
+          dxo[v] = d * (sq[j][v] * si[j][v]);
+          acc_v[h0 + v] = acc_v[h0 + v] + (ok ? dv * sr[j][v] : 0.0f);
+          acc_r[h0 + v] = acc_r[h0 + v] + (ok ? dro[v] : 0.0f);
+          acc_i[h0 + v] = acc_i[h0 + v] + (ok ? dio[v] : 0.0f);
+          ein[v] = d * a;
+        }
+        if constexpr (SPLIT) {
+          pack_part(odr[j], dro, h0);
+          pack_part(odi[j], dio, h0);
+          pack_part(odx[j], dxo, h0);
+        } else if (cv && ok) {
+          const int t = t0 + j;
+          stv(drgb + t * drg_rs, dro);
+          stv(drgb + t * drg_rs + H, dio);
+          stv(dxcb + t * dxc_rs, dxo);
+        }
       }
-      if (cv && ok) stv(dzb + (t0 + j) * dz_rs, dzo);
-    }
+      if (tile == 0 && q == 0 && cv) stv(dh0_part + b * H + c0 + h0, ein);
+      if constexpr (SPLIT) {   // the pass's results exist before the next pass starts
 #pragma unroll
-    for (int j = TC - 1; j >= 0; --j) {
-      const bool ok = t0 + j < L;
-      float dro[VEC], dio[VEC], dxo[VEC];
+        for (int j = 0; j < TC; ++j) {
+          opaque_part<VH>(odz[j], h0);
+          opaque_part<VH>(odr[j], h0);
+          opaque_part<VH>(odi[j], h0);
+          opaque_part<VH>(odx[j], h0);
+        }
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        const float a = al[j][v];
-        const float d = ein[v] + gs[j][v];   // dL/dh_t
-        const float dbeta = d * in.x[j][v];
-        const float du = (dbeta * si[j][v]) * (0.5f * frcp(sq[j][v]));
-        const float da = hp[j][v] * d + (-du) * (2.0f * a);
-        const float dv = da * a;
-        dro[v] = (dv * nsp[v]) * ((1.0f - sr[j][v]) * sr[j][v]);
-        dio[v] = (dbeta * sq[j][v]) * ((1.0f - si[j][v]) * si[j][v]);
-        dxo[v] = d * (sq[j][v] * si[j][v]);
-        acc_v[v] = acc_v[v] + (ok ? dv * sr[j][v] : 0.0f);
-        acc_r[v] = acc_r[v] + (ok ? dro[v] : 0.0f);
-        acc_i[v] = acc_i[v] + (ok ? dio[v] : 0.0f);
-        ein[v] = d * a;
-      }
-      if (cv && ok) {
-        const int t = t0 + j;
-        stv(drgb + t * drg_rs, dro);
-        stv(drgb + t * drg_rs + H, dio);
-        stv(dxcb + t * dxc_rs, dxo);
+        for (int v = 0; v < VH; ++v)
+          asm volatile("" : "+v"(ecarry[h0 + v]), "+v"(acc_v[h0 + v]), "+v"(acc_r[h0 + v]),
+                       "+v"(acc_i[h0 + v]));
       }
     }
-    if (tile == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ein);
+    if constexpr (SPLIT) {
+#pragma unroll
+      for (int j = 0; j < TC; ++j)
+        if (cv && t0 + j < L) stv_raw(dzb + (t0 + j) * dz_rs, odz[j]);
+#pragma unroll
+      for (int j = TC - 1; j >= 0; --j) {
+        if (cv && t0 + j < L) {
+          const int t = t0 + j;
+          stv_raw(drgb + t * drg_rs, odr[j]);
+          stv_raw(drgb + t * drg_rs + H, odi[j]);
+          stv_raw(dxcb + t * dxc_rs, odx[j]);
+        }
+      }
+    }
   };
 
   BwdIn<T, VEC, TC> bufA, bufB;
-  const float nohc[VEC] = {};
   const int nseq = (pair && B - 1 - bw != bw) ? 2 : 1;
   for (int sq_i = 0; sq_i < nseq; ++sq_i) {
     bind(sq_i == 0 ? bw : B - 1 - bw);
@@ -461,16 +514,16 @@ k_gate_scan_bwd(const T* __restrict__ rg, int rg_rs, const T* __restrict__ xc, i
       if (nT > 0) load(bufA, nT - 1);
       for (int tile = nT - 1; tile >= 0; tile -= 2) {
         if (tile - 1 >= 0) load(bufB, tile - 1);
-        process(bufA, tile, nohc);
+        process(bufA, tile);
         if (tile - 1 >= 0) {
           if (tile - 2 >= 0) load(bufA, tile - 2);
-          process(bufB, tile - 1, nohc);
+          process(bufB, tile - 1);
         }
       }
     } else {
       for (int tile = nT - 1; tile >= 0; --tile) {
         load(bufA, tile);
-        process(bufA, tile, nohc);
+        process(bufA, tile);
       }
     }
     if (nT == 0 && q == 0 && cv) stv(dh0_part + b * H + c0, ecarry);   // empty row: zeros
@@ -542,7 +595,7 @@ int gate_fwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   return launch_status("rb_gate_scan_fwd");
 }
 
-template <typename T, int V, int Q = kBwdQ, int TC = kBwdTC, bool PF = false>
+template <typename T, int V, int Q = kBwdQ, int TC = kBwdTC, bool PF = false, int VH = V>
 int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* z,
                int64_t z_rs, const float* lam, const float* gb, const float* carries,
                const T* dy, T* drg, int64_t drg_rs, T* dxc, int64_t dxc_rs, T* dz, int64_t dz_rs,
@@ -554,7 +607,7 @@ int gate_bwd_v(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
   const int pair = offs != nullptr && kBwdPair;
   const int64_t Bw = pair ? (B + 1) / 2 : B;
   const int64_t blocks = (Bw * ncw + 3) / 4;
-  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((k_gate_scan_bwd<T, V, Q, TC, PF, VH>), dim3((unsigned)blocks),
                      dim3(256), 0, st, rg, (int)rg_rs, xc, (int)xc_rs, z, (int)z_rs, lam, gb,
                      carries, dy, drg, (int)drg_rs, dxc, (int)dxc_rs, dz, (int)dz_rs, part,
                      dh0_part, B, (int)L, (int)H, ncw, offs, pair, dy_last, order);
@@ -596,17 +649,17 @@ int gate_bwd_t(const T* rg, int64_t rg_rs, const T* xc, int64_t xc_rs, const T* 
                     (const void*)drg, (const void*)dxc, (const void*)dz, (const void*)dy_last};
   const auto f32 = {(const void*)lam, (const void*)gb, (const void*)carries, (const void*)part,
                     (const void*)dh0_part};
-  // bf16 (configs[4], L = 2048): 4 chunks x 4 steps with the next tile
-  // prefetched in storage format — one wave walks 128 tiles, so it needs two
-  // tiles of loads in flight (tools/kbench.hip: 0.36 -> 0.59 of 8 TB/s)
+  // bf16 (configs[4], L = 2048): 4 chunks x 4 steps (128-B row pieces per
+  // wave), the tile's math in two passes of 2 channels so the kernel fits 256
+  // registers: 2 waves per SIMD hide the loads that one wave with a register
+  // prefetch of the next tile (417 registers, round 1-4) could not —
+  // 3.89 vs 4.37 ms at configs[4], bit-identical (tools/gate_bf16_probe.hip,
+  // profiles/r05_gb_probe.txt)
   if constexpr (sizeof(T) == 2) {
-    // (an LDS-DMA ring of three tiles per wave instead of the register
-    // prefetch measured slower: 0.564 vs 0.592 of 8 TB/s at configs[4],
-    // profiles/r03_kbench_c5_gate_bwd_dma.txt; kept in git history)
     if (vec_ok<T, VW>(H, strides, act, f32))
-      return gate_bwd_v<T, VW, 4, 4, true>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy,
-                                           drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part, dh0_part,
-                                           B, L, H, offs, st, dy_last, order);
+      return gate_bwd_v<T, VW, 4, 4, false, 2>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries,
+                                               dy, drg, drg_rs, dxc, dxc_rs, dz, dz_rs, part,
+                                               dh0_part, B, L, H, offs, st, dy_last, order);
   }
   if (vec_ok<T, VW>(H, strides, act, f32)) {
     return gate_bwd_v<T, VW>(rg, rg_rs, xc, xc_rs, z, z_rs, lam, gb, carries, dy, drg, drg_rs,
