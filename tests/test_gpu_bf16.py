@@ -168,11 +168,10 @@ def test_grl_bf16_vs_oracle(cuda, B, L, d):
 
 @pytest.mark.parametrize("B,L,H", [(3, 2048, 512), (5, 64, 256)])
 def test_gate_bwd_bf16_dense_equals_packed(cuda, B, L, H):
-    """The bf16 gate backward on dense rows (whole tiles, 64-channel spans:
-    the rows the LDS-DMA ring variant takes when built with
-    -DRB_GATE_BWD_DMA=1) and on the same rows as a packed batch of equal
-    lengths (the register-prefetch path): the same per-tile arithmetic, so
-    dz, drg and dxc are bit-identical and the partial sums equal to 1e-6."""
+    """The bf16 gate backward on dense rows and on the same rows as a packed
+    batch of equal lengths (one wave per sequence pair): the same per-tile
+    arithmetic (two 2-channel passes per tile), so dz, drg and dxc are
+    bit-identical and the partial sums equal to 1e-6."""
     from datamining_recblr_amd import kernels
     from datamining_recblr_amd.kernels import Packed
 
@@ -198,3 +197,37 @@ def test_gate_bwd_bf16_dense_equals_packed(cuda, B, L, H):
     assert torch.equal(flat(dense[1]).view(torch.int16), packed[1].view(torch.int16)), "dxc"
     for k, n in ((2, "dLambda"), (3, "dgate_b"), (4, "dh0")):
         _close(dense[k], packed[k], rtol=1e-6, what=n)
+
+
+@pytest.mark.parametrize("H", [512, 192])
+def test_gate_bwd_bf16_packed_ragged_vs_fp32(cuda, H):
+    """The bf16 gate backward (channel passes) on a ragged packed batch —
+    lengths 1..300 sorted longest first, partial tiles, a length-1 sequence —
+    against the fp32 kernel on the same bf16-rounded operands: within one
+    bf16 ulp elementwise, the per-channel sums to 1e-4."""
+    from datamining_recblr_amd import kernels
+    from datamining_recblr_amd.kernels import Packed
+
+    g = torch.Generator().manual_seed(H)
+    lengths = sorted([300, 257, 200, 129, 64, 33, 17, 16, 15, 2, 1], reverse=True)
+    B, L = len(lengths), max(lengths)
+    offs = torch.tensor([0] + lengths, dtype=torch.int64).cumsum(0)
+    n = int(offs[-1])
+    seq = Packed(offs.to(cuda), L, n)
+    rg = _rb(torch.randn(n, 2 * H, generator=g)).to(cuda)
+    xc = _rb(torch.randn(n, H, generator=g)).to(cuda)
+    z = _rb(torch.randn(n, H, generator=g)).to(cuda)
+    dy = _rb(torch.randn(n, H, generator=g)).to(cuda)
+    lam = torch.linspace(-2.2, -6.9, H).to(cuda)
+    gb = (0.1 * torch.randn(2 * H, generator=g)).to(cuda)
+    _, c32 = kernels.gate_scan_fwd(rg, xc, z, lam, None, gate_b=gb, seq=seq)
+    dz32 = torch.empty_like(z)
+    r32 = kernels.gate_scan_bwd(rg, xc, z, lam, c32, dy, dz32, gate_b=gb, seq=seq)
+    dz16 = torch.empty_like(z, dtype=BF)
+    r16 = kernels.gate_scan_bwd(rg.to(BF), xc.to(BF), z.to(BF), lam, c32, dy.to(BF), dz16,
+                                gate_b=gb, seq=seq)
+    _within_ulp(dz16, dz32, "dz")
+    _within_ulp(r16[0], r32[0], "drg")
+    _within_ulp(r16[1], r32[1], "dxc")
+    for k, nm in ((2, "dLambda"), (3, "dgate_b"), (4, "dh0")):
+        _close(r16[k], r32[k], rtol=1e-4, what=nm)
