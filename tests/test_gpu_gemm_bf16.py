@@ -11,6 +11,7 @@ import pytest
 import torch
 
 from datamining_recblr_amd import kernels, linear
+from tests.placement import bit31_alloc_bytes, bit31_offset
 
 BF = torch.bfloat16
 pytestmark = pytest.mark.gpu
@@ -175,11 +176,9 @@ def test_gemm_tn_bf16_operands_above_bit_31(cuda):
     g = torch.Generator(device=cuda).manual_seed(31)
     dy0 = torch.randn(M, N, device=cuda, generator=g).to(BF)
     x0 = torch.randn(M, K, device=cuda, generator=g).to(BF)
-    need = 2 * M * (N + K) + 1024
-    buf = torch.empty((1 << 31) + need, dtype=torch.uint8, device=cuda)
-    base = buf.data_ptr()
-    off = 0 if (base >> 31) & 1 else ((1 << 31) - (base & 0x7FFFFFFF))
-    off += (-(base + off)) % 256
+    need = 2 * M * (N + K)
+    buf = torch.empty(bit31_alloc_bytes(need), dtype=torch.uint8, device=cuda)
+    off = bit31_offset(buf.data_ptr(), need)
     dy = buf[off: off + 2 * M * N].view(BF).view(M, N)
     off += 2 * M * N
     x = buf[off: off + 2 * M * K].view(BF).view(M, K)

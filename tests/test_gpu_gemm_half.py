@@ -9,6 +9,7 @@ the whole fp32 range (the per-row scale, and the exact recompute of rows that
 outgrow their first scale)."""
 import pytest
 import torch
+from tests.placement import bit31_alloc_bytes, bit31_offset
 
 pytestmark = pytest.mark.gpu
 
@@ -489,16 +490,11 @@ def test_few_rows_weight_gradient(cuda, M, N, K):
 
 
 def _bit31_views(cuda, shapes):
-    """fp32 views, 16-B aligned, whose device addresses all have bit 31 set,
-    sliced from one allocation of 2 GiB + the operands (some offset of any
-    2 GiB window has its low address word at or above 2^31).  Round 4's TN
-    fault: the buffer descriptor's base went through readfirstlane's int and
-    was sign-extended into the high word for exactly such addresses."""
+    """fp32 views, 16-B aligned, whose device addresses all have bit 31 set
+    (tests/placement.py), sliced from one allocation."""
     need = sum(4 * (r * c) + 256 for r, c in shapes)
-    buf = torch.empty((1 << 31) + need + 256, dtype=torch.uint8, device=cuda)
-    base = buf.data_ptr()
-    off = 0 if (base >> 31) & 1 else ((1 << 31) - (base & 0x7FFFFFFF))
-    off += (-(base + off)) % 256
+    buf = torch.empty(bit31_alloc_bytes(need), dtype=torch.uint8, device=cuda)
+    off = bit31_offset(buf.data_ptr(), need)
     views = []
     for r, c in shapes:
         v = buf[off: off + 4 * r * c].view(torch.float32).view(r, c)

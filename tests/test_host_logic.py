@@ -322,3 +322,25 @@ def test_ce_f16_grads_fall_back_past_the_weight_gradient_width(monkeypatch):
     assert scoring._f16_grads_ok(seq, torch.empty(65536, 128))
     assert not scoring._f16_grads_ok(seq, torch.empty(65537, 128))
     assert not scoring._f16_grads_ok(torch.empty(300, 128), torch.empty(1000, 128))
+
+
+def test_bit31_placement_keeps_the_whole_run_in_an_upper_half():
+    """tests/placement.bit31_offset (the GPU tests' operands above bit 31):
+    every byte of the run has bit 31 set and stays inside the allocation,
+    for allocation bases anywhere in a 4 GiB block, including bases whose
+    upper half is too short for the run."""
+    import random
+
+    from tests.placement import bit31_alloc_bytes, bit31_offset
+
+    rng = random.Random(31)
+    need = 4 * 204632 * (512 + 256) + 512
+    bases = [k * 256 for k in (0, 1)] + [(1 << 31) - 256, 1 << 31, (1 << 32) - 256,
+                                         (1 << 32) - need // 2 // 256 * 256]
+    bases += [rng.randrange(0, 1 << 47) // 256 * 256 for _ in range(2000)]
+    for base in bases:
+        off = bit31_offset(base, need)
+        a, end = base + off, base + off + need - 1
+        assert a % 256 == 0
+        assert (a >> 31) & 1 and (end >> 31) & 1 and (a >> 32) == (end >> 32), hex(base)
+        assert off + need <= bit31_alloc_bytes(need)
