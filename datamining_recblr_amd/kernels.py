@@ -663,8 +663,8 @@ def embedding_bwd(idx, grad, num_rows, padding_idx=0, plan=None):
 
 
 def embedding_plan(idx, num_rows, d, stream=None):
-    """Sort + segment the ids for embedding_bwd (index work only; may run on a
-    side stream during the forward).  Returns the uint8 workspace."""
+    """Sort + segment the ids for embedding_bwd (index work only, run in the
+    forward; `stream`: another stream to run on).  Returns the uint8 workspace."""
     M = idx.numel()
     if idx.dtype != torch.int64 or not idx.is_contiguous():
         raise ValueError("idx must be contiguous int64")
