@@ -105,9 +105,12 @@ def _colsum_tickets(x: torch.Tensor, n: int) -> torch.Tensor:
     """rb_colsum_chunked's ticket counters for torch's current stream on x's
     device: zeroed once here, back at zero after every complete launch (the
     kernel's wrapping increment; calls on one stream are ordered, another
-    stream gets its own).  A counter found out of range is pulled back into
-    range by the launch that meets it; a failed native call drops every cached
-    counter (_lib.on_failure), so the next call starts from fresh zeros."""
+    stream gets its own).  The counters do NOT recover from a launch that did
+    not complete: a stale value makes the last-arriver test fire early or
+    never.  So any failed native call drops every cached counter
+    (_lib.on_failure) and the next call allocates fresh zeros; a kernel that
+    faults mid-launch leaves the HIP context unusable anyway (every later
+    call fails, and fails loudly)."""
     key = (x.device, _stream(x))
     t = _tickets.get(key)
     if t is None or t.numel() < n:

@@ -180,6 +180,11 @@ def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
 # The weight's bf16 fragment images (W for the forward, W^T for the input
 # gradient) are cached per weight version like the split images.
 BF16_NT_MAX_R = 512
+# auto: our NT kernel only from one persistent round of 256-row tiles per CU
+# (256 CUs x 256 rows): it was measured against hipBLASLt only at configs[4]'s
+# 2,097,152 rows, and below a round the persistent grid runs partly empty —
+# smaller bf16 GEMMs stay on hipBLASLt ("1" forces ours at any size)
+BF16_NT_MIN_ROWS = 65536
 BF16_TN_MAX_N = 0   # auto: no weight-gradient shape on rb_gemm_tn_bf16
 _BF16_MODES = ("auto", "1", "0")
 _bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "auto")
@@ -214,7 +219,8 @@ def _bf16_image(w: torch.Tensor, transpose: bool) -> torch.Tensor:
 
 
 def _bf16_ok(a: torch.Tensor, w: torch.Tensor, C: int, R: int) -> bool:
-    return (_bf16_gemm != "0" and (_bf16_gemm == "1" or R <= BF16_NT_MAX_R)
+    return (_bf16_gemm != "0"
+            and (_bf16_gemm == "1" or (R <= BF16_NT_MAX_R and a.shape[0] >= BF16_NT_MIN_ROWS))
             and a.dtype == torch.bfloat16 and w.dtype == torch.float32 and a.is_cuda
             and a.dim() == 2 and a.shape[0] > 0 and a.stride(1) == 1 and a.stride(0) % 8 == 0
             and a.data_ptr() % 16 == 0 and w.stride(1) == 1 and R % 64 == 0 and C % 256 == 0)

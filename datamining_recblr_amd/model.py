@@ -44,14 +44,28 @@ class _PinnedRing:
     """A few reusable page-locked staging buffers for the per-batch host ->
     device copy of the packed layout (offsets, order): no pinned allocation
     per step; slot i is reused only after the copy from it has completed
-    (its event; only waits if the device runs >= k batches behind)."""
+    (its event; only waits if the device runs >= k batches behind).
+
+    Under HIP-graph capture the ring is bypassed: a captured non_blocking
+    copy reads its pinned source when the graph is REPLAYED, so a ring slot
+    overwritten by a later stage() would change what the graph uploads.  A
+    captured stage() therefore copies into a pinned buffer of its own that is
+    kept alive (and never rewritten) for the life of the process — the graph
+    replays exactly the batch layout it captured."""
 
     def __init__(self, k: int = 4):
         self.k, self.i = k, 0
         self.bufs = [None] * k
         self.events = [None] * k
+        self.captured = []   # pinned sources of captured copies (kept alive)
 
     def stage(self, host: torch.Tensor, device) -> torch.Tensor:
+        if torch.cuda.is_current_stream_capturing():
+            buf = torch.empty(host.numel(), dtype=host.dtype, pin_memory=True)
+            buf.copy_(host.reshape(-1))
+            self.captured.append(buf)
+            with torch.cuda.device(device):
+                return buf.to(device, non_blocking=True)
         i = self.i
         self.i = (i + 1) % self.k
         n = host.numel()
@@ -59,8 +73,8 @@ class _PinnedRing:
         if buf is None or buf.numel() < n or buf.dtype != host.dtype:
             buf = self.bufs[i] = torch.empty(max(n, 4096), dtype=host.dtype, pin_memory=True)
             self.events[i] = None
-        if self.events[i] is not None and not torch.cuda.is_current_stream_capturing():
-            self.events[i].synchronize()   # (under graph capture: no host sync allowed)
+        if self.events[i] is not None:
+            self.events[i].synchronize()
         buf[:n].copy_(host)
         # the copy and its event on the TARGET device's current stream (the
         # current device may be another one)

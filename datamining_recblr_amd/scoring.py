@@ -38,11 +38,20 @@ def supported(seq: torch.Tensor, table: torch.Tensor) -> bool:
 # a time (rb_item_ce_probs, at most PROBS_SLICE_BYTES) and runs dseq += P W,
 # ditems = P^T seq as library GEMMs; "fused" (rb_item_ce_bwd) recomputes the
 # logits inside the MFMA kernels and needs no [B, V] buffer at all.
-CE_BACKWARD = os.environ.get("RECBLR_CE_BACKWARD", "slices")
+def _env_choice(name: str, default: str, allowed: tuple) -> str:
+    """An environment switch checked at import: a value outside `allowed`
+    raises instead of silently selecting another path."""
+    v = os.environ.get(name, default)
+    if v not in allowed:
+        raise ValueError(f"{name}={v!r}: expected one of {allowed}")
+    return v
+
+
+CE_BACKWARD = _env_choice("RECBLR_CE_BACKWARD", "slices", ("slices", "fused"))
 PROBS_SLICE_BYTES = 1 << 30
 # Logits pipe of the CE forward and of the sliced backward's P: "f16" (two-part
 # split operands on the f16 MFMA, fp32-level accuracy; default) or "f32".
-CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
+CE_PIPE = _env_choice("RECBLR_CE_PIPE", "f16", ("f16", "f32"))
 # The backward's two products dseq = P W, ditems = P^T seq: "f16" (default:
 # P written in both layouts, both products on the f16x3 weight-gradient
 # kernel, _bwd_f16) or "torch" (hipBLASLt fp32 on P, sliced).  Measured and
@@ -51,7 +60,7 @@ CE_PIPE = os.environ.get("RECBLR_CE_PIPE", "f16")
 # outgrow; profiles/r03_ce_grads_probe.log), and rb_item_ce_bwd_h (round 4:
 # each product inside a kernel that recomputes the logits, P never stored —
 # equal step time, profiles/r04_ce_bench_*.log; in git history up to round 4).
-CE_GRADS = os.environ.get("RECBLR_CE_GRADS", "f16")
+CE_GRADS = _env_choice("RECBLR_CE_GRADS", "f16", ("f16", "torch"))
 
 
 def set_ce_grads(mode: str) -> str:

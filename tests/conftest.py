@@ -13,6 +13,20 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm MI355X GPU (run with -m gpu)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line(
+        "markers", "experimental: the opt-in experimental library's kernels (not the product "
+        "path); skipped unless RECBLR_TEST_EXPERIMENTAL=1")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Experimental kernels (datamining_recblr_amd/experimental/, slower than the
+    product path and off by default) stay out of the default GPU suite."""
+    if os.environ.get("RECBLR_TEST_EXPERIMENTAL") == "1":
+        return
+    skip = pytest.mark.skip(reason="experimental kernels: set RECBLR_TEST_EXPERIMENTAL=1")
+    for item in items:
+        if item.get_closest_marker("experimental") is not None:
+            item.add_marker(skip)
 
 
 def load_golden(name):

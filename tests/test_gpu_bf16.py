@@ -231,3 +231,60 @@ def test_gate_bwd_bf16_packed_ragged_vs_fp32(cuda, H):
     _within_ulp(r16[1], r32[1], "dxc")
     for k, nm in ((2, "dLambda"), (3, "dgate_b"), (4, "dh0")):
         _close(r16[k], r32[k], rtol=1e-4, what=nm)
+
+
+def test_c5_bf16_full_batch_rows_match_oracle(cuda, monkeypatch):
+    """configs[4] at the size the bench times: GatedRecurrentLayer fwd + bwd
+    at B = 1,024, L = 2,048, d = 256 on bf16 activations through the default
+    per-shape GEMM dispatch (RECBLR_BF16_GEMM=auto), with our bf16 NT kernel
+    asserted engaged at M = 2,097,152 rows (the three forward projections and
+    out's input gradient) and the three weight gradients on the library's
+    split-K path (rb_gemm_tn_bf16 not called in auto) at the same M.  Three
+    batch rows are re-run on the fp32 CPU oracle with the same bf16-rounded
+    input and output gradient: y and dx rows within the 1.2e-2 bar of
+    test_grl_bf16_vs_oracle (batch rows are independent in the layer, so the
+    rows carry the full-batch GEMM dispatch's arithmetic)."""
+    from datamining_recblr_amd import kernels, linear
+    from datamining_recblr_amd.model import GatedRecurrentLayer
+
+    B, L, d = 1024, 2048, 256
+    M = B * L
+    nt_rows, tn_calls, wg = [], [], []
+    nt0, tn0, wg0 = kernels.gemm_nt_bf16, kernels.gemm_tn_bf16, linear.wgrad
+    monkeypatch.setattr(kernels, "gemm_nt_bf16",
+                        lambda a, *r, **k: nt_rows.append(a.shape[0]) or nt0(a, *r, **k))
+    monkeypatch.setattr(kernels, "gemm_tn_bf16",
+                        lambda *a, **k: tn_calls.append(1) or tn0(*a, **k))
+    monkeypatch.setattr(linear, "wgrad",
+                        lambda dy2, x2, *a, **k: wg.append((dy2.shape[0], dy2.dtype))
+                        or wg0(dy2, x2, *a, **k))
+    prev = linear.set_bf16_gemm("auto")
+    try:
+        torch.manual_seed(13)
+        layer = GatedRecurrentLayer(d_model=d).to(cuda)
+        g = torch.Generator(device=cuda).manual_seed(17)
+        x = torch.randn(B, L, d, device=cuda, generator=g).to(BF).requires_grad_()
+        gy = torch.randn(B, L, d, device=cuda, generator=g).to(BF)
+        y = layer(x)
+        assert y.dtype == BF
+        y.backward(gy)
+        torch.cuda.synchronize()
+    finally:
+        linear.set_bf16_gemm(prev)
+    assert nt_rows == [M] * 4, nt_rows
+    assert not tn_calls
+    assert wg == [(M, BF)] * 3, wg
+    rows = torch.tensor([0, 511, 1023], device=cuda)
+    params = {k: v.detach().cpu().requires_grad_() for k, v in layer.state_dict().items()}
+    xs = x.detach()[rows].float().cpu().requires_grad_()
+    ys = orc.grl_forward(params, "", xs)
+    (ys * gy[rows].float().cpu()).sum().backward()
+
+    def rel(a, b):
+        return ((a.float().cpu() - b).abs().max() / b.abs().max()).item()
+
+    tol = 1.2e-2
+    assert rel(y.detach()[rows], ys.detach()) < tol
+    assert rel(x.grad[rows], xs.grad) < tol
+    for n, p in layer.named_parameters():
+        assert p.grad.dtype == torch.float32 and torch.isfinite(p.grad).all(), n

@@ -135,6 +135,7 @@ def test_bpr_c3_matches_oracle(cuda, split_gemm_calls):
     assert len(split_gemm_calls) >= 12
 
 
+@pytest.mark.experimental
 @pytest.mark.parametrize("bwd", [False, True], ids=["fused_fwd", "fused_fwd_bwd"])
 @pytest.mark.parametrize("B,L", [(192, 200), (2048, 50)], ids=["C2", "C3"])
 def test_fused_grl_kernels_match_oracle(cuda, monkeypatch, B, L, bwd):

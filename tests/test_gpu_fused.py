@@ -13,7 +13,7 @@ exact."""
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.experimental]
 
 
 def _packed_batch(cuda, B, L, H, seed, fixed=False):

@@ -111,7 +111,8 @@ def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     """configs[4]'s GatedRecurrentLayer (d = 256, L = 2048) with
     RECBLR_BF16_GEMM=1 runs all three projections' forward, input-gradient and
     weight-gradient GEMMs on the bf16 kernels, the default per-shape mode
-    (auto) four of the nine, and both agree with the hipBLASLt path
+    (auto) four of the nine from BF16_NT_MIN_ROWS rows on (none below), and
+    both agree with the hipBLASLt path
     (RECBLR_BF16_GEMM=0) to bf16 accuracy."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
@@ -150,9 +151,17 @@ def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     assert calls == {"nt": 6, "tn": 3}, calls
     y0, dx0, g0 = run(False)
     assert calls == {"nt": 6, "tn": 3}
-    # the default per-shape mode: ours for the R <= 512 NT GEMMs (in / gates /
-    # out forward, out's input gradient); hipBLASLt for in.dX, gates.dX and
+    # the default per-shape mode below its row minimum (4,096 rows here):
+    # every GEMM on hipBLASLt, so the results equal the "0" run bit for bit
+    ys, dxs, gs = run("auto")
+    assert calls == {"nt": 6, "tn": 3}, calls
+    assert torch.equal(ys, y0) and torch.equal(dxs, dx0)
+    for n in g0:
+        assert torch.equal(gs[n], g0[n]), n
+    # ... and from the minimum on: ours for the R <= 512 NT GEMMs (in / gates
+    # / out forward, out's input gradient); hipBLASLt for in.dX, gates.dX and
     # the three weight gradients
+    monkeypatch.setattr(linear, "BF16_NT_MIN_ROWS", 4096)
     ya, dxa, ga = run("auto")
     assert calls == {"nt": 10, "tn": 3}, calls
 

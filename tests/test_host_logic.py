@@ -194,6 +194,7 @@ def test_bf16_gemm_modes_and_shape_rule(monkeypatch):
             linear.set_bf16_gemm("yes")
         assert linear._bf16_gemm == "auto"
         assert linear.BF16_NT_MAX_R == 512 and linear.BF16_TN_MAX_N == 0
+        assert linear.BF16_NT_MIN_ROWS == 65536
     finally:
         linear.set_bf16_gemm(prev)
 
@@ -344,3 +345,18 @@ def test_bit31_placement_keeps_the_whole_run_in_an_upper_half():
         assert a % 256 == 0
         assert (a >> 31) & 1 and (end >> 31) & 1 and (a >> 32) == (end >> 32), hex(base)
         assert off + need <= bit31_alloc_bytes(need)
+
+
+def test_ce_env_switches_are_checked(monkeypatch):
+    """RECBLR_CE_* switches are validated at import: an unknown value (e.g. the
+    removed CE_GRADS=fused) raises instead of silently choosing a slower
+    path, as RECBLR_GEMM / RECBLR_BF16_GEMM do."""
+    from datamining_recblr_amd import scoring
+
+    monkeypatch.setenv("RECBLR_CE_GRADS", "fused")
+    with pytest.raises(ValueError, match="RECBLR_CE_GRADS"):
+        scoring._env_choice("RECBLR_CE_GRADS", "f16", ("f16", "torch"))
+    monkeypatch.setenv("RECBLR_CE_GRADS", "torch")
+    assert scoring._env_choice("RECBLR_CE_GRADS", "f16", ("f16", "torch")) == "torch"
+    monkeypatch.delenv("RECBLR_CE_GRADS")
+    assert scoring._env_choice("RECBLR_CE_GRADS", "f16", ("f16", "torch")) == "f16"
