@@ -962,6 +962,24 @@ def main():
         ffn_act_ab["note"] = ("RECBLR_FFN_ACT A/B on the headline's batches: w_1 with "
                               "dropout(silu(.)) in its epilogue vs the GEMM and "
                               "rb_silu_dropout_fwd, best of 3 alternated runs each")
+    nt_ab = None
+    if not args.no_full_tail:
+        # rb_gemm_nt_h's kernel for the encoder's projections: the weight-
+        # stationary kernel (round 6, csrc/gemm_ws.hip) against round 5's
+        # persistent tiles, alternated 3x on the lease
+        from datamining_recblr_amd import linear as _lin
+        saved_w = _lin.set_nt_ws(True)
+        runs = {"weight_stationary": [], "persistent_tiles": []}
+        for _ in range(3):
+            for name, on in (("weight_stationary", True), ("persistent_tiles", False)):
+                _lin.set_nt_ws(on)
+                runs[name].append(timed_variant(True, True)["ms_per_step"])
+        _lin.set_nt_ws(saved_w)
+        nt_ab = {k: {"ms_per_step": min(v), "all": v} for k, v in runs.items()}
+        nt_ab["headline"] = "weight_stationary" if saved_w else "persistent_tiles"
+        nt_ab["note"] = ("RECBLR_NT_WS A/B on the headline's batches: the projections' forward "
+                         "/ input-gradient GEMMs from 16,384 rows on the weight-stationary "
+                         "kernel vs the persistent 256-row tiles; best of 3 alternated runs")
     order_ab = None
     if not args.no_full_tail:
         # the gate backward's consumers: the conv backward right behind the
@@ -1108,6 +1126,7 @@ def main():
             "ffn_act": ffn_act_ab,
             "adam": adam_ab,
             "bwd_order": order_ab,
+            "nt_kernel": nt_ab,
             "ddp_overhead": ddp_ab,
             "dense_batch": dense,
             "all_positions_tail": full_tail,

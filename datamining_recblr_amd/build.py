@@ -33,7 +33,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 # -ffp-contract=off: the reference scan is compiled with enable_fp_fusion=False
 # (parallel_scan.py:92) and its gate math is separate torch ops, so no FMA
 # contraction anywhere keeps our rounding close to it.
-FLAGS = ["-O3", "-std=c++17", "-shared", "-fPIC", f"--offload-arch={ARCH}",
+FLAGS = ["-O3", "-std=c++20", "-shared", "-fPIC", f"--offload-arch={ARCH}",
          "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
 
 

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 41; }
+int rb_version(void) { return 42; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -622,7 +622,11 @@ int rb_pack_plan(const int64_t* item_seq, int64_t seq_rs, const int64_t* seq_off
                           reinterpret_cast<hipStream_t>(stream));
 }
 
-int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R) { return C * R * 4 + ((C * 4 + 15) / 16) * 16; }
+int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R) {
+  // + the weight-stationary kernel's planes where it can run (R % 32 == 0)
+  return ws_image_offset(C, R) + (R % 32 == 0 ? C * R * 4 : 0);
+}
+int rb_gemm_nt_h_mode(int mode) { return gemm_nt_h_mode(mode); }
 
 int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {
   if (!jobs || n < 1 || n > RB_MAX_SPLIT_JOBS)

@@ -391,6 +391,15 @@ int launch_gemm_tn_bf16(const void* Y, int64_t ldy, const void* X, int64_t ldx, 
 int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
                      int K, const float* ymax, const float* xmax, float* parts, int S,
                      hipStream_t st);
+// byte offset of the weight-stationary kernel's planes inside an f16 weight
+// image of Bm [C, K] (after the persistent kernel's planes and the exponents)
+__host__ __device__ inline int64_t ws_image_offset(int64_t C, int64_t K) {
+  return C * K * 4 + ((C * 4 + 15) / 16) * 16;
+}
+bool nt_ws_ok(int64_t M, int K, int C, const float* A, int64_t lda, const float* out, int64_t ldo);
+int launch_gemm_nt_ws(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                      const float* bias, float* out, int64_t ldo, float* rmax, hipStream_t st);
+int gemm_nt_h_mode(int mode);
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st);

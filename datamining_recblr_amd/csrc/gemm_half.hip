@@ -180,6 +180,34 @@ __global__ void __launch_bounds__(256) k_split_weights_h(const SplitJobsH jobs) 
     dst[0] = o0;
     dst[64] = o1;
   }
+  // the weight-stationary kernel's image of the same 32 columns (gemm_ws.hip,
+  // v_mfma_f32_16x16x32_f16 operand order, same column exponents) at
+  // ws_image_offset(C, R): Wi[((c16 * KS + s) * 2 + p) * 64 + lane] = plane p
+  // of Bm[16 c16 + (lane & 15)][32 s + 8 (lane >> 4) + 0..7]
+  if (R % 32 == 0) {
+    f16x8* wi = reinterpret_cast<f16x8*>(reinterpret_cast<char*>(jobs.Wf[j]) + ws_image_offset(C, R));
+    const int KS = R / 32;
+    for (int it = tid; it < 2 * KS * 64; it += 256) {
+      const int h = it / (KS * 64), s = (it >> 6) % KS, lane = it & 63;
+      const int cl = 16 * h + (lane & 15);
+      const int c = cb * 32 + cl;
+      const int r0 = 32 * s + 8 * (lane >> 4);
+      const int sh = kTW - sexp[cl];
+      f16x8 o0, o1;
+#pragma unroll
+      for (int q = 0; q < 8; q += 2) {
+        const f32x2 x = {__builtin_amdgcn_ldexpf(bm(c, r0 + q), sh),
+                         __builtin_amdgcn_ldexpf(bm(c, r0 + q + 1), sh)};
+        f16x2 h0, h1;
+        split2h(x, h0, h1);
+        o0[q] = h0[0]; o0[q + 1] = h0[1];
+        o1[q] = h1[0]; o1[q + 1] = h1[1];
+      }
+      f16x8* dst = wi + ((int64_t)((2 * cb + h) * KS + s) * 2) * 64 + lane;
+      dst[0] = o0;
+      dst[64] = o1;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1352,10 +1380,25 @@ int launch_split_weights_h(const rb_split_job* jobs, int n, hipStream_t st) {
   return launch_status("rb_gemm_h_split_weights");
 }
 
+// Which kernel takes rb_gemm_nt_h's large-M calls (rb_gemm_nt_h_mode): 1 the
+// weight-stationary kernel (gemm_ws.hip, default since round 6), 0 the
+// persistent tiles below (A/B).  Below NT_WS_MIN_ROWS rows the launches here
+// (tail tiles, the few-rows kernel) keep every call: a weight-stationary
+// workgroup loads its 32 KB weight slice per wave before its first block.
+static int g_nt_mode = 1;
+constexpr int64_t NT_WS_MIN_ROWS = 16384;
+int gemm_nt_h_mode(int mode) {
+  const int prev = g_nt_mode;
+  if (mode == 0 || mode == 1) g_nt_mode = mode;
+  return prev;
+}
+
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st) {
   (void)accumulate;  // rejected by rb_gemm_nt_h
+  if (g_nt_mode == 1 && M >= NT_WS_MIN_ROWS && nt_ws_ok(M, R, C, A, lda, out, ldo))
+    return launch_gemm_nt_ws(A, lda, M, R, Wf, C, bias, out, ldo, rmax, st);
   const bool wide = (reinterpret_cast<uintptr_t>(out) & 15) == 0 && ldo % 4 == 0;
   const bool nb8 = wide && C % 256 == 0;
   // The persistent grid runs whole rounds of G tiles; the rows past the last

@@ -1083,6 +1083,23 @@ def gemm_nt_h(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | No
     return out
 
 
+def gemm_nt_h_mode(mode: int = -1) -> int:
+    """rb_gemm_nt_h's kernel for calls from 16,384 rows (rb_gemm_nt_h_mode):
+    1 weight-stationary (csrc/gemm_ws.hip), 0 persistent tiles; -1 queries.
+    Returns the previous mode."""
+    return int(_lib.load().rb_gemm_nt_h_mode(int(mode)))
+
+
+@contextlib.contextmanager
+def nt_h_mode(mode: int):
+    """Run a block with rb_gemm_nt_h_mode(mode), restoring the previous mode."""
+    prev = gemm_nt_h_mode(mode)
+    try:
+        yield
+    finally:
+        gemm_nt_h_mode(prev)
+
+
 def gemm_nt_h_act_ok(a: torch.Tensor, C: int) -> bool:
     """Whether gemm_nt_h_act takes a [M, R] operand with C outputs (freshly
     allocated contiguous outputs): rb_gemm_nt_h_act's shape contract."""

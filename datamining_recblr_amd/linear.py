@@ -33,7 +33,7 @@ import weakref
 
 import torch
 
-from . import gemm_tuning, kernels
+from . import _lib, gemm_tuning, kernels
 
 __all__ = ["linear", "wgrad", "LinearFn", "mm_nt", "mm_nn", "split_gemm_enabled",
            "HipLinearForward", "has_hooks", "fire_hooks"]
@@ -152,6 +152,34 @@ def gemm_format() -> str:
     return _GEMM if _split_on else "torch"
 
 
+# rb_gemm_nt_h's kernel for its large calls (>= 16,384 rows): the weight-
+# stationary kernel (csrc/gemm_ws.hip, round 6: the weight slice resident in
+# registers, A streamed once per column tile, exact row scales) or, with
+# RECBLR_NT_WS=0, round 5's persistent 256-row tiles (csrc/gemm_half.hip).
+_NT_WS = os.environ.get("RECBLR_NT_WS", "1")
+if _NT_WS not in ("0", "1"):
+    raise ValueError(f"RECBLR_NT_WS must be 0 or 1, got {_NT_WS!r}")
+_nt_ws_applied = None
+
+
+def _apply_nt_ws() -> None:
+    global _nt_ws_applied
+    if _nt_ws_applied != _NT_WS:
+        _lib.load().rb_gemm_nt_h_mode(int(_NT_WS))
+        _nt_ws_applied = _NT_WS
+
+
+def set_nt_ws(on: bool) -> bool:
+    """Select the weight-stationary NT kernel (True) or the persistent tiles
+    (False) for rb_gemm_nt_h's large calls (bench A/B); returns the previous
+    setting."""
+    global _NT_WS
+    prev = _NT_WS == "1"
+    _NT_WS = "1" if on else "0"
+    _apply_nt_ws()
+    return prev
+
+
 def rmax_wanted() -> bool:
     """Whether weight gradients take the f16 pipe's row-group maxima (rmax)."""
     return _half and _tn_on and _split_on
@@ -239,6 +267,7 @@ def mm_nt(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None,
         return torch.addmm(bias.to(a.dtype), a, wb.t()) if bias is not None else a @ wb.t()
     N, K = w.shape
     if _split_ok(a, N, K):
+        _apply_nt_ws()
         return kernels.gemm_nt_h(a, _weight_split(w, False), N, bias=bias, rmax=rmax)
     return torch.addmm(bias, a, w.t()) if bias is not None else torch.mm(a, w.t())
 
@@ -303,6 +332,7 @@ def mm_nn(dy: torch.Tensor, w: torch.Tensor, out: torch.Tensor | None = None,
         return out.addmm_(dy, wb) if out is not None else dy @ wb
     N, K = w.shape
     if _split_ok(dy, K, N):
+        _apply_nt_ws()
         r = kernels.gemm_nt_h(dy, _weight_split(w, True), K, rmax=rmax)
         return r if out is None else out.add_(r)
     if out is not None:

@@ -479,9 +479,12 @@ int rb_adam_step(const rb_adam_job* jobs, int64_t n, double lr, double beta1, do
  * fp16 parts, x = 2^-s (x0 + x1) (22 significant bits); the three products
  * a0b0 + a0b1 + a1b0 accumulate in fp32 (error vs fp64 within a few fp32
  * units, tests/test_gpu_gemm.py).  Weights: one scale per output column;
- * A rows: one scale per row, chosen online by the kernel.
+ * A rows: one scale per row (the weight-stationary kernel: from the row's
+ * exact max; the persistent kernel: chosen online).
  *
- * Bytes of the f16 weight image of Bm [C, R] (two planes + C exponents). */
+ * Bytes of the f16 weight image of Bm [C, R]: the persistent kernel's two
+ * planes, C exponents, then (R % 32 == 0) the weight-stationary kernel's two
+ * planes (csrc/gemm_ws.hip). */
 int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R);
 
 /* Build the f16 weight images of up to RB_MAX_SPLIT_JOBS weights in one
@@ -509,13 +512,22 @@ int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream);
  * accumulate must be 0.  rmax (optional, [ceil(M/32)] floats): max |A| over each
  * 32-row group, the operand scale of rb_gemm_tn_h on the same rows.  Replaces
  * nn.Linear's forward / input-gradient GEMM (RecBLR.py:162,165,167,213,214).
- * Whole rounds of 256-row tiles run on the persistent kernel; the rows past
- * the last whole round, and every row when M is below one round (the
- * gathered last-layer tail, B rows) or C % 128 != 0, on the few-rows kernel
- * (csrc/gemm_small.hip: exact per-row scales). */
+ * From 16,384 rows with R in {128, 256, 512}, C % 128 == 0, A and out 16-B
+ * aligned and lda, ldo multiples of 4: the weight-stationary kernel
+ * (csrc/gemm_ws.hip; rb_gemm_nt_h_mode).  Otherwise whole rounds of 256-row
+ * tiles run on the persistent kernel; the rows past the last whole round,
+ * and every row when M is below one round (the gathered last-layer tail, B
+ * rows) or C % 128 != 0, on the few-rows kernel (csrc/gemm_small.hip: exact
+ * per-row scales). */
 int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
                  const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                  void* stream);
+
+/* Which kernel takes rb_gemm_nt_h's calls from 16,384 rows: mode 1 the
+ * weight-stationary kernel (default), 0 the persistent 256-row tiles (A/B);
+ * any other value only queries.  Returns the previous mode.  Process-wide
+ * host setting (not per stream). */
+int rb_gemm_nt_h_mode(int mode);
 
 /* rb_gemm_nt_h with the FeedForward's activation in its epilogue
  * (RecBLR.py:219-221, w_1 then dropout(silu(.))): out = A Bm^T + bias and

@@ -244,7 +244,7 @@ def test_c5_bf16_full_batch_rows_match_oracle(cuda, monkeypatch):
     input and output gradient: y and dx rows within the 1.2e-2 bar of
     test_grl_bf16_vs_oracle (batch rows are independent in the layer, so the
     rows carry the full-batch GEMM dispatch's arithmetic)."""
-    from datamining_recblr_amd import kernels, linear
+    from datamining_recblr_amd import kernels, linear, recurrence
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     B, L, d = 1024, 2048, 256
@@ -255,9 +255,10 @@ def test_c5_bf16_full_batch_rows_match_oracle(cuda, monkeypatch):
                         lambda a, *r, **k: nt_rows.append(a.shape[0]) or nt0(a, *r, **k))
     monkeypatch.setattr(kernels, "gemm_tn_bf16",
                         lambda *a, **k: tn_calls.append(1) or tn0(*a, **k))
-    monkeypatch.setattr(linear, "wgrad",
-                        lambda dy2, x2, *a, **k: wg.append((dy2.shape[0], dy2.dtype))
-                        or wg0(dy2, x2, *a, **k))
+    counted = (lambda dy2, x2, *a, **k: wg.append((dy2.shape[0], dy2.dtype))
+               or wg0(dy2, x2, *a, **k))
+    monkeypatch.setattr(linear, "wgrad", counted)
+    monkeypatch.setattr(recurrence, "wgrad", counted)   # (imported by name there)
     prev = linear.set_bf16_gemm("auto")
     try:
         torch.manual_seed(13)

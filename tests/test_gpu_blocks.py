@@ -218,7 +218,7 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
     mm_nn_dact) == the GEMMs + rb_silu_dropout_fwd/bwd path, bit for bit: the
     output and every gradient but db1 (the w_1 bias gradient: the same
     values summed in another fixed order, within fp32 re-association)."""
-    from datamining_recblr_amd import linear
+    from datamining_recblr_amd import kernels, linear
     from datamining_recblr_amd.blocks import _FeedForward
 
     g = torch.Generator(device="cpu").manual_seed(22)
@@ -229,22 +229,30 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
             0.1 * torch.randn(d, generator=g)]
     dy = torch.randn(M, d, generator=g).to(cuda)
     res = []
-    for fused in (True, False):
+    # the fused epilogues ride on the persistent kernel (rb_gemm_nt_h_mode 0):
+    # bitwise against the unfused path on that kernel; the unfused path on
+    # the weight-stationary kernel (the default for the other projections)
+    # agrees at fp32 accuracy
+    for fused, mode in ((True, 0), (False, 0), (False, 1)):
         prev = linear.set_ffn_act_fused(fused)
         try:
-            leaves = [t.to(cuda).requires_grad_() for t in base]
-            assert linear.mm_nt_act_ok(leaves[0], leaves[1]) == fused
-            assert linear.mm_nn_dact_ok(dy, leaves[3]) == fused
-            y = _FeedForward.apply(*leaves, 41, 42, 0.2, 1e-12)
-            y.backward(dy)
-            res.append([y.detach()] + [t.grad for t in leaves])
+            with kernels.nt_h_mode(mode):
+                leaves = [t.to(cuda).requires_grad_() for t in base]
+                assert linear.mm_nt_act_ok(leaves[0], leaves[1]) == fused
+                assert linear.mm_nn_dact_ok(dy, leaves[3]) == fused
+                y = _FeedForward.apply(*leaves, 41, 42, 0.2, 1e-12)
+                y.backward(dy)
+                res.append([y.detach()] + [t.grad for t in leaves])
         finally:
             linear.set_ffn_act_fused(prev)
-    for name, u, v in zip(("y", "dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta"), *res):
+    names = ("y", "dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta")
+    for name, u, v in zip(names, res[0], res[1]):
         if name == "db1":
             close(u, v, atol=1e-6 * v.abs().max().item(), rtol=1e-5, what=name)
         else:
             assert torch.equal(u, v), name
+    for name, u, v in zip(names, res[2], res[1]):
+        close(u, v, atol=1e-5 * v.abs().max().item(), rtol=1e-5, what=name + " (ws)")
 
 
 def test_train_mode_dropout(cuda):

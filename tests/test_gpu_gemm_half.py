@@ -154,7 +154,8 @@ def test_fused_activation_epilogue(cuda, M, p, bias):
     r1 = torch.full((nr,), -1.0, device=cuda)
     r2 = torch.full((nr,), -1.0, device=cuda)
     out, act = kernels.gemm_nt_h_act(a, wi, C, b, seed=1234567, p=p, rmax=r1)
-    ref = kernels.gemm_nt_h(a, wi, C, bias=b, rmax=r2)
+    with kernels.nt_h_mode(0):   # the persistent kernel the fused epilogue rides on
+        ref = kernels.gemm_nt_h(a, wi, C, bias=b, rmax=r2)
     assert torch.equal(out, ref)
     assert torch.equal(act, kernels.silu_dropout_fwd(ref, seed=1234567, p=p))
     assert torch.equal(r1, r2)
@@ -188,7 +189,8 @@ def test_fused_activation_backward_epilogue(cuda, M, p):
     r1 = torch.full((nr,), -1.0, device=cuda)
     r2 = torch.full((nr,), -1.0, device=cuda)
     da, db = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p, rmax=r1)
-    du = kernels.gemm_nt_h(a, wi, C, rmax=r2)
+    with kernels.nt_h_mode(0):   # the persistent kernel the fused epilogue rides on
+        du = kernels.gemm_nt_h(a, wi, C, rmax=r2)
     da_ref, db_ref = kernels.silu_dropout_bwd(pre, du, seed=7654321, p=p, want_dbias=True)
     assert torch.equal(da, da_ref)
     assert torch.equal(r1, r2)
@@ -553,3 +555,125 @@ def test_weight_image_strided_views_and_column_exponents(cuda, C, R):
     wt = kernels.gemm_h_weight(bt, transpose=True)             # Bm = W^T
     assert torch.equal(wt.view(torch.int16),
                        kernels.gemm_h_weight(bt.t().contiguous()).view(torch.int16))
+
+
+# ---- the weight-stationary kernel (csrc/gemm_ws.hip; rb_gemm_nt_h from 16,384 rows)
+
+WS_SHAPES = [(128, 512), (512, 128), (256, 512), (512, 256), (256, 128), (128, 256)]
+
+
+def _adversarial_rows(a):
+    """rows over 2^+-60, zero rows, zero / tiny prefixes (the persistent
+    kernel's recompute tail), growth by 2^32 along K, a 3e30 entry"""
+    M, K = a.shape
+    g = torch.Generator().manual_seed(M + K)
+    a *= torch.exp2(torch.randint(-60, 60, (M, 1), generator=g).float())
+    a[5] = 0
+    a[6, :K // 4] = 0
+    a[7, :16] *= 1e-12
+    a[8] = torch.randn(K, generator=g) * torch.exp2(torch.arange(K).float() * (32.0 / K))
+    a[9] = torch.randn(K, generator=g)
+    a[9, K // 2] = 3e30
+    a[31] = 0
+    a[32] = 0
+    a[32, K - 1] = 1e-30
+    a[M - 1] = torch.randn(K, generator=g) * 2.0 ** 40
+    return a
+
+
+@pytest.mark.parametrize("R,C", WS_SHAPES)
+@pytest.mark.parametrize("M", [16384, 16384 + 32 * 257 + 5, 204632])
+def test_ws_kernel_matches_fp64_per_row(cuda, R, C, M):
+    """The encoder's projection shapes on the weight-stationary kernel: every
+    output element of 600 sampled rows (the block edges, the partial last
+    block, adversarial rows) within fp32 accuracy of fp64 relative to
+    sum |a||b| (the dot product's own rounding scale), on a par with
+    hipBLASLt's fp32 GEMM on the same rows; bias; rmax exact; rows past M
+    untouched; the persistent kernel (mode 0) agrees at the same bar."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(M + R + C)
+    a = _adversarial_rows(torch.randn(M, R, generator=g))
+    w = torch.randn(C, R, generator=g) / R ** 0.5
+    w[3] *= 1e-25
+    w[5] = 0
+    b = torch.randn(C, generator=g)
+    a, w, b = a.to(cuda), w.to(cuda), b.to(cuda)
+    wi = kernels.gemm_h_weight(w)
+    outbig = torch.full((M + 3, C), 7.0, device=cuda)
+    out = outbig[:M]
+    nr = (M + 31) // 32
+    rmax = torch.full((nr,), -1.0, device=cuda)
+    assert kernels.gemm_nt_h_mode() == 1
+    kernels.gemm_nt_h(a, wi, C, bias=b, out=out, rmax=rmax)
+    assert (outbig[M:] == 7.0).all()
+    ref_rmax = torch.nn.functional.pad(a.abs().amax(1), (0, (-M) % 32)).view(-1, 32).amax(1)
+    assert torch.equal(rmax, ref_rmax)
+    rows = torch.cat([torch.arange(0, 40), torch.arange(M - 40, M),
+                      torch.randint(0, M, (520,), generator=g)]).unique()
+    ad, wd = a[rows].double().cpu(), w.double().cpu()
+    ref = ad @ wd.t() + b.double().cpu()
+    den = ad.abs() @ wd.abs().t() + b.double().cpu().abs()
+    ok = den > 1e-30
+    y = out[rows].double().cpu()
+    yt = (a[rows] @ w.t() + b).double().cpu()
+    e_h = ((y - ref).abs() / den)[ok].max().item()
+    e_t = ((yt - ref).abs() / den)[ok].max().item()
+    assert torch.isfinite(out).all()
+    assert e_h < 4 * max(e_t, 6e-8), (e_h, e_t)
+    with kernels.nt_h_mode(0):
+        y0 = kernels.gemm_nt_h(a, wi, C, bias=b)[rows].double().cpu()
+    assert (((y0 - ref).abs() / den)[ok].max().item()) < 4 * max(e_t, 6e-8)
+
+
+def test_ws_kernel_non_finite_rows_and_transpose(cuda):
+    """inf / NaN entries poison exactly their rows (as the fp32 GEMM's,
+    NaN where it gives +-inf); the transposed weight image (the dX GEMM's
+    Bm = W^T) gives the same outputs as the image of the materialised
+    transpose; bitwise deterministic; differs from the persistent kernel only
+    at rounding level (so the two kernels are distinct launches)."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(17)
+    M, N, K = 40000 + 13, 512, 256       # dY [M, N] @ W [N, K]
+    dy = torch.randn(M, N, generator=g)
+    bad = [3, 33, 20000, M - 1]
+    dy[3, 7] = float("inf")
+    dy[33, 0] = -float("inf")
+    dy[20000, 300] = float("nan")
+    dy[M - 1, 511] = float("inf")
+    dy = dy.to(cuda)
+    w = (torch.randn(N, K, generator=g) / N ** 0.5).to(cuda)
+    wt = kernels.gemm_h_weight(w, transpose=True)
+    dx = kernels.gemm_nt_h(dy, wt, K)
+    bits = lambda t: t.view(torch.int32)   # noqa: E731 (NaN rows compare by bits)
+    assert torch.equal(bits(dx), bits(kernels.gemm_nt_h(dy, kernels.gemm_h_weight(w.t().contiguous()), K)))
+    assert torch.equal(bits(dx), bits(kernels.gemm_nt_h(dy, wt, K)))
+    ref = dy @ w
+    assert torch.equal(torch.isfinite(dx), torch.isfinite(ref))
+    good = torch.ones(M, dtype=torch.bool, device=cuda)
+    good[bad] = False
+    assert not torch.isfinite(dx[~good]).any()
+    r64 = dy[good].double() @ w.double()
+    assert _rel_err(dx[good], r64) < 2e-6
+    with kernels.nt_h_mode(0):
+        dx0 = kernels.gemm_nt_h(dy, wt, K)
+    assert not torch.equal(dx0[good], dx[good])
+    assert _rel_err(dx0[good], r64) < 2e-6
+
+
+def test_ws_kernel_row_strided_views(cuda):
+    """A as the z half of an [M, 2H] activation (row stride 2H), out a
+    column slice of a wider buffer (the dxz halves the encoder hands over)."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(23)
+    M = 30000
+    big = torch.randn(M, 512, generator=g).to(cuda)
+    x = big[:, 256:]
+    w = (torch.randn(256, 256, generator=g) / 16).to(cuda)
+    outbig = torch.zeros(M, 512, device=cuda)
+    out = outbig[:, 256:]
+    kernels.gemm_nt_h(x, kernels.gemm_h_weight(w), 256, out=out)
+    assert _rel_err(out, x.double() @ w.double().t()) < 2e-6
+    assert outbig[:, :256].abs().max().item() == 0.0
