@@ -400,6 +400,14 @@ bool nt_ws_ok(int64_t M, int K, int C, const float* A, int64_t lda, const float*
 int launch_gemm_nt_ws(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
                       const float* bias, float* out, int64_t ldo, float* rmax, hipStream_t st);
 int gemm_nt_h_mode(int mode);
+bool nt_ws_act_ok(int64_t M, int K, int C, const float* A, int64_t lda, const float* out,
+                  const float* other, int64_t ldo);
+int launch_gemm_nt_ws_act(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                          const float* bias, float* out, int64_t ldo, float* rmax, float* act,
+                          DropSpec drop, hipStream_t st);
+int launch_gemm_nt_ws_dact(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                           float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
+                           float* dpart, int64_t n_parts, hipStream_t st);
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st);

@@ -1497,6 +1497,8 @@ constexpr int ACT_NB = 8;
 int launch_gemm_nt_h_act(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                          const float* bias, float* out, int64_t ldo, float* rmax, float* act,
                          DropSpec drop, hipStream_t st) {
+  if (g_nt_mode == 1 && M >= NT_WS_MIN_ROWS && nt_ws_act_ok(M, R, C, A, lda, out, act, ldo))
+    return launch_gemm_nt_ws_act(A, lda, M, R, Wf, C, bias, out, ldo, rmax, act, drop, st);
   if (!nt_h_act_ok(M, R, C, out, act, ldo))
     return fail("rb_gemm_nt_h_act: shape or alignment without a wide-epilogue launch");
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);
@@ -1549,6 +1551,8 @@ int64_t nt_h_dact_parts() { return 2 * (int64_t)(num_cus() / 8 * 8 * (8 / N_WAVE
 int launch_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                           float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
                           float* dpart, int64_t n_parts, hipStream_t st) {
+  if (g_nt_mode == 1 && M >= NT_WS_MIN_ROWS && nt_ws_act_ok(M, R, C, A, lda, out, pre, ldo))
+    return launch_gemm_nt_ws_dact(A, lda, M, R, Wf, C, out, ldo, rmax, pre, drop, dpart, n_parts, st);
   if (!nt_h_act_ok(M, R, C, out, pre, ldo) || C > N_DACT_MAXC)
     return fail("rb_gemm_nt_h_dact: shape or alignment without a wide-epilogue launch");
   const int G0 = num_cus() / 8 * 8 * (8 / N_WAVES);

@@ -165,14 +165,24 @@ __device__ __forceinline__ void wait_vm() {
 //   exps: int32 e_c at byte offset C * K * 4 (shared with the persistent
 //   kernel's image: the same column exponents)
 // ABL (timing-only ablations, results not meaningful): 1 no MFMAs, 2 no
-// split (loads still waited), 4 no stores, 8 no A loads
-template <int K, int NCB, int D, bool BIAS, bool DEFER, int ABL>
+// split (loads still waited), 4 no stores, 8 no A loads, 16 no fragment reads.
+// EPI: 0 out (+ bias); 1 (ACT, the FeedForward's w_1, RecBLR.py:219-221)
+// out = A Bm^T + bias and act = dropout(silu(out)) — the keep-flags drop's
+// Philox stream at element index row * C + col, as rb_silu_dropout_fwd draws
+// them; 2 (DACT, its backward fused into dU = dA2 W_2) out = dU * keep *
+// scale * silu'(pre), dU never stored, and the columns' sums of out per
+// workgroup into dpart (the w_1 bias gradient's partials, a fixed order).
+template <int K, int NCB, int D, bool BIAS, bool DEFER, int ABL, int EPI = 0>
 __global__ void __launch_bounds__(THREADS, 1)
 k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* __restrict__ Wi,
              const int* __restrict__ ew, int C, const float* __restrict__ bias,
-             float* __restrict__ out, int64_t ldo, float* __restrict__ rmax) {
+             float* __restrict__ out, int64_t ldo, float* __restrict__ rmax,
+             float* __restrict__ act, DropSpec drop, const float* __restrict__ pre,
+             float* __restrict__ dpart) {
   using CF = Cfg<K, NCB, D>;
   constexpr int KS = CF::KS, WC = CF::WC, NT = CF::NT, NLD = CF::NLD, NST = CF::NST;
+  constexpr int NSTT = EPI == 1 ? 2 * NST : NST;   // stores per block (ACT: out and act)
+  constexpr int NPRE = EPI == 2 ? 2 * NCB : 0;     // DACT: `pre` loads per block
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -187,7 +197,13 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   const int64_t rb0 = (int64_t)(bid / (8 * nct)) * 8 + (bid & 7);
   const int64_t rbs = (int64_t)(G / (8 * nct)) * 8;
   const int nb = rb0 < nrb ? (int)((nrb - 1 - rb0) / rbs + 1) : 0;
-  if (nb == 0) return;
+  // DACT: this workgroup's row of dpart among its column tile's G / nct
+  const int64_t prow = (int64_t)(bid / (8 * nct)) * 8 + (bid & 7);
+  if (nb == 0) {
+    if constexpr (EPI == 2)
+      for (int c = tid; c < NT; c += THREADS) dpart[prow * C + ct * NT + c] = 0.0f;
+    return;
+  }
 
   const uint32_t sbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)smem;
   const uint32_t s_info = sbase + CF::INFO;   // [2][RB] exps, then [2][RB] maxima
@@ -224,12 +240,12 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
     woff[j] = (uint32_t)(((rb16 * KS + s) * 2) * 1024 + pos * 16 + half * 8);
   }
   f32x4 ra[CF::STG ? 1 : D][NLD];
-  auto blk_r0 = [&](int b) -> int64_t { return (rb0 + (int64_t)b * rbs) * RB; };
+  auto blk_r0 = [&](int b) __attribute__((always_inline)) -> int64_t { return (rb0 + (int64_t)b * rbs) * RB; };
   // wave-uniform buffer descriptor over rows [r0, r0 + n) of a row-major
   // matrix (readfirstlane returns int: through uint32_t, or the low word's
   // sign would extend into the high one); lane offsets past the range read
   // zeros / drop the store, so rows past M need no clamp or branch
-  auto rsrc_of = [&](const float* p, int64_t r0, int64_t ld) {
+  auto rsrc_of = [&](const float* p, int64_t r0, int64_t ld) __attribute__((always_inline)) {
     const uint64_t u = reinterpret_cast<uint64_t>(p + r0 * ld);
     const uint64_t ub = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u) |
                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32);
@@ -238,10 +254,12 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   };
   const uint32_t a_voff = (uint32_t)(my_row * lda * 4) + (uint32_t)(lane & 15) * 16;
   const uint32_t s_stage = sbase + CF::STAGE;   // [D][WAVES][NLD] 1-KB DMA pieces (STG)
-  auto stage_of = [&](int set) -> uint32_t { return s_stage + (uint32_t)((set * WAVES + wave) * NLD) * 1024; };
-  auto issue = [&](int b, f32x4 (&dst)[NLD], int set) {
+  auto stage_of = [&](int set) __attribute__((always_inline)) -> uint32_t { return s_stage + (uint32_t)((set * WAVES + wave) * NLD) * 1024; };
+  auto issue = [&](int b, f32x4 (&dst)[NLD], int set) __attribute__((always_inline)) {
     if constexpr ((ABL & 8) != 0) return;
     const auto rs = rsrc_of(A, blk_r0(b), lda);
+    // (a compiler barrier after the batch, below: no later vector-memory op
+    // may be hoisted above these, or the hand-counted waits would be short)
     if constexpr (CF::STG) {
       // lane l's 16 B of piece j land at stage + j KB + 16 l (M0 = the wave's
       // piece base): the lane that loaded them reads them back
@@ -254,11 +272,12 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
       for (int j = 0; j < NLD; ++j)
         dst[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, a_voff + j * 256, 0, 0));
     }
+    asm volatile("" ::: "memory");
   };
 
   // split of the block whose raw data is in src into image buffer ib: the
   // lane's row max over its chunks, then over the row's 16 lanes (DPP)
-  auto split = [&](f32x4 (&src)[NLD], int ib, int set) {
+  auto split = [&](f32x4 (&src)[NLD], int ib, int set) __attribute__((always_inline)) {
     if constexpr (CF::STG) {
 #pragma unroll
       for (int j = 0; j < NLD; ++j) src[j] = lds_read16<f32x4>(stage_of(set) + j * 1024 + lane * 16);
@@ -304,7 +323,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   // accumulators: acc[r][cb] = the block's rows 16 r + l % 16 (one per lane),
   // columns 16 cb + 4 (l / 16) + 0..3 (the weight slice is the first operand)
   f32x4 acc[2][NCB];
-  auto multiply = [&](int ib, auto&& hook) {
+  auto multiply = [&](int ib, auto&& hook) __attribute__((always_inline)) {
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -312,14 +331,14 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
     if constexpr ((ABL & 1) != 0) return;
     const uint32_t img = sbase + ib * CF::IMG;
     f16x8 fa[2][2];   // (plane 0, plane 1) of one (step, rb16) unit, two slots
-    auto rd = [&](auto uc, int t) {   // unit u = 2 s + r
+    auto rd = [&](auto uc, int t) __attribute__((always_inline)) {   // unit u = 2 s + r
       constexpr int u = decltype(uc)::value, s = u >> 1, r = u & 1;
       const uint32_t a = img + rpos[s & 3];
       fa[t][0] = lds_read16o<((r * KS + s) * 2 + 0) * 1024, f16x8>(a);
       fa[t][1] = lds_read16o<((r * KS + s) * 2 + 1) * 1024, f16x8>(a);
     };
     rd(std::integral_constant<int, 0>{}, 0);
-    auto unit = [&](auto uc) {
+    auto unit = [&](auto uc) __attribute__((always_inline)) {
       constexpr int u = decltype(uc)::value, t = u & 1, s = u >> 1, r = u & 1;
       if constexpr ((ABL & 16) != 0) {
         // timing ablation: no fragment reads past the first unit
@@ -339,7 +358,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
       }
       hook(uc);
     };
-    [&]<int... U>(std::integer_sequence<int, U...>) {
+    [&]<int... U>(std::integer_sequence<int, U...>) __attribute__((always_inline)) {
       (unit(std::integral_constant<int, U>{}), ...);
     }(std::make_integer_sequence<int, 2 * KS>{});
   };
@@ -368,11 +387,39 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
     }
   }
   __amdgpu_buffer_rsrc_t pending_rs = rsrc_of(out, M, ldo);   // no records: dummy stores
-  auto flush = [&](int i) {
-    if constexpr ((ABL & 4) == 0)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[i]), pending_rs, soff[i], 0, 2);
+  f32x4 pend2[EPI == 1 ? NST : 1];                            // ACT: act in store layout
+  __amdgpu_buffer_rsrc_t pending_act = rsrc_of(EPI == 1 ? act : out, M, ldo);
+  auto flush = [&](int i) __attribute__((always_inline)) {
+    if constexpr ((ABL & 4) == 0) {
+      if (i < NST)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[i]), pending_rs, soff[i], 0, 2);
+      else if constexpr (EPI == 1)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend2[i - NST]), pending_act,
+                                               soff[i - NST], 0, 2);
+    }
   };
-  auto finish = [&](int b, int ib) {
+  // DACT: the block's `pre` values at the lane's accumulator positions (row
+  // 16 r + l % 16, columns 16 cb + 4 (l / 16) ..), loaded when the block's
+  // MFMAs start; the lane's running column sums of out
+  f32x4 prv[EPI == 2 ? 2 : 1][EPI == 2 ? NCB : 1];
+  f32x4 csum[EPI == 2 ? NCB : 1];
+  if constexpr (EPI == 2)
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) csum[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  auto load_pre = [&](int b) __attribute__((always_inline)) {
+    if constexpr (EPI == 2) {
+      const auto rs = rsrc_of(pre, blk_r0(b), ldo);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+          prv[r][cb] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+              rs, (uint32_t)((16 * r + (lane & 15)) * ldo4) + (uint32_t)(col0 + 16 * cb + 4 * (lane >> 4)) * 4,
+              0, 0));
+      asm volatile("" ::: "memory");
+    }
+  };
+  auto finish = [&](int b, int ib) __attribute__((always_inline)) {
     const int64_t r0 = blk_r0(b);
     // the lane's two rows' exponents; its columns' exponents and bias read
     // per pair of column blocks (fewer live registers)
@@ -400,16 +447,35 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         f32x4 v[NG];
+        f32x4 av[NG];   // ACT: dropout(silu(v))
+        const int64_t row = r0 + 16 * r + (lane & 15);
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NG; ++g) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             v[g][i] = __builtin_amdgcn_ldexpf(acc[r][NG * q + g][i], er[r] + ec[g][i]);
             if (BIAS) v[g][i] += bc[g][i];
           }
+          if constexpr (EPI != 0) {
+            // keep-flags of the lane's 4 consecutive columns (element index a
+            // multiple of 4: C % 4 == 0)
+            float mk[4];
+            drop.get4(row * C + col0 + 16 * (NG * q + g) + 4 * (lane >> 4), mk);
+            if constexpr (EPI == 1) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) av[g][i] = fsilu(v[g][i]) * mk[i];
+            } else {
+              const f32x4 pv = prv[r][NG * q + g];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[g][i] = (v[g][i] * mk[i]) * fdsilu(pv[i] + 0.0f);
+              csum[NG * q + g] += v[g];   // rows past M: du = 0, pre = 0 -> 0
+            }
+          }
+        }
         if constexpr (NG == 1) {
           // lane: row 16 r + l % 16, columns 4 (l / 16) .. + 3: 64-B row pieces
           pend[r] = v[0];
+          if constexpr (EPI == 1) pend2[r] = av[0];
         } else {
           // blocks 2q, 2q + 1 = 32 columns: lanes with (l & 8) take the other
           // block's value from 8 lanes away (DPP row_ror:8, bank-masked), so
@@ -428,15 +494,27 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
           }
           pend[(q * 2 + r) * 2] = x1;
           pend[(q * 2 + r) * 2 + 1] = x2;
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float f0 = av[0][i], f1 = av[1][i];
+              const int a0 = __float_as_int(f0), a1 = __float_as_int(f1);
+              x1[i] = __int_as_float(__builtin_amdgcn_update_dpp(a0, a1, 0x128, 0xF, 0xC, false));
+              x2[i] = __int_as_float(__builtin_amdgcn_update_dpp(a1, a0, 0x128, 0xF, 0x3, false));
+            }
+            pend2[(q * 2 + r) * 2] = x1;
+            pend2[(q * 2 + r) * 2 + 1] = x2;
+          }
         }
       }
     }
     pending_rs = rsrc_of(out, r0, ldo);   // nt stores (aux 2), rows past M dropped
+    if constexpr (EPI == 1) pending_act = rsrc_of(act, r0, ldo);
   };
   // rmax: the block's max |A| (its rows' maxima from the split), stored by
   // wave 0 of column tile 0.  Every wave runs this and issues the store (a
   // zero-record descriptor drops it): no branch around a store
-  auto rmax_store = [&](int b, int ib) {
+  auto rmax_store = [&](int b, int ib) __attribute__((always_inline)) {
     const int64_t r0 = blk_r0(b);
     float x = 0.0f;
     if (lane < RB)
@@ -453,7 +531,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
 
   // ---- prologue: blocks 0 .. D - 1 in flight, block 0 split
   // (STG: the raw sets are LDS pieces, ra[0] is only the split's scratch)
-  [&]<int... P>(std::integer_sequence<int, P...>) {
+  [&]<int... P>(std::integer_sequence<int, P...>) __attribute__((always_inline)) {
     (issue(P, ra[CF::STG ? 0 : P], P), ...);
   }(std::make_integer_sequence<int, D>{});
   if constexpr (CF::STG) wait_vm<(D - 1) * NLD>();   // block 0's pieces landed
@@ -476,14 +554,14 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   // K = 512 (registers): the compiler waits for its own loads.
   // One block: P = b % D (compile time: the raw register sets are never
   // indexed at run time); LATE: split block b + 1 after the MFMAs.
-  auto loop = [&](auto late_c) {
+  auto loop = [&](auto late_c) __attribute__((always_inline)) {
     constexpr bool LATE = decltype(late_c)::value;
-    constexpr int YS = (LATE ? D : D - 1) * (NST + 1) + (D - 1) * NLD;
-    constexpr int Y0 = (D - 1) * NLD + (LATE ? NST + 1 : 0);
-    auto body = [&](int b, auto par) {
+    constexpr int YS = (LATE ? D : D - 1) * (NSTT + 1) + D * NPRE + (D - 1) * NLD;
+    constexpr int Y0 = (D - 1) * NLD + NPRE + (LATE ? NSTT + 1 : 0);
+    auto body = [&](int b, auto par) __attribute__((always_inline)) {
       constexpr int P = decltype(par)::value;
       const int ib = b & 1;
-      auto do_split = [&]() {
+      auto do_split = [&]() __attribute__((always_inline)) {
         if constexpr (CF::STG) {
           if (b >= D - 1) wait_vm<(YS > 63 ? 63 : YS)>();
           else wait_vm<(Y0 > 63 ? 63 : Y0)>();
@@ -491,22 +569,24 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
         split(ra[CF::STG ? 0 : (P + 1) % D], ib ^ 1, (P + 1) % D);
       };
       issue(b + D, ra[CF::STG ? 0 : P], P);   // into the set block b held (split in iteration b - 1)
+      load_pre(b);
       if constexpr (!LATE) do_split();
       if constexpr (DEFER) {
         // block b - 1's stores (dummies before block 0) between this block's
         // MFMA units, then its rmax word
-        constexpr int U = 2 * KS, STEP = U / NST;
-        multiply(ib, [&](auto uc) {
+        constexpr int U = 2 * KS, STEP = U / NSTT;
+        static_assert(STEP >= 1, "more stores than MFMA units");
+        multiply(ib, [&](auto uc) __attribute__((always_inline)) {
           constexpr int u = decltype(uc)::value;
-          if constexpr (u % STEP == 0 && u / STEP < NST) flush(u / STEP);
+          if constexpr (u % STEP == 0 && u / STEP < NSTT) flush(u / STEP);
         });
         rmax_store(b, ib);
         finish(b, ib);
       } else {
-        multiply(ib, [](auto) {});
+        multiply(ib, [](auto) __attribute__((always_inline)) {});
         finish(b, ib);
 #pragma unroll
-        for (int i = 0; i < NST; ++i) flush(i);
+        for (int i = 0; i < NSTT; ++i) flush(i);
         rmax_store(b, ib);
       }
       if constexpr (LATE) do_split();
@@ -514,7 +594,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
       __builtin_amdgcn_s_barrier();
     };
     for (int b = 0; b < nb; b += D) {
-      [&]<int... P>(std::integer_sequence<int, P...>) {
+      [&]<int... P>(std::integer_sequence<int, P...>) __attribute__((always_inline)) {
         (body(b + P, std::integral_constant<int, P>{}), ...);
       }(std::make_integer_sequence<int, D>{});
     }
@@ -523,22 +603,42 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   else loop(std::false_type{});
   if constexpr (DEFER) {
 #pragma unroll
-    for (int i = 0; i < NST; ++i) flush(i);   // the last block's results
+    for (int i = 0; i < NSTT; ++i) flush(i);   // the last block's results
+  }
+  if constexpr (EPI == 2) {
+    // the wave's column sums: the lane's rows, then the 16 lanes of each
+    // 4-column group (DPP, a fixed tree); lanes 0, 16, 32, 48 write them
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float x = csum[cb][i];
+        x += dpp_x1(x);
+        x += dpp_x2(x);
+        x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x124, 0xF, 0xF, false));
+        x += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x128, 0xF, 0xF, false));
+        csum[cb][i] = x;
+      }
+      if ((lane & 15) == 0)
+        *reinterpret_cast<f32x4*>(dpart + prow * C + col0 + 16 * cb + 4 * (lane >> 4)) = csum[cb];
+    }
   }
 }
 
-template <int K, int NCB, int D, bool BIAS, bool DEFER, int ABL>
+template <int K, int NCB, int D, bool BIAS, bool DEFER, int ABL, int EPI = 0>
 void run(const float* A, int64_t lda, int64_t M, const void* Wi, const int* ew, int C,
-         const float* bias, float* out, int64_t ldo, float* rmax, int grid, hipStream_t st) {
+         const float* bias, float* out, int64_t ldo, float* rmax, int grid, hipStream_t st,
+         float* act = nullptr, DropSpec drop = DropSpec{}, const float* pre = nullptr,
+         float* dpart = nullptr) {
   using CF = Cfg<K, NCB, D>;
   static bool done = false;   // benign race: idempotent
   if (!done) {
-    (void)hipFuncSetAttribute((const void*)k_gemm_nt_ws<K, NCB, D, BIAS, DEFER, ABL>,
+    (void)hipFuncSetAttribute((const void*)k_gemm_nt_ws<K, NCB, D, BIAS, DEFER, ABL, EPI>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS);
     done = true;
   }
-  k_gemm_nt_ws<K, NCB, D, BIAS, DEFER, ABL><<<grid, THREADS, CF::LDS, st>>>(
-      A, lda, M, (const f16x8*)Wi, ew, C, bias, out, ldo, rmax);
+  k_gemm_nt_ws<K, NCB, D, BIAS, DEFER, ABL, EPI><<<grid, THREADS, CF::LDS, st>>>(
+      A, lda, M, (const f16x8*)Wi, ew, C, bias, out, ldo, rmax, act, drop, pre, dpart);
 }
 
 // prefetch depth per K (blocks of A in flight): the LDS-DMA sets that fit
@@ -594,6 +694,48 @@ int launch_gemm_nt_ws(const float* A, int64_t lda, int64_t M, int K, const void*
   else if (K == 256 && ncb == 1) go(integral_constant<int, 256>{}, integral_constant<int, 1>{});
   else go(integral_constant<int, 512>{}, integral_constant<int, 1>{});
   return launch_status("rb_gemm_nt_h");
+}
+
+// The FeedForward's fused activation on this kernel (EPI 1 / 2): K = 128 only
+// (w_1 forward, 128 -> 4d; the dU GEMM, 128 -> 4d), two 16-column blocks per
+// wave (the second output or the `pre` operand needs the registers of the
+// other two)
+bool nt_ws_act_ok(int64_t M, int K, int C, const float* A, int64_t lda, const float* out,
+                  const float* other, int64_t ldo) {
+  return K == 128 && C % 256 == 0 && nt_ws_ok(M, K, C, A, lda, out, ldo) && aligned16(other);
+}
+
+int launch_gemm_nt_ws_act(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                          const float* bias, float* out, int64_t ldo, float* rmax, float* act,
+                          DropSpec drop, hipStream_t st) {
+  if (!nt_ws_act_ok(M, K, C, A, lda, out, act, ldo)) return fail("rb_gemm_nt_h_act: shape");
+  const void* Wi = reinterpret_cast<const char*>(Wf) + ws_image_offset(C, K);
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * K * 4);
+  const int grid = ws::grid_for(M, C, 2);
+  if (bias) ws::run<128, 2, ws::depth<128>(), true, true, 0, 1>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, st, act, drop);
+  else ws::run<128, 2, ws::depth<128>(), false, true, 0, 1>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, st, act, drop);
+  return launch_status("rb_gemm_nt_h_act");
+}
+
+// dpart [n_parts, C]: the workgroups of each column tile write rows
+// [0, grid / column tiles); the rest are zeroed here
+int launch_gemm_nt_ws_dact(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                           float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
+                           float* dpart, int64_t n_parts, hipStream_t st) {
+  if (!nt_ws_act_ok(M, K, C, A, lda, out, pre, ldo)) return fail("rb_gemm_nt_h_dact: shape");
+  const void* Wi = reinterpret_cast<const char*>(Wf) + ws_image_offset(C, K);
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * K * 4);
+  const int grid = ws::grid_for(M, C, 2);
+  const int64_t used = grid / (C / 256);
+  if (used > n_parts) return fail("rb_gemm_nt_h_dact: dpart has too few rows");
+  ws::run<128, 2, ws::depth<128>(), false, true, 0, 2>(A, lda, M, Wi, ew, C, nullptr, out, ldo, rmax, grid,
+                                                      st, nullptr, drop, pre, dpart);
+  const int rc = launch_status("rb_gemm_nt_h_dact");
+  if (rc) return rc;
+  if (used < n_parts &&
+      hipMemsetAsync(dpart + used * C, 0, (size_t)(n_parts - used) * C * 4, st) != hipSuccess)
+    return fail("rb_gemm_nt_h_dact: hipMemsetAsync failed");
+  return 0;
 }
 
 }  // namespace rb

@@ -229,11 +229,10 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
             0.1 * torch.randn(d, generator=g)]
     dy = torch.randn(M, d, generator=g).to(cuda)
     res = []
-    # the fused epilogues ride on the persistent kernel (rb_gemm_nt_h_mode 0):
-    # bitwise against the unfused path on that kernel; the unfused path on
-    # the weight-stationary kernel (the default for the other projections)
-    # agrees at fp32 accuracy
-    for fused, mode in ((True, 0), (False, 0), (False, 1)):
+    # fused vs unfused, bitwise on either NT kernel (rb_gemm_nt_h_mode 0: the
+    # persistent tiles; 1: the weight-stationary kernel, EPI 1 / 2, from
+    # 16,384 rows); the two kernels agree at fp32 accuracy
+    for fused, mode in ((True, 0), (False, 0), (True, 1), (False, 1)):
         prev = linear.set_ffn_act_fused(fused)
         try:
             with kernels.nt_h_mode(mode):
@@ -246,12 +245,13 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
         finally:
             linear.set_ffn_act_fused(prev)
     names = ("y", "dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta")
-    for name, u, v in zip(names, res[0], res[1]):
-        if name == "db1":
-            close(u, v, atol=1e-6 * v.abs().max().item(), rtol=1e-5, what=name)
-        else:
-            assert torch.equal(u, v), name
-    for name, u, v in zip(names, res[2], res[1]):
+    for f, u_ in ((0, 1), (2, 3)):
+        for name, u, v in zip(names, res[f], res[u_]):
+            if name == "db1":
+                close(u, v, atol=1e-6 * v.abs().max().item(), rtol=1e-5, what=name)
+            else:
+                assert torch.equal(u, v), name
+    for name, u, v in zip(names, res[3], res[1]):
         close(u, v, atol=1e-5 * v.abs().max().item(), rtol=1e-5, what=name + " (ws)")
 
 

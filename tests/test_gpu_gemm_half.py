@@ -127,9 +127,10 @@ def test_non_finite_rows(cuda, N):
     assert _rel_err(y[good.to(cuda)], ref) < 2e-6
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["persistent", "weight_stationary"])
 @pytest.mark.parametrize("M", [5000, 70001, 196608 + 8024])
 @pytest.mark.parametrize("p,bias", [(0.0, True), (0.2, True), (0.2, False)])
-def test_fused_activation_epilogue(cuda, M, p, bias):
+def test_fused_activation_epilogue(cuda, M, p, bias, mode):
     """rb_gemm_nt_h_act (the FeedForward's w_1 with dropout(silu(.)) in the
     epilogue, RecBLR.py:219-221): out bit-identical to rb_gemm_nt_h with the
     bias, act bit-identical to rb_silu_dropout_fwd(out) with the same seed —
@@ -153,17 +154,18 @@ def test_fused_activation_epilogue(cuda, M, p, bias):
     nr = (M + 31) // 32
     r1 = torch.full((nr,), -1.0, device=cuda)
     r2 = torch.full((nr,), -1.0, device=cuda)
-    out, act = kernels.gemm_nt_h_act(a, wi, C, b, seed=1234567, p=p, rmax=r1)
-    with kernels.nt_h_mode(0):   # the persistent kernel the fused epilogue rides on
+    with kernels.nt_h_mode(mode):   # (from 16,384 rows: mode 1 = gemm_ws.hip, EPI 1)
+        out, act = kernels.gemm_nt_h_act(a, wi, C, b, seed=1234567, p=p, rmax=r1)
         ref = kernels.gemm_nt_h(a, wi, C, bias=b, rmax=r2)
     assert torch.equal(out, ref)
     assert torch.equal(act, kernels.silu_dropout_fwd(ref, seed=1234567, p=p))
     assert torch.equal(r1, r2)
 
 
+@pytest.mark.parametrize("mode", [0, 1], ids=["persistent", "weight_stationary"])
 @pytest.mark.parametrize("M", [5000, 70001, 196608 + 8024])
 @pytest.mark.parametrize("p", [0.0, 0.2])
-def test_fused_activation_backward_epilogue(cuda, M, p):
+def test_fused_activation_backward_epilogue(cuda, M, p, mode):
     """rb_gemm_nt_h_dact (dU = dA2 W_2 with the activation's backward in the
     epilogue; dU never stored): da bit-identical to rb_gemm_nt_h +
     rb_silu_dropout_bwd with the same seed, on both launches (the 256 x 64 one
@@ -188,9 +190,10 @@ def test_fused_activation_backward_epilogue(cuda, M, p):
     nr = (M + 31) // 32
     r1 = torch.full((nr,), -1.0, device=cuda)
     r2 = torch.full((nr,), -1.0, device=cuda)
-    da, db = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p, rmax=r1)
-    with kernels.nt_h_mode(0):   # the persistent kernel the fused epilogue rides on
+    with kernels.nt_h_mode(mode):   # (from 16,384 rows: mode 1 = gemm_ws.hip, EPI 2)
+        da, db = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p, rmax=r1)
         du = kernels.gemm_nt_h(a, wi, C, rmax=r2)
+        da2, db2 = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p)
     da_ref, db_ref = kernels.silu_dropout_bwd(pre, du, seed=7654321, p=p, want_dbias=True)
     assert torch.equal(da, da_ref)
     assert torch.equal(r1, r2)
@@ -198,7 +201,6 @@ def test_fused_activation_backward_epilogue(cuda, M, p):
     tol = 1e-6 * da_ref.double().abs().sum(0).max().item()
     assert (db.double() - ref64).abs().max().item() < tol
     assert (db_ref.double() - ref64).abs().max().item() < tol
-    da2, db2 = kernels.gemm_nt_h_dact(a, wi, C, pre, seed=7654321, p=p)
     assert torch.equal(da2, da) and torch.equal(db2, db)
 
 
