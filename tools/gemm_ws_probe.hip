@@ -44,10 +44,11 @@ static int run_ws(const float* A, int64_t lda, int64_t M, int K, const void* Wf,
   const bool defer = variant & 1;
   const int abl = variant >> 4;
   int rc = 0;
+  const bool deep = variant & 2;   // K = 512: two register sets (D = 2) instead of one
   auto go = [&](auto kc, auto nc) {
-    constexpr int KK = decltype(kc)::value, NC = decltype(nc)::value, DD = ws::depth<KK>();
-    auto g2 = [&](auto ac) {
-      constexpr int AB = decltype(ac)::value;
+    constexpr int KK = decltype(kc)::value, NC = decltype(nc)::value;
+    auto g3 = [&](auto ac, auto dc) {
+      constexpr int AB = decltype(ac)::value, DD = decltype(dc)::value;
       if (bias) {
         if (defer) ws::run<KK, NC, DD, true, true, AB>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, 0);
         else ws::run<KK, NC, DD, true, false, AB>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, 0);
@@ -55,6 +56,10 @@ static int run_ws(const float* A, int64_t lda, int64_t M, int K, const void* Wf,
         if (defer) ws::run<KK, NC, DD, false, true, AB>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, 0);
         else ws::run<KK, NC, DD, false, false, AB>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, 0);
       }
+    };
+    auto g2 = [&](auto ac) {
+      if (KK == 512 && deep) g3(ac, std::integral_constant<int, 2>{});
+      else g3(ac, std::integral_constant<int, ws::depth<KK>()>{});
     };
     switch (abl) {
       case 0: g2(std::integral_constant<int, 0>{}); break;
@@ -158,7 +163,7 @@ int main(int argc, char** argv) {
         for (int a = 0; a < 3; ++a)
           ta[a].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, abl[a]); }));
       t[0].push_back(timeit([&] { gemm_nt_h_mode(0); return launch_gemm_nt_h(A, R, M, R, Wf, C, bp, O0, C, 0, rm0, 0); }));
-      t[1].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, 0); }));
+      t[1].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, 1 | 2); }));
       t[2].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, 1); }));
     }
     if (ablate) {
@@ -210,7 +215,7 @@ int main(int argc, char** argv) {
       tot[v] += us[v];
     }
     const double bytes = (double)M * (R + C) * 4;
-    printf("%-10s R=%3d C=%3d bias=%d  shipped %7.1f (min %7.1f)  ws %7.1f (min %7.1f)  ws-defer %7.1f (min %7.1f)  ws/shipped %.3f  [%.2f TB/s]  err shipped %.2e ws %.2e  rmax mismatches %lld\n",
+    printf("%-10s R=%3d C=%3d bias=%d  shipped %7.1f (min %7.1f)  ws-deep %7.1f (min %7.1f)  ws-defer %7.1f (min %7.1f)  ws/shipped %.3f  [%.2f TB/s]  err shipped %.2e ws %.2e  rmax mismatches %lld\n",
            s.name, R, C, (int)use_bias, us[0], mn[0], us[1], mn[1], us[2], mn[2],
            std::min(us[1], us[2]) / us[0], bytes / std::min(us[1], us[2]) / 1e6, err0, err1, (long long)rbad);
     fflush(stdout);
