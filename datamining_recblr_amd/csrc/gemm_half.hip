@@ -1106,33 +1106,53 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>(cbu), 0, (int)(nrows * ld4), 0x00020000);
   const uint32_t voff = (uint32_t)(rg * 8) * ld4 + (uint32_t)(16 * cc);
+  // (scheduling barriers on both sides keep each batch in program order
+  // between the conversions: loads the scheduler moved into a conversion made
+  // the compiler's counted waits drain the other register set)
   auto load = [&](int t, f32x4 (&r)[8]) {
-    if (!loader) return;
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int q = 0; q < 8; ++q)
       r[q] = __builtin_bit_cast(
           f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + (uint32_t)(t * 32 + q) * ld4, 0, 0));
+    __builtin_amdgcn_sched_barrier(0);
   };
-  // one column c of the thread's 8 x 4 block of step t into image `buf`
-  // (rows past the chunk are zeros from the loads: no branch, so the
-  // conversion sits in one basic block with the MFMAs it overlaps)
-  auto convert_col = [&](const f32x4 (&r)[8], int t, int buf, int c) {
-    (void)t;
+  // columns 2p, 2p + 1 of the thread's 8 x 4 block of step t into image
+  // `buf` (rows past the chunk are zeros from the loads: no branch, so the
+  // conversion sits in one basic block with the MFMAs it overlaps).  The
+  // packed scale / residual operate on the two columns of one row — a register
+  // pair as the 16-B load left it; pairing two rows of one column instead made
+  // hipcc regroup every loaded register at the loop's back edge, which waits
+  // for the loads just issued — and the fp16 results are regrouped into each
+  // column's 8 rows by the packs that build the LDS chunk.
+  auto convert_pair = [&](const f32x4 (&r)[8], int buf, int p) {
     const uint32_t img = smem_base + buf * CF::STAGE + (op == 0 ? 0 : 2 * CF::YPLANE);
     const uint32_t plane = op == 0 ? CF::YPLANE : CF::XPLANE;
-    f16x8 h0, h1;
+    const f32x2 sc{scv[2 * p], scv[2 * p + 1]};
+    f16x8 h0[2], h1[2];
 #pragma unroll
-    for (int q = 0; q < 8; q += 2) {
-      const float v0 = r[q][c], v1 = r[q + 1][c];
-      if constexpr (!PERCOL) cm[c] = max3abs(cm[c], v0, v1);
+    for (int q = 0; q < 8; ++q) {
+      const f32x2 v{r[q][2 * p], r[q][2 * p + 1]};
       f16x2 p0, p1;
-      split2h(f32x2{v0, v1} * scv[c], p0, p1);
-      h0[q] = p0[0]; h0[q + 1] = p0[1];
-      h1[q] = p1[0]; h1[q + 1] = p1[1];
+      split2h(v * sc, p0, p1);
+      h0[0][q] = p0[0]; h0[1][q] = p0[1];
+      h1[0][q] = p1[0]; h1[1][q] = p1[1];
     }
-    const uint32_t off = tn_off(4 * cc + c, rg);
-    hds_write16(img + off, h0);
-    hds_write16(img + plane + off, h1);
+    if constexpr (!PERCOL) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int q = 0; q < 8; q += 4) {
+          cm[2 * p + c] = max3abs(cm[2 * p + c], r[q][2 * p + c], r[q + 1][2 * p + c]);
+          cm[2 * p + c] = max3abs(cm[2 * p + c], r[q + 2][2 * p + c], r[q + 3][2 * p + c]);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const uint32_t off = tn_off(4 * cc + 2 * p + c, rg);
+      hds_write16(img + off, h0[c]);
+      hds_write16(img + plane + off, h1[c]);
+    }
   };
 
   f32x16 acc[2][2];
@@ -1150,15 +1170,13 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   // substep 0's MFMAs execute (each substep: two columns, fragment reads,
   // their wait, 12 MFMAs).
   auto mma = [&](int buf, auto conv_c, const f32x4 (&r)[8], int t, int nbuf) {
+    (void)t;
     constexpr bool CONV = decltype(conv_c)::value;
     const uint32_t iy = smem_base + buf * CF::STAGE;
     const uint32_t ix = iy + 2 * CF::YPLANE;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      if constexpr (CONV) {
-        convert_col(r, t, nbuf, 2 * st);
-        convert_col(r, t, nbuf, 2 * st + 1);
-      }
+      if constexpr (CONV) convert_pair(r, nbuf, st);
       // B fragments of both column blocks, then the A fragments one row
       // block at a time (24 fragment registers live, not 32)
       f16x8 b[2][2];
@@ -1195,23 +1213,34 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   // ahead; image t & 1 holds step t.  Step t's products run with step t+1's
   // conversion into the other image (last read by step t-1's products, which
   // every wave finished before the previous barrier); one barrier per step.
-  if (T > 0) load(0, raw0);
-  if (T > 1) load(1, raw1);
-  if (T > 0 && loader) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) convert_col(raw0, 0, 0, c);
-  }
-  if (T > 2) load(2, raw0);
-  __syncthreads();
-  for (int t = 0; t < T; t += 2) {
-    if (loader && t + 1 < T) mma(0, conv_t{}, raw1, t + 1, 1);
-    else mma(0, noconv_t{}, raw1, 0, 0);
-    if (t + 3 < T) load(t + 3, raw1);
+  // The loop is branch-free (T rounded up to even; steps past the chunk load
+  // and multiply zeros) and loader and non-loader waves run their own copy:
+  // with no VMEM under a branch the compiler's vmcnt waits for step t+1's
+  // registers count step t+2's loads as still in flight instead of draining
+  // them (a load under a branch made it wait for all of them, which left one
+  // step of lead instead of two).
+  const int Tp = (T + 1) & ~1;
+  if (__builtin_amdgcn_readfirstlane(tid >> 6) < CF::LOADERS / 64) {
+    load(0, raw0);
+    load(1, raw1);
+    convert_pair(raw0, 0, 0);
+    convert_pair(raw0, 0, 1);
+    load(2, raw0);
     __syncthreads();
-    if (t + 1 < T) {
-      if (loader && t + 2 < T) mma(1, conv_t{}, raw0, t + 2, 0);
-      else mma(1, noconv_t{}, raw0, 0, 0);
-      if (t + 4 < T) load(t + 4, raw0);
+    for (int t = 0; t < Tp; t += 2) {
+      mma(0, conv_t{}, raw1, t + 1, 1);
+      load(t + 3, raw1);
+      __syncthreads();
+      mma(1, conv_t{}, raw0, t + 2, 0);
+      load(t + 4, raw0);
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();
+    for (int t = 0; t < Tp; t += 2) {
+      mma(0, noconv_t{}, raw1, 0, 0);
+      __syncthreads();
+      mma(1, noconv_t{}, raw0, 0, 0);
       __syncthreads();
     }
   }
