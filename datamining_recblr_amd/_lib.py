@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 42
+ABI_VERSION = 43
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -105,6 +105,8 @@ SIGNATURES = {
     "rb_pack_plan": (ctypes.c_int, [_fp, _i64, _fp, _fp, _i64, _i64, _fp, _fp, _fp, _fp, _fp]),
     "rb_gemm_h_weight_bytes": (ctypes.c_int64, [_i64, _i64]),
     "rb_gemm_nt_h_mode": (ctypes.c_int, [ctypes.c_int]),
+    "rb_gemm_nt_h_ln": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _fp, _fp, _f32,
+                                       _u64, _f32, _fp, _fp, _fp, _fp, _i64, _fp, _fp]),
     "rb_gemm_h_split_weights": (ctypes.c_int, [_fp, _i64, _fp]),
     "rb_gemm_nt_h": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, ctypes.c_int,
                                     _fp, _fp]),

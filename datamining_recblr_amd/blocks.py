@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from . import kernels
 from ._lib import RecBLRNativeError
 from .linear import (_timed, fire_hooks, has_hooks, linear, mm_nn, mm_nn_dact, mm_nn_dact_ok, mm_nt,
-                     mm_nt_act, mm_nt_act_ok, rmax_buffer, wgrad)
+                     mm_nt_act, mm_nt_act_ok, mm_nt_ln, mm_nt_ln_ok, rmax_buffer, wgrad)
 
 __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm",
            "silu_dropout", "feed_forward", "set_defer_residual", "defer_residual"]
@@ -233,15 +233,22 @@ class _FeedForward(torch.autograd.Function):
             u = kernels.silu_dropout_fwd(a1, seed=seed1, p=p, bias=b1)
             a1_bias = b1
         r_u = rmax_buffer(u, d, inner) if want else None
-        a2 = _timed("gemm", f, mm_nt, u, w2, b2, rmax=r_u)
-        ctx.r_x, ctx.r_u = r_x, r_u
-        if observe is not None:   # module hooks of w_1 / w_2 (feed_forward)
-            pre = a1 if a1_bias is None else a1 + a1_bias
-            observe(x2.view(x.shape), pre.view(*x.shape[:-1], inner), u.view(*x.shape[:-1], inner),
-                    a2.view(x.shape))
         save = any(ctx.needs_input_grad)
-        y, s, mean, rstd = kernels.add_ln_fwd(a2, x2.contiguous(), gamma, beta, eps, seed=seed2,
-                                              p=p, save=save)
+        x2c = x2.contiguous()
+        if observe is None and mm_nt_ln_ok(u, w2):
+            # a2 = u W2^T + b2 never stored: the residual + dropout + LayerNorm
+            # in the GEMM's epilogue (rb_gemm_nt_h_ln)
+            y, s, mean, rstd = _timed("gemm", f, mm_nt_ln, u, w2, b2, x2c, gamma, beta, eps,
+                                      seed2, p, rmax=r_u)
+        else:
+            a2 = _timed("gemm", f, mm_nt, u, w2, b2, rmax=r_u)
+            if observe is not None:   # module hooks of w_1 / w_2 (feed_forward)
+                pre = a1 if a1_bias is None else a1 + a1_bias
+                observe(x2.view(x.shape), pre.view(*x.shape[:-1], inner),
+                        u.view(*x.shape[:-1], inner), a2.view(x.shape))
+            y, s, mean, rstd = kernels.add_ln_fwd(a2, x2c, gamma, beta, eps, seed=seed2, p=p,
+                                                  save=save)
+        ctx.r_x, ctx.r_u = r_x, r_u
         ctx.seed1, ctx.seed2, ctx.p = seed1, seed2, p
         ctx.a1_has_bias = a1_bias is None
         # in_addend: x's producer takes the residual's gradient (see ResidualGrad)

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 42; }
+int rb_version(void) { return 43; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -627,6 +627,27 @@ int64_t rb_gemm_h_weight_bytes(int64_t C, int64_t R) {
   return ws_image_offset(C, R) + (R % 32 == 0 ? C * R * 4 : 0);
 }
 int rb_gemm_nt_h_mode(int mode) { return gemm_nt_h_mode(mode); }
+
+int rb_gemm_nt_h_ln(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                    const float* bias, const float* resid, const float* gamma, const float* beta,
+                    float eps, uint64_t seed, float p, float* y, float* s_out, float* mean,
+                    float* rstd, int64_t ldo, float* rmax, void* stream) {
+  if (!A || !Wf || !resid || !gamma || !beta || !y || !s_out || !mean || !rstd)
+    return fail("rb_gemm_nt_h_ln: null pointer");
+  if (M <= 0 || R <= 0 || C != 128) return fail("rb_gemm_nt_h_ln: C must be 128, M and R positive");
+  if (R != 128 && R != 256 && R != 512) return fail("rb_gemm_nt_h_ln: R must be 128, 256 or 512");
+  if (lda < R || lda % 4 || ldo < C || ldo % 4) return fail("rb_gemm_nt_h_ln: bad row strides");
+  if (!aligned16(A) || !aligned16(Wf) || !aligned16(resid) || !aligned16(y) || !aligned16(s_out) ||
+      !aligned16(gamma) || !aligned16(beta) || (bias && !aligned16(bias)))
+    return fail("rb_gemm_nt_h_ln: A, Wf, resid, y, s_out, gamma, beta and bias must be 16-byte aligned");
+  if (!(p >= 0.0f && p < 1.0f)) return fail("rb_gemm_nt_h_ln: dropout p must be in [0, 1)");
+  if (!(eps > 0.0f)) return fail("rb_gemm_nt_h_ln: eps must be positive");
+  if ((M + 31) / 32 > 0x3fffffffLL) return fail("rb_gemm_nt_h_ln: grid too large");
+  if (gemm_nt_h_mode(-1) != 1) return fail("rb_gemm_nt_h_ln: needs the weight-stationary kernel (rb_gemm_nt_h_mode 1)");
+  return launch_gemm_nt_ws_ln(A, lda, M, (int)R, Wf, (int)C, bias, resid, make_drop(nullptr, seed, p),
+                              gamma, beta, eps, y, s_out, mean, rstd, ldo, rmax,
+                              reinterpret_cast<hipStream_t>(stream));
+}
 
 int rb_gemm_h_split_weights(const rb_split_job* jobs, int64_t n, void* stream) {
   if (!jobs || n < 1 || n > RB_MAX_SPLIT_JOBS)

@@ -408,6 +408,12 @@ int launch_gemm_nt_ws_act(const float* A, int64_t lda, int64_t M, int K, const v
 int launch_gemm_nt_ws_dact(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
                            float* out, int64_t ldo, float* rmax, const float* pre, DropSpec drop,
                            float* dpart, int64_t n_parts, hipStream_t st);
+bool nt_ws_ln_ok(int64_t M, int K, int C, const float* A, int64_t lda, const float* y,
+                 const float* s_out, const float* resid, int64_t ldo);
+int launch_gemm_nt_ws_ln(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                         const float* bias, const float* resid, DropSpec drop, const float* gamma,
+                         const float* beta, float eps, float* y, float* s_out, float* mean,
+                         float* rstd, int64_t ldo, float* rmax, hipStream_t st);
 int launch_gemm_nt_h(const float* A, int64_t lda, int64_t M, int R, const void* Wf, int C,
                      const float* bias, float* out, int64_t ldo, int accumulate, float* rmax,
                      hipStream_t st);

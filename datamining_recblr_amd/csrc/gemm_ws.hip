@@ -77,11 +77,14 @@ struct Cfg {
   // two images, (exp, max) per row and buffer, column exponents + bias
   static constexpr int INFO = 2 * IMG;
   static constexpr int COLS = INFO + 2 * RB * 8;
+  // LN epilogue (EPI 3): per buffer, row and wave the (mean, M2) of the wave's
+  // 16 columns of the row
+  static constexpr int STATS = COLS + NT * 8;
   // STG (K <= 256): the raw A rows land in LDS by LDS-DMA (each wave its own
   // rows, read back by the same lanes: no barrier, hand-counted vmcnt waits,
   // no registers held by loads in flight); K = 512: in registers (D = 1)
   static constexpr bool STG = K <= 256;
-  static constexpr int STAGE = COLS + NT * 8;
+  static constexpr int STAGE = STATS + 2 * 2 * RB * WAVES * 4;
   static constexpr int LDS = STAGE + (STG ? D * WAVES * NLD * 1024 : 0);
   static_assert(KS * NCB <= 16 && NCB >= 1, "B slice <= 128 VGPRs");
   static_assert(LDS <= 160 * 1024, "LDS");
@@ -171,18 +174,39 @@ __device__ __forceinline__ void wait_vm() {
 // Philox stream at element index row * C + col, as rb_silu_dropout_fwd draws
 // them; 2 (DACT, its backward fused into dU = dA2 W_2) out = dU * keep *
 // scale * silu'(pre), dU never stored, and the columns' sums of out per
-// workgroup into dpart (the w_1 bias gradient's partials, a fixed order).
+// workgroup into dpart (the w_1 bias gradient's partials, a fixed order);
+// 3 (LN, C = 128: the residual + dropout + LayerNorm after the FeedForward's
+// w_2 / the out-projection, RecBLR.py:142, 225-227) s = dropout(out) + pre
+// (the residual, [M, 128] at ldo) into `out`, y = LayerNorm(s) into `act`,
+// the rows' mean and rstd into ln — rb_add_ln_fwd's outputs, its s bit for
+// bit (the same keep-flags per element).  The row statistics need all 8
+// waves' columns: each wave leaves its 16 columns' (mean, M2) per row in LDS,
+// and after the block's barrier the next iteration combines them (Chan's
+// pairwise formula, a fixed order) and normalises the block, whose y is then
+// stored between the next block's MFMA units like every deferred result.
+struct LnSpec {
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float eps = 0.0f;
+  float* mean = nullptr;
+  float* rstd = nullptr;
+};
+
 template <int K, int NCB, int D, bool BIAS, bool DEFER, int ABL, int EPI = 0>
 __global__ void __launch_bounds__(THREADS, 1)
 k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* __restrict__ Wi,
              const int* __restrict__ ew, int C, const float* __restrict__ bias,
              float* __restrict__ out, int64_t ldo, float* __restrict__ rmax,
              float* __restrict__ act, DropSpec drop, const float* __restrict__ pre,
-             float* __restrict__ dpart) {
+             float* __restrict__ dpart, LnSpec ln) {
   using CF = Cfg<K, NCB, D>;
   constexpr int KS = CF::KS, WC = CF::WC, NT = CF::NT, NLD = CF::NLD, NST = CF::NST;
-  constexpr int NSTT = EPI == 1 ? 2 * NST : NST;   // stores per block (ACT: out and act)
-  constexpr int NPRE = EPI == 2 ? 2 * NCB : 0;     // DACT: `pre` loads per block
+  constexpr bool TWO = EPI == 1 || EPI == 3;        // a second output (act / y)
+  constexpr bool PRE = EPI == 2 || EPI == 3;        // a second [M, C] operand (pre / residual)
+  constexpr int NSTT = TWO ? 2 * NST : NST;         // result stores per block
+  constexpr int NPRE = PRE ? 2 * NCB : 0;           // `pre` loads per block
+  constexpr int NSO = NSTT + 1 + (EPI == 3 ? 2 : 0);   // stores per block: + rmax (+ mean, rstd)
+  static_assert(EPI != 3 || (NCB == 1 && DEFER), "LN epilogue: whole 128-column rows, deferred stores");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -387,13 +411,13 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
     }
   }
   __amdgpu_buffer_rsrc_t pending_rs = rsrc_of(out, M, ldo);   // no records: dummy stores
-  f32x4 pend2[EPI == 1 ? NST : 1];                            // ACT: act in store layout
-  __amdgpu_buffer_rsrc_t pending_act = rsrc_of(EPI == 1 ? act : out, M, ldo);
+  f32x4 pend2[TWO ? NST : 1];                                 // act / y in store layout
+  __amdgpu_buffer_rsrc_t pending_act = rsrc_of(TWO ? act : out, M, ldo);
   auto flush = [&](int i) __attribute__((always_inline)) {
     if constexpr ((ABL & 4) == 0) {
       if (i < NST)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend[i]), pending_rs, soff[i], 0, 2);
-      else if constexpr (EPI == 1)
+      else if constexpr (TWO)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, pend2[i - NST]), pending_act,
                                                soff[i - NST], 0, 2);
     }
@@ -401,13 +425,13 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   // DACT: the block's `pre` values at the lane's accumulator positions (row
   // 16 r + l % 16, columns 16 cb + 4 (l / 16) ..), loaded when the block's
   // MFMAs start; the lane's running column sums of out
-  f32x4 prv[EPI == 2 ? 2 : 1][EPI == 2 ? NCB : 1];
+  f32x4 prv[PRE ? 2 : 1][PRE ? NCB : 1];
   f32x4 csum[EPI == 2 ? NCB : 1];
   if constexpr (EPI == 2)
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) csum[cb] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   auto load_pre = [&](int b) __attribute__((always_inline)) {
-    if constexpr (EPI == 2) {
+    if constexpr (PRE) {
       const auto rs = rsrc_of(pre, blk_r0(b), ldo);
 #pragma unroll
       for (int r = 0; r < 2; ++r)
@@ -417,6 +441,91 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
               rs, (uint32_t)((16 * r + (lane & 15)) * ldo4) + (uint32_t)(col0 + 16 * cb + 4 * (lane >> 4)) * 4,
               0, 0));
       asm volatile("" ::: "memory");
+    }
+  };
+  // LN (EPI 3).  The wave's (mean, M2) of its 16 columns of row 16 r + l % 16:
+  // over the lane's 4 values, then the lanes l ^ 16 and l ^ 32 holding the
+  // row's other column groups (equal counts: M2 = M2a + M2b + (ma - mb)^2 n / 2;
+  // both lanes of a pair compute the same sums), into LDS by lanes 0-15
+  const uint32_t s_stats = sbase + CF::STATS;   // [2][RB][WAVES] means, then M2s
+  constexpr uint32_t kQ = 2 * RB * WAVES * 4;
+  f32x4 gm{}, bt{};                              // the lane's 4 columns' gamma, beta
+  float lmu[2] = {0.0f, 0.0f}, lrs[2] = {0.0f, 0.0f};   // the previous block's rows' stats
+  if constexpr (EPI == 3) {
+    gm = *reinterpret_cast<const f32x4*>(ln.gamma + col0 + 4 * (lane >> 4));
+    bt = *reinterpret_cast<const f32x4*>(ln.beta + col0 + 4 * (lane >> 4));
+  }
+  auto ln_part = [&](f32x4 sv, int ib, int r) __attribute__((always_inline)) {
+    float m = ((sv[0] + sv[1]) + (sv[2] + sv[3])) * 0.25f;
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float d = sv[i] - m;
+      q += d * d;
+    }
+#pragma unroll
+    for (int o = 16, n2 = 2; o <= 32; o <<= 1, n2 <<= 1) {
+      const float mo = __shfl_xor(m, o), qo = __shfl_xor(q, o);
+      const float d = mo - m;
+      m = (m + mo) * 0.5f;
+      q = (q + qo) + (d * d) * (float)n2;
+    }
+    if (lane < 16) {
+      const uint32_t a = s_stats + ((ib * RB + 16 * r + lane) * WAVES + wave) * 4;
+      asm volatile("ds_write_b32 %0, %1" ::"v"(a), "v"(m) : "memory");
+      asm volatile("ds_write_b32 %0, %1 offset:%2" ::"v"(a), "v"(q), "n"(kQ) : "memory");
+    }
+  };
+  // the previous block (image buffer ibp): its rows' statistics from the 8
+  // waves' parts, then y = (s - mean) rstd gamma + beta from pend into pend2
+  auto normalize = [&](int ibp) __attribute__((always_inline)) {
+    f32x4 pm[2][2], pq[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t a = s_stats + ((ibp * RB + 16 * r + (lane & 15)) * WAVES) * 4;
+      pm[r][0] = lds_read16<f32x4>(a);
+      pm[r][1] = lds_read16o<16, f32x4>(a);
+      pq[r][0] = lds_read16o<kQ, f32x4>(a);
+      pq[r][1] = lds_read16o<kQ + 16, f32x4>(a);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pm[0][0]), "+v"(pm[0][1]), "+v"(pm[1][0]), "+v"(pm[1][1]),
+                 "+v"(pq[0][0]), "+v"(pq[0][1]), "+v"(pq[1][0]), "+v"(pq[1][1]));
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const f32x4 m0 = pm[r][0], m1 = pm[r][1], q0 = pq[r][0], q1 = pq[r][1];
+      const float mu = (((m0[0] + m0[1]) + (m0[2] + m0[3])) + ((m1[0] + m1[1]) + (m1[2] + m1[3]))) * 0.125f;
+      float dev = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float d0 = m0[i] - mu, d1 = m1[i] - mu;
+        dev += d0 * d0;
+        dev += d1 * d1;
+      }
+      const float m2 = (((q0[0] + q0[1]) + (q0[2] + q0[3])) + ((q1[0] + q1[1]) + (q1[2] + q1[3]))) + dev * 16.0f;
+      const float rs = 1.0f / sqrtf(m2 * (1.0f / (float)(8 * WC)) + ln.eps);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pend2[r][i] = (pend[r][i] - mu) * rs * gm[i] + bt[i];
+      lmu[r] = mu;
+      lrs[r] = rs;
+    }
+  };
+  // the previous block's mean / rstd: lanes 0-31 hold rows 0-31 (lane l < 16:
+  // r = 0, else r = 1); wave 0 stores, every other wave (and lanes 32-63)
+  // issues the same store into no records
+  auto ln_store = [&](int bprev) __attribute__((always_inline)) {
+    const int64_t r0 = bprev >= 0 ? blk_r0(bprev) : M;
+    const bool mine = wave == 0 && r0 < M;
+    const int64_t n = mine ? (M - r0 < RB ? M - r0 : RB) : 0;
+    const uint32_t off = lane < RB ? (uint32_t)lane * 4 : 0x40000000u;
+    const float* bases[2] = {ln.mean, ln.rstd};
+    const float vals[2] = {lane < 16 ? lmu[0] : lmu[1], lane < 16 ? lrs[0] : lrs[1]};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const uint64_t u = reinterpret_cast<uint64_t>(bases[k] + (mine ? r0 : 0));
+      const uint64_t ub = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)u) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(u >> 32)) << 32);
+      const auto rr = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(ub), 0, (int)(n * 4), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vals[k]), rr, off, 0, 0);
     }
   };
   auto finish = [&](int b, int ib) __attribute__((always_inline)) {
@@ -464,11 +573,16 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
             if constexpr (EPI == 1) {
 #pragma unroll
               for (int i = 0; i < 4; ++i) av[g][i] = fsilu(v[g][i]) * mk[i];
-            } else {
+            } else if constexpr (EPI == 2) {
               const f32x4 pv = prv[r][NG * q + g];
 #pragma unroll
               for (int i = 0; i < 4; ++i) v[g][i] = (v[g][i] * mk[i]) * fdsilu(pv[i] + 0.0f);
               csum[NG * q + g] += v[g];   // rows past M: du = 0, pre = 0 -> 0
+            } else {
+              // s = out * keep * scale + residual (rb_add_ln_fwd's order)
+              const f32x4 pv = prv[r][NG * q + g];
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[g][i] = v[g][i] * mk[i] + pv[i];
             }
           }
         }
@@ -476,6 +590,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
           // lane: row 16 r + l % 16, columns 4 (l / 16) .. + 3: 64-B row pieces
           pend[r] = v[0];
           if constexpr (EPI == 1) pend2[r] = av[0];
+          if constexpr (EPI == 3) ln_part(v[0], ib, r);
         } else {
           // blocks 2q, 2q + 1 = 32 columns: lanes with (l & 8) take the other
           // block's value from 8 lanes away (DPP row_ror:8, bank-masked), so
@@ -509,7 +624,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
       }
     }
     pending_rs = rsrc_of(out, r0, ldo);   // nt stores (aux 2), rows past M dropped
-    if constexpr (EPI == 1) pending_act = rsrc_of(act, r0, ldo);
+    if constexpr (TWO) pending_act = rsrc_of(act, r0, ldo);
   };
   // rmax: the block's max |A| (its rows' maxima from the split), stored by
   // wave 0 of column tile 0.  Every wave runs this and issues the store (a
@@ -556,8 +671,8 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   // indexed at run time); LATE: split block b + 1 after the MFMAs.
   auto loop = [&](auto late_c) __attribute__((always_inline)) {
     constexpr bool LATE = decltype(late_c)::value;
-    constexpr int YS = (LATE ? D : D - 1) * (NSTT + 1) + D * NPRE + (D - 1) * NLD;
-    constexpr int Y0 = (D - 1) * NLD + NPRE + (LATE ? NSTT + 1 : 0);
+    constexpr int YS = (LATE ? D : D - 1) * NSO + D * NPRE + (D - 1) * NLD;
+    constexpr int Y0 = (D - 1) * NLD + NPRE + (LATE ? NSO : 0);
     auto body = [&](int b, auto par) __attribute__((always_inline)) {
       constexpr int P = decltype(par)::value;
       const int ib = b & 1;
@@ -573,14 +688,17 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
       if constexpr (!LATE) do_split();
       if constexpr (DEFER) {
         // block b - 1's stores (dummies before block 0) between this block's
-        // MFMA units, then its rmax word
+        // MFMA units, then its rmax word (LN: block b - 1 normalised first,
+        // its statistics stored after the rmax word)
         constexpr int U = 2 * KS, STEP = U / NSTT;
         static_assert(STEP >= 1, "more stores than MFMA units");
+        if constexpr (EPI == 3) normalize(ib ^ 1);
         multiply(ib, [&](auto uc) __attribute__((always_inline)) {
           constexpr int u = decltype(uc)::value;
           if constexpr (u % STEP == 0 && u / STEP < NSTT) flush(u / STEP);
         });
         rmax_store(b, ib);
+        if constexpr (EPI == 3) ln_store(b - 1);
         finish(b, ib);
       } else {
         multiply(ib, [](auto) __attribute__((always_inline)) {});
@@ -602,8 +720,11 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   if (D == 1 || wave < 4) loop(std::true_type{});
   else loop(std::false_type{});
   if constexpr (DEFER) {
+    const int blast = (nb + D - 1) / D * D - 1;   // the last block the loop ran (maybe a dummy)
+    if constexpr (EPI == 3) normalize(blast & 1);
 #pragma unroll
     for (int i = 0; i < NSTT; ++i) flush(i);   // the last block's results
+    if constexpr (EPI == 3) ln_store(blast);
   }
   if constexpr (EPI == 2) {
     // the wave's column sums: the lane's rows, then the 16 lanes of each
@@ -629,7 +750,7 @@ template <int K, int NCB, int D, bool BIAS, bool DEFER, int ABL, int EPI = 0>
 void run(const float* A, int64_t lda, int64_t M, const void* Wi, const int* ew, int C,
          const float* bias, float* out, int64_t ldo, float* rmax, int grid, hipStream_t st,
          float* act = nullptr, DropSpec drop = DropSpec{}, const float* pre = nullptr,
-         float* dpart = nullptr) {
+         float* dpart = nullptr, LnSpec ln = LnSpec{}) {
   using CF = Cfg<K, NCB, D>;
   static bool done = false;   // benign race: idempotent
   if (!done) {
@@ -638,7 +759,7 @@ void run(const float* A, int64_t lda, int64_t M, const void* Wi, const int* ew, 
     done = true;
   }
   k_gemm_nt_ws<K, NCB, D, BIAS, DEFER, ABL, EPI><<<grid, THREADS, CF::LDS, st>>>(
-      A, lda, M, (const f16x8*)Wi, ew, C, bias, out, ldo, rmax, act, drop, pre, dpart);
+      A, lda, M, (const f16x8*)Wi, ew, C, bias, out, ldo, rmax, act, drop, pre, dpart, ln);
 }
 
 // prefetch depth per K (blocks of A in flight): the LDS-DMA sets that fit
@@ -736,6 +857,42 @@ int launch_gemm_nt_ws_dact(const float* A, int64_t lda, int64_t M, int K, const 
       hipMemsetAsync(dpart + used * C, 0, (size_t)(n_parts - used) * C * 4, st) != hipSuccess)
     return fail("rb_gemm_nt_h_dact: hipMemsetAsync failed");
   return 0;
+}
+
+// The residual + dropout + LayerNorm after a C = 128 projection (EPI 3):
+// y = LN(dropout(A Bm^T + bias) + resid) into y, s (the LN input) into s_out,
+// the rows' mean / rstd; resid, y and s_out [M, 128] at row stride ldo
+bool nt_ws_ln_ok(int64_t M, int K, int C, const float* A, int64_t lda, const float* y,
+                 const float* s_out, const float* resid, int64_t ldo) {
+  return C == 128 && nt_ws_ok(M, K, C, A, lda, y, ldo) && ws::ncb_for(K, C) == 1 &&
+         aligned16(s_out) && aligned16(resid);
+}
+
+int launch_gemm_nt_ws_ln(const float* A, int64_t lda, int64_t M, int K, const void* Wf, int C,
+                         const float* bias, const float* resid, DropSpec drop, const float* gamma,
+                         const float* beta, float eps, float* y, float* s_out, float* mean,
+                         float* rstd, int64_t ldo, float* rmax, hipStream_t st) {
+  if (!nt_ws_ln_ok(M, K, C, A, lda, y, s_out, resid, ldo) || !gamma || !beta || !mean || !rstd ||
+      !aligned16(gamma) || !aligned16(beta))
+    return fail("rb_gemm_nt_h_ln: shape, alignment or null pointer");
+  const void* Wi = reinterpret_cast<const char*>(Wf) + ws_image_offset(C, K);
+  const int* ew = reinterpret_cast<const int*>(reinterpret_cast<const char*>(Wf) + (int64_t)C * K * 4);
+  const int grid = ws::grid_for(M, C, 1);
+  ws::LnSpec ln;
+  ln.gamma = gamma;
+  ln.beta = beta;
+  ln.eps = eps;
+  ln.mean = mean;
+  ln.rstd = rstd;
+  auto go = [&](auto kc) {
+    constexpr int KK = decltype(kc)::value;
+    if (bias) ws::run<KK, 1, ws::depth<KK>(), true, true, 0, 3>(A, lda, M, Wi, ew, C, bias, s_out, ldo, rmax, grid, st, y, drop, resid, nullptr, ln);
+    else ws::run<KK, 1, ws::depth<KK>(), false, true, 0, 3>(A, lda, M, Wi, ew, C, bias, s_out, ldo, rmax, grid, st, y, drop, resid, nullptr, ln);
+  };
+  if (K == 128) go(std::integral_constant<int, 128>{});
+  else if (K == 256) go(std::integral_constant<int, 256>{});
+  else go(std::integral_constant<int, 512>{});
+  return launch_status("rb_gemm_nt_h_ln");
 }
 
 }  // namespace rb

@@ -1100,6 +1100,50 @@ def nt_h_mode(mode: int):
         gemm_nt_h_mode(prev)
 
 
+def gemm_nt_h_ln_ok(a: torch.Tensor, C: int) -> bool:
+    """Whether gemm_nt_h_ln takes a [M, R] operand with C outputs:
+    rb_gemm_nt_h_ln's shape contract and the weight-stationary kernel selected."""
+    return (a.dim() == 2 and C == 128 and a.shape[1] in (128, 256, 512) and a.stride(1) == 1
+            and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0 and gemm_nt_h_mode() == 1)
+
+
+def gemm_nt_h_ln(a: torch.Tensor, wf: torch.Tensor, C: int, bias: torch.Tensor | None,
+                 resid: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float,
+                 seed: int, p: float, rmax: torch.Tensor | None = None):
+    """(y, s, mean, rstd) of LayerNorm(dropout(a @ Bm^T + bias) + resid) from
+    one GEMM epilogue (rb_gemm_nt_h_ln): add_ln_fwd(a @ Bm^T + bias, resid,
+    gamma, beta, eps, seed=seed, p=p)'s outputs, s bit for bit, mean / rstd
+    to fp32 rounding (RecBLR.py:142, 225-227)."""
+    _check(a, "a")
+    _check(resid, "resid")
+    _check_p(p)
+    if not gemm_nt_h_ln_ok(a, C):
+        raise ValueError(f"gemm_nt_h_ln: no fused launch for {tuple(a.shape)} -> {C}")
+    M, R = a.shape
+    if resid.shape != (M, C) or not resid.is_contiguous():
+        raise ValueError("resid must be a contiguous [M, C] tensor")
+    for t, n in ((gamma, "gamma"), (beta, "beta")):
+        _check(t, n)
+        if t.numel() != C or t.data_ptr() % 16:
+            raise ValueError(f"{n} must hold C floats, 16-byte aligned")
+    if bias is not None:
+        _check(bias, "bias")
+    if rmax is not None:
+        _check(rmax, "rmax")
+        if rmax.numel() < (M + 31) // 32:
+            raise ValueError("rmax needs ceil(M/32) entries")
+    y = torch.empty((M, C), device=a.device, dtype=torch.float32)
+    s = torch.empty_like(y)
+    mean = torch.empty(M, device=a.device, dtype=torch.float32)
+    rstd = torch.empty_like(mean)
+    _lib.call("rb_gemm_nt_h_ln", a.data_ptr(), a.stride(0), M, R, wf.data_ptr(), C,
+              0 if bias is None else bias.data_ptr(), resid.data_ptr(), gamma.data_ptr(),
+              beta.data_ptr(), float(eps), int(seed), float(p), y.data_ptr(), s.data_ptr(),
+              mean.data_ptr(), rstd.data_ptr(), y.stride(0),
+              0 if rmax is None else rmax.data_ptr(), _stream(a))
+    return y, s, mean, rstd
+
+
 def gemm_nt_h_act_ok(a: torch.Tensor, C: int) -> bool:
     """Whether gemm_nt_h_act takes a [M, R] operand with C outputs (freshly
     allocated contiguous outputs): rb_gemm_nt_h_act's shape contract."""

@@ -305,6 +305,44 @@ def mm_nt_act(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, seed:
     return kernels.gemm_nt_h_act(a, _weight_split(w, False), w.shape[0], bias, seed, p, rmax=rmax)
 
 
+# The residual + dropout + LayerNorm after a projection to d = 128 in the
+# GEMM's epilogue (rb_gemm_nt_h_ln; the FeedForward's w_2 and the recurrent
+# layer's out-projection): the LayerNorm kernel's re-read of the GEMM output
+# and the output's write are gone.  RECBLR_LN_EPI=0: the GEMM and
+# rb_add_ln_fwd as two launches.
+_ln_fused = os.environ.get("RECBLR_LN_EPI", "1") != "0"
+if os.environ.get("RECBLR_LN_EPI", "1") not in ("0", "1"):
+    raise ValueError("RECBLR_LN_EPI must be 0 or 1")
+
+
+def set_ln_fused(on: bool) -> bool:
+    """Switch the LayerNorm GEMM epilogue (A/B in bench.py); returns the
+    previous setting."""
+    global _ln_fused
+    prev, _ln_fused = _ln_fused, bool(on)
+    return prev
+
+
+def mm_nt_ln_ok(a: torch.Tensor, w: torch.Tensor) -> bool:
+    """Whether mm_nt_ln applies to a [M, K] @ w [N, K]^T (N = 128; else the
+    GEMM and rb_add_ln_fwd as two launches)."""
+    N, K = w.shape
+    if not (_ln_fused and _half and a.dtype == w.dtype and a.shape[0] >= ACT_MIN_ROWS
+            and _split_ok(a, N, K)):
+        return False
+    _apply_nt_ws()
+    return kernels.gemm_nt_h_ln_ok(a, N)
+
+
+def mm_nt_ln(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None, resid: torch.Tensor,
+             gamma: torch.Tensor, beta: torch.Tensor, eps: float, seed: int, p: float,
+             rmax: torch.Tensor | None = None):
+    """(y, s, mean, rstd) = LayerNorm(dropout(a @ w^T + bias) + resid) and its
+    saved statistics from one f16x3 GEMM launch (where mm_nt_ln_ok)."""
+    return kernels.gemm_nt_h_ln(a, _weight_split(w, False), w.shape[0], bias, resid, gamma, beta,
+                                eps, seed, p, rmax=rmax)
+
+
 def mm_nn_dact_ok(dy: torch.Tensor, w: torch.Tensor) -> bool:
     """Whether mm_nn_dact applies to dy [M, N] @ w [N, K]."""
     N, K = w.shape

@@ -529,6 +529,23 @@ int rb_gemm_nt_h(const float* A, int64_t lda, int64_t M, int64_t R, const void* 
  * host setting (not per stream). */
 int rb_gemm_nt_h_mode(int mode);
 
+/* rb_gemm_nt_h with the residual + dropout + LayerNorm that follows a
+ * projection to d = 128 in its epilogue (RecBLR.py:142 after the
+ * out-projection, :225-227 after the FeedForward's w_2): with
+ * out = A Bm^T + bias (never stored), s = out * keep * scale + resid and
+ * y = (s - mean) * rstd * gamma + beta — rb_add_ln_fwd(out, resid, ...)'s
+ * outputs, s bit for bit (the same Philox keep-flags per element), mean and
+ * rstd from a fixed-order combination of per-column-group moments (fp32
+ * rounding apart from rb_add_ln_fwd's).  C = 128, R in {128, 256, 512};
+ * resid, y and s_out [M, 128] at row stride ldo; all 16-B aligned; the
+ * weight-stationary kernel only (rb_gemm_nt_h_mode 1, any M); mean and
+ * rstd [M]; rmax as rb_gemm_nt_h.  Replaces nn.Linear + dropout + residual
+ * + nn.LayerNorm's forward. */
+int rb_gemm_nt_h_ln(const float* A, int64_t lda, int64_t M, int64_t R, const void* Wf, int64_t C,
+                    const float* bias, const float* resid, const float* gamma, const float* beta,
+                    float eps, uint64_t seed, float p, float* y, float* s_out, float* mean,
+                    float* rstd, int64_t ldo, float* rmax, void* stream);
+
 /* rb_gemm_nt_h with the FeedForward's activation in its epilogue
  * (RecBLR.py:219-221, w_1 then dropout(silu(.))): out = A Bm^T + bias and
  * act = dropout(silu(out)), both [M, C] with row stride ldo — act equals

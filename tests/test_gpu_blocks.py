@@ -232,8 +232,10 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
     # fused vs unfused, bitwise on either NT kernel (rb_gemm_nt_h_mode 0: the
     # persistent tiles; 1: the weight-stationary kernel, EPI 1 / 2, from
     # 16,384 rows); the two kernels agree at fp32 accuracy
+    # (the LayerNorm epilogue off: its row moments are another fp32 order)
     for fused, mode in ((True, 0), (False, 0), (True, 1), (False, 1)):
         prev = linear.set_ffn_act_fused(fused)
+        prev_ln = linear.set_ln_fused(False)
         try:
             with kernels.nt_h_mode(mode):
                 leaves = [t.to(cuda).requires_grad_() for t in base]
@@ -244,6 +246,7 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
                 res.append([y.detach()] + [t.grad for t in leaves])
         finally:
             linear.set_ffn_act_fused(prev)
+            linear.set_ln_fused(prev_ln)
     names = ("y", "dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta")
     for f, u_ in ((0, 1), (2, 3)):
         for name, u, v in zip(names, res[f], res[u_]):
@@ -253,6 +256,45 @@ def test_feed_forward_fused_activation_bitwise(cuda, M):
                 assert torch.equal(u, v), name
     for name, u, v in zip(names, res[3], res[1]):
         close(u, v, atol=1e-5 * v.abs().max().item(), rtol=1e-5, what=name + " (ws)")
+
+
+@pytest.mark.parametrize("M", [20000, 204632])
+def test_feed_forward_ln_epilogue(cuda, M, monkeypatch):
+    """The FeedForward with the residual + dropout + LayerNorm in w_2's GEMM
+    epilogue (RECBLR_LN_EPI, linear.mm_nt_ln: rb_add_ln_fwd gone) == the GEMM
+    + rb_add_ln_fwd path: the output and every gradient within fp32 rounding
+    of the row moments (the same s, the same keep-flags)."""
+    from datamining_recblr_amd import kernels, linear
+    from datamining_recblr_amd.blocks import _FeedForward
+
+    g = torch.Generator(device="cpu").manual_seed(23)
+    d = 128
+    base = [torch.randn(M, d, generator=g), 0.05 * torch.randn(4 * d, d, generator=g),
+            0.1 * torch.randn(4 * d, generator=g), 0.05 * torch.randn(d, 4 * d, generator=g),
+            0.1 * torch.randn(d, generator=g), 1 + 0.1 * torch.randn(d, generator=g),
+            0.1 * torch.randn(d, generator=g)]
+    dy = torch.randn(M, d, generator=g).to(cuda)
+    res = []
+    for on in (True, False):
+        prev = linear.set_ln_fused(on)
+        calls = []
+        orig = kernels.add_ln_fwd
+        monkeypatch.setattr(kernels, "add_ln_fwd", lambda *a, **k: calls.append(1) or orig(*a, **k))
+        try:
+            with kernels.nt_h_mode(1):
+                leaves = [t.to(cuda).requires_grad_() for t in base]
+                u = torch.empty(M, 4 * d, device=cuda)
+                assert linear.mm_nt_ln_ok(u, leaves[3]) == on
+                y = _FeedForward.apply(*leaves, 51, 52, 0.2, 1e-12)
+                y.backward(dy)
+                res.append([y.detach()] + [t.grad for t in leaves])
+        finally:
+            linear.set_ln_fused(prev)
+            monkeypatch.setattr(kernels, "add_ln_fwd", orig)
+        assert len(calls) == (0 if on else 1)
+    names = ("y", "dx", "dw1", "db1", "dw2", "db2", "dgamma", "dbeta")
+    for name, u, v in zip(names, res[0], res[1]):
+        close(u, v, atol=2e-5 * v.abs().max().item(), rtol=1e-4, what=name + " (ln epilogue)")
 
 
 def test_train_mode_dropout(cuda):

@@ -679,3 +679,67 @@ def test_ws_kernel_row_strided_views(cuda):
     kernels.gemm_nt_h(x, kernels.gemm_h_weight(w), 256, out=out)
     assert _rel_err(out, x.double() @ w.double().t()) < 2e-6
     assert outbig[:, :256].abs().max().item() == 0.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [128, 256, 512])
+@pytest.mark.parametrize("M", [16384 + 37, 70000])
+@pytest.mark.parametrize("p,bias", [(0.0, False), (0.2, True)])
+def test_ln_epilogue_matches_gemm_then_add_ln(cuda, K, M, p, bias):
+    """rb_gemm_nt_h_ln (the weight-stationary kernel's LayerNorm epilogue,
+    RecBLR.py:142, 225-227) == rb_gemm_nt_h + rb_add_ln_fwd: s bit for bit
+    (the same GEMM output and Philox keep-flags), mean / rstd / y within fp32
+    re-association of the row moments; and against fp64 LayerNorm of s."""
+    from datamining_recblr_amd import kernels
+
+    g = torch.Generator().manual_seed(31 + K)
+    d = 128
+    a = torch.randn(M, K, generator=g).to(cuda)
+    w = (torch.randn(d, K, generator=g) / K ** 0.5).to(cuda)
+    b = (0.1 * torch.randn(d, generator=g)).to(cuda) if bias else None
+    r = torch.randn(M, d, generator=g)
+    r[::97] += 300.0                                  # rows whose mean dwarfs their spread
+    r = r.to(cuda)
+    gamma = (1 + 0.1 * torch.randn(d, generator=g)).to(cuda)
+    beta = (0.1 * torch.randn(d, generator=g)).to(cuda)
+    wi = kernels.gemm_h_weight(w)
+    rm = torch.empty((M + 31) // 32, device=cuda)
+    with kernels.nt_h_mode(1):
+        assert kernels.gemm_nt_h_ln_ok(a, d)
+        y, s, mean, rstd = kernels.gemm_nt_h_ln(a, wi, d, b, r, gamma, beta, 1e-12, 77, p, rmax=rm)
+        o = kernels.gemm_nt_h(a, wi, d, bias=b)
+    y2, s2, mean2, rstd2 = kernels.add_ln_fwd(o, r, gamma, beta, 1e-12, seed=77, p=p)
+    assert torch.equal(s, s2)
+    assert torch.equal(rm, _row_group_max(a))
+    sd = s2.double()
+    md = sd.mean(1)
+    vd = ((sd - md[:, None]) ** 2).mean(1)
+    yd = (sd - md[:, None]) / torch.sqrt(vd[:, None] + 1e-12) * gamma.double() + beta.double()
+    scale = sd.abs().amax(1)
+    assert ((mean.double() - md).abs() / scale).max().item() < 1e-6
+    assert ((rstd.double() - 1 / torch.sqrt(vd + 1e-12)).abs() / rstd.double()).max().item() < 2e-5
+    assert (y.double() - yd).abs().max().item() < 2e-4
+    # the same rounding class as rb_add_ln_fwd's two-pass moments
+    assert (y - y2).abs().max().item() < 2e-4
+    assert ((rstd - rstd2).abs() / rstd2).max().item() < 2e-5
+
+
+@pytest.mark.gpu
+def test_ln_epilogue_needs_the_weight_stationary_kernel(cuda):
+    """rb_gemm_nt_h_ln runs only on the weight-stationary kernel: with
+    rb_gemm_nt_h_mode 0 the eligibility check says no and a direct call fails
+    loudly (no silent fallback)."""
+    from datamining_recblr_amd import _lib, kernels
+
+    M, d = 20000, 128
+    a = torch.randn(M, 256, device=cuda)
+    w = torch.randn(d, 256, device=cuda) / 16
+    r = torch.randn(M, d, device=cuda)
+    one = torch.ones(d, device=cuda)
+    with kernels.nt_h_mode(0):
+        assert not kernels.gemm_nt_h_ln_ok(a, d)
+        with pytest.raises(_lib.RecBLRNativeError):
+            _lib.call("rb_gemm_nt_h_ln", a.data_ptr(), 256, M, 256,
+                      kernels.gemm_h_weight(w).data_ptr(), d, 0, r.data_ptr(), one.data_ptr(),
+                      one.data_ptr(), 1e-12, 0, 0.0, r.data_ptr(), r.data_ptr(), one.data_ptr(),
+                      one.data_ptr(), d, 0, 0)
