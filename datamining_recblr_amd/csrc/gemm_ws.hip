@@ -168,7 +168,8 @@ __device__ __forceinline__ void wait_vm() {
 //   exps: int32 e_c at byte offset C * K * 4 (shared with the persistent
 //   kernel's image: the same column exponents)
 // ABL (timing-only ablations, results not meaningful): 1 no MFMAs, 2 no
-// split (loads still waited), 4 no stores, 8 no A loads, 16 no fragment reads.
+// split (loads still waited), 4 no stores, 8 no A loads, 16 no fragment reads;
+// 32 (results exact): depth 1 with every wave in the late role.
 // EPI: 0 out (+ bias); 1 (ACT, the FeedForward's w_1, RecBLR.py:219-221)
 // out = A Bm^T + bias and act = dropout(silu(out)) — the keep-flags drop's
 // Philox stream at element index row * C + col, as rb_silu_dropout_fwd draws
@@ -207,6 +208,12 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   constexpr int NPRE = PRE ? 2 * NCB : 0;           // `pre` loads per block
   constexpr int NSO = NSTT + 1 + (EPI == 3 ? 2 : 0);   // stores per block: + rmax (+ mean, rstd)
   static_assert(EPI != 3 || (NCB == 1 && DEFER), "LN epilogue: whole 128-column rows, deferred stores");
+  // depth 1 (K = 512, registers): waves 4-7 take the early role too — they
+  // split block b + 1 (loaded during block b - 1) and then issue block b + 2's
+  // loads into the freed registers before multiplying block b (2-4% on the
+  // K = 512 shapes against all waves late, profiles/r06_early1_probe.txt;
+  // ABL bit 32 restores all-late for that A/B)
+  constexpr bool EARLY1 = D == 1 && (ABL & 32) == 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -651,6 +658,9 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
   }(std::make_integer_sequence<int, D>{});
   if constexpr (CF::STG) wait_vm<(D - 1) * NLD>();   // block 0's pieces landed
   split(ra[0], 0, 0);
+  if constexpr (EARLY1) {
+    if (wave >= 4) issue(1, ra[0], 0);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 
@@ -683,9 +693,15 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
         }
         split(ra[CF::STG ? 0 : (P + 1) % D], ib ^ 1, (P + 1) % D);
       };
-      issue(b + D, ra[CF::STG ? 0 : P], P);   // into the set block b held (split in iteration b - 1)
-      load_pre(b);
-      if constexpr (!LATE) do_split();
+      if constexpr (EARLY1 && !LATE) {
+        do_split();
+        issue(b + 2, ra[0], 0);
+        load_pre(b);
+      } else {
+        issue(b + D, ra[CF::STG ? 0 : P], P);   // into the set block b held (split in iteration b - 1)
+        load_pre(b);
+        if constexpr (!LATE) do_split();
+      }
       if constexpr (DEFER) {
         // block b - 1's stores (dummies before block 0) between this block's
         // MFMA units, then its rmax word (LN: block b - 1 normalised first,
@@ -717,7 +733,7 @@ k_gemm_nt_ws(const float* __restrict__ A, int64_t lda, int64_t M, const f16x8* _
       }(std::make_integer_sequence<int, D>{});
     }
   };
-  if (D == 1 || wave < 4) loop(std::true_type{});
+  if ((D == 1 && !EARLY1) || wave < 4) loop(std::true_type{});
   else loop(std::false_type{});
   if constexpr (DEFER) {
     const int blast = (nb + D - 1) / D * D - 1;   // the last block the loop ran (maybe a dummy)

@@ -44,7 +44,7 @@ static int run_ws(const float* A, int64_t lda, int64_t M, int K, const void* Wf,
   const bool defer = variant & 1;
   const int abl = variant >> 4;
   int rc = 0;
-  const bool deep = variant & 2;   // K = 512: two register sets (D = 2) instead of one
+  const bool early1 = variant & 2;   // K = 512: every wave late at depth 1 (ABL bit 32; round 6's first form)
   auto go = [&](auto kc, auto nc) {
     constexpr int KK = decltype(kc)::value, NC = decltype(nc)::value;
     auto g3 = [&](auto ac, auto dc) {
@@ -57,12 +57,10 @@ static int run_ws(const float* A, int64_t lda, int64_t M, int K, const void* Wf,
         else ws::run<KK, NC, DD, false, false, AB>(A, lda, M, Wi, ew, C, bias, out, ldo, rmax, grid, 0);
       }
     };
-    auto g2 = [&](auto ac) {
-      if (KK == 512 && deep) g3(ac, std::integral_constant<int, 2>{});
-      else g3(ac, std::integral_constant<int, ws::depth<KK>()>{});
-    };
-    switch (abl) {
+    auto g2 = [&](auto ac) { g3(ac, std::integral_constant<int, ws::depth<KK>()>{}); };
+    switch (abl | (early1 ? 32 : 0)) {
       case 0: g2(std::integral_constant<int, 0>{}); break;
+      case 32: g2(std::integral_constant<int, 32>{}); break;
       case 1: g2(std::integral_constant<int, 1>{}); break;
       case 4: g2(std::integral_constant<int, 4>{}); break;
       case 16: g2(std::integral_constant<int, 16>{}); break;
@@ -163,8 +161,9 @@ int main(int argc, char** argv) {
         for (int a = 0; a < 3; ++a)
           ta[a].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, abl[a]); }));
       t[0].push_back(timeit([&] { gemm_nt_h_mode(0); return launch_gemm_nt_h(A, R, M, R, Wf, C, bp, O0, C, 0, rm0, 0); }));
-      t[1].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, 1 | 2); }));
       t[2].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, 1); }));
+      // last: the checks below read this variant's output
+      t[1].push_back(timeit([&] { return run_ws(A, R, M, R, Wf, C, bp, O1, C, rm1, 1 | 2); }));
     }
     if (ablate) {
       for (int a = 0; a < 3; ++a) std::sort(ta[a].begin(), ta[a].end());
@@ -215,7 +214,7 @@ int main(int argc, char** argv) {
       tot[v] += us[v];
     }
     const double bytes = (double)M * (R + C) * 4;
-    printf("%-10s R=%3d C=%3d bias=%d  shipped %7.1f (min %7.1f)  ws-deep %7.1f (min %7.1f)  ws-defer %7.1f (min %7.1f)  ws/shipped %.3f  [%.2f TB/s]  err shipped %.2e ws %.2e  rmax mismatches %lld\n",
+    printf("%-10s R=%3d C=%3d bias=%d  shipped %7.1f (min %7.1f)  ws-d1late %7.1f (min %7.1f)  ws-defer %7.1f (min %7.1f)  ws/shipped %.3f  [%.2f TB/s]  err shipped %.2e ws %.2e  rmax mismatches %lld\n",
            s.name, R, C, (int)use_bias, us[0], mn[0], us[1], mn[1], us[2], mn[2],
            std::min(us[1], us[2]) / us[0], bytes / std::min(us[1], us[2]) / 1e6, err0, err1, (long long)rbad);
     fflush(stdout);
