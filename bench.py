@@ -389,9 +389,9 @@ def long_seq_c5(args, env, dev, steps=3, warmup=2):
     ranks (weak scaling, max-over-ranks time).  The HBM fraction is that of
     the bf16 conv + gate-scan kernels (algorithmic bytes 20*N*2 per step,
     N = B*L*H).  The projections run per shape on our bf16 kernels
-    (rb_gemm_nt_bf16 / rb_gemm_tn_bf16) or torch's bf16 GEMMs (hipBLASLt):
-    RECBLR_BF16_GEMM=auto (default: ours where faster), 1 (ours on all nine),
-    0 (hipBLASLt on all nine); projection_gemms_ab times the three."""
+    (rb_gemm_nt_bf16; weight gradients on hipBLASLt's split-K) or torch's bf16 GEMMs (hipBLASLt):
+    RECBLR_BF16_GEMM=auto (default: ours where faster), 1 (ours on the six NT
+    shapes), 0 (hipBLASLt on all nine); projection_gemms_ab times the three."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
     B, L, d = args.c5_batch, 2048, 256
@@ -423,7 +423,7 @@ def long_seq_c5(args, env, dev, steps=3, warmup=2):
             one()
         torch.cuda.synchronize()
     summ = t.summary()
-    # the projections on our bf16 kernels (rb_gemm_nt_bf16 / rb_gemm_tn_bf16)
+    # the projections on our bf16 kernel (rb_gemm_nt_bf16)
     # vs torch's bf16 GEMMs (hipBLASLt), alternated, best of 2 per variant
     from datamining_recblr_amd import linear as _lin
     saved_g = _lin.set_bf16_gemm(_lin._bf16_gemm)

@@ -19,7 +19,7 @@ HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "recblr_hip.h")
 
 RB_EINVAL = -1
 RB_TILE = 16
-ABI_VERSION = 43
+ABI_VERSION = 44
 
 _i64 = ctypes.c_int64
 _fp = ctypes.c_void_p  # device pointers are passed as integers
@@ -120,7 +120,6 @@ SIGNATURES = {
                                          _u64, _f32, _fp, _i64, _fp]),
     "rb_gemm_bf16_weight_image": (ctypes.c_int, [_fp, _i64, _i64, _i64, ctypes.c_int, _fp, _fp]),
     "rb_gemm_nt_bf16": (ctypes.c_int, [_fp, _i64, _i64, _i64, _fp, _i64, _fp, _fp, _i64, _fp]),
-    "rb_gemm_tn_bf16": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, _i64, _fp]),
     "rb_gemm_tn_h": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, _fp, _fp, _i64,
                                     _fp]),
     "rb_gemm_tn_hs": (ctypes.c_int, [_fp, _i64, _fp, _i64, _i64, _i64, _i64, _fp, ctypes.c_int, _fp]),

@@ -71,7 +71,7 @@ using namespace rb;
 
 extern "C" {
 
-int rb_version(void) { return 43; }
+int rb_version(void) { return 44; }
 
 const char* rb_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -780,27 +780,6 @@ int rb_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int64_t R, const void
   return launch_gemm_nt_bf16(A, lda, M, (int)R, img, (int)C, bias, out, ldo,
                              reinterpret_cast<hipStream_t>(stream));
 }
-
-int rb_gemm_tn_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t M, int64_t N,
-                    int64_t K, float* parts, int64_t splits, void* stream) {
-  if (!dY || !X || !parts) return fail("rb_gemm_tn_bf16: null pointer");
-  if (M <= 0 || N <= 0 || K <= 0) return fail("rb_gemm_tn_bf16: empty shape");
-  if (N % 256 || K % 256 || N > 65536 || K > 65536)
-    return fail("rb_gemm_tn_bf16: N and K must be multiples of 256 (<= 65536)");
-  if (splits < 8 || splits % 8 || splits > 65536)
-    return fail("rb_gemm_tn_bf16: splits must be a positive multiple of 8");
-  if (ldy < N || ldx < K || ldy % 8 || ldx % 8) return fail("rb_gemm_tn_bf16: bad row strides");
-  if (!aligned16(dY) || !aligned16(X) || !aligned16(parts))
-    return fail("rb_gemm_tn_bf16: dY, X and parts must be 16-byte aligned");
-  const int64_t chunk = ((M + splits - 1) / splits + 63) / 64 * 64;
-  if (chunk * (ldy > ldx ? ldy : ldx) * 2 >= 0x7fffffffLL)
-    return fail("rb_gemm_tn_bf16: a row chunk exceeds 2 GiB (use more splits)");
-  if ((N / 256) * (K / 256) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_bf16: grid too large");
-  return launch_gemm_tn_bf16(dY, ldy, X, ldx, M, (int)N, (int)K, parts, (int)splits,
-                             reinterpret_cast<hipStream_t>(stream));
-}
-
-
 
 int rb_gemm_tn_hs(const float* dY, int64_t ldy, const float* X, int64_t ldx, int64_t M, int64_t N,
                   int64_t K, float* dw, int accumulate, void* stream) {

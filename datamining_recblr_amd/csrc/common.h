@@ -386,8 +386,6 @@ int launch_bf16_weight_image(const float* W, int64_t ldw, int C, int R, int tran
                              hipStream_t st);
 int launch_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int R, const void* img, int C,
                         const float* bias, void* out, int64_t ldo, hipStream_t st);
-int launch_gemm_tn_bf16(const void* Y, int64_t ldy, const void* X, int64_t ldx, int64_t M, int N,
-                        int K, float* parts, int S, hipStream_t st);
 int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, int64_t M, int N,
                      int K, const float* ymax, const float* xmax, float* parts, int S,
                      hipStream_t st);

@@ -1,6 +1,6 @@
 // gemm_bf16.hip — the projections of bf16 activations (BASELINE configs[4]:
 // L = 2,048, d = 256, H = 512, 2M rows per step) on the bf16 MFMA pipe
-// (NT: v_mfma_f32_16x16x32_bf16, TN: 32x32x16), fp32 accumulation.
+// (v_mfma_f32_16x16x32_bf16), fp32 accumulation.
 //
 // rb_gemm_nt_bf16: out[M, C] = A[M, R] . Bm[C, R]^T (+ bias[C]), bf16 out
 //   nn.Linear's forward (Bm = W) and input gradient (Bm = W^T) on bf16
@@ -11,17 +11,15 @@
 //   .. + 7), so a k-step's weight slice is a run of contiguous 1 KB DMAs
 //   from L2.
 //   The bias is added in fp32 before the one rounding to bf16.
-// rb_gemm_tn_bf16: part[s][N, K] = dY[chunk_s]^T . X[chunk_s], fp32
-//   The weight gradients of the same Linears over row chunks; the fixed-order
-//   column sum (rb_colsum) adds the partials.
+// The weight gradients of these Linears run on hipBLASLt's batched split-K
+// (linear.wgrad): round 5's bf16 TN kernel here measured 4-24% behind it
+// (profiles/r05_tn48_shapes.txt) and was removed in round 6 (git history).
 //
-// Both: one 512-thread workgroup per CU, 256 x 256 output tiles, waves 4 x 2
-// owning 64 x 128 each (NT: 4 x 8 blocks of 16 x 16, TN: 2 x 4 blocks of
-// 32 x 32), every operand global -> LDS
+// One 512-thread workgroup per CU, 256 x 256 output tiles, waves 4 x 2
+// owning 64 x 128 each (4 x 8 blocks of 16 x 16), every operand global -> LDS
 // by LDS-DMA, the next k-step issued right after the barrier that frees its
-// slot.  LDS: the NT kernel 160 KB, all of a gfx950 CU (3 A stages, A two
-// k-steps ahead, + 2 weight stages); the TN kernel 128 KB (2 stages of both
-// operands).  The launchers check that the device grants it.
+// slot.  LDS: 160 KB, all of a gfx950 CU (3 A stages, A two k-steps ahead,
+// + 2 weight stages).  The launcher checks that the device grants it.
 #include "common.h"
 
 #include <type_traits>
@@ -31,16 +29,10 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __fp16 fp16x4_t __attribute__((__vector_size__(8)));
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(3))) fp16x4_t* lds_h4_ptr;
 
-__device__ __forceinline__ f32x16 mfma_bf(bf16x8 a, bf16x8 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
 __device__ __forceinline__ f32x4 mfma_bf16x16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -64,27 +56,6 @@ __device__ __forceinline__ void bwait_vm() {
 }
 // workgroup barrier that no LDS access is moved across
 __device__ __forceinline__ void bbarrier() { asm volatile("s_barrier" ::: "memory"); }
-
-// 4 x 4 transpose inside each lane quad (lane k of a quad holds column k,
-// v[r] = row r on entry; row k, v[c] = column c on exit)
-__device__ __forceinline__ float bdpp(float x, int ctl) {
-  return __builtin_bit_cast(float, ctl == 0xB1
-      ? __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0xB1, 0xF, 0xF, false)
-      : __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x4E, 0xF, 0xF, false));
-}
-__device__ __forceinline__ void quad_t(float (&v)[4], int lane) {
-  const bool b1 = (lane & 2) != 0, b0 = (lane & 1) != 0;
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const float y = bdpp(b1 ? v[r] : v[r + 2], 0x4E);
-    if (b1) v[r] = y; else v[r + 2] = y;
-  }
-#pragma unroll
-  for (int r = 0; r < 4; r += 2) {
-    const float y = bdpp(b0 ? v[r] : v[r + 1], 0xB1);
-    if (b0) v[r] = y; else v[r + 1] = y;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // weight image: Bm[c][k] = W[c * ldw + k] (transpose = 0) or W[k * ldw + c]
@@ -332,132 +303,6 @@ k_gemm_nt_bf(const __bf16* __restrict__ A, int64_t lda, int64_t M, int R,
   }
 }
 
-// ---------------------------------------------------------------------------
-// TN: the output tile (256 rows n of dY's columns x 256 columns k of X's) of
-// one row chunk.  Each k-step stages 64 rows of both operands as 512-B rows
-// (16-B chunk c of row r at chunk c ^ 4 (r & 3)), read into MFMA fragments by
-// ds_read_b64_tr_b16: per 16-lane group a 4-row x 16-column block, lane
-// 4q + p addressing row q, columns 4p .. 4p + 3, lane i receiving column i
-// (row q in element q), so two reads give a lane its column's 8 rows
-// 8 (lane / 32) .. + 7 of the 16-row block — the same rows for both operands.
-// Rows past the chunk read as zeros (buffer descriptor range check).
-// (32-row k-steps with 3 in flight measured slower: 1.91 vs 1.59 ms per call
-// at configs[4], profiles/r04_bf2_c5_kernel_stats.csv)
-constexpr int TB_BN = 256, TB_BK = 256, TB_ROWS = 64, TB_NS = 2;
-constexpr int TB_STAGE = TB_ROWS * 512;              // 32 KB per operand
-constexpr int TB_LDS = TB_NS * 2 * TB_STAGE;         // 128 KB: 1 k-step in flight
-
-__device__ __forceinline__ bf16x8 tr_frag(uint32_t stage, int kb, int c0, int lane) {
-  const int q = (lane >> 2) & 3;
-  const int col = c0 + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  const uint32_t cpart = ((((col >> 3) ^ (q << 2))) << 4) + (col & 7) * 2;
-  bf16x8 r;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int row = 16 * kb + 8 * (lane >> 5) + 4 * i + q;
-    const fp16x4_t v =
-        __builtin_amdgcn_ds_read_tr16_b64_v4f16((lds_h4_ptr)(uintptr_t)(stage + row * 512 + cpart));
-    const bf16x4 w = __builtin_bit_cast(bf16x4, v);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) r[4 * i + e] = w[e];
-  }
-  return r;
-}
-
-__global__ void __launch_bounds__(BF_THREADS, 1)
-k_gemm_tn_bf(const __bf16* __restrict__ Y, int64_t ldy, const __bf16* __restrict__ X, int64_t ldx,
-             int64_t M, int N, int K, int64_t chunk, float* __restrict__ parts, int S) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
-  const int nkt = K / TB_BK, ntile = (N / TB_BN) * nkt;
-  // the tiles of one chunk: neighbouring workgroups of one XCD
-  const int bid = blockIdx.x, li = bid >> 3;
-  const int tile = li % ntile, s = (li / ntile) * 8 + (bid & 7);
-  if (s >= S) return;
-  const int n0 = (tile / nkt) * TB_BN, k0 = (tile % nkt) * TB_BK;
-  const int64_t r_begin = (int64_t)s * chunk;
-  const int64_t left = M - r_begin;
-  const int rows = left <= 0 ? 0 : (int)(left < chunk ? left : chunk);
-  const int T = (rows + TB_ROWS - 1) / TB_ROWS;
-
-  auto rsrc_of = [&](const __bf16* base, int64_t ld) {
-    const uint64_t p = reinterpret_cast<uint64_t>(base + (rows ? r_begin * ld : 0));
-    const uint64_t pu = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)p) |
-                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(p >> 32)) << 32);
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(pu), 0,
-                                             (int)((int64_t)rows * ld * 2), 0x00020000);
-  };
-  const auto ry = rsrc_of(Y + n0, ldy);
-  const auto rx = rsrc_of(X + k0, ldx);
-  const uint32_t ldy2 = (uint32_t)(ldy * 2), ldx2 = (uint32_t)(ldx * 2);
-  // DMA: instruction j = 4 wave + q moves rows 2j, 2j + 1 of the step
-  // (per wave and k-step 4 + 4 DMAs)
-  auto issue = [&](int t) {
-    char* st = smem + (t % TB_NS) * 2 * TB_STAGE;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = wave * 4 + q;
-      const int row = 2 * j + (lane >> 5);
-      const int lc = (lane & 31) ^ ((row & 3) << 2);
-      const uint32_t r = (uint32_t)(t * TB_ROWS + row);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ry, (lds_ptr_t)(st + j * 1024), 16, r * ldy2 + lc * 16, 0, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(st + TB_STAGE + j * 1024), 16,
-                                           r * ldx2 + lc * 16, 0, 0, 0);
-    }
-  };
-
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[m][n][e] = 0.0f;
-
-  const uint32_t smem_base = (uint32_t)(uintptr_t)(lds_ptr_t)smem;
-  for (int t = 0; t < TB_NS - 1 && t < T; ++t) issue(t);
-  for (int t = 0; t < T; ++t) {
-    // own DMAs of step t landed (nothing younger is in flight)
-    bwait_vm<0>();
-    bbarrier();
-    if (t + TB_NS - 1 < T) issue(t + TB_NS - 1);
-    const uint32_t sy = smem_base + (t % TB_NS) * 2 * TB_STAGE, sx = sy + TB_STAGE;
-#pragma unroll
-    for (int kb = 0; kb < TB_ROWS / 16; ++kb) {
-      bf16x8 a[2], b[4];
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) a[rb] = tr_frag(sy, kb, wr * 64 + rb * 32, lane);
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) b[cb] = tr_frag(sx, kb, wc * 128 + cb * 32, lane);
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb) acc[rb][cb] = mfma_bf(a[rb], b[cb], acc[rb][cb]);
-    }
-  }
-
-  // partial tile: lane quads transposed, 16-B stores
-  float* P = parts + (int64_t)s * N * K;
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-    for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[rb][cb][4 * g + r];
-        quad_t(v, lane);
-        const int n = n0 + wr * 64 + rb * 32 + 8 * g + 4 * (lane >> 5) + (lane & 3);
-        const int k = k0 + wc * 128 + cb * 32 + (lane & 28);
-        __builtin_nontemporal_store(f32x4{v[0], v[1], v[2], v[3]},
-                                    reinterpret_cast<f32x4*>(P + (int64_t)n * K + k));
-      }
-}
-
 template <typename F>
 bool set_lds(F* f, int bytes) {
   return hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) ==
@@ -493,22 +338,6 @@ int launch_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int R, const void
   else
     k_gemm_nt_bf<false><<<grid, BF_THREADS, BF_LDS, st>>>(a, lda, M, R, w, C, bias, o, ldo, m_tiles);
   return launch_status("rb_gemm_nt_bf16");
-}
-
-int launch_gemm_tn_bf16(const void* Y, int64_t ldy, const void* X, int64_t ldx, int64_t M, int N,
-                        int K, float* parts, int S, hipStream_t st) {
-  static bool attr = false;
-  if (!attr) {
-    if (!set_lds(k_gemm_tn_bf, TB_LDS))
-      return fail("rb_gemm_tn_bf16: the device refused 128 KB of LDS per workgroup (gfx950 only)");
-    attr = true;
-  }
-  const int64_t per = (M + S - 1) / S;
-  const int64_t chunk = (per + 63) / 64 * 64;   // the C-ABI's chunking (64-row multiples)
-  const int ntile = (N / TB_BN) * (K / TB_BK);
-  k_gemm_tn_bf<<<(unsigned)(ntile * S), BF_THREADS, TB_LDS, st>>>(
-      (const __bf16*)Y, ldy, (const __bf16*)X, ldx, M, N, K, chunk, parts, S);
-  return launch_status("rb_gemm_tn_bf16");
 }
 
 }  // namespace rb

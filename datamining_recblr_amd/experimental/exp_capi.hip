@@ -59,7 +59,7 @@ int launch_grl_bwd(const float* xz, int64_t xz_rs, const float* conv_w, int KC,
 using namespace rb;
 
 namespace {
-constexpr int RB_EXP_ABI = 43;   // = the product library's rb_version() it pairs with
+constexpr int RB_EXP_ABI = 44;   // = the product library's rb_version() it pairs with
 }  // namespace
 
 extern "C" {

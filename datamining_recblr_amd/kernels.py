@@ -1266,23 +1266,6 @@ def gemm_nt_bf16(a: torch.Tensor, img: torch.Tensor, C: int,
     return out
 
 
-def gemm_tn_bf16(dy: torch.Tensor, x: torch.Tensor, splits: int) -> torch.Tensor:
-    """Row-chunk partials of dW = dy^T x on bf16 operands (rb_gemm_tn_bf16):
-    fp32 [splits, N, K]."""
-    _check(dy, "dy", torch.bfloat16)
-    _check(x, "x", torch.bfloat16)
-    if dy.dim() != 2 or x.dim() != 2 or dy.stride(1) != 1 or x.stride(1) != 1:
-        raise ValueError("dy and x must be 2-D with unit inner stride")
-    M, N = dy.shape
-    K = x.shape[1]
-    if x.shape[0] != M:
-        raise ValueError("dy and x must have the same rows")
-    parts = torch.empty((splits, N, K), device=dy.device, dtype=torch.float32)
-    _lib.call("rb_gemm_tn_bf16", dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), M, N, K,
-              parts.data_ptr(), splits, _stream(dy))
-    return parts
-
-
 def gemm_tn_hs(dy: torch.Tensor, x: torch.Tensor, out: torch.Tensor | None = None,
                accumulate: bool = False) -> torch.Tensor:
     """dW = dy^T x [N, K] for few rows on the f16 pipe (rb_gemm_tn_hs: exact

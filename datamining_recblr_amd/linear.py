@@ -201,10 +201,11 @@ def rmax_buffer(a: torch.Tensor, C: int, R: int) -> torch.Tensor | None:
 #     NT kernel for R <= 512 inputs (the three forward GEMMs and out's input
 #     gradient: 4-9% faster than hipBLASLt, profiles/r05_bfmid_shapes.txt);
 #     hipBLASLt for the K = 1024 input gradients of the in / gates
-#     projections (7-14% faster there) and for the three weight gradients
-#     (torch's batched split-K + rb_colsum, 4-24% faster than
-#     rb_gemm_tn_bf16, profiles/r05_tn48_shapes.txt);
-#   "1" — ours on every shape; "0" — hipBLASLt on every shape.
+#     projections (7-14% faster there);
+#   "1" — ours on every NT shape; "0" — hipBLASLt on every shape.
+# The weight gradients of bf16 activations always run on torch's batched
+# split-K + rb_colsum (round 5's rb_gemm_tn_bf16 measured 4-24% behind it,
+# profiles/r05_tn48_shapes.txt, and was removed in round 6).
 # The weight's bf16 fragment images (W for the forward, W^T for the input
 # gradient) are cached per weight version like the split images.
 BF16_NT_MAX_R = 512
@@ -213,7 +214,6 @@ BF16_NT_MAX_R = 512
 # 2,097,152 rows, and below a round the persistent grid runs partly empty —
 # smaller bf16 GEMMs stay on hipBLASLt ("1" forces ours at any size)
 BF16_NT_MIN_ROWS = 65536
-BF16_TN_MAX_N = 0   # auto: no weight-gradient shape on rb_gemm_tn_bf16
 _BF16_MODES = ("auto", "1", "0")
 _bf16_gemm = os.environ.get("RECBLR_BF16_GEMM", "auto")
 if _bf16_gemm not in _BF16_MODES:
@@ -388,8 +388,6 @@ MIN_ROWS_FOR_SPLIT = 16384
 # another lease) — the step then runs no library GEMM (RECBLR_TN_FEW=0:
 # hipBLASLt)
 TN_FEW_MIN_ROWS = 2048
-# bf16 operands (configs[4]): the bf16 weight-gradient kernel from this many rows
-TN_BF16_MIN_ROWS = 4096
 _tn_few = os.environ.get("RECBLR_TN_FEW", "1") != "0"
 
 
@@ -408,9 +406,9 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
     """dW = dy2^T @ x2 for dy2 [M, N], x2 [M, K] (row-strided views allowed).
     With both operands' row-group maxima (ymax, xmax: the rmax outputs of the
     f16 GEMMs that read dy2 and x2), on the f16 pipe (rb_gemm_tn_h: fixed-order
-    row-chunk partials); else hipBLASLt's batched split-K.  bf16 activations
-    (config 5): bf16 MFMA partials, summed in fp32; the result is fp32 like
-    the parameter."""
+    row-chunk partials); else hipBLASLt's batched split-K (bf16 activations,
+    config 5: bf16 partials, summed in fp32; the result is fp32 like the
+    parameter)."""
     M = dy2.shape[0]
     N, K = dy2.shape[1], x2.shape[1]
     if (ymax is not None and xmax is not None
@@ -423,16 +421,6 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, splits: int = SPLIT_K,
         if M < MIN_ROWS_FOR_SPLIT:   # at least one 32-row group per split
             S = max(8, min(S, M // 32 // 8 * 8))
         parts = kernels.gemm_tn_h(dy2, x2, ymax, xmax, S)
-        return kernels.colsum(parts.view(S, -1)).view(N, K)
-    if (_bf16_gemm != "0" and (_bf16_gemm == "1" or N <= BF16_TN_MAX_N)
-            and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16
-            and M >= TN_BF16_MIN_ROWS and N % 256 == 0 and K % 256 == 0
-            and dy2.stride(1) == 1 and x2.stride(1) == 1 and dy2.stride(0) % 8 == 0
-            and x2.stride(0) % 8 == 0 and dy2.data_ptr() % 16 == 0 and x2.data_ptr() % 16 == 0):
-        # one 256 x 256 tile per chunk and CU: splits x tiles ~ one round
-        nt = (N // 256) * (K // 256)
-        S = max(8, min(_tn_splits(dy2.device, nt) // 2 // 8 * 8, M // 64 // 8 * 8))
-        parts = kernels.gemm_tn_bf16(dy2, x2, S)
         return kernels.colsum(parts.view(S, -1)).view(N, K)
     if (_small_tn and _half and _split_on and _tn_on and M < MIN_ROWS_FOR_SPLIT and N % 32 == 0
             and K % 32 == 0 and dy2.dtype == torch.float32 and x2.dtype == torch.float32

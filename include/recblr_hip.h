@@ -610,14 +610,6 @@ int rb_gemm_bf16_weight_image(const float* W, int64_t ldw, int64_t C, int64_t R,
 int rb_gemm_nt_bf16(const void* A, int64_t lda, int64_t M, int64_t R, const void* img, int64_t C,
                     const float* bias, void* out, int64_t ldo, void* stream);
 
-/* Weight gradient on bf16 operands: parts[s][n, k] (fp32, every slot
- * written) = sum over the rows m of chunk s of dY[m, n] X[m, k] (bf16;
- * chunks of a multiple of 64 rows); sum the partials in order (rb_colsum).
- * N % 256 == 0, K % 256 == 0, splits % 8 == 0, row strides multiples of 8,
- * pointers 16-byte aligned. */
-int rb_gemm_tn_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx, int64_t M, int64_t N,
-                    int64_t K, float* parts, int64_t splits, void* stream);
-
 /* dW (+)= dY^T X for few rows M (F.linear's weight gradient on the gathered
  * last-layer tail, RecBLR.py:167,213,214 at B rows; any M up to 2^24, fastest
  * below ~16k): dW [N, K] row-major fp32, written (accumulate = 0) or added to

@@ -239,7 +239,7 @@ def test_c5_bf16_full_batch_rows_match_oracle(cuda, monkeypatch):
     per-shape GEMM dispatch (RECBLR_BF16_GEMM=auto), with our bf16 NT kernel
     asserted engaged at M = 2,097,152 rows (the three forward projections and
     out's input gradient) and the three weight gradients on the library's
-    split-K path (rb_gemm_tn_bf16 not called in auto) at the same M.  Three
+    split-K path at the same M.  Three
     batch rows are re-run on the fp32 CPU oracle with the same bf16-rounded
     input and output gradient: y and dx rows within the 1.2e-2 bar of
     test_grl_bf16_vs_oracle (batch rows are independent in the layer, so the
@@ -249,12 +249,10 @@ def test_c5_bf16_full_batch_rows_match_oracle(cuda, monkeypatch):
 
     B, L, d = 1024, 2048, 256
     M = B * L
-    nt_rows, tn_calls, wg = [], [], []
-    nt0, tn0, wg0 = kernels.gemm_nt_bf16, kernels.gemm_tn_bf16, linear.wgrad
+    nt_rows, wg = [], []
+    nt0, wg0 = kernels.gemm_nt_bf16, linear.wgrad
     monkeypatch.setattr(kernels, "gemm_nt_bf16",
                         lambda a, *r, **k: nt_rows.append(a.shape[0]) or nt0(a, *r, **k))
-    monkeypatch.setattr(kernels, "gemm_tn_bf16",
-                        lambda *a, **k: tn_calls.append(1) or tn0(*a, **k))
     counted = (lambda dy2, x2, *a, **k: wg.append((dy2.shape[0], dy2.dtype))
                or wg0(dy2, x2, *a, **k))
     monkeypatch.setattr(linear, "wgrad", counted)
@@ -273,7 +271,6 @@ def test_c5_bf16_full_batch_rows_match_oracle(cuda, monkeypatch):
     finally:
         linear.set_bf16_gemm(prev)
     assert nt_rows == [M] * 4, nt_rows
-    assert not tn_calls
     assert wg == [(M, BF)] * 3, wg
     rows = torch.tensor([0, 511, 1023], device=cuda)
     params = {k: v.detach().cpu().requires_grad_() for k, v in layer.state_dict().items()}

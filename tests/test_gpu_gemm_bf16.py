@@ -1,12 +1,12 @@
 """bf16-operand projection GEMMs (csrc/gemm_bf16.hip: rb_gemm_nt_bf16,
-rb_gemm_tn_bf16, rb_gemm_bf16_weight_image) — the configs[4] Linears
-(RecBLR.py:162,165,167 and their autograd) on bf16 activations.
+rb_gemm_bf16_weight_image) — the configs[4] Linears (RecBLR.py:162,165,167
+and their autograd) on bf16 activations; their weight gradients run on
+hipBLASLt's split-K (round 5's rb_gemm_tn_bf16 was removed in round 6).
 
 Reference: the same bf16 operands in fp64 on the host.  The NT output is one
 rounding of an fp32 sum to bf16, so each element must sit within a bf16
 half-ulp (2^-9 relative, tested at 2^-8) plus the fp32 accumulation bound
-(K 2^-24 sum |a w|, tested at 1e-5 of that sum); the weight-gradient partials
-are fp32 sums of exact bf16 products (tested at 1e-5 of sum |dy x|)."""
+(K 2^-24 sum |a w|, tested at 1e-5 of that sum)."""
 import pytest
 import torch
 
@@ -82,53 +82,23 @@ def test_bf16_weight_image_layout(cuda):
     assert torch.equal(imt[2, 1, 37], wb[48:56, 37])
 
 
-@pytest.mark.parametrize("M,N,K,S", [
-    (4096, 1024, 256, 64),
-    (100000, 256, 512, 16),      # chunks of 6,272 rows, the last one short
-    (300, 512, 256, 16),         # most chunks empty: their slots written as zeros
-    (4096 + 33, 1024, 512, 8),
-])
-def test_gemm_tn_bf16_vs_fp64(cuda, M, N, K, S):
-    g = torch.Generator(device=cuda).manual_seed(M + N + K)
-    dy = torch.randn(M, N, device=cuda, generator=g).to(BF)
-    x = torch.randn(M, K, device=cuda, generator=g).to(BF)
-    parts = kernels.gemm_tn_bf16(dy, x, S)
-    assert bool(torch.isfinite(parts).all())
-    dw = parts.sum(0).double().cpu()
-    ref = dy.double().cpu().t() @ x.double().cpu()
-    mag = dy.double().abs().cpu().t() @ x.double().abs().cpu()
-    assert bool(((dw - ref).abs() <= 1e-5 * mag).all())
-    # each slot is its own chunk's product
-    chunk = ((M + S - 1) // S + 63) // 64 * 64
-    s = 1 if M > chunk else 0
-    r0, r1 = s * chunk, min(M, (s + 1) * chunk)
-    ref1 = dy[r0:r1].double().cpu().t() @ x[r0:r1].double().cpu()
-    mag1 = dy[r0:r1].double().abs().cpu().t() @ x[r0:r1].double().abs().cpu()
-    assert bool(((parts[s].double().cpu() - ref1).abs() <= 1e-5 * mag1 + 1e-30).all())
-
-
 def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     """configs[4]'s GatedRecurrentLayer (d = 256, L = 2048) with
-    RECBLR_BF16_GEMM=1 runs all three projections' forward, input-gradient and
-    weight-gradient GEMMs on the bf16 kernels, the default per-shape mode
-    (auto) four of the nine from BF16_NT_MIN_ROWS rows on (none below), and
-    both agree with the hipBLASLt path
+    RECBLR_BF16_GEMM=1 runs all three projections' forward and input-gradient
+    GEMMs on the bf16 NT kernel, the default per-shape mode (auto) four of the
+    six from BF16_NT_MIN_ROWS rows on (none below), the weight gradients on
+    hipBLASLt's split-K in every mode, and both agree with the hipBLASLt path
     (RECBLR_BF16_GEMM=0) to bf16 accuracy."""
     from datamining_recblr_amd.model import GatedRecurrentLayer
 
-    calls = {"nt": 0, "tn": 0}
-    nt0, tn0 = kernels.gemm_nt_bf16, kernels.gemm_tn_bf16
+    calls = {"nt": 0}
+    nt0 = kernels.gemm_nt_bf16
 
     def nt(*a, **k):
         calls["nt"] += 1
         return nt0(*a, **k)
 
-    def tn(*a, **k):
-        calls["tn"] += 1
-        return tn0(*a, **k)
-
     monkeypatch.setattr(kernels, "gemm_nt_bf16", nt)
-    monkeypatch.setattr(kernels, "gemm_tn_bf16", tn)
     torch.manual_seed(5)
     layer = GatedRecurrentLayer(d_model=256).to(cuda)
     g = torch.Generator(device=cuda).manual_seed(9)
@@ -148,22 +118,21 @@ def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
             linear.set_bf16_gemm(prev)
 
     y1, dx1, g1 = run(True)
-    assert calls == {"nt": 6, "tn": 3}, calls
+    assert calls == {"nt": 6}, calls
     y0, dx0, g0 = run(False)
-    assert calls == {"nt": 6, "tn": 3}
+    assert calls == {"nt": 6}
     # the default per-shape mode below its row minimum (4,096 rows here):
     # every GEMM on hipBLASLt, so the results equal the "0" run bit for bit
     ys, dxs, gs = run("auto")
-    assert calls == {"nt": 6, "tn": 3}, calls
+    assert calls == {"nt": 6}, calls
     assert torch.equal(ys, y0) and torch.equal(dxs, dx0)
     for n in g0:
         assert torch.equal(gs[n], g0[n]), n
     # ... and from the minimum on: ours for the R <= 512 NT GEMMs (in / gates
-    # / out forward, out's input gradient); hipBLASLt for in.dX, gates.dX and
-    # the three weight gradients
+    # / out forward, out's input gradient); hipBLASLt for in.dX and gates.dX
     monkeypatch.setattr(linear, "BF16_NT_MIN_ROWS", 4096)
     ya, dxa, ga = run("auto")
-    assert calls == {"nt": 10, "tn": 3}, calls
+    assert calls == {"nt": 10}, calls
 
     def rel(a, b):
         return ((a - b).abs().max() / b.abs().max()).item()
@@ -175,27 +144,6 @@ def test_grl_bf16_projections_on_own_kernels(cuda, monkeypatch):
     for n in g0:
         assert rel(g1[n], g0[n]) < 2e-2, n
         assert rel(ga[n], g0[n]) < 2e-2, n
-
-
-def test_gemm_tn_bf16_operands_above_bit_31(cuda):
-    """rb_gemm_tn_bf16 with both operands at device addresses whose bit 31 is
-    set (the descriptor base of round 4's TN fault), bitwise
-    equal to the same operands placed by the allocator."""
-    M, N, K, S = 100000, 256, 512, 16
-    g = torch.Generator(device=cuda).manual_seed(31)
-    dy0 = torch.randn(M, N, device=cuda, generator=g).to(BF)
-    x0 = torch.randn(M, K, device=cuda, generator=g).to(BF)
-    need = 2 * M * (N + K)
-    buf = torch.empty(bit31_alloc_bytes(need), dtype=torch.uint8, device=cuda)
-    off = bit31_offset(buf.data_ptr(), need)
-    dy = buf[off: off + 2 * M * N].view(BF).view(M, N)
-    off += 2 * M * N
-    x = buf[off: off + 2 * M * K].view(BF).view(M, K)
-    for t in (dy, x):
-        assert (t.data_ptr() >> 31) & 1 and t.data_ptr() % 16 == 0
-    dy.copy_(dy0)
-    x.copy_(x0)
-    assert torch.equal(kernels.gemm_tn_bf16(dy, x, S), kernels.gemm_tn_bf16(dy0, x0, S))
 
 
 def test_bf16_linear_with_no_rows(cuda, monkeypatch):

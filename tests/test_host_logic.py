@@ -193,7 +193,7 @@ def test_bf16_gemm_modes_and_shape_rule(monkeypatch):
         with pytest.raises(ValueError):
             linear.set_bf16_gemm("yes")
         assert linear._bf16_gemm == "auto"
-        assert linear.BF16_NT_MAX_R == 512 and linear.BF16_TN_MAX_N == 0
+        assert linear.BF16_NT_MAX_R == 512
         assert linear.BF16_NT_MIN_ROWS == 65536
     finally:
         linear.set_bf16_gemm(prev)
