@@ -1169,14 +1169,18 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   // substep's fragment reads — substep 1's splits and LDS writes issue while
   // substep 0's MFMAs execute (each substep: two columns, fragment reads,
   // their wait, 12 MFMAs).
-  auto mma = [&](int buf, auto conv_c, const f32x4 (&r)[8], int t, int nbuf) {
+  // LATE (loader waves 4-7 of a 512-thread workgroup): each substep's MFMAs
+  // first, then its columns' conversion, so the two waves of a SIMD alternate
+  // between the split and the matrix pipe instead of converting in lock step
+  auto mma = [&](int buf, auto conv_c, const f32x4 (&r)[8], int t, int nbuf, auto late_c) {
     (void)t;
     constexpr bool CONV = decltype(conv_c)::value;
+    constexpr bool LATE = decltype(late_c)::value;
     const uint32_t iy = smem_base + buf * CF::STAGE;
     const uint32_t ix = iy + 2 * CF::YPLANE;
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      if constexpr (CONV) convert_pair(r, nbuf, st);
+      if constexpr (CONV && !LATE) convert_pair(r, nbuf, st);
       // B fragments of both column blocks, then the A fragments one row
       // block at a time (24 fragment registers live, not 32)
       f16x8 b[2][2];
@@ -1204,6 +1208,7 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
           acc[i][j] = mfma_h(a0, b[j][0], acc[i][j]);
         }
       }
+      if constexpr (CONV && LATE) convert_pair(r, nbuf, st);
     }
   };
   using conv_t = std::true_type;
@@ -1220,7 +1225,7 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   // them (a load under a branch made it wait for all of them, which left one
   // step of lead instead of two).
   const int Tp = (T + 1) & ~1;
-  if (__builtin_amdgcn_readfirstlane(tid >> 6) < CF::LOADERS / 64) {
+  auto loader_loop = [&](auto late_c) {
     load(0, raw0);
     load(1, raw1);
     convert_pair(raw0, 0, 0);
@@ -1228,19 +1233,24 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
     load(2, raw0);
     __syncthreads();
     for (int t = 0; t < Tp; t += 2) {
-      mma(0, conv_t{}, raw1, t + 1, 1);
+      mma(0, conv_t{}, raw1, t + 1, 1, late_c);
       load(t + 3, raw1);
       __syncthreads();
-      mma(1, conv_t{}, raw0, t + 2, 0);
+      mma(1, conv_t{}, raw0, t + 2, 0, late_c);
       load(t + 4, raw0);
       __syncthreads();
     }
+  };
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (wv < CF::LOADERS / 64) {
+    if (CF::THREADS == 512 && wv >= 4) loader_loop(std::true_type{});
+    else loader_loop(std::false_type{});
   } else {
     __syncthreads();
     for (int t = 0; t < Tp; t += 2) {
-      mma(0, noconv_t{}, raw1, 0, 0);
+      mma(0, noconv_t{}, raw1, 0, 0, std::false_type{});
       __syncthreads();
-      mma(1, noconv_t{}, raw0, 0, 0);
+      mma(1, noconv_t{}, raw0, 0, 0, std::false_type{});
       __syncthreads();
     }
   }
