@@ -10,7 +10,7 @@ mkdir -p "$tmp/pkg/csrc" "$tmp/include"
 cp include/* "$tmp/include/"
 cp datamining_recblr_amd/csrc/* "$tmp/pkg/csrc/"
 for kv in "$@"; do cp "${kv#*=}" "$tmp/pkg/csrc/${kv%%=*}"; done
-/opt/rocm/bin/hipcc -parallel-jobs=8 -O3 -std=c++17 -shared -fPIC --offload-arch=gfx950 \
+/opt/rocm/bin/hipcc -parallel-jobs=8 -O3 -std=c++20 -shared -fPIC --offload-arch=gfx950 \
   -ffp-contract=off -Wno-unused-function -I "$tmp/include" \
   -o datamining_recblr_amd/lib/ab_$name.so "$tmp"/pkg/csrc/*.hip
 rm -rf "$tmp"
