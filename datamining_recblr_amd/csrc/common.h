@@ -269,11 +269,15 @@ __device__ __forceinline__ void stv_raw(bf16_t* p, const RawVec<bf16_t, V>& r) {
 // ---- dropout keep-flags ------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11): counter = element index / 4, key =
 // 64-bit seed, 4 uniform u32 per call -> keep flags of 4 consecutive elements.
+// (each round's two 32 x 32 -> 64 products as one v_mad_u64_u32 each, not a
+// v_mul_lo_u32 + v_mul_hi_u32 pair: the same bits in half the quarter-rate
+// instructions — the dropout epilogues are bound by this VALU work)
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
-    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+    const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
