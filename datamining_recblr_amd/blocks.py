@@ -31,7 +31,8 @@ from .linear import (_timed, fire_hooks, has_hooks, linear, mm_nn, mm_nn_dact, m
                      mm_nt_act, mm_nt_act_ok, mm_nt_ln, mm_nt_ln_ok, rmax_buffer, wgrad)
 
 __all__ = ["draw_seed", "ResidualGrad", "add_dropout_layer_norm", "embed_dropout_layer_norm",
-           "silu_dropout", "feed_forward", "set_defer_residual", "defer_residual"]
+           "linear_add_dropout_layer_norm", "silu_dropout", "feed_forward", "set_defer_residual",
+           "defer_residual"]
 
 
 _GOLDEN = 0x9E3779B97F4A7C15   # odd 64-bit constant (2^64 / golden ratio)
@@ -158,6 +159,51 @@ class _AddDropoutLN(torch.autograd.Function):
             ds, need_r = None, False
         return (da.view(shape) if need_a else None, ds.view(shape) if need_r else None,
                 dg, db, None, None, None, None, None, None)
+
+
+class _LinearAddDropoutLN(torch.autograd.Function):
+    """LayerNorm(dropout(x W^T) + residual) with the projection's GEMM and the
+    residual LayerNorm in one launch (rb_gemm_nt_h_ln): the recurrent layer's
+    out-projection and its residual LayerNorm, RecBLR.py:142, 167.  Backward:
+    rb_add_ln_bwd2, then the projection's input and weight gradients as
+    LinearFn's (the projection has no bias)."""
+
+    @staticmethod
+    def forward(ctx, x, w, residual, gamma, beta, seed, p, eps, slot=None, addend=None):
+        d = w.shape[0]
+        x2 = x.reshape(-1, x.shape[-1])
+        r2 = residual.reshape(-1, d).contiguous()
+        f = 2 * x2.shape[0] * x2.shape[1] * d
+        rx = rmax_buffer(x2, d, x2.shape[1]) if ctx.needs_input_grad[1] else None
+        y, s, mean, rstd = _timed("gemm", f, mm_nt_ln, x2, w, None, r2, gamma, beta, eps, seed, p,
+                                  rmax=rx)
+        ctx.seed, ctx.p, ctx.slot, ctx.rx = seed, p, slot, rx
+        ctx.xshape = x.shape
+        ctx.addend = _take(addend)
+        ctx.save_for_backward(x2, w, s, mean, rstd, gamma)
+        return y.view(residual.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, s, mean, rstd, gamma = ctx.saved_tensors
+        need_x, need_w, need_r = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        ds, da, dg, db, _ = kernels.add_ln_bwd(dy, s, gamma, mean, rstd, seed=ctx.seed, p=ctx.p,
+                                               want_ds=need_r, want_da=True,
+                                               dy2=_pop(ctx.addend))
+        if need_r and ctx.slot is not None:   # handed to the GRL input projection
+            ctx.slot.ds = ds
+            ds, need_r = None, False
+        d = w.shape[0]
+        da2 = da.reshape(-1, d)
+        f = 2 * x2.shape[0] * x2.shape[1] * d
+        dx = dw = ry = None
+        if need_x:
+            ry = rmax_buffer(da2, x2.shape[1], d) if ctx.rx is not None else None
+            dx = _timed("gemm", f, mm_nn, da2, w, rmax=ry).view(ctx.xshape)
+        if need_w:
+            dw = _timed("gemm", f, wgrad, da2, x2, ymax=ry, xmax=ctx.rx)
+        return (dx, dw, ds.view(dy.shape) if need_r else None, dg, db, None, None, None, None,
+                None)
 
 
 class _EmbedDropoutLN(torch.autograd.Function):
@@ -298,6 +344,24 @@ def add_dropout_layer_norm(a, residual, dropout: torch.nn.Dropout, ln: torch.nn.
     p, seed = _drop(dropout, training)
     return _AddDropoutLN.apply(a, residual, ln.weight, ln.bias, None, seed, p, ln.eps, slot,
                                addend)
+
+
+def linear_add_dropout_layer_norm(x, proj: torch.nn.Linear, residual, dropout: torch.nn.Dropout,
+                                  ln: torch.nn.LayerNorm, training: bool,
+                                  slot: ResidualGrad | None = None,
+                                  addend: ResidualGrad | None = None):
+    """ln(dropout(proj(x)) + residual) — RecBLR.py:142 after :167 — as one
+    GEMM launch with the LayerNorm in its epilogue where rb_gemm_nt_h_ln
+    applies (d = 128 outputs, no bias, from 16,384 rows on the
+    weight-stationary kernel); else the projection (its module call, hooks
+    included) and add_dropout_layer_norm.  slot / addend as there."""
+    _require_gpu(x)
+    x2 = x.reshape(-1, x.shape[-1])
+    if proj.bias is None and ln.weight.shape[0] == proj.weight.shape[0] and mm_nt_ln_ok(x2, proj.weight):
+        p, seed = _drop(dropout, training)
+        return _LinearAddDropoutLN.apply(x, proj.weight, residual, ln.weight, ln.bias, seed, p,
+                                         ln.eps, slot, addend)
+    return add_dropout_layer_norm(proj(x), residual, dropout, ln, training, slot, addend)
 
 
 def embed_dropout_layer_norm(idx, emb: torch.nn.Embedding, dropout: torch.nn.Dropout,

@@ -29,7 +29,7 @@ from torch import nn
 
 from ._lib import RecBLRNativeError
 from .blocks import (ResidualGrad, add_dropout_layer_norm, embed_dropout_layer_norm,
-                     feed_forward)
+                     feed_forward, linear_add_dropout_layer_norm)
 from .kernels import Packed, grl_max_tiles, grl_pieces, pack_plan
 from .linear import HipLinearForward, fire_hooks, has_hooks, linear
 from .recbole_compat import BPRLoss, SequentialRecommender, install_interaction_hook
@@ -142,7 +142,7 @@ class GatedRecurrentLayer(nn.Module):
         for m in (self.input, self.output):
             m.forward = HipLinearForward(m)
 
-    def forward(self, x, pad=None, slot=None, rows=None, seq=None):
+    def forward(self, x, pad=None, slot=None, rows=None, seq=None, project=True):
         """pad: None (the reference's pow2 pad prefix for x's length) or an
         int64 tensor [B] of per-row pad lengths (see recurrence.bd_lru).
         slot: blocks.ResidualGrad of the enclosing RecurrentLayer.
@@ -175,7 +175,9 @@ class GatedRecurrentLayer(nn.Module):
                 y = y.index_select(0, seq.inv)
         elif rows is not None:
             y = y.reshape(-1, y.shape[-1]).index_select(0, rows)
-        return self.output(y)
+        # project=False: y before the out-projection (the caller fuses the
+        # projection with its residual LayerNorm, blocks.linear_add_dropout_layer_norm)
+        return self.output(y) if project else y
 
     @staticmethod
     def pad_len(seq_len: int) -> int:
@@ -226,15 +228,25 @@ class RecurrentLayer(nn.Module):
         residual = input_tensor
         if rows is not None:
             residual = input_tensor.reshape(-1, input_tensor.shape[-1]).index_select(0, rows)
-        y = self.behavior_modeling(input_tensor, pad, slot, rows, seq)
-        if self.disable_ffn:
+        out = self.behavior_modeling.output
+        # full rows: the out-projection and the residual LayerNorm in one
+        # launch where it applies (blocks.linear_add_dropout_layer_norm)
+        fuse = rows is None and not has_hooks(out)
+        y = self.behavior_modeling(input_tensor, pad, slot, rows, seq, project=not fuse)
+
+        def add_ln(addend):
+            if fuse:
+                return linear_add_dropout_layer_norm(y, out, residual, self.dropout,
+                                                     self.layer_norm, self.training, slot, addend)
             return add_dropout_layer_norm(y, residual, self.dropout, self.layer_norm,
-                                          self.training, slot, out_addend)
+                                          self.training, slot, addend)
+
+        if self.disable_ffn:
+            return add_ln(out_addend)
         # the FFN's own residual gradient goes back through h_slot to the
         # LayerNorm that produced h
         h_slot = ResidualGrad() if grad else None
-        h = add_dropout_layer_norm(y, residual, self.dropout, self.layer_norm, self.training,
-                                   slot, h_slot)
+        h = add_ln(h_slot)
         return self.ffn(h, h_slot, out_addend)
 
 

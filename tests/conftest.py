@@ -47,13 +47,13 @@ def cuda():
 @pytest.fixture
 def split_gemm_calls(monkeypatch):
     """Records every launch of the f16x3 split-operand GEMM (kernels.gemm_nt_h
-    / rb_gemm_nt_h and its fused-activation variants kernels.gemm_nt_h_act /
-    gemm_nt_h_dact) as (M, R, C): tests use it to assert that the path they
-    claim to check actually ran the kernel."""
+    / rb_gemm_nt_h and its fused-epilogue variants kernels.gemm_nt_h_act /
+    gemm_nt_h_dact / gemm_nt_h_ln) as (M, R, C): tests use it to assert that
+    the path they claim to check actually ran the kernel."""
     from datamining_recblr_amd import kernels
 
     calls = []
-    for name in ("gemm_nt_h", "gemm_nt_h_act", "gemm_nt_h_dact"):
+    for name in ("gemm_nt_h", "gemm_nt_h_act", "gemm_nt_h_dact", "gemm_nt_h_ln"):
         orig = getattr(kernels, name)
 
         def counted(a, wf, C, *args, _orig=orig, **kw):

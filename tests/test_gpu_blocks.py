@@ -297,6 +297,45 @@ def test_feed_forward_ln_epilogue(cuda, M, monkeypatch):
         close(u, v, atol=2e-5 * v.abs().max().item(), rtol=1e-4, what=name + " (ln epilogue)")
 
 
+def test_recurrent_layer_out_projection_ln_epilogue(cuda, monkeypatch):
+    """RecurrentLayer with the out-projection and its residual LayerNorm in
+    one launch (RecBLR.py:142, 167: rb_gemm_nt_h_ln, rb_add_ln_fwd not called
+    for that LayerNorm) == the projection + rb_add_ln_fwd path: output and
+    every parameter / input gradient within fp32 rounding of the LayerNorm
+    moments, in train mode with dropout (same seeds)."""
+    from datamining_recblr_amd import blocks, kernels, linear
+    from datamining_recblr_amd.model import RecurrentLayer
+
+    torch.manual_seed(3)
+    layer = RecurrentLayer(d_model=128, d_conv=4, expand=2, dropout=0.2, num_layers=2,
+                           bd_lru_only=False, disable_conv1d=False, disable_ffn=False).to(cuda)
+    layer.train()
+    g = torch.Generator(device="cpu").manual_seed(4)
+    x0 = torch.randn(96, 200, 128, generator=g).to(cuda)   # 19,200 rows
+    dy = torch.randn(96, 200, 128, generator=g).to(cuda)
+    res = []
+    for on in (True, False):
+        prev = linear.set_ln_fused(on)
+        calls = []
+        orig = kernels.gemm_nt_h_ln
+        monkeypatch.setattr(kernels, "gemm_nt_h_ln", lambda *a, **k: calls.append(a[0].shape[1]) or orig(*a, **k))
+        try:
+            torch.manual_seed(11)   # the same dropout seeds both ways
+            layer.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_()
+            y = layer(x)
+            y.backward(dy)
+            res.append([y.detach(), x.grad] + [p.grad.clone() for p in layer.parameters()])
+        finally:
+            linear.set_ln_fused(prev)
+            monkeypatch.setattr(kernels, "gemm_nt_h_ln", orig)
+        # the out-projection (K = 256) and the FeedForward's w_2 (K = 512)
+        assert sorted(calls) == ([256, 512] if on else []), calls
+    names = ["y", "dx"] + [n for n, _ in layer.named_parameters()]
+    for name, u, v in zip(names, res[0], res[1]):
+        close(u, v, atol=2e-5 * v.abs().max().item(), rtol=1e-4, what=name + " (out-proj ln)")
+
+
 def test_train_mode_dropout(cuda):
     """Train-mode model: fresh dropout per call (outputs differ run to run),
     reproducible under torch.manual_seed, and p = 0 in train mode == eval."""
