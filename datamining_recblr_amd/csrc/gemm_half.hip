@@ -1292,7 +1292,9 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   }
 
   // un-scale and store the partial tile (every split writes its slot, empty
-  // chunks zeros): the chunk exponents, or (pass 1) each column's
+  // chunks zeros; nontemporal: no dirty L2 lines for the kernel boundary to
+  // write back before the column sum, 5.546-5.551 vs 5.553-5.565 ms per step,
+  // profiles/r06_ab_tnnt.txt): the chunk exponents, or (pass 1) each column's
   float* out = parts + (int64_t)s * N * K;
   if constexpr (pass == 0) {
     const int sh = ey + ex - 2 * kTT;
@@ -1304,7 +1306,7 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int row = n0 + 64 * wm + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
-          out[(int64_t)row * K + col] = __builtin_amdgcn_ldexpf(acc[i][j][e], sh);
+          __builtin_nontemporal_store(__builtin_amdgcn_ldexpf(acc[i][j][e], sh), out + (int64_t)row * K + col);
         }
       }
   } else {
@@ -1318,7 +1320,7 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
         for (int j = 0; j < 2; ++j) {
           const int kl = 64 * wk + 32 * j + (lane & 31);
           const int ek = *reinterpret_cast<const int*>(smem + 2 * CF::YPLANE + kl * T_PITCH + 64);
-          out[(int64_t)(n0 + nl) * K + k0 + kl] = __builtin_amdgcn_ldexpf(acc[i][j][e], en + ek);
+          __builtin_nontemporal_store(__builtin_amdgcn_ldexpf(acc[i][j][e], en + ek), out + (int64_t)(n0 + nl) * K + k0 + kl);
         }
       }
   }
