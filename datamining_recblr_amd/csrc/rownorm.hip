@@ -22,11 +22,14 @@
 namespace rb {
 namespace {
 
-// Store policy of the LayerNorm outputs: the forward's (y, s) nontemporal
-// (its consumers, the in-projection GEMM and through it the conv, read
-// faster: conv forward 0.65 -> 0.69), the backward's (ds, da) default (nt
-// cost the backward kernel 0.68 -> 0.61); profiles/r02_ab_ln_store_policy.log.
-constexpr bool kLnFwdNT = true, kLnBwdNT = false;
+// Store policy of the LayerNorm outputs: nontemporal both ways.  The
+// forward's (y, s): its consumers, the in-projection GEMM and through it the
+// conv, read faster (conv forward 0.65 -> 0.69,
+// profiles/r02_ab_ln_store_policy.log).  The backward's (ds, da): round 2
+// measured the kernel alone slower with nt (0.68 -> 0.61), but in the round-6
+// step (its consumers the weight-stationary dU / dX GEMMs) the whole step
+// runs 5.406-5.419 vs 5.411-5.434 ms (profiles/r06_ab_ln_bwd_store_policy.txt).
+constexpr bool kLnFwdNT = true, kLnBwdNT = true;
 template <bool NT, int V>
 __device__ __forceinline__ void st_ln(float* p, const float (&o)[V]) {
   if constexpr (NT) stv(p, o); else stc(p, o);
