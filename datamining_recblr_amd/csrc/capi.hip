@@ -741,8 +741,7 @@ int rb_gemm_tn_h(const float* dY, int64_t ldy, const float* X, int64_t ldx, int6
   if (M <= 0 || N <= 0 || K <= 0) return fail("rb_gemm_tn_h: empty shape");
   if (N % 128 || K % 128 || N > 65536 || K > 65536)
     return fail("rb_gemm_tn_h: N and K must be multiples of 128 (<= 65536)");
-  if (splits < 8 || splits % 8 || splits > 65536)
-    return fail("rb_gemm_tn_h: splits must be a positive multiple of 8");
+  if (splits < 1 || splits > 65536) return fail("rb_gemm_tn_h: splits must be in [1, 65536]");
   if (ldy < N || ldx < K || ldy % 4 || ldx % 4) return fail("rb_gemm_tn_h: bad row strides");
   if (!aligned16(dY) || !aligned16(X)) return fail("rb_gemm_tn_h: dY and X must be 16-byte aligned");
   if ((N / 128) * (K / 128) * splits > 0x7fffffffLL) return fail("rb_gemm_tn_h: grid too large");

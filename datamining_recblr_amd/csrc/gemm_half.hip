@@ -1030,6 +1030,7 @@ __device__ __forceinline__ void tn_body(char* smem, const float* __restrict__ Y,
   const int idx = (blockIdx.x & 7) * (G >> 3) + (blockIdx.x >> 3);
   const int nt = (N / CF::YC) * nt_k;
   const int tile = idx % nt, s = idx / nt;
+  if (s >= S) return;   // the grid's padding to a multiple of 8 (workgroup-uniform)
   const int n0 = (tile / nt_k) * CF::YC, k0 = (tile % nt_k) * CF::XC;
   const int64_t r_begin = (int64_t)s * mk;
   const int64_t r_end = r_begin + mk < M ? r_begin + mk : M;
@@ -1662,7 +1663,9 @@ int launch_gemm_tn_h(const float* Y, int64_t ldy, const float* X, int64_t ldx, i
     }
     const int nt_k = K / CF::XC;
     const int nt = (N / CF::YC) * nt_k;
-    k_gemm_tn_h<NBN, NBK><<<(unsigned)(nt * S), CF::THREADS, CF::LDS, st>>>(
+    // (the block -> (tile, split) map needs a multiple of 8 workgroups: any
+    // split count, the padding workgroups return at once)
+    k_gemm_tn_h<NBN, NBK><<<(unsigned)((nt * S + 7) / 8 * 8), CF::THREADS, CF::LDS, st>>>(
         Y, ldy, X, ldx, M, N, K, ymax, xmax, parts, S, mk, nt_k);
   };
   switch (tn_tile_shape(N, K)) {

@@ -98,6 +98,29 @@ def _f16_grads_ok(seq, table) -> bool:
             and (V + 255) // 256 * 256 <= GEMM_TN_MAX_N)
 
 
+# RECBLR_CE_ROUND_SPLITS=0: the item-table product's split count as round 5
+# chose it (a multiple of 8; A/B)
+_ROUND_SPLITS = _env_choice("RECBLR_CE_ROUND_SPLITS", "1", ("0", "1")) == "1"
+
+
+def _round_splits(dev, nt: int, rows: int) -> int:
+    """Split count for a weight-gradient product of nt one-per-CU tiles over
+    `rows` rows: the fewest (launch rounds x 32-row steps per workgroup, + 3
+    steps of fixed cost); the smallest such count (fewer partials to sum).
+    The item table's product at B = 2,048: 42 tiles x 6 splits in one round
+    instead of 8 splits in 1.3."""
+    from .linear import _ncus
+    n = _ncus.get(dev)
+    if n is None:
+        n = _ncus[dev] = torch.cuda.get_device_properties(dev).multi_processor_count
+    best, best_cost = 1, None
+    for s in range(1, max(1, rows // 32) + 1):
+        cost = -(-nt * s // n) * (-(-(-(-rows // s)) // 32) + 3)
+        if best_cost is None or cost < best_cost:
+            best, best_cost = s, cost
+    return best
+
+
 def _group_max(x: torch.Tensor) -> torch.Tensor:
     """max |x| over each 32-row group of a [n, c] tensor (a partial last group
     too): the weight-gradient kernel's operand scale."""
@@ -123,7 +146,9 @@ def _bwd_f16(seq, table, target, lse, dloss, want_seq, want_items, split):
     dseq = dtable = None
     if want_items:
         Vp = p.shape[1]
-        S1 = max(8, min(_tn_splits8(seq.device, (Vp // 256) * (d // 128)), B // 256 // 8 * 8))
+        nt = (Vp // 256) * (d // 128)
+        S1 = (_round_splits(seq.device, nt, B) if _ROUND_SPLITS
+              else max(8, min(_tn_splits8(seq.device, nt), B // 256 // 8 * 8)))
         smax = s_seq.gmax if s_seq.gmax is not None else kernels.group_absmax(seq)
         parts = _timed("gemm", fl, kernels.gemm_tn_h, p, seq, bmax, smax, S1)
         dtable = kernels.colsum(parts.view(S1, -1)).view(Vp, d)[:V]

@@ -579,7 +579,7 @@ int rb_gemm_nt_h_dact(const float* A, int64_t lda, int64_t M, int64_t R, const v
  * N, K] fp32, every slot written; sum them in order, e.g. rb_colsum).
  * ymax / xmax [ceil(M/32)]: max |dY| / |X| over each 32-row group — the rmax
  * side outputs of the rb_gemm_nt_h calls that read the same operands (the
- * operand scales).  N % 128 == 0, K % 128 == 0, splits % 8 == 0, row strides
+ * operand scales).  N % 128 == 0, K % 128 == 0, splits >= 1, row strides
  * multiples of 4, operands 16-B aligned.  A row chunk (ceil(ceil(M/splits)/32)
  * * 32 rows) must span < 2 GiB of either operand, max(ldy, ldx) * 4 bytes per
  * row: the kernel addresses a chunk with 32-bit offsets; pass more splits

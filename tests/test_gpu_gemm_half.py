@@ -303,7 +303,8 @@ def _row_group_max(a):
 
 @pytest.mark.parametrize("M,N,K,S", [(204632, 512, 256, 64), (70001, 512, 128, 128),
                                      (4096 + 77, 128, 256, 256), (5000, 128, 512, 8),
-                                     (300, 256, 128, 64)])
+                                     (300, 256, 128, 64), (2048 + 45, 10752, 128, 6),
+                                     (3000, 128, 128, 5)])
 def test_weight_gradient_tn_matches_fp64(cuda, M, N, K, S):
     """rb_gemm_tn_h: dW = dY^T X from fixed-order row-chunk partials (empty
     chunks write zeros) at fp32-level error next to hipBLASLt's fp32 GEMM, with
