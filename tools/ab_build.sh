@@ -5,6 +5,6 @@
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
-/opt/rocm/bin/hipcc -parallel-jobs=4 -O3 -std=c++17 -shared -fPIC --offload-arch=gfx950 \
+/opt/rocm/bin/hipcc -parallel-jobs=4 -O3 -std=c++20 -shared -fPIC --offload-arch=gfx950 \
   -ffp-contract=off -Wno-unused-function "$@" -I include \
   -o datamining_recblr_amd/lib/ab_$name.so datamining_recblr_amd/csrc/*.hip
